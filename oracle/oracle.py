@@ -1,0 +1,141 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of the CPU oracle.
+
+Two back-ends with one calling convention (numpy in, numpy out):
+
+* ``Oracle("port")``  -> ``oracle/liboracle_pfdr.so``, the clean-room C
+  restatement (``oracle/pfdr_oracle_body.h``), single-threaded;
+* ``Oracle("ref")``   -> ``oracle/_ref/libpfdr_ref_seq.so``, the REFERENCE
+  sources compiled without OpenMP (bit-exact pin of the restatement);
+* ``Oracle("ref_omp")`` -> ``oracle/_ref/libpfdr_ref_omp.so``, the reference
+  with its OpenMP loops (CPU baseline timing only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product package never does.
+
+The argument lists mirror the reference functions
+(include/PFDR_graph_quadratic_d1_l1.hpp:36-42,
+ include/PFDR_graph_quadratic_d1_bounds.hpp:34-40,
+ include/PFDR_graph_loss_d1_simplex.hpp:24-30,
+ include/proj_simplex.hpp:33-35) minus ``verbose``; outputs follow the MEX
+wrappers (octave/mex/PFDR_*_mex.cpp): X (or P), it, Obj[itMax+1], Dif[itMax].
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBS = {
+    "port": (os.path.join(HERE, "liboracle_pfdr.so"), "oracle_"),
+    "ref": (os.path.join(HERE, "_ref", "libpfdr_ref_seq.so"), "ref_"),
+    "ref_omp": (os.path.join(HERE, "_ref", "libpfdr_ref_omp.so"), "ref_"),
+}
+_CACHE = {}
+
+
+def build(ref=True):
+    """Compile the restatement (and, where /root/reference exists, _ref)."""
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+    if ref:
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def available(kind):
+    return os.path.exists(_LIBS[kind][0])
+
+
+def _ptr(a, ct):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def _real(dtype):
+    dtype = np.dtype(dtype)
+    if dtype == np.float32:
+        return C.c_float, "f32"
+    if dtype == np.float64:
+        return C.c_double, "f64"
+    raise TypeError("oracle supports float32/float64 only, got %s" % dtype)
+
+
+class Oracle:
+    def __init__(self, kind="port"):
+        path, prefix = _LIBS[kind]
+        if path not in _CACHE:
+            if not os.path.exists(path):
+                raise FileNotFoundError(
+                    "%s missing: run `make -C oracle %s`" %
+                    (path, "ref" if kind != "port" else "all"))
+            _CACHE[path] = C.CDLL(path)
+        self.lib = _CACHE[path]
+        self.prefix = prefix
+        self.kind = kind
+
+    def _fn(self, name, sfx):
+        return getattr(self.lib, "%s%s_%s" % (self.prefix, name, sfx))
+
+    # ---------------------------------------------------------------- l1 --
+    def quadratic_d1_l1(self, X0, Y, A, N, Eu, Ev, La_d1, La_l1=None,
+                        positivity=0, Ltype=0, L=None, rho=1.5, condMin=1e-3,
+                        difRcd=0.0, difTol=1e-5, itMax=1000, obj=False,
+                        dif=False):
+        X = np.array(X0, copy=True)
+        ct, sfx = _real(X.dtype)
+        V, E = X.size, Eu.size
+        Obj = np.zeros(itMax + 1, X.dtype) if obj else None
+        Dif = np.zeros(max(itMax, 1), X.dtype) if dif else None
+        it = C.c_int(0)
+        fn = self._fn("pfdr_quadratic_d1_l1", sfx)
+        fn(C.c_int(V), C.c_int(E), C.c_int(N), _ptr(X, ct), _ptr(Y, ct),
+           _ptr(A, ct), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(La_d1, ct), _ptr(La_l1, ct), C.c_int(positivity),
+           C.c_int(Ltype), _ptr(L, ct), ct(rho), ct(condMin), ct(difRcd),
+           ct(difTol), C.c_int(itMax), C.byref(it), _ptr(Obj, ct),
+           _ptr(Dif, ct))
+        return X, it.value, Obj, Dif
+
+    # ------------------------------------------------------------ bounds --
+    def quadratic_d1_bounds(self, X0, Y, A, N, Eu, Ev, La_d1, lo=-np.inf,
+                            hi=np.inf, Ltype=0, L=None, rho=1.5,
+                            condMin=1e-3, difRcd=0.0, difTol=1e-5,
+                            itMax=1000, obj=False, dif=False):
+        X = np.array(X0, copy=True)
+        ct, sfx = _real(X.dtype)
+        V, E = X.size, Eu.size
+        Obj = np.zeros(itMax + 1, X.dtype) if obj else None
+        Dif = np.zeros(max(itMax, 1), X.dtype) if dif else None
+        it = C.c_int(0)
+        fn = self._fn("pfdr_quadratic_d1_bounds", sfx)
+        fn(C.c_int(V), C.c_int(E), C.c_int(N), _ptr(X, ct), _ptr(Y, ct),
+           _ptr(A, ct), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(La_d1, ct), ct(lo), ct(hi), C.c_int(Ltype), _ptr(L, ct),
+           ct(rho), ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax),
+           C.byref(it), _ptr(Obj, ct), _ptr(Dif, ct))
+        return X, it.value, Obj, Dif
+
+    # ----------------------------------------------------------- simplex --
+    def loss_d1_simplex(self, P0, Q, K, Eu, Ev, La_d1, al=0.1, La_f=None,
+                        rho=1.0, condMin=0.1, difRcd=0.0, difTol=1e-4,
+                        itMax=1000, obj=False, dif=False):
+        P = np.array(P0, copy=True)
+        ct, sfx = _real(P.dtype)
+        V, E = P.size // K, Eu.size
+        Obj = np.zeros(itMax + 1, P.dtype) if obj else None
+        Dif = np.zeros(max(itMax, 1), P.dtype) if dif else None
+        it = C.c_int(0)
+        fn = self._fn("pfdr_loss_d1_simplex", sfx)
+        fn(C.c_int(K), C.c_int(V), C.c_int(E), ct(al), _ptr(La_f, ct),
+           _ptr(P, ct), _ptr(Q, ct), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(La_d1, ct), ct(rho), ct(condMin), ct(difRcd), ct(difTol),
+           C.c_int(itMax), C.byref(it), _ptr(Obj, ct), _ptr(Dif, ct))
+        return P, it.value, Obj, Dif
+
+    def proj_simplex_metric(self, X0, M, D, N, nm, A, na):
+        X = np.array(X0, copy=True)
+        ct, sfx = _real(X.dtype)
+        fn = self._fn("proj_simplex_metric", sfx)
+        fn(_ptr(X, ct), _ptr(M, ct), C.c_int(D), C.c_int(N), C.c_int(nm),
+           _ptr(A, ct), C.c_int(na))
+        return X
