@@ -1,0 +1,147 @@
+// Shared device/host helpers of the MI355X PFDR library (gfx950 only).
+//
+// Everything here is written for CDNA4: 64-lane wavefronts, 256-thread
+// workgroups (4 waves, one per SIMD), 16-byte per-lane vector memory
+// accesses on every streamed array.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../../include/pfdr_mi355x.h"
+
+namespace pfdr {
+
+constexpr int kBlock = 256;   // threads per workgroup (4 wave64)
+constexpr int kWave = 64;
+
+// --------------------------------------------------------------- errors --
+struct HipError {
+    hipError_t err;
+    const char *what;
+    int line;
+};
+
+#define PFDR_HIP(call)                                                     \
+    do {                                                                   \
+        hipError_t _e = (call);                                            \
+        if (_e != hipSuccess) throw ::pfdr::HipError{_e, #call, __LINE__}; \
+    } while (0)
+
+// convert an exception escaping a solver into a C status code
+int report_error(const char *fn, const HipError &h);
+int report_error(const char *fn, const char *msg);
+
+// ----------------------------------------------------------- real types --
+template <typename real> struct Vec;
+template <> struct Vec<float> {
+    using v2 = float2;
+    using v4 = float4;
+    static constexpr int kPer16B = 4;
+};
+template <> struct Vec<double> {
+    using v2 = double2;
+    using v4 = double4;
+    static constexpr int kPer16B = 2;
+};
+
+// machine epsilon / huge of the reference (src/PFDR_graph_quadratic_d1_l1.cpp:286-292,
+// src/PFDR_graph_quadratic_d1_bounds.cpp:260-278)
+template <typename real> struct Lim;
+template <> struct Lim<float> {
+    static constexpr float eps = 1.19209290e-07f;
+    static constexpr float huge = __builtin_huge_valf();
+};
+template <> struct Lim<double> {
+    static constexpr double eps = 2.2204460492503131e-16;
+    static constexpr double huge = __builtin_huge_val();
+};
+
+// ---------------------------------------------------- loop control block --
+// Device-resident iteration state.  The per-iteration kernels return at once
+// when `halt` is set, so the host can enqueue iterations in chunks and read
+// the state back only between chunks (no per-iteration host round trip).
+template <typename real>
+struct Ctrl {
+    int it;        // completed iterations (reference it_)
+    int halt;      // 1: stop issuing updates (stop or reconditioning)
+    int stop;      // 1: converged or itMax reached
+    int recond;    // 1: reconditioning requested (dif < difRcd)
+    int obj_it;    // last iteration index whose objective has been written
+    int itMax;
+    real dif;      // last iterate evolution (reference dif)
+    real difTol;   // compared with dif (squared for the quadratic solvers)
+    real difRcd;   // idem, updated by the host after each reconditioning
+    real eps;      // denominator floor of the relative evolution
+    real c;        // scratch scalar: amplitude of the preconditioner
+    int cnt;       // scratch count
+};
+
+// ------------------------------------------------------------ reductions --
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Deterministic block sum (fixed tree), result valid in thread 0.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *lds /* >= kBlock/64 */) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds[w] = v;
+    __syncthreads();
+    T s = T(0);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kBlock / kWave; i++) s += lds[i];
+    }
+    __syncthreads();
+    return s;
+}
+
+inline int grid_for(long n, int per_thread = 1) {
+    long t = (n + per_thread - 1) / per_thread;
+    long g = (t + kBlock - 1) / kBlock;
+    return (int)(g > 0 ? g : 1);
+}
+
+// ------------------------------------------------------- device buffers --
+// RAII device allocation (hipMalloc'd, freed on scope exit).
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) PFDR_HIP(hipMalloc(&p, count * sizeof(T)));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DevBuf() { release(); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    T *get() const { return p; }
+};
+
+// Library-owned stream of the calling thread's current device.
+hipStream_t lib_stream();
+
+// Upload a host array into a fresh device buffer (nullptr stays nullptr).
+template <typename T>
+void upload(DevBuf<T> &d, const T *h, size_t n, hipStream_t s) {
+    if (!h || !n) { d.release(); return; }
+    d.alloc(n);
+    PFDR_HIP(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+}  // namespace pfdr

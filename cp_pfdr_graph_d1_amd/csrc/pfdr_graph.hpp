@@ -1,0 +1,21 @@
+// Vertex -> incidence CSR (see pfdr_graph.hip).
+#pragma once
+#include "pfdr_dev.hpp"
+
+namespace pfdr {
+
+struct Incidence {
+    int V = 0;          // vertices with a row
+    long n = 0;         // incidence slots (2E, plus received halo slots)
+    DevBuf<int> ptr;    // V + 1 row offsets
+    DevBuf<unsigned> idx;  // slot ids, sorted by (vertex, e, side)
+};
+
+// Throws std::runtime_error unless every endpoint lies in [0, V).
+void check_endpoints(const int *dEu, const int *dEv, long E, int V, hipStream_t s);
+
+// Build the CSR (validates the endpoints first) of the 2E slots of edges (Eu, Ev) over vertices [0, V).
+void build_incidence(const int *dEu, const int *dEv, int V, long E,
+                     Incidence &inc, hipStream_t s);
+
+}  // namespace pfdr

@@ -1,0 +1,211 @@
+// Runtime pieces of libpfdr_mi355x.so that are not kernels: error state,
+// library stream, profiler, session C ABI dispatch.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "pfdr_session.hpp"
+
+namespace pfdr {
+
+static thread_local std::string g_last_error;
+
+static void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+int report_error(const char *fn, const HipError &h) {
+    set_error("%s: HIP error %d (%s) in `%s` (line %d)", fn, (int)h.err,
+              hipGetErrorString(h.err), h.what, h.line);
+    return PFDR_ERR_HIP;
+}
+
+int report_error(const char *fn, const char *msg) {
+    set_error("%s: %s", fn, msg);
+    return PFDR_ERR_ARG;
+}
+
+hipStream_t lib_stream() {
+    // one non-blocking stream per (thread, device)
+    static thread_local hipStream_t streams[64] = {};
+    int dev = 0;
+    PFDR_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) throw HipError{hipErrorInvalidDevice, "device id", __LINE__};
+    if (!streams[dev]) {
+        PFDR_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+    }
+    return streams[dev];
+}
+
+// ------------------------------------------------------------ Profiler --
+Profiler::~Profiler() {
+    for (auto &p : pend_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : pool_) (void)hipEventDestroy(e);
+    if (open_ev_) (void)hipEventDestroy(open_ev_);
+}
+
+hipEvent_t Profiler::take() {
+    if (!pool_.empty()) {
+        hipEvent_t e = pool_.back();
+        pool_.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    PFDR_HIP(hipEventCreate(&e));
+    return e;
+}
+
+void Profiler::begin(const char *name, hipStream_t s) {
+    auto it = ids_.find(name);
+    int id;
+    if (it == ids_.end()) {
+        id = (int)total_ms_.size();
+        ids_[name] = id;
+        total_ms_.push_back(0.0);
+        count_.push_back(0);
+    } else {
+        id = it->second;
+    }
+    open_id_ = id;
+    open_ev_ = take();
+    PFDR_HIP(hipEventRecord(open_ev_, s));
+}
+
+void Profiler::end(hipStream_t s) {
+    hipEvent_t b = take();
+    PFDR_HIP(hipEventRecord(b, s));
+    pend_.push_back({open_id_, open_ev_, b});
+    open_ev_ = nullptr;
+    open_id_ = -1;
+}
+
+void Profiler::resolve() {
+    for (auto &p : pend_) {
+        float ms = 0.f;
+        PFDR_HIP(hipEventSynchronize(p.b));
+        PFDR_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        total_ms_[p.id] += ms;
+        count_[p.id] += 1;
+        pool_.push_back(p.a);
+        pool_.push_back(p.b);
+    }
+    pend_.clear();
+}
+
+bool Profiler::stats(const char *name, int *launches, double *mean_ms) const {
+    auto it = ids_.find(name);
+    if (it == ids_.end()) { *launches = 0; *mean_ms = 0.0; return false; }
+    int c = count_[it->second];
+    *launches = c;
+    *mean_ms = c ? total_ms_[it->second] / c : 0.0;
+    return true;
+}
+
+// defined in the solver translation units
+SessionBase *create_quadratic_session(const pfdr_problem *p);
+SessionBase *create_simplex_session(const pfdr_problem *p);
+
+}  // namespace pfdr
+
+using namespace pfdr;
+
+#define PFDR_GUARD(fn, body)                                         \
+    try {                                                            \
+        body;                                                        \
+    } catch (const HipError &h) {                                    \
+        return report_error(fn, h);                                  \
+    } catch (const std::exception &ex) {                             \
+        return report_error(fn, ex.what());                          \
+    }
+
+extern "C" const char *pfdr_last_error(void) { return g_last_error.c_str(); }
+extern "C" int pfdr_abi_version(void) { return 1; }
+extern "C" int pfdr_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+    return n;
+}
+
+extern "C" int pfdr_session_create(pfdr_session **out, const pfdr_problem *p) {
+    if (!out || !p) return report_error("pfdr_session_create", "null argument");
+    *out = nullptr;
+    PFDR_GUARD("pfdr_session_create", {
+        SessionBase *impl = nullptr;
+        if (p->kind == PFDR_KIND_L1 || p->kind == PFDR_KIND_BOUNDS)
+            impl = create_quadratic_session(p);
+        else if (p->kind == PFDR_KIND_SIMPLEX)
+            impl = create_simplex_session(p);
+        else
+            return report_error("pfdr_session_create", "unknown problem kind");
+        *out = new pfdr_session{impl};
+    });
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_session_run(pfdr_session *s, int iters, int *it_total) {
+    if (!s) return report_error("pfdr_session_run", "null session");
+    PFDR_GUARD("pfdr_session_run", {
+        int it = s->impl->run(iters);
+        if (it_total) *it_total = it;
+    });
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_session_result(pfdr_session *s, void *X, int *it,
+                                   void *Obj, void *Dif) {
+    if (!s) return report_error("pfdr_session_result", "null session");
+    PFDR_GUARD("pfdr_session_result", { s->impl->result(X, it, Obj, Dif); });
+    return PFDR_OK;
+}
+
+extern "C" void *pfdr_session_device_x(pfdr_session *s) {
+    return s ? s->impl->device_x() : nullptr;
+}
+
+extern "C" int pfdr_session_set_profiling(pfdr_session *s, int on) {
+    if (!s) return report_error("pfdr_session_set_profiling", "null session");
+    s->impl->prof.on = (on != 0);
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_session_kernel_stats(pfdr_session *s, const char *kernel,
+                                         int *launches, double *mean_ms) {
+    if (!s || !kernel || !launches || !mean_ms)
+        return report_error("pfdr_session_kernel_stats", "null argument");
+    PFDR_GUARD("pfdr_session_kernel_stats", {
+        PFDR_HIP(hipStreamSynchronize(s->impl->stream));
+        s->impl->prof.resolve();
+        s->impl->prof.stats(kernel, launches, mean_ms);
+    });
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_session_sync(pfdr_session *s) {
+    if (!s) return report_error("pfdr_session_sync", "null session");
+    PFDR_GUARD("pfdr_session_sync", {
+        PFDR_HIP(hipStreamSynchronize(s->impl->stream));
+    });
+    return PFDR_OK;
+}
+
+extern "C" int64_t pfdr_session_device_bytes(pfdr_session *s) {
+    return s ? s->impl->device_bytes : -1;
+}
+
+extern "C" void pfdr_session_destroy(pfdr_session *s) {
+    if (!s) return;
+    try {
+        (void)hipStreamSynchronize(s->impl->stream);
+        delete s->impl;
+    } catch (...) {
+    }
+    delete s;
+}

@@ -1,0 +1,64 @@
+// Session base class shared by the quadratic and simplex solvers: stream,
+// kernel-launch profiling with HIP events, chunked device-controlled
+// iteration loop bookkeeping.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "pfdr_dev.hpp"
+
+namespace pfdr {
+
+// HIP-event timing of named kernels on the session stream.  When enabled,
+// every launch of a profiled kernel is bracketed by two events; durations
+// are resolved after the stream has been synchronised.
+class Profiler {
+  public:
+    bool on = false;
+    ~Profiler();
+    void begin(const char *name, hipStream_t s);
+    void end(hipStream_t s);
+    void resolve();  // call after the stream has been synchronised
+    bool stats(const char *name, int *launches, double *mean_ms) const;
+
+  private:
+    struct Pending { int id; hipEvent_t a, b; };
+    std::vector<Pending> pend_;
+    std::vector<hipEvent_t> pool_;
+    std::map<std::string, int> ids_;
+    std::vector<double> total_ms_;
+    std::vector<int> count_;
+    int open_id_ = -1;
+    hipEvent_t open_ev_ = nullptr;
+    hipEvent_t take();
+};
+
+struct ProfScope {
+    Profiler &p;
+    hipStream_t s;
+    bool on;
+    ProfScope(Profiler &pr, const char *name, hipStream_t st)
+        : p(pr), s(st), on(pr.on) { if (on) p.begin(name, s); }
+    ~ProfScope() { if (on) p.end(s); }
+};
+
+class SessionBase {
+  public:
+    virtual ~SessionBase() = default;
+    // run up to `iters` more iterations; returns total iterations so far
+    virtual int run(int iters) = 0;
+    virtual void result(void *X_host, int *it, void *Obj_host,
+                        void *Dif_host) = 0;
+    virtual void *device_x() = 0;
+    int64_t device_bytes = 0;
+    hipStream_t stream = nullptr;
+    Profiler prof;
+    int device = 0;
+};
+
+}  // namespace pfdr
+
+struct pfdr_session {
+    pfdr::SessionBase *impl;
+};

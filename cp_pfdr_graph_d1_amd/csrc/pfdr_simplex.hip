@@ -1,0 +1,973 @@
+// MI355X PFDR solver for
+//     F(p) = f(p; q) + sum_{e,k} la_e |p_uk - p_vk| + i_simplex(p)
+// (linear, quadratic or smoothed Kullback-Leibler loss), the algorithm of
+// reference src/PFDR_graph_loss_d1_simplex.cpp:372-715, and the metric
+// simplex projection of src/proj_simplex_metric.cpp:18-83.
+//
+//   per iteration:
+//     k_sx_edge_sweep   : K-wide TV prox on every (edge, label) + relaxed Z
+//                         update + DR contributions W*Z      ref :589-634
+//     k_sx_average      : ordered per-(vertex, label) DR average over the
+//                         incidence CSR (the reference parallelises this
+//                         over labels only, :636-648)
+//     k_sx_project      : per-vertex metric simplex projection, evolution
+//                         partials (l1 or label changes) and the NEXT
+//                         explicit step FP                  ref :651-691,
+//                                                               :567-587
+//     k_sx_finalize     : stop / recondition flags (when tracked)
+// Layouts: P, Q, Ga, GaQ, FP are K-by-V (index v*K + k) as in the reference;
+// edge state is K-by-E; the DR contributions are wz[side][e][k].
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+
+#include "pfdr_graph.hpp"
+#include "pfdr_session.hpp"
+
+namespace pfdr {
+
+enum Loss : int { LOSS_LINEAR = 0, LOSS_QUAD = 1, LOSS_KL = 2 };
+
+template <typename real>
+struct SxConst {
+    int K;
+    int loss;
+    real alK, al1, alKal1;
+};
+
+// ------------------------------------------------ metric projection ----
+// Projection of x (D values, stride 1) onto {x >= 0, sum x = a} in the
+// metric diag(1/m): active-set sweep of ref src/proj_simplex_metric.cpp:41-80,
+// operation for operation.  Works in place; the active set lives in a
+// register bit mask (D <= 64) or in a small local array (D <= 1024).
+template <typename real, int W>
+__device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
+    unsigned long long act[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) act[w] = 0ull;
+    real la = (x[0] - a) / m[0];
+    x[0] = x[0] / m[0];
+    act[0] = 1ull;
+    real s = m[0];
+    for (int d = 1; d < D; d++) {
+        const real md = m[d];
+        const real xd = x[d] / md;
+        x[d] = xd;
+        if (xd > la) {
+            act[d >> 6] |= 1ull << (d & 63);
+            s += md;
+            la += md * (xd - la) / s;
+        }
+    }
+    bool changed = true;
+    while (changed) {
+        changed = false;
+        for (int d = 0; d < D; d++) {
+            if ((act[d >> 6] >> (d & 63)) & 1ull) {
+                const real xd = x[d];
+                if (xd < la) {
+                    act[d >> 6] &= ~(1ull << (d & 63));
+                    const real md = m[d];
+                    s -= md;
+                    la += md * (la - xd) / s;
+                    changed = true;
+                }
+            }
+        }
+    }
+    for (int d = 0; d < D; d++) {
+        x[d] = ((act[d >> 6] >> (d & 63)) & 1ull) ? (x[d] - la) * m[d] : real(0);
+    }
+}
+
+template <typename real, int W>
+__global__ void k_proj_simplex(real *X, const real *M, int D, int N, int nm,
+                               const real *A, int na) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const real *m = (nm > n) ? M + (size_t)D * n : M + (size_t)D * (nm - 1);
+    const real a = (na > n) ? A[n] : A[na - 1];
+    proj_simplex_column<real, W>(X + (size_t)D * n, m, D, a);
+}
+
+// ------------------------------------------------------------- kernels --
+template <typename real>
+__global__ void k_sx_z_init(long EK, int K, const int *__restrict__ Eu,
+                            const int *__restrict__ Ev,
+                            const real *__restrict__ P, real *__restrict__ Zu,
+                            real *__restrict__ Zv) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    Zu[i] = P[(long)Eu[e] * K + k];
+    Zv[i] = P[(long)Ev[e] * K + k];
+}
+
+// reconditioning, step 1: retrieve the metric before its normalisation
+// (ref :92-135).  One thread per vertex.
+template <typename real>
+__global__ void k_sx_recover(int V, SxConst<real> c, const real *__restrict__ La_f,
+                             const real *__restrict__ Q,
+                             const real *__restrict__ GaQ,
+                             real *__restrict__ Ga) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int K = c.K;
+    const long b = (long)v * K;
+    if (c.loss == LOSS_QUAD) {
+        if (!La_f) {
+            for (int k = 0; k < K; k++) Ga[b + k] = GaQ[b + k];
+        } else {
+            const real s = real(1) / La_f[v];
+            for (int k = 0; k < K; k++) Ga[b + k] = s * GaQ[b + k];
+        }
+    } else if (c.loss == LOSS_KL) {
+        if (!La_f) {
+            for (int k = 0; k < K; k++) Ga[b + k] = GaQ[b + k] / (c.alK + c.al1 * Q[b + k]);
+        } else {
+            const real s = real(1) / La_f[v];
+            for (int k = 0; k < K; k++) Ga[b + k] = s * GaQ[b + k] / (c.alK + c.al1 * Q[b + k]);
+        }
+    } else {
+        int imax = 0;
+        real qmax = Q[b];
+        for (int k = 1; k < K; k++) {
+            if (qmax < Q[b + k]) { qmax = Q[b + k]; imax = k; }
+        }
+        const real s = GaQ[b + imax] / qmax / Ga[b + imax];
+        for (int k = 0; k < K; k++) Ga[b + k] *= s;
+    }
+}
+
+// reconditioning, step 2: auxiliary variables -> subgradients (ref :136-156)
+template <typename real>
+__global__ void k_sx_subgrad(long EK, SxConst<real> c, const int *__restrict__ Eu,
+                             const int *__restrict__ Ev,
+                             const real *__restrict__ P,
+                             const real *__restrict__ Q,
+                             const real *__restrict__ Ga,
+                             const real *__restrict__ GaQ,
+                             const real *__restrict__ Wu,
+                             const real *__restrict__ Wv,
+                             real *__restrict__ Zu, real *__restrict__ Zv) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const int K = c.K;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    if (c.loss == LOSS_LINEAR) {
+        Zu[i] = (Wu[i] / Ga[u]) * (P[u] + GaQ[u] - Zu[i]);
+        Zv[i] = (Wv[i] / Ga[v]) * (P[v] + GaQ[v] - Zv[i]);
+    } else if (c.loss == LOSS_QUAD) {
+        Zu[i] = (Wu[i] / Ga[u]) * (P[u] - GaQ[u] * (P[u] - Q[u]) - Zu[i]);
+        Zv[i] = (Wv[i] / Ga[v]) * (P[v] - GaQ[v] * (P[v] - Q[v]) - Zv[i]);
+    } else {
+        Zu[i] = (Wu[i] / Ga[u]) * (P[u] + GaQ[u] / (c.alKal1 + P[u]) - Zu[i]);
+        Zv[i] = (Wv[i] / Ga[v]) * (P[v] + GaQ[v] / (c.alKal1 + P[v]) - Zv[i]);
+    }
+}
+
+// Hessian of the loss (ref :159-190), one thread per (v, k)
+template <typename real>
+__global__ void k_sx_hessian(long VK, SxConst<real> c, const real *__restrict__ La_f,
+                             const real *__restrict__ P,
+                             const real *__restrict__ Q,
+                             real *__restrict__ Ga) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VK) return;
+    if (c.loss == LOSS_LINEAR) {
+        Ga[i] = real(0);
+    } else if (c.loss == LOSS_QUAD) {
+        Ga[i] = La_f ? La_f[i / c.K] : real(1);
+    } else {
+        const real t = c.alKal1 + P[i];
+        if (La_f) Ga[i] = La_f[i / c.K] * (c.alK + c.al1 * Q[i]) / (t * t);
+        else Ga[i] = (c.alK + c.al1 * Q[i]) / (t * t);
+    }
+}
+
+// d1 splitting weights (ref :192-221) into W and both contribution slots
+template <typename real>
+__global__ void k_sx_d1_weights(long EK, int K, const int *__restrict__ Eu,
+                                const int *__restrict__ Ev,
+                                const real *__restrict__ La_d1, int init,
+                                real condMin, const real *__restrict__ P,
+                                real *__restrict__ Wu, real *__restrict__ Wv,
+                                real *__restrict__ wz) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    real w;
+    if (init) {
+        w = La_d1[e];
+    } else {
+        real a = P[(long)Eu[e] * K + k] - P[(long)Ev[e] * K + k];
+        if (a < real(0)) a = -a;
+        if (a < condMin) a = condMin;
+        w = La_d1[e] / a;
+    }
+    Wu[i] = w;
+    Wv[i] = w;
+    wz[i] = w;
+    wz[EK + i] = w;
+}
+
+// ordered per-(v, k) sum over the incidence CSR: slot s = 2e + side lives at
+// wz[side*EK + e*K + k]
+template <typename real>
+__device__ __forceinline__ real sx_gather(long i, int K, long EK,
+                                          const int *__restrict__ ptr,
+                                          const unsigned *__restrict__ idx,
+                                          const real *__restrict__ wz) {
+    const long v = i / K;
+    const int k = (int)(i - v * K);
+    const int j0 = ptr[v], j1 = ptr[v + 1];
+    real s = real(0);
+    for (int j = j0; j < j1; j++) {
+        const unsigned slot = idx[j];
+        s += wz[(long)(slot & 1u) * EK + (long)(slot >> 1) * K + k];
+    }
+    return s;
+}
+
+// metric of every (v, k), prox weights input and first-order information
+// (ref :192-285 per element, :307-335)
+template <typename real>
+__global__ void k_sx_precond_vertex(long VK, SxConst<real> c, long EK,
+                                    const int *__restrict__ ptr,
+                                    const unsigned *__restrict__ idx,
+                                    const real *__restrict__ wz,
+                                    const real *__restrict__ La_f,
+                                    const real *__restrict__ Q, real cap,
+                                    real *__restrict__ Ga,
+                                    real *__restrict__ invAux,
+                                    real *__restrict__ GaQ) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VK) return;
+    const int K = c.K;
+    const real s = sx_gather(i, K, EK, ptr, idx, wz);
+    real g;
+    if (c.loss == LOSS_LINEAR) {
+        // Ga itself accumulated the weights from zero, then was inverted
+        g = real(1) / s;
+        invAux[i] = g;
+    } else {
+        g = Ga[i];
+        g += s;
+        invAux[i] = real(1) / s;
+        g = real(1) / g;
+    }
+    const long v = i / K;
+    // cap by the Lipschitz constant of the loss (ref :249-285)
+    if (c.loss == LOSS_QUAD) {
+        if (La_f) {
+            const real cv = cap / La_f[v];
+            if (g > cv) g = cv;
+        } else if (cap < real(1)) {
+            if (g > cap) g = cap;
+        }
+    } else if (c.loss == LOSS_KL) {
+        real b;
+        if (!La_f) b = real(1) / (c.alKal1 * c.alKal1);
+        else b = La_f[v] * real(1) / (c.alKal1 * c.alKal1);
+        const real cv = cap / ((c.alK + c.al1 * Q[i]) * b);
+        if (g > cv) g = cv;
+    }
+    Ga[i] = g;
+    // metric times first-order information (ref :307-335)
+    if (c.loss == LOSS_LINEAR) {
+        GaQ[i] = g * Q[i];
+    } else if (c.loss == LOSS_QUAD) {
+        GaQ[i] = La_f ? La_f[v] * g : g;
+    } else {
+        GaQ[i] = La_f ? La_f[v] * g * (c.alK + c.al1 * Q[i]) : g * (c.alK + c.al1 * Q[i]);
+    }
+}
+
+// normalised splitting weights, prox weights/thresholds (ref :230-241,
+// :287-306) and, on reconditioning, subgradients -> auxiliary (:337-358)
+template <typename real>
+__global__ void k_sx_precond_edge(long EK, SxConst<real> c,
+                                  const int *__restrict__ Eu,
+                                  const int *__restrict__ Ev,
+                                  const real *__restrict__ La_d1,
+                                  const real *__restrict__ invAux,
+                                  const real *__restrict__ Ga,
+                                  const real *__restrict__ GaQ,
+                                  const real *__restrict__ P,
+                                  const real *__restrict__ Q,
+                                  real *__restrict__ Wu, real *__restrict__ Wv,
+                                  real *__restrict__ Wd1u,
+                                  real *__restrict__ Wd1v,
+                                  real *__restrict__ Th, int recond,
+                                  real *__restrict__ Zu, real *__restrict__ Zv) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const int K = c.K;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    const real wu = Wu[i] * invAux[u];
+    const real wv = Wv[i] * invAux[v];
+    Wu[i] = wu;
+    Wv[i] = wv;
+    if (c.loss != LOSS_LINEAR) {
+        const real a = wu / Ga[u], b = wv / Ga[v], s = a + b;
+        Th[i] = La_d1[e] * s / (a * b);
+        Wd1u[i] = a / s;
+        Wd1v[i] = b / s;
+    }
+    if (recond) {
+        if (c.loss == LOSS_LINEAR) {
+            Zu[i] = P[u] + GaQ[u] - (Ga[u] / wu) * Zu[i];
+            Zv[i] = P[v] + GaQ[v] - (Ga[v] / wv) * Zv[i];
+        } else if (c.loss == LOSS_QUAD) {
+            Zu[i] = P[u] - GaQ[u] * (P[u] - Q[u] + Zu[i] / wu);
+            Zv[i] = P[v] - GaQ[v] * (P[v] - Q[v] + Zv[i] / wv);
+        } else {
+            Zu[i] = P[u] + GaQ[u] / (c.alKal1 + P[u]) - (Ga[u] / wu) * Zu[i];
+            Zv[i] = P[v] + GaQ[v] / (c.alKal1 + P[v]) - (Ga[v] / wv) * Zv[i];
+        }
+    }
+}
+
+// normalise the metric of each vertex by its maximum (ref :360-369)
+template <typename real>
+__global__ void k_sx_normalise(int V, int K, real *__restrict__ Ga) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const long b = (long)v * K;
+    real mx = Ga[b];
+    for (int k = 1; k < K; k++) if (Ga[b + k] > mx) mx = Ga[b + k];
+    for (int k = 0; k < K; k++) Ga[b + k] /= mx;
+}
+
+// explicit step FP (ref :567-587)
+template <typename real>
+__device__ __forceinline__ real sx_explicit(const SxConst<real> &c, real p,
+                                            real gaq, real q) {
+    if (c.loss == LOSS_LINEAR) return real(2) * p + gaq;
+    if (c.loss == LOSS_QUAD) return real(2) * p - gaq * (p - q);
+    return real(2) * p + gaq / (c.alKal1 + p);
+}
+
+template <typename real>
+__global__ void k_sx_explicit(long VK, SxConst<real> c,
+                              const real *__restrict__ P,
+                              const real *__restrict__ GaQ,
+                              const real *__restrict__ Q,
+                              real *__restrict__ FP) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VK) return;
+    FP[i] = sx_explicit(c, P[i], GaQ[i], Q[i]);
+}
+
+// labels of the maximum-likelihood class (ref :447-466)
+template <typename real>
+__global__ void k_sx_labels(int V, int K, const real *__restrict__ P,
+                            real *__restrict__ lab) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const long b = (long)v * K;
+    real a = P[b];
+    real l = real(0);
+    for (int k = 1; k < K; k++) {
+        if (P[b + k] > a) { a = P[b + k]; l = (real)k; }
+    }
+    lab[v] = l;
+}
+
+// --------------------------------------------------------- iteration ---
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_edge_sweep(
+    long EK, SxConst<real> c, const int *__restrict__ Eu,
+    const int *__restrict__ Ev, const real *__restrict__ FP,
+    const real *__restrict__ P, real *__restrict__ Zu, real *__restrict__ Zv,
+    const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
+    const real *__restrict__ Th, const real *__restrict__ Wu,
+    const real *__restrict__ Wv, real *__restrict__ wz, real rho,
+    const Ctrl<real> *ctrl) {
+    if (ctrl && ctrl->halt) return;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const int K = c.K;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    real a = FP[u] - Zu[i];
+    const real b = FP[v] - Zv[i];
+    real zu = Zu[i], zv = Zv[i];
+    const real pu = P[u], pv = P[v];
+    if (c.loss == LOSS_LINEAR) {
+        const real h = real(0.5) * (a + b);
+        a = a - b;
+        if (a > real(2)) {
+            a = real(0.5) * (a - real(2));
+            zu += rho * (h + a - pu);
+            zv += rho * (h - a - pv);
+        } else if (a < real(-2)) {
+            a = real(0.5) * (a + real(2));
+            zu += rho * (h + a - pu);
+            zv += rho * (h - a - pv);
+        } else {
+            zu += rho * (h - pu);
+            zv += rho * (h - pv);
+        }
+    } else {
+        const real wu = Wd1u[i], wv = Wd1v[i], th = Th[i];
+        const real h = wu * a + wv * b;
+        a = a - b;
+        if (a > th) {
+            a -= th;
+            zu += rho * (h + wv * a - pu);
+            zv += rho * (h - wu * a - pv);
+        } else if (a < -th) {
+            a += th;
+            zu += rho * (h + wv * a - pu);
+            zv += rho * (h - wu * a - pv);
+        } else {
+            zu += rho * (h - pu);
+            zv += rho * (h - pv);
+        }
+    }
+    Zu[i] = zu;
+    Zv[i] = zv;
+    wz[i] = Wu[i] * zu;
+    wz[EK + i] = Wv[i] * zv;
+}
+
+template <typename real>
+__global__ void k_sx_average(long VK, int K, long EK, const int *__restrict__ ptr,
+                             const unsigned *__restrict__ idx,
+                             const real *__restrict__ wz,
+                             real *__restrict__ Pavg, const Ctrl<real> *ctrl) {
+    if (ctrl && ctrl->halt) return;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VK) return;
+    Pavg[i] = sx_gather(i, K, EK, ptr, idx, wz);
+}
+
+template <typename real>
+struct SxProjArgs {
+    int V;
+    SxConst<real> c;
+    const real *Pavg, *Ga, *GaQ, *Q;
+    real *P, *FP, *lab;
+    int track;   // 0 none, 1 l1 evolution, 2 label changes
+    real *part;
+    const Ctrl<real> *ctrl;
+};
+
+// projection + evolution + next explicit step, one thread per vertex
+template <typename real, int W>
+__global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real red[kBlock / kWave];
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int K = a.c.K;
+    real dif = real(0);
+    if (v < a.V) {
+        const long b = (long)v * K;
+        real *x = const_cast<real *>(a.Pavg) + b;  // projected in place
+        proj_simplex_column<real, W>(x, a.Ga + b, K, real(1));
+        if (a.track == 1) {
+            for (int k = 0; k < K; k++) {
+                real d = a.P[b + k] - x[k];
+                if (d < real(0)) d = -d;
+                dif += d;
+            }
+        } else if (a.track == 2) {
+            real mx = x[0];
+            int l = 0;
+            for (int k = 1; k < K; k++) if (x[k] > mx) { mx = x[k]; l = k; }
+            const real fl = (real)l;
+            if (fl != a.lab[v]) { dif = real(1); a.lab[v] = fl; }
+        }
+        for (int k = 0; k < K; k++) {
+            const real p = x[k];
+            a.P[b + k] = p;
+            a.FP[b + k] = sx_explicit(a.c, p, a.GaQ[b + k], a.Q[b + k]);
+        }
+    }
+    if (a.track) {
+        dif = block_sum(dif, red);
+        if (threadIdx.x == 0) a.part[blockIdx.x] = dif;
+    }
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_finalize(int nparts,
+                                                     const real *__restrict__ part,
+                                                     int V, int track,
+                                                     Ctrl<real> *ctrl,
+                                                     real *__restrict__ Dif) {
+    __shared__ real red[kBlock / kWave];
+    if (ctrl->halt) return;
+    real s = real(0);
+    if (track) {
+        for (int i = threadIdx.x; i < nparts; i += kBlock) s += part[i];
+        s = block_sum(s, red);
+    }
+    if (threadIdx.x != 0) return;
+    int it = ctrl->it;
+    if (track) {
+        real dif = s;
+        if (track == 1) dif /= V;  // relative l1 evolution (ref :688)
+        ctrl->dif = dif;
+        if (Dif) Dif[it] = dif;
+    }
+    it++;
+    ctrl->it = it;
+    const real dif = ctrl->dif;
+    if (it >= ctrl->itMax || dif < ctrl->difTol) {
+        ctrl->stop = 1;
+        ctrl->halt = 1;
+    } else if (dif < ctrl->difRcd) {
+        ctrl->recond = 1;
+        ctrl->halt = 1;
+    }
+}
+
+// objective (ref :476-544): loss partials per vertex, TV partials per edge
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_obj_vertex(int V, SxConst<real> c,
+                                                       const real *__restrict__ La_f,
+                                                       const real *__restrict__ P,
+                                                       const real *__restrict__ Q,
+                                                       real *__restrict__ part,
+                                                       const Ctrl<real> *ctrl) {
+    if (ctrl && ctrl->obj_it >= ctrl->it) return;
+    __shared__ real red[kBlock / kWave];
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    real t = real(0);
+    if (v < V) {
+        const int K = c.K;
+        const long b = (long)v * K;
+        if (c.loss == LOSS_LINEAR) {
+            for (int k = 0; k < K; k++) t -= P[b + k] * Q[b + k];
+        } else if (c.loss == LOSS_QUAD) {
+            real s = real(0);
+            for (int k = 0; k < K; k++) { const real d = P[b + k] - Q[b + k]; s += d * d; }
+            t = La_f ? La_f[v] * s : s;
+        } else {
+            real s = real(0);
+            for (int k = 0; k < K; k++) {
+                const real q = c.alK + c.al1 * Q[b + k];
+                // the reference evaluates log in double (C ::log)
+                s = (real)((double)s + (double)q * log((double)(q / (c.alK + c.al1 * P[b + k]))));
+            }
+            t = La_f ? La_f[v] * s : s;
+        }
+    }
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_obj_edge(long E, int K,
+                                                     const int *__restrict__ Eu,
+                                                     const int *__restrict__ Ev,
+                                                     const real *__restrict__ La_d1,
+                                                     const real *__restrict__ P,
+                                                     real *__restrict__ part,
+                                                     const Ctrl<real> *ctrl) {
+    if (ctrl && ctrl->obj_it >= ctrl->it) return;
+    __shared__ real red[kBlock / kWave];
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    real t = real(0);
+    if (e < E) {
+        const long u = (long)Eu[e] * K, v = (long)Ev[e] * K;
+        real b = real(0);
+        for (int k = 0; k < K; k++) {
+            const real d = P[u + k] - P[v + k];
+            if (d < real(0)) b -= d; else b += d;
+        }
+        t = La_d1[e] * b;
+    }
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_obj_finalize(const real *__restrict__ part,
+                                                         int nbv, int nbe, int quad,
+                                                         Ctrl<real> *ctrl,
+                                                         real *__restrict__ Obj) {
+    __shared__ real red[2][kBlock / kWave];
+    if (ctrl->obj_it >= ctrl->it) return;
+    real l = real(0), tv = real(0);
+    for (int i = threadIdx.x; i < nbv; i += kBlock) l += part[i];
+    for (int i = threadIdx.x; i < nbe; i += kBlock) tv += part[nbv + i];
+    l = block_sum(l, red[0]);
+    tv = block_sum(tv, red[1]);
+    if (threadIdx.x != 0) return;
+    if (quad) l *= real(0.5);
+    Obj[ctrl->it] = l + tv;
+    ctrl->obj_it = ctrl->it;
+}
+
+// ---------------------------------------------------------------- session
+template <typename real>
+static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s) {
+    if (!src || !n) { d.release(); return; }
+    d.alloc(n);
+    PFDR_HIP(hipMemcpyAsync(d.p, src, n * sizeof(real),
+                            mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+}
+
+static int mask_words(int D) { return (D + 63) / 64; }
+
+template <typename real>
+static void launch_proj(real *X, const real *M, int D, int N, int nm,
+                        const real *A, int na, hipStream_t s) {
+    const int w = mask_words(D);
+    const int g = grid_for(N);
+    if (w <= 1) k_proj_simplex<real, 1><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
+    else if (w <= 4) k_proj_simplex<real, 4><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
+    else k_proj_simplex<real, 16><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
+    PFDR_HIP(hipGetLastError());
+}
+
+template <typename real>
+class SimplexSession final : public SessionBase {
+  public:
+    explicit SimplexSession(const pfdr_problem *p);
+    ~SimplexSession() override { if (hctrl_) (void)hipHostFree(hctrl_); }
+    int run(int iters) override;
+    void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
+    void *device_x() override { return P_.p; }
+
+  private:
+    SxConst<real> c_;
+    int V_, K_, itMax_, verbose_;
+    long E_, EK_, VK_;
+    real rho_, condMin_, difTol_, difRcd_, cap_;
+    bool rec_obj_, rec_dif_;
+    int track_;  // 0, 1 (l1 evolution), 2 (labels)
+    DevBuf<int> Eu_, Ev_;
+    DevBuf<real> La_d1_, La_f_, Q_, P_, FP_, Pavg_, Ga_, GaQ_, invAux_, lab_;
+    DevBuf<real> Zu_, Zv_, Wu_, Wv_, Wd1u_, Wd1v_, Th_, wz_, part_, opart_, Obj_, Dif_;
+    DevBuf<Ctrl<real>> ctrl_;
+    Ctrl<real> *hctrl_ = nullptr;
+    Incidence inc_;
+    int nbv_, nbe_;
+    int it_ = 0;
+    bool stopped_ = false;
+    int chunk_ = 32;
+    int next_print_ = 0;
+
+    void precondition(bool init);
+    void objective();
+    void body();
+    void launch_project(const SxProjArgs<real> &a);
+};
+
+template <typename real>
+void SimplexSession<real>::launch_project(const SxProjArgs<real> &a) {
+    const int w = mask_words(K_);
+    if (w <= 1) k_sx_project<real, 1><<<nbv_, kBlock, 0, stream>>>(a);
+    else if (w <= 4) k_sx_project<real, 4><<<nbv_, kBlock, 0, stream>>>(a);
+    else k_sx_project<real, 16><<<nbv_, kBlock, 0, stream>>>(a);
+}
+
+template <typename real>
+SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
+    if (p->K <= 0 || p->V <= 0 || p->E < 0) throw std::runtime_error("K, V must be > 0 and E >= 0");
+    if (p->K > 1024) throw std::runtime_error("K > 1024 labels is not supported");
+    if (!p->X || !p->Y || !p->Eu || !p->Ev || !p->La_d1)
+        throw std::runtime_error("P, Q, Eu, Ev and La_d1 are required");
+    if (p->nranks > 1) throw std::runtime_error("distributed simplex sessions are not supported yet");
+    PFDR_HIP(hipGetDevice(&device));
+    stream = lib_stream();
+    hipStream_t s = stream;
+    V_ = p->V; K_ = p->K; E_ = p->E;
+    EK_ = E_ * K_; VK_ = (long)V_ * K_;
+    itMax_ = p->itMax; verbose_ = p->verbose;
+    const real al = (real)p->al;
+    c_.K = K_;
+    c_.alK = c_.al1 = c_.alKal1 = real(0);
+    if (al == real(0)) c_.loss = LOSS_LINEAR;
+    else if (al == real(1)) c_.loss = LOSS_QUAD;
+    else c_.loss = LOSS_KL;  // al > 0 branch of the reference (also al > 1)
+    if (real(0) < al && al < real(1)) {  // ref :387-391
+        c_.alK = al / K_;
+        c_.al1 = real(1) - al;
+        c_.alKal1 = c_.alK / c_.al1;
+    }
+    if (al < real(0)) throw std::runtime_error("al must be >= 0");
+    rho_ = (real)p->rho; condMin_ = (real)p->condMin;
+    difTol_ = (real)p->difTol; difRcd_ = (real)p->difRcd;
+    rec_obj_ = p->record_obj != 0;
+    rec_dif_ = p->record_dif != 0;
+    track_ = (difTol_ > real(0) || difRcd_ > real(0) || rec_dif_) ? (difTol_ >= real(1) ? 2 : 1) : 0;
+    cap_ = real(1.9) * (real(2) - rho_);
+
+    const int mem = p->mem;
+    const auto kind = mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    Eu_.alloc(E_ ? E_ : 1); Ev_.alloc(E_ ? E_ : 1);
+    if (E_) {
+        PFDR_HIP(hipMemcpyAsync(Eu_.p, p->Eu, E_ * sizeof(int), kind, s));
+        PFDR_HIP(hipMemcpyAsync(Ev_.p, p->Ev, E_ * sizeof(int), kind, s));
+    }
+    sx_copy_in(La_d1_, p->La_d1, E_, mem, s);
+    if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s);
+    sx_copy_in(Q_, p->Y, VK_, mem, s);
+    sx_copy_in(P_, p->X, VK_, mem, s);
+    FP_.alloc(VK_); Pavg_.alloc(VK_); Ga_.alloc(VK_); GaQ_.alloc(VK_); invAux_.alloc(VK_);
+    const size_t EKn = EK_ ? EK_ : 1;
+    Zu_.alloc(EKn); Zv_.alloc(EKn); Wu_.alloc(EKn); Wv_.alloc(EKn);
+    if (c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
+    wz_.alloc(2 * EKn);
+    nbv_ = grid_for(V_);
+    nbe_ = grid_for(E_);
+    part_.alloc(nbv_);
+    if (rec_obj_) { opart_.alloc((size_t)nbv_ + nbe_ + 1); Obj_.alloc((size_t)itMax_ + 1); }
+    if (rec_dif_) Dif_.alloc(itMax_ > 0 ? itMax_ : 1);
+    if (track_ == 2) {
+        lab_.alloc(V_);
+        k_sx_labels<real><<<nbv_, kBlock, 0, s>>>(V_, K_, P_.p, lab_.p);
+    }
+
+    ctrl_.alloc(1);
+    PFDR_HIP(hipHostMalloc(&hctrl_, sizeof(Ctrl<real>), hipHostMallocDefault));
+    std::memset(hctrl_, 0, sizeof(Ctrl<real>));
+    hctrl_->obj_it = -1;
+    hctrl_->itMax = itMax_;
+    hctrl_->dif = difTol_ > difRcd_ ? difTol_ : difRcd_;  // ref :445
+    hctrl_->difTol = difTol_;
+    hctrl_->difRcd = difRcd_;
+    PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, s));
+
+    build_incidence(Eu_.p, Ev_.p, V_, E_, inc_, s);
+    if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, Zv_.p);
+    precondition(true);
+    k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
+    PFDR_HIP(hipGetLastError());
+    if (rec_obj_) objective();
+    PFDR_HIP(hipStreamSynchronize(s));
+    stopped_ = itMax_ <= 0;
+    device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
+    for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &FP_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
+                            &Zu_, &Zv_, &Wu_, &Wv_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_,
+                            &Obj_, &Dif_})
+        device_bytes += (int64_t)(b->n * sizeof(real));
+}
+
+// ref :64-370
+template <typename real>
+void SimplexSession<real>::precondition(bool init) {
+    hipStream_t s = stream;
+    ProfScope ps(prof, init ? "precondition" : "recondition", s);
+    const int gE = grid_for(EK_), gV = grid_for(VK_);
+    if (!init) {
+        k_sx_recover<real><<<nbv_, kBlock, 0, s>>>(V_, c_, La_f_.p, Q_.p, GaQ_.p, Ga_.p);
+        if (EK_) k_sx_subgrad<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, P_.p, Q_.p, Ga_.p,
+                                                          GaQ_.p, Wu_.p, Wv_.p, Zu_.p, Zv_.p);
+    }
+    k_sx_hessian<real><<<gV, kBlock, 0, s>>>(VK_, c_, La_f_.p, P_.p, Q_.p, Ga_.p);
+    if (EK_) k_sx_d1_weights<real><<<gE, kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, La_d1_.p, init ? 1 : 0,
+                                                         condMin_, P_.p, Wu_.p, Wv_.p, wz_.p);
+    k_sx_precond_vertex<real><<<gV, kBlock, 0, s>>>(VK_, c_, EK_, inc_.ptr.p, inc_.idx.p, wz_.p,
+                                                    La_f_.p, Q_.p, cap_, Ga_.p, invAux_.p, GaQ_.p);
+    if (EK_) k_sx_precond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, La_d1_.p, invAux_.p,
+                                                           Ga_.p, GaQ_.p, P_.p, Q_.p, Wu_.p, Wv_.p,
+                                                           Wd1u_.p, Wd1v_.p, Th_.p, init ? 0 : 1,
+                                                           Zu_.p, Zv_.p);
+    k_sx_normalise<real><<<nbv_, kBlock, 0, s>>>(V_, K_, Ga_.p);
+    PFDR_HIP(hipGetLastError());
+}
+
+template <typename real>
+void SimplexSession<real>::objective() {
+    hipStream_t s = stream;
+    k_sx_obj_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, c_, La_f_.p, P_.p, Q_.p, opart_.p, ctrl_.p);
+    if (E_) k_sx_obj_edge<real><<<nbe_, kBlock, 0, s>>>(E_, K_, Eu_.p, Ev_.p, La_d1_.p, P_.p,
+                                                        opart_.p + nbv_, ctrl_.p);
+    k_sx_obj_finalize<real><<<1, kBlock, 0, s>>>(opart_.p, nbv_, E_ ? nbe_ : 0,
+                                                 c_.loss == LOSS_QUAD, ctrl_.p, Obj_.p);
+    PFDR_HIP(hipGetLastError());
+}
+
+template <typename real>
+void SimplexSession<real>::body() {
+    hipStream_t s = stream;
+    const bool gated = track_ || rec_obj_;
+    const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
+    if (EK_) {
+        ProfScope ps(prof, "sx_edge_sweep", s);
+        k_sx_edge_sweep<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+                                                               Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
+                                                               Wu_.p, Wv_.p, wz_.p, rho_, c);
+    }
+    {
+        ProfScope ps(prof, "sx_average", s);
+        k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, EK_, inc_.ptr.p, inc_.idx.p,
+                                                            wz_.p, Pavg_.p, c);
+    }
+    {
+        SxProjArgs<real> a{};
+        a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
+        a.P = P_.p; a.FP = FP_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        ProfScope ps(prof, "sx_project", s);
+        launch_project(a);
+    }
+    if (gated)
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(nbv_, part_.p, V_, track_, ctrl_.p,
+                                                 rec_dif_ ? Dif_.p : nullptr);
+    PFDR_HIP(hipGetLastError());
+    if (rec_obj_) objective();
+}
+
+template <typename real>
+int SimplexSession<real>::run(int iters) {
+    const bool gated = track_ || rec_obj_;
+    const int target = (int)std::min<long>((long)it_ + std::max(iters, 0), (long)itMax_);
+    while (!stopped_ && it_ < target) {
+        const int n = std::min(target - it_, chunk_);
+        for (int i = 0; i < n; i++) body();
+        if (gated) {
+            PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
+            PFDR_HIP(hipStreamSynchronize(stream));
+            it_ = hctrl_->it;
+            if (hctrl_->stop) {
+                stopped_ = true;
+            } else if (hctrl_->recond) {
+                if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
+                precondition(false);
+                k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
+                PFDR_HIP(hipGetLastError());
+                difRcd_ *= real(0.1);  // ref :563
+                hctrl_->difRcd = difRcd_;
+                hctrl_->recond = 0;
+                hctrl_->halt = 0;
+                PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, stream));
+                if (verbose_) { printf("done.\n"); fflush(stdout); }
+            }
+        } else {
+            it_ += n;
+            if (it_ >= itMax_) stopped_ = true;
+        }
+        if (verbose_ && (it_ >= next_print_ || stopped_)) {
+            printf("iteration %d (max. %d)\n", it_, itMax_);
+            if (track_ == 2)
+                printf("label evolution %d (recond. %d; tol. %d)\n", (int)hctrl_->dif,
+                       (int)hctrl_->difRcd, (int)difTol_);
+            else if (track_ == 1)
+                printf("iterate evolution %g (recond. %g; tol. %g)\n", (double)hctrl_->dif,
+                       (double)hctrl_->difRcd, (double)difTol_);
+            fflush(stdout);
+            next_print_ = it_ + verbose_;
+        }
+    }
+    PFDR_HIP(hipStreamSynchronize(stream));
+    if (prof.on) prof.resolve();
+    return it_;
+}
+
+template <typename real>
+void SimplexSession<real>::result(void *X_host, int *it, void *Obj_host, void *Dif_host) {
+    hipStream_t s = stream;
+    if (X_host) PFDR_HIP(hipMemcpyAsync(X_host, P_.p, sizeof(real) * VK_, hipMemcpyDeviceToHost, s));
+    if (it) *it = it_;
+    if (Obj_host && rec_obj_)
+        PFDR_HIP(hipMemcpyAsync(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost, s));
+    if (Dif_host && rec_dif_ && it_ > 0)
+        PFDR_HIP(hipMemcpyAsync(Dif_host, Dif_.p, sizeof(real) * it_, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+SessionBase *create_simplex_session(const pfdr_problem *p) {
+    if (p->dtype == PFDR_F32) return new SimplexSession<float>(p);
+    if (p->dtype == PFDR_F64) return new SimplexSession<double>(p);
+    throw std::runtime_error("dtype must be PFDR_F32 or PFDR_F64");
+}
+
+template <typename real>
+static int simplex_host(const char *fn, int K, int V, int E, real al, const real *La_f, real *P,
+                        const real *Q, const int *Eu, const int *Ev, const real *La_d1, real rho,
+                        real condMin, real difRcd, real difTol, int itMax, int *it, real *Obj,
+                        real *Dif, int verbose) {
+    pfdr_problem p{};
+    p.kind = PFDR_KIND_SIMPLEX;
+    p.dtype = sizeof(real) == 4 ? PFDR_F32 : PFDR_F64;
+    p.mem = PFDR_MEM_HOST;
+    p.V = V; p.E = E; p.K = K; p.al = al;
+    p.X = P; p.Y = Q; p.Eu = Eu; p.Ev = Ev; p.La_d1 = La_d1; p.La_l1 = La_f;
+    p.rho = rho; p.condMin = condMin; p.difRcd = difRcd; p.difTol = difTol;
+    p.itMax = itMax; p.verbose = verbose;
+    p.record_obj = Obj != nullptr;
+    p.record_dif = Dif != nullptr;
+    try {
+        if (verbose) { printf("Initializing constants and variables... "); fflush(stdout); }
+        std::unique_ptr<SimplexSession<real>> s(new SimplexSession<real>(&p));
+        if (verbose) { printf("done.\nPreconditioned forward-Douglas-Rachford algorithm\n"); fflush(stdout); }
+        s->run(itMax);
+        int its = 0;
+        s->result(P, &its, Obj, Dif);
+        if (it) *it = its;
+    } catch (const HipError &h) {
+        return report_error(fn, h);
+    } catch (const std::exception &ex) {
+        return report_error(fn, ex.what());
+    }
+    return PFDR_OK;
+}
+
+template <typename real>
+static int proj_host(const char *fn, real *X, const real *M, int D, int N, int nm, const real *A,
+                     int na) {
+    if (D <= 0 || N < 0 || nm <= 0 || na <= 0 || !X || !M || !A)
+        return report_error(fn, "invalid arguments");
+    if (D > 1024) return report_error(fn, "D > 1024 is not supported");
+    if (N == 0) return PFDR_OK;
+    try {
+        hipStream_t s = lib_stream();
+        const int mm = std::min(nm, N), aa = std::min(na, N);
+        DevBuf<real> dX, dM, dA;
+        dX.alloc((size_t)D * N);
+        dM.alloc((size_t)D * mm);
+        dA.alloc(aa);
+        PFDR_HIP(hipMemcpyAsync(dX.p, X, sizeof(real) * D * (size_t)N, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemcpyAsync(dM.p, M, sizeof(real) * D * (size_t)mm, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemcpyAsync(dA.p, A, sizeof(real) * aa, hipMemcpyHostToDevice, s));
+        launch_proj<real>(dX.p, dM.p, D, N, mm, dA.p, aa, s);
+        PFDR_HIP(hipMemcpyAsync(X, dX.p, sizeof(real) * D * (size_t)N, hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    } catch (const HipError &h) {
+        return report_error(fn, h);
+    }
+    return PFDR_OK;
+}
+
+}  // namespace pfdr
+
+extern "C" int pfdr_loss_d1_simplex_f32(int K, int V, int E, float al, const float *La_f, float *P,
+                                        const float *Q, const int *Eu, const int *Ev,
+                                        const float *La_d1, float rho, float condMin,
+                                        float difRcd, float difTol, int itMax, int *it,
+                                        float *Obj, float *Dif, int verbose) {
+    return pfdr::simplex_host<float>("pfdr_loss_d1_simplex_f32", K, V, E, al, La_f, P, Q, Eu, Ev,
+                                     La_d1, rho, condMin, difRcd, difTol, itMax, it, Obj, Dif,
+                                     verbose);
+}
+extern "C" int pfdr_loss_d1_simplex_f64(int K, int V, int E, double al, const double *La_f,
+                                        double *P, const double *Q, const int *Eu, const int *Ev,
+                                        const double *La_d1, double rho, double condMin,
+                                        double difRcd, double difTol, int itMax, int *it,
+                                        double *Obj, double *Dif, int verbose) {
+    return pfdr::simplex_host<double>("pfdr_loss_d1_simplex_f64", K, V, E, al, La_f, P, Q, Eu, Ev,
+                                      La_d1, rho, condMin, difRcd, difTol, itMax, it, Obj, Dif,
+                                      verbose);
+}
+extern "C" int pfdr_proj_simplex_metric_f32(float *X, const float *M, int D, int N, int nm,
+                                            const float *A, int na) {
+    return pfdr::proj_host<float>("pfdr_proj_simplex_metric_f32", X, M, D, N, nm, A, na);
+}
+extern "C" int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N, int nm,
+                                            const double *A, int na) {
+    return pfdr::proj_host<double>("pfdr_proj_simplex_metric_f64", X, M, D, N, nm, A, na);
+}

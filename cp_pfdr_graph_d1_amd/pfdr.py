@@ -1,0 +1,488 @@
+"""Python host side of the MI355X PFDR solvers (ctypes over libpfdr_mi355x.so).
+
+Two layers, both calling the C ABI of ``include/pfdr_mi355x.h``:
+
+* ``Lib`` — one method per C entry point, same argument order as the
+  reference C++ templates (include/PFDR_graph_quadratic_d1_l1.hpp:36-42 and
+  friends) minus the outputs, numpy in / numpy out.
+* MEX-style front-ends mirroring the reference's Octave wrappers
+  (octave/mex/PFDR_*_mex.cpp): ``PFDR_graph_quadratic_d1_l1``,
+  ``PFDR_graph_l22_d1_l1``, ``PFDR_graph_quadratic_d1_l1_AtA`` and the bounds
+  and simplex counterparts, returning ``(X, it, Obj, Dif)`` like
+  ``[X, it, Obj, Dif] = PFDR_..._mex(...)``.
+
+There is no CPU fallback: if the shared library is missing, or the HIP device
+is unusable, every call raises ``PFDRError``.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpfdr_mi355x.so")
+
+PFDR_F32, PFDR_F64 = 0, 1
+PFDR_MEM_HOST, PFDR_MEM_DEVICE = 0, 1
+PFDR_KIND_L1, PFDR_KIND_BOUNDS, PFDR_KIND_SIMPLEX = 0, 1, 2
+SCAL, DIAG = 0, 1
+
+# every C entry point of include/pfdr_mi355x.h
+EXPORTED = (
+    "pfdr_last_error", "pfdr_abi_version", "pfdr_device_count",
+    "pfdr_quadratic_d1_l1_f32", "pfdr_quadratic_d1_l1_f64",
+    "pfdr_quadratic_d1_bounds_f32", "pfdr_quadratic_d1_bounds_f64",
+    "pfdr_loss_d1_simplex_f32", "pfdr_loss_d1_simplex_f64",
+    "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
+    "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
+    "pfdr_session_device_x", "pfdr_session_set_profiling",
+    "pfdr_session_kernel_stats", "pfdr_session_sync",
+    "pfdr_session_device_bytes", "pfdr_session_destroy",
+    "pfdr_comm_unique_id", "pfdr_comm_init", "pfdr_comm_destroy",
+    "pfdr_comm_allreduce_max_f64",
+    "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
+    "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
+)
+
+
+class PFDRError(RuntimeError):
+    pass
+
+
+class Problem(C.Structure):
+    """Mirror of ``pfdr_problem`` (include/pfdr_mi355x.h)."""
+    _fields_ = [
+        ("kind", C.c_int), ("dtype", C.c_int), ("mem", C.c_int),
+        ("V", C.c_int), ("E", C.c_int), ("N", C.c_int), ("K", C.c_int),
+        ("X", C.c_void_p), ("Y", C.c_void_p), ("A", C.c_void_p),
+        ("Eu", C.c_void_p), ("Ev", C.c_void_p),
+        ("La_d1", C.c_void_p), ("La_l1", C.c_void_p),
+        ("positivity", C.c_int), ("min", C.c_double), ("max", C.c_double),
+        ("al", C.c_double), ("Ltype", C.c_int), ("L", C.c_void_p),
+        ("rho", C.c_double), ("condMin", C.c_double),
+        ("difRcd", C.c_double), ("difTol", C.c_double),
+        ("itMax", C.c_int), ("verbose", C.c_int),
+        ("record_obj", C.c_int), ("record_dif", C.c_int),
+        ("nranks", C.c_int), ("rank", C.c_int), ("comm", C.c_void_p),
+        ("vtx_begin", C.c_int64), ("V_global", C.c_int64),
+        ("e_global", C.c_void_p), ("e_offset", C.c_int64),
+    ]
+
+
+_LIB = None
+
+
+def load():
+    """Load libpfdr_mi355x.so (built by __graft_entry__.build() / make)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise PFDRError("%s is missing: build it with "
+                            "`make -C cp_pfdr_graph_d1_amd/csrc`" % LIB_PATH)
+        lib = C.CDLL(LIB_PATH)
+        lib.pfdr_last_error.restype = C.c_char_p
+        lib.pfdr_session_device_x.restype = C.c_void_p
+        lib.pfdr_session_device_bytes.restype = C.c_int64
+        lib.pfdr_gen_knn_jitter_grid.restype = C.c_int64
+        lib.pfdr_gen_grid_edges.restype = C.c_int64
+        lib.pfdr_gen_knn_jitter_grid.argtypes = [
+            C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_double,
+            C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+        lib.pfdr_gen_grid_edges.argtypes = [
+            C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64,
+            C.c_void_p, C.c_void_p]
+        for nm, ct in (("pfdr_gen_piecewise_f32", C.c_float),
+                       ("pfdr_gen_piecewise_f64", C.c_double)):
+            getattr(lib, nm).argtypes = [C.c_int, C.c_uint64, C.c_double,
+                                         C.c_int64, C.c_int64, C.c_void_p]
+        lib.pfdr_comm_allreduce_max_f64.argtypes = [C.c_void_p,
+                                                    C.POINTER(C.c_double)]
+        lib.pfdr_comm_init.argtypes = [C.POINTER(C.c_void_p), C.c_int,
+                                       C.c_int, C.c_void_p]
+        lib.pfdr_comm_destroy.argtypes = [C.c_void_p]
+        _LIB = lib
+    return _LIB
+
+
+def _check(status, what):
+    if status != 0:
+        raise PFDRError("%s failed (%d): %s" % (
+            what, status, load().pfdr_last_error().decode()))
+
+
+def _real(dtype):
+    dtype = np.dtype(dtype)
+    if dtype == np.float32:
+        return C.c_float, "f32", PFDR_F32
+    if dtype == np.float64:
+        return C.c_double, "f64", PFDR_F64
+    raise TypeError("PFDR supports float32 and float64, got %s" % dtype)
+
+
+def _arr(a, dtype):
+    if a is None:
+        return None
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _ptr(a, ct):
+    return None if a is None else a.ctypes.data_as(C.POINTER(ct))
+
+
+class Lib:
+    """Raw C-ABI calls (host pointers, synchronous)."""
+
+    def __init__(self):
+        self.lib = load()
+
+    def quadratic_d1_l1(self, X0, Y, A, N, Eu, Ev, La_d1, La_l1=None,
+                        positivity=0, Ltype=SCAL, L=None, rho=1.5,
+                        condMin=1e-3, difRcd=0.0, difTol=1e-5, itMax=1000,
+                        obj=False, dif=False, verbose=0):
+        X = np.array(X0, copy=True)
+        ct, sfx, _ = _real(X.dtype)
+        dt = X.dtype
+        Y, A, La_d1, La_l1, L = (_arr(a, dt) for a in (Y, A, La_d1, La_l1, L))
+        Eu, Ev = _arr(Eu, np.int32), _arr(Ev, np.int32)
+        Obj = np.zeros(itMax + 1, dt) if obj else None
+        Dif = np.zeros(max(itMax, 1), dt) if dif else None
+        it = C.c_int(0)
+        fn = getattr(self.lib, "pfdr_quadratic_d1_l1_" + sfx)
+        _check(fn(C.c_int(X.size), C.c_int(Eu.size), C.c_int(N), _ptr(X, ct),
+                  _ptr(Y, ct), _ptr(A, ct), _ptr(Eu, C.c_int),
+                  _ptr(Ev, C.c_int), _ptr(La_d1, ct), _ptr(La_l1, ct),
+                  C.c_int(positivity), C.c_int(Ltype), _ptr(L, ct), ct(rho),
+                  ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax),
+                  C.byref(it), _ptr(Obj, ct), _ptr(Dif, ct),
+                  C.c_int(verbose)), "pfdr_quadratic_d1_l1_" + sfx)
+        return X, it.value, Obj, Dif
+
+    def quadratic_d1_bounds(self, X0, Y, A, N, Eu, Ev, La_d1, lo=-np.inf,
+                            hi=np.inf, Ltype=SCAL, L=None, rho=1.5,
+                            condMin=1e-3, difRcd=0.0, difTol=1e-5,
+                            itMax=1000, obj=False, dif=False, verbose=0):
+        X = np.array(X0, copy=True)
+        ct, sfx, _ = _real(X.dtype)
+        dt = X.dtype
+        Y, A, La_d1, L = (_arr(a, dt) for a in (Y, A, La_d1, L))
+        Eu, Ev = _arr(Eu, np.int32), _arr(Ev, np.int32)
+        Obj = np.zeros(itMax + 1, dt) if obj else None
+        Dif = np.zeros(max(itMax, 1), dt) if dif else None
+        it = C.c_int(0)
+        fn = getattr(self.lib, "pfdr_quadratic_d1_bounds_" + sfx)
+        _check(fn(C.c_int(X.size), C.c_int(Eu.size), C.c_int(N), _ptr(X, ct),
+                  _ptr(Y, ct), _ptr(A, ct), _ptr(Eu, C.c_int),
+                  _ptr(Ev, C.c_int), _ptr(La_d1, ct), ct(lo), ct(hi),
+                  C.c_int(Ltype), _ptr(L, ct), ct(rho), ct(condMin),
+                  ct(difRcd), ct(difTol), C.c_int(itMax), C.byref(it),
+                  _ptr(Obj, ct), _ptr(Dif, ct), C.c_int(verbose)),
+               "pfdr_quadratic_d1_bounds_" + sfx)
+        return X, it.value, Obj, Dif
+
+    def loss_d1_simplex(self, P0, Q, K, Eu, Ev, La_d1, al=0.1, La_f=None,
+                        rho=1.0, condMin=0.1, difRcd=0.0, difTol=1e-4,
+                        itMax=1000, obj=False, dif=False, verbose=0):
+        P = np.array(P0, copy=True)
+        ct, sfx, _ = _real(P.dtype)
+        dt = P.dtype
+        Q, La_d1, La_f = (_arr(a, dt) for a in (Q, La_d1, La_f))
+        Eu, Ev = _arr(Eu, np.int32), _arr(Ev, np.int32)
+        Obj = np.zeros(itMax + 1, dt) if obj else None
+        Dif = np.zeros(max(itMax, 1), dt) if dif else None
+        it = C.c_int(0)
+        fn = getattr(self.lib, "pfdr_loss_d1_simplex_" + sfx)
+        _check(fn(C.c_int(K), C.c_int(P.size // K), C.c_int(Eu.size), ct(al),
+                  _ptr(La_f, ct), _ptr(P, ct), _ptr(Q, ct), _ptr(Eu, C.c_int),
+                  _ptr(Ev, C.c_int), _ptr(La_d1, ct), ct(rho), ct(condMin),
+                  ct(difRcd), ct(difTol), C.c_int(itMax), C.byref(it),
+                  _ptr(Obj, ct), _ptr(Dif, ct), C.c_int(verbose)),
+               "pfdr_loss_d1_simplex_" + sfx)
+        return P, it.value, Obj, Dif
+
+    def proj_simplex_metric(self, X0, M, D, N, nm, A, na):
+        X = np.array(X0, copy=True)
+        ct, sfx, _ = _real(X.dtype)
+        M, A = _arr(M, X.dtype), _arr(A, X.dtype)
+        fn = getattr(self.lib, "pfdr_proj_simplex_metric_" + sfx)
+        _check(fn(_ptr(X, ct), _ptr(M, ct), C.c_int(D), C.c_int(N),
+                  C.c_int(nm), _ptr(A, ct), C.c_int(na)),
+               "pfdr_proj_simplex_metric_" + sfx)
+        return X
+
+
+# ------------------------------------------------------ MEX-style API -----
+def _edges(Eu, Ev):
+    # the Python binding reinterprets uint32 edge arrays as int
+    # (reference python/CP_quadratic_l1_py.cpp:228-258); accept any integer
+    return (np.ascontiguousarray(Eu).astype(np.int32, copy=False),
+            np.ascontiguousarray(Ev).astype(np.int32, copy=False))
+
+
+def _scal_or_vec(x, n, dt):
+    """MEX wrappers pass scalars for 'none' (numel == 1 -> NULL)."""
+    if x is None:
+        return None
+    a = np.asarray(x, dt).ravel()
+    return None if a.size <= 1 else a
+
+
+def PFDR_graph_quadratic_d1_l1(Y, A, Eu, Ev, La_d1, La_l1, positivity, L,
+                               rho, condMin, difRcd, difTol, itMax,
+                               verbose=0, obj=False, dif=False):
+    """[X, it, Obj, Dif] = PFDR_graph_quadratic_d1_l1_mex(Y, A, Eu, Ev, La_d1,
+    La_l1, positivity, L, rho, condMin, difRcd, difTol, itMax, verbose)
+    (octave/mex/PFDR_graph_quadratic_d1_l1_mex.cpp): A is N-by-V."""
+    A = np.asarray(A)
+    dt = np.result_type(Y, np.float32)
+    N, V = A.shape
+    L = np.asarray(L, dt).ravel()
+    Ltype = SCAL if L.size == 1 else DIAG
+    Eu, Ev = _edges(Eu, Ev)
+    return Lib().quadratic_d1_l1(
+        np.zeros(V, dt), np.asarray(Y, dt), np.asfortranarray(A, dt).ravel(order="F"),
+        N, Eu, Ev, np.asarray(La_d1, dt), _scal_or_vec(La_l1, V, dt),
+        positivity, Ltype, L, rho, condMin, difRcd, difTol, itMax, obj, dif,
+        verbose)
+
+
+def PFDR_graph_quadratic_d1_l1_AtA(AtY, AtA, Eu, Ev, La_d1, La_l1, positivity,
+                                   L, rho, condMin, difRcd, difTol, itMax,
+                                   verbose=0, obj=False, dif=False):
+    """octave/mex/PFDR_graph_quadratic_d1_l1_AtA_mex.cpp: N = -V."""
+    dt = np.result_type(AtY, np.float32)
+    V = np.asarray(AtY).size
+    L = np.asarray(L, dt).ravel()
+    Eu, Ev = _edges(Eu, Ev)
+    return Lib().quadratic_d1_l1(
+        np.zeros(V, dt), np.asarray(AtY, dt),
+        np.asfortranarray(AtA, dt).ravel(order="F"), -V, Eu, Ev,
+        np.asarray(La_d1, dt), _scal_or_vec(La_l1, V, dt), positivity,
+        SCAL if L.size == 1 else DIAG, L, rho, condMin, difRcd, difTol, itMax,
+        obj, dif, verbose)
+
+
+def PFDR_graph_l22_d1_l1(Y, La_l2, Eu, Ev, La_d1, La_l1, positivity, rho,
+                         condMin, difRcd, difTol, itMax, verbose=0,
+                         obj=False, dif=False):
+    """octave/mex/PFDR_graph_l22_d1_l1_mex.cpp:54-83: Y <- La_l2*Y, N = 0,
+    A = La_l2 (diagonal), Ltype DIAG, L = La_l2; Obj += 1/2 ||y||^2_La_l2."""
+    Y = np.asarray(Y)
+    dt = np.result_type(Y, np.float32)
+    V = Y.size
+    La_l2 = _scal_or_vec(La_l2, V, dt)
+    Yw = (La_l2 * Y).astype(dt) if La_l2 is not None else Y.astype(dt)
+    Eu, Ev = _edges(Eu, Ev)
+    X, it, Obj, Dif = Lib().quadratic_d1_l1(
+        np.zeros(V, dt), Yw, La_l2, 0, Eu, Ev, np.asarray(La_d1, dt),
+        _scal_or_vec(La_l1, V, dt), positivity, DIAG, La_l2, rho, condMin,
+        difRcd, difTol, itMax, obj, dif, verbose)
+    if Obj is not None:
+        y = Y.astype(dt)
+        w = La_l2 if La_l2 is not None else np.ones(V, dt)
+        y2 = float(np.sum(w.astype(np.float64) * y * y)) / 2.0
+        Obj[: it + 1] += y2
+    return X, it, Obj, Dif
+
+
+def PFDR_graph_quadratic_d1_bounds(Y, A, Eu, Ev, La_d1, Bnd, L, rho, condMin,
+                                   difRcd, difTol, itMax, verbose=0,
+                                   obj=False, dif=False):
+    """octave/mex/PFDR_graph_quadratic_d1_bounds_mex.cpp (Bnd = [min, max])."""
+    A = np.asarray(A)
+    dt = np.result_type(Y, np.float32)
+    N, V = A.shape
+    L = np.asarray(L, dt).ravel()
+    Eu, Ev = _edges(Eu, Ev)
+    return Lib().quadratic_d1_bounds(
+        np.zeros(V, dt), np.asarray(Y, dt), np.asfortranarray(A, dt).ravel(order="F"),
+        N, Eu, Ev, np.asarray(La_d1, dt), Bnd[0], Bnd[1],
+        SCAL if L.size == 1 else DIAG, L, rho, condMin, difRcd, difTol, itMax,
+        obj, dif, verbose)
+
+
+def PFDR_graph_l22_d1_bounds(Y, La_l2, Eu, Ev, La_d1, Bnd, rho, condMin,
+                             difRcd, difTol, itMax, verbose=0, obj=False,
+                             dif=False):
+    """octave/mex/PFDR_graph_l22_d1_bounds_mex.cpp."""
+    Y = np.asarray(Y)
+    dt = np.result_type(Y, np.float32)
+    V = Y.size
+    La_l2 = _scal_or_vec(La_l2, V, dt)
+    Yw = (La_l2 * Y).astype(dt) if La_l2 is not None else Y.astype(dt)
+    Eu, Ev = _edges(Eu, Ev)
+    X, it, Obj, Dif = Lib().quadratic_d1_bounds(
+        np.zeros(V, dt), Yw, La_l2, 0, Eu, Ev, np.asarray(La_d1, dt), Bnd[0],
+        Bnd[1], DIAG, La_l2, rho, condMin, difRcd, difTol, itMax, obj, dif,
+        verbose)
+    if Obj is not None:
+        y = Y.astype(dt)
+        w = La_l2 if La_l2 is not None else np.ones(V, dt)
+        Obj[: it + 1] += float(np.sum(w.astype(np.float64) * y * y)) / 2.0
+    return X, it, Obj, Dif
+
+
+def PFDR_graph_loss_d1_simplex(Q, al, Eu, Ev, La_d1, rho, condMin, difRcd,
+                               difTol, itMax, verbose=0, obj=False,
+                               dif=False, La_f=None, P0=None):
+    """octave/mex/PFDR_graph_loss_d1_simplex_mex.cpp: Q is K-by-V (column v
+    = Q[:, v]); P starts at Q (:33) and La_f is NULL (:46) unless given."""
+    Q = np.asarray(Q)
+    dt = np.result_type(Q, np.float32)
+    K = Q.shape[0]
+    q = np.asfortranarray(Q, dt).ravel(order="F")
+    p0 = q if P0 is None else np.asfortranarray(P0, dt).ravel(order="F")
+    Eu, Ev = _edges(Eu, Ev)
+    P, it, Obj, Dif = Lib().loss_d1_simplex(
+        p0, q, K, Eu, Ev, np.asarray(La_d1, dt), al, La_f, rho, condMin,
+        difRcd, difTol, itMax, obj, dif, verbose)
+    return P.reshape(Q.shape, order="F"), it, Obj, Dif
+
+
+def proj_simplex_metric(X, M, A):
+    """Column-wise metric simplex projection of the D-by-N array X
+    (include/proj_simplex.hpp:33-35); M is D-by-nm, A has na entries."""
+    X = np.asarray(X)
+    dt = np.result_type(X, np.float32)
+    D = X.shape[0]
+    N = X.shape[1] if X.ndim > 1 else 1
+    M = np.asarray(M, dt)
+    nm = M.shape[1] if M.ndim > 1 else 1
+    A = np.atleast_1d(np.asarray(A, dt))
+    out = Lib().proj_simplex_metric(np.asfortranarray(X, dt).ravel(order="F"),
+                                    np.asfortranarray(M, dt).ravel(order="F"),
+                                    D, N, nm, A, A.size)
+    return out.reshape(X.shape, order="F")
+
+
+# ------------------------------------------------------------- sessions ---
+class Session:
+    """Device-resident solve: setup once, iterate in steps (benchmarks,
+    repeated solves).  Arrays may be numpy (host) or torch CUDA tensors
+    (device pointers, mem = PFDR_MEM_DEVICE)."""
+
+    def __init__(self, kind, dtype, V, E, Eu, Ev, La_d1, X0, Y, N=0, A=None,
+                 La_l1=None, positivity=0, lo=-np.inf, hi=np.inf, K=0,
+                 al=0.0, Ltype=SCAL, L=None, rho=1.5, condMin=1e-3,
+                 difRcd=0.0, difTol=0.0, itMax=1000, record_obj=False,
+                 record_dif=False, verbose=0, device=False):
+        self.lib = load()
+        ct, _, dcode = _real(dtype)
+        self._keep = []
+
+        def addr(a, is_int=False):
+            if a is None:
+                return None
+            if device:
+                return C.c_void_p(a.data_ptr())
+            a = np.ascontiguousarray(a, np.int32 if is_int else dtype)
+            self._keep.append(a)
+            return C.c_void_p(a.ctypes.data)
+
+        p = Problem()
+        p.kind, p.dtype = kind, dcode
+        p.mem = PFDR_MEM_DEVICE if device else PFDR_MEM_HOST
+        p.V, p.E, p.N, p.K = V, E, N, K
+        p.X, p.Y, p.A = addr(X0), addr(Y), addr(A)
+        p.Eu, p.Ev = addr(Eu, True), addr(Ev, True)
+        p.La_d1, p.La_l1, p.L = addr(La_d1), addr(La_l1), addr(L)
+        p.positivity, p.min, p.max, p.al = positivity, lo, hi, al
+        p.Ltype = Ltype
+        p.rho, p.condMin, p.difRcd, p.difTol = rho, condMin, difRcd, difTol
+        p.itMax, p.verbose = itMax, verbose
+        p.record_obj, p.record_dif = int(record_obj), int(record_dif)
+        self.problem = p
+        self.dtype = np.dtype(dtype)
+        self.V, self.K = V, max(K, 1)
+        self.itMax = itMax
+        self.record_obj, self.record_dif = record_obj, record_dif
+        h = C.c_void_p()
+        _check(self.lib.pfdr_session_create(C.byref(h), C.byref(p)),
+               "pfdr_session_create")
+        self.h = h
+
+    def run(self, iters):
+        it = C.c_int(0)
+        _check(self.lib.pfdr_session_run(self.h, C.c_int(iters), C.byref(it)),
+               "pfdr_session_run")
+        return it.value
+
+    def sync(self):
+        _check(self.lib.pfdr_session_sync(self.h), "pfdr_session_sync")
+
+    def profile(self, on=True):
+        _check(self.lib.pfdr_session_set_profiling(self.h, C.c_int(int(on))),
+               "pfdr_session_set_profiling")
+
+    def kernel_stats(self, name):
+        n, ms = C.c_int(0), C.c_double(0.0)
+        _check(self.lib.pfdr_session_kernel_stats(
+            self.h, name.encode(), C.byref(n), C.byref(ms)),
+            "pfdr_session_kernel_stats")
+        return n.value, ms.value
+
+    def device_bytes(self):
+        return int(self.lib.pfdr_session_device_bytes(self.h))
+
+    def result(self):
+        X = np.zeros(self.V * self.K, self.dtype)
+        it = C.c_int(0)
+        Obj = np.zeros(self.itMax + 1, self.dtype) if self.record_obj else None
+        Dif = np.zeros(max(self.itMax, 1), self.dtype) if self.record_dif else None
+        _check(self.lib.pfdr_session_result(
+            self.h, C.c_void_p(X.ctypes.data), C.byref(it),
+            None if Obj is None else C.c_void_p(Obj.ctypes.data),
+            None if Dif is None else C.c_void_p(Dif.ctypes.data)),
+            "pfdr_session_result")
+        return X, it.value, Obj, Dif
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pfdr_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------- native inputs ----
+def gen_knn_jitter_grid(shape, k=6, seed=6, jitter=0.25, v_range=None):
+    """Native twin of graphs.knn_jitter_grid (multi-threaded C++)."""
+    nx, ny, nz = shape
+    V = nx * ny * nz
+    v0, v1 = (0, V) if v_range is None else v_range
+    n = (v1 - v0) * k
+    Eu = np.empty(n, np.int32)
+    Ev = np.empty(n, np.int32)
+    got = load().pfdr_gen_knn_jitter_grid(nx, ny, nz, k, seed, jitter, v0, v1,
+                                          Eu.ctypes.data, Ev.ctypes.data)
+    if got != n:
+        raise PFDRError("pfdr_gen_knn_jitter_grid failed")
+    return Eu, Ev
+
+
+def gen_grid_edges(shape, conn, v_range=None):
+    nx, ny = shape[0], shape[1]
+    nz = shape[2] if len(shape) > 2 else 1
+    V = nx * ny * nz
+    v0, v1 = (0, V) if v_range is None else v_range
+    lib = load()
+    n = lib.pfdr_gen_grid_edges(nx, ny, nz, conn, v0, v1, None, None)
+    if n < 0:
+        raise PFDRError("pfdr_gen_grid_edges: unsupported connectivity")
+    Eu = np.empty(n, np.int32)
+    Ev = np.empty(n, np.int32)
+    lib.pfdr_gen_grid_edges(nx, ny, nz, conn, v0, v1, Eu.ctypes.data,
+                            Ev.ctypes.data)
+    return Eu, Ev
+
+
+def gen_piecewise(nx, V, seed, dtype=np.float32, noise=0.2, v_range=None):
+    v0, v1 = (0, V) if v_range is None else v_range
+    Y = np.empty(v1 - v0, dtype)
+    fn = (load().pfdr_gen_piecewise_f32 if np.dtype(dtype) == np.float32
+          else load().pfdr_gen_piecewise_f64)
+    fn(nx, seed, noise, v0, v1, Y.ctypes.data)
+    return Y

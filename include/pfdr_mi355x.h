@@ -1,0 +1,191 @@
+/* ==========================================================================
+ * pfdr_mi355x.h — C ABI of the MI355X-native PFDR solvers (libpfdr_mi355x.so)
+ *
+ * Plain C, fixed-width scalars, plain pointers and sizes; no C++ or torch
+ * types.  Two layers:
+ *
+ *  1. Drop-in entry points.  Same argument list and meaning as the reference
+ *     C++ templates they replace, host pointers, synchronous (device work is
+ *     finished and every output copied back before return), status return
+ *     instead of void.  The C++ drop-in symbols
+ *     (include/PFDR_graph_quadratic_d1_l1.hpp etc.) forward to these.
+ *       pfdr_quadratic_d1_l1_{f32,f64}
+ *           replaces PFDR_graph_quadratic_d1_l1<real>
+ *           (reference include/PFDR_graph_quadratic_d1_l1.hpp:36-42,
+ *            src/PFDR_graph_quadratic_d1_l1.cpp:270-553)
+ *       pfdr_quadratic_d1_bounds_{f32,f64}
+ *           replaces PFDR_graph_quadratic_d1_bounds<real>
+ *           (reference include/PFDR_graph_quadratic_d1_bounds.hpp:34-40,
+ *            src/PFDR_graph_quadratic_d1_bounds.cpp:244-530)
+ *       pfdr_loss_d1_simplex_{f32,f64}
+ *           replaces PFDR_graph_loss_d1_simplex<real>
+ *           (reference include/PFDR_graph_loss_d1_simplex.hpp:24-30,
+ *            src/PFDR_graph_loss_d1_simplex.cpp:372-715)
+ *       pfdr_proj_simplex_metric_{f32,f64}
+ *           replaces proj_simplex_metric<real>
+ *           (reference include/proj_simplex.hpp:33-35,
+ *            src/proj_simplex_metric.cpp:18-83)
+ *
+ *  2. Sessions: the same solvers with inputs that may already live in HBM,
+ *     setup separated from iterations (benchmarks, repeated solves) and the
+ *     1-D vertex-range partition across GPUs (RCCL halo exchange).
+ *
+ * Every entry returns PFDR_OK (0) or an error code; pfdr_last_error() gives
+ * the message of the calling thread's last failure.  There is no CPU
+ * fallback: without a usable gfx950 device every compute entry fails.
+ * ======================================================================== */
+#ifndef PFDR_MI355X_H
+#define PFDR_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFDR_OK 0
+#define PFDR_ERR_ARG 1    /* invalid argument */
+#define PFDR_ERR_HIP 2    /* HIP runtime failure (no device, OOM, fault) */
+#define PFDR_ERR_RCCL 3   /* collective failure */
+#define PFDR_ERR_STATE 4  /* session used out of order */
+
+/* Lipschitz information type, same values as the reference's
+ * typedef enum {SCAL, DIAG} Lipschtype (include/PFDR_graph_quadratic_d1_l1.hpp:34) */
+#define PFDR_LIPSCHITZ_SCAL 0
+#define PFDR_LIPSCHITZ_DIAG 1
+
+const char *pfdr_last_error(void);
+int pfdr_abi_version(void);          /* 1 */
+int pfdr_device_count(void);         /* visible HIP devices, <0 on error */
+
+/* ------------------------------------------------------------------ l1 -- */
+int pfdr_quadratic_d1_l1_f32(int V, int E, int N, float *X, const float *Y,
+    const float *A, const int *Eu, const int *Ev, const float *La_d1,
+    const float *La_l1, int positivity, int Ltype, const float *L,
+    float rho, float condMin, float difRcd, float difTol, int itMax,
+    int *it, float *Obj, float *Dif, int verbose);
+int pfdr_quadratic_d1_l1_f64(int V, int E, int N, double *X, const double *Y,
+    const double *A, const int *Eu, const int *Ev, const double *La_d1,
+    const double *La_l1, int positivity, int Ltype, const double *L,
+    double rho, double condMin, double difRcd, double difTol, int itMax,
+    int *it, double *Obj, double *Dif, int verbose);
+
+/* -------------------------------------------------------------- bounds -- */
+int pfdr_quadratic_d1_bounds_f32(int V, int E, int N, float *X,
+    const float *Y, const float *A, const int *Eu, const int *Ev,
+    const float *La_d1, float min, float max, int Ltype, const float *L,
+    float rho, float condMin, float difRcd, float difTol, int itMax,
+    int *it, float *Obj, float *Dif, int verbose);
+int pfdr_quadratic_d1_bounds_f64(int V, int E, int N, double *X,
+    const double *Y, const double *A, const int *Eu, const int *Ev,
+    const double *La_d1, double min, double max, int Ltype, const double *L,
+    double rho, double condMin, double difRcd, double difTol, int itMax,
+    int *it, double *Obj, double *Dif, int verbose);
+
+/* ------------------------------------------------------------- simplex -- */
+int pfdr_loss_d1_simplex_f32(int K, int V, int E, float al,
+    const float *La_f, float *P, const float *Q, const int *Eu,
+    const int *Ev, const float *La_d1, float rho, float condMin,
+    float difRcd, float difTol, int itMax, int *it, float *Obj, float *Dif,
+    int verbose);
+int pfdr_loss_d1_simplex_f64(int K, int V, int E, double al,
+    const double *La_f, double *P, const double *Q, const int *Eu,
+    const int *Ev, const double *La_d1, double rho, double condMin,
+    double difRcd, double difTol, int itMax, int *it, double *Obj,
+    double *Dif, int verbose);
+
+int pfdr_proj_simplex_metric_f32(float *X, const float *M, int D, int N,
+    int nm, const float *A, int na);
+int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
+    int nm, const double *A, int na);
+
+/* ------------------------------------------------------------ sessions -- */
+#define PFDR_KIND_L1 0
+#define PFDR_KIND_BOUNDS 1
+#define PFDR_KIND_SIMPLEX 2
+
+#define PFDR_F32 0
+#define PFDR_F64 1
+
+#define PFDR_MEM_HOST 0    /* pointers are host memory (copied in) */
+#define PFDR_MEM_DEVICE 1  /* pointers are device memory of the current device */
+
+typedef struct pfdr_problem {
+    int kind;             /* PFDR_KIND_* */
+    int dtype;            /* PFDR_F32 / PFDR_F64: type of every real array */
+    int mem;              /* PFDR_MEM_*: location of every array below */
+    int V, E, N, K;       /* as the reference (K only for simplex) */
+    void *X;              /* X (quadratic) or P (simplex), initial value */
+    const void *Y;        /* Y / A^tY (quadratic) or Q (simplex) */
+    const void *A;        /* quadratic only, NULL for identity */
+    const int *Eu, *Ev;   /* endpoints (global vertex ids when distributed) */
+    const void *La_d1;    /* length E */
+    const void *La_l1;    /* l1 weights (V) or La_f (simplex, V); may be NULL */
+    int positivity;       /* l1 only */
+    double min, max;      /* bounds only (+-HUGE_VAL for none) */
+    double al;            /* simplex only */
+    int Ltype;            /* PFDR_LIPSCHITZ_* */
+    const void *L;        /* NULL, scalar or length V */
+    double rho, condMin, difRcd, difTol;
+    int itMax;
+    int verbose;
+    int record_obj;       /* keep Obj[0..itMax] on the device */
+    int record_dif;       /* keep Dif[0..itMax-1] on the device */
+    /* --- 1-D vertex-range partition (leave zero for one GPU) ------------ */
+    int nranks, rank;     /* rank r owns global vertices [vtx_begin, vtx_begin+V) */
+    void *comm;           /* ncclComm_t created with pfdr_comm_init */
+    int64_t vtx_begin;    /* first owned global vertex */
+    int64_t V_global;     /* total vertices over all ranks */
+    const int64_t *e_global; /* global id of each local edge; NULL: e_offset + e */
+    int64_t e_offset;
+} pfdr_problem;
+
+typedef struct pfdr_session pfdr_session;
+
+int pfdr_session_create(pfdr_session **out, const pfdr_problem *p);
+/* Run up to `iters` more iterations (stopping early on difTol / itMax as the
+ * reference does).  *it_total receives the total iteration count so far. */
+int pfdr_session_run(pfdr_session *s, int iters, int *it_total);
+/* Copy X (or P) back to host memory, and the iteration count; Obj/Dif copy
+ * it+1 / it values when recorded (may be NULL). */
+int pfdr_session_result(pfdr_session *s, void *X_host, int *it, void *Obj_host,
+                        void *Dif_host);
+/* Device pointer of the current iterate (valid until destroy). */
+void *pfdr_session_device_x(pfdr_session *s);
+/* Kernel timing: when enabled, HIP events bracket each launch of the named
+ * kernels on the session stream; stats give launches and mean duration. */
+int pfdr_session_set_profiling(pfdr_session *s, int on);
+int pfdr_session_kernel_stats(pfdr_session *s, const char *kernel,
+                              int *launches, double *mean_ms);
+/* Synchronise the session stream. */
+int pfdr_session_sync(pfdr_session *s);
+/* Bytes of device memory held by the session. */
+int64_t pfdr_session_device_bytes(pfdr_session *s);
+void pfdr_session_destroy(pfdr_session *s);
+
+/* ------------------------------------------------------ multi-GPU comm -- */
+#define PFDR_COMM_ID_BYTES 128
+/* rank 0 creates the id, the caller broadcasts it, every rank inits */
+int pfdr_comm_unique_id(void *id_out /* PFDR_COMM_ID_BYTES */);
+int pfdr_comm_init(void **comm_out, int nranks, int rank, const void *id);
+int pfdr_comm_destroy(void *comm);
+int pfdr_comm_allreduce_max_f64(void *comm, double *value);
+
+/* -------------------------------------------------- synthetic inputs -- */
+/* Host-side deterministic generators (no device needed), identical laws to
+ * cp_pfdr_graph_d1_amd/graphs.py.  Edges are written for emitters
+ * [v_begin, v_end); the k-NN graph writes exactly k*(v_end-v_begin). */
+int64_t pfdr_gen_knn_jitter_grid(int nx, int ny, int nz, int k, uint64_t seed,
+    double jitter, int64_t v_begin, int64_t v_end, int *Eu, int *Ev);
+int64_t pfdr_gen_grid_edges(int nx, int ny, int nz, int conn,
+    int64_t v_begin, int64_t v_end, int *Eu, int *Ev);
+int pfdr_gen_piecewise_f32(int nx, uint64_t seed, double noise,
+    int64_t v_begin, int64_t v_end, float *Y);
+int pfdr_gen_piecewise_f64(int nx, uint64_t seed, double noise,
+    int64_t v_begin, int64_t v_end, double *Y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFDR_MI355X_H */
