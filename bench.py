@@ -206,6 +206,7 @@ def main():
             "global_graph": "%dx%dx%d" % gshape,
             "V_per_gpu": V, "E_per_gpu": E,
             "parallelism": "replicas" if world > 1 else "single",
+            "average": os.environ.get("PFDR_AVERAGE", "split"),
             "setup_s": round(setup_s, 3),
             "device_bytes": dev_bytes,
             "finite": finite,

@@ -103,6 +103,18 @@ __device__ __forceinline__ T block_sum(T v, T *lds /* >= kBlock/64 */) {
     return s;
 }
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8
+// XCDs (blocks b, b+8, ... share one L2), so give each XCD a CONTIGUOUS range
+// of logical blocks: neighbouring blocks, which gather the same neighbour
+// bands of the graph, then share an L2.  Placement is a speed hint only.
+// Launch xcd_grid(nb) blocks; a block whose logical id is >= nb returns.
+__device__ __forceinline__ int xcd_block(int b, int nb, int on) {
+    if (!on) return b;
+    const int per = (nb + 7) >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+inline int xcd_grid(int nb, int on) { return on ? ((nb + 7) >> 3) << 3 : nb; }
+
 inline int grid_for(long n, int per_thread = 1) {
     long t = (n + per_thread - 1) / per_thread;
     long g = (t + kBlock - 1) / kBlock;

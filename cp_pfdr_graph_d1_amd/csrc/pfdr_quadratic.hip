@@ -71,14 +71,26 @@ __device__ __forceinline__ bool gated(const Ctrl<real> *c, int gate) {
 
 // Ordered sum over the incidence slots of the block's vertices.  The slots
 // of the block's contiguous vertex range are gathered cooperatively (all
-// lanes busy whatever the degrees, coalesced index reads) into LDS chunks,
-// then each lane adds its own vertex's slots in CSR order.
-template <typename real, int CAP>
+// lanes busy whatever the degrees, coalesced index reads, GB = 16 index
+// loads then 16 value gathers in flight per lane) into LDS chunks, then each
+// lane adds its own vertex's slots in CSR order.
+// Slot value source (MODE): AVG_WZ: wz[slot] written by the edge sweep;
+// AVG_GATHER: W2[slot] * Z2[slot] formed here (the reference's Wu*Zu);
+// AVG_SCATTER: the edge sweep stored W*Z straight at its CSR position, so the
+// row segment is read as one coalesced stream (no index).
+// AVG_SPLIT: as AVG_WZ with the contributions stored side-major,
+// wz[side * E + e], so the u-side run of a vertex is contiguous.
+enum AvgMode : int { AVG_WZ = 0, AVG_GATHER = 1, AVG_SCATTER = 2, AVG_SPLIT = 3 };
+constexpr int GB = 16;
+template <typename real, int CAP, int MODE = AVG_WZ>
 __device__ __forceinline__ real gather_sum(int V, int v0,
                                            const int *__restrict__ ptr,
                                            const unsigned *__restrict__ idx,
                                            const real *__restrict__ wz,
-                                           real *lds) {
+                                           real *lds,
+                                           const real *__restrict__ z2 = nullptr,
+                                           long E = 0) {
+    static_assert(CAP % (kBlock * GB) == 0, "chunk must be a whole batch");
     const int tid = threadIdx.x;
     const int v = v0 + tid;
     const int vend = min(v0 + kBlock, V);
@@ -87,11 +99,40 @@ __device__ __forceinline__ real gather_sum(int V, int v0,
     const long my1 = (v < V) ? (long)ptr[v + 1] : seg1;
     real s = real(0);
     for (long c0 = seg0; c0 < seg1; c0 += CAP) {
-        const long c1 = min(c0 + (long)CAP, seg1);
-        for (long j = c0 + tid; j < c1; j += kBlock) lds[j - c0] = wz[idx[j]];
+        const int n = (int)min((long)CAP, seg1 - c0);
+        for (int b = 0; b < n; b += kBlock * GB) {
+            real w[GB];
+            if (MODE == AVG_SCATTER) {
+#pragma unroll
+                for (int u = 0; u < GB; u++) {
+                    const int j = b + u * kBlock + tid;
+                    w[u] = (j < n) ? wz[c0 + j] : real(0);
+                }
+            } else {
+                unsigned id[GB];
+#pragma unroll
+                for (int u = 0; u < GB; u++) {
+                    const int j = b + u * kBlock + tid;
+                    id[u] = (j < n) ? idx[c0 + j] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < GB; u++) {
+                    const int j = b + u * kBlock + tid;
+                    if (MODE == AVG_GATHER) w[u] = (j < n) ? wz[id[u]] * z2[id[u]] : real(0);
+                    else if (MODE == AVG_SPLIT)
+                        w[u] = (j < n) ? wz[(long)(id[u] & 1u) * E + (id[u] >> 1)] : real(0);
+                    else w[u] = (j < n) ? wz[id[u]] : real(0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < GB; u++) {
+                const int j = b + u * kBlock + tid;
+                if (j < n) lds[j] = w[u];
+            }
+        }
         __syncthreads();
-        const long a = max(my0, c0), b = min(my1, c1);
-        for (long j = a; j < b; j++) s += lds[j - c0];
+        const long a = max(my0, c0), e = min(my1, c0 + (long)n);
+        for (long j = a; j < e; j++) s += lds[j - c0];
         __syncthreads();
     }
     return s;
@@ -99,7 +140,7 @@ __device__ __forceinline__ real gather_sum(int V, int v0,
 
 template <typename real> struct GatherCap;
 template <> struct GatherCap<float> { static constexpr int v = 4096; };
-template <> struct GatherCap<double> { static constexpr int v = 2048; };
+template <> struct GatherCap<double> { static constexpr int v = 4096; };
 
 // ====================================================================== //
 //                                kernels                                  //
@@ -122,16 +163,16 @@ __global__ void k_x_extract(int V, const R2<real> *__restrict__ xp,
     if (v < V) X[v] = xp[v].x;
 }
 
-// Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324)
+// Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324); half-edge layout Z2[2e + side]
 template <typename real>
 __global__ void k_z_init(long E, const int *__restrict__ Eu,
                          const int *__restrict__ Ev,
                          const R2<real> *__restrict__ xp,
-                         real *__restrict__ Zu, real *__restrict__ Zv) {
+                         real *__restrict__ Z2) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
-    Zu[e] = xp[Eu[e]].x;
-    Zv[e] = xp[Ev[e]].x;
+    Z2[2 * e] = xp[Eu[e]].x;
+    Z2[2 * e + 1] = xp[Ev[e]].x;
 }
 
 // diagonal of A^t A for the identity / diagonal / A^tA modes (ref :101-122)
@@ -357,21 +398,19 @@ __global__ __launch_bounds__(256) void k_seq_c(int V,
     }
 }
 
-// d1 splitting weights (ref :156-192).  On reconditioning, first turn the
-// auxiliary variables into subgradients with the OLD weights and metric
-// (ref :89-99).  wz receives the weight at both slots for the ordered
-// per-vertex sums.
+// d1 splitting weights (ref :156-192) into both half-edges W2[2e + side].
+// On reconditioning, first turn the auxiliary variables into subgradients
+// with the OLD weights and metric (ref :89-99).
 template <typename real>
 __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
                              const int *__restrict__ Ev,
                              const real *__restrict__ La_d1,
                              const Ctrl<real> *__restrict__ ctrl, int init,
                              real condMin, const R2<real> *__restrict__ xp,
-                             real *__restrict__ Wu, real *__restrict__ Wv,
-                             real *__restrict__ wz,
+                             real *__restrict__ W2,
                              const real *__restrict__ Ga,
                              const real *__restrict__ grad,
-                             real *__restrict__ Zu, real *__restrict__ Zv) {
+                             real *__restrict__ Z2) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const real c = ctrl->c;
@@ -382,8 +421,8 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
         const int u = Eu[e], v = Ev[e];
         const real xu = xp[u].x, xv = xp[v].x;
         const real gu = Ga[u], gv = Ga[v];
-        Zu[e] = (Wu[e] / gu) * (xu - gu * grad[u] - Zu[e]);
-        Zv[e] = (Wv[e] / gv) * (xv - gv * grad[v] - Zv[e]);
+        Z2[2 * e] = (W2[2 * e] / gu) * (xu - gu * grad[u] - Z2[2 * e]);
+        Z2[2 * e + 1] = (W2[2 * e + 1] / gv) * (xv - gv * grad[v] - Z2[2 * e + 1]);
         real a = xu, b = xv, d = a - b;
         if (a < real(0)) a = -a;
         if (b < real(0)) b = -b;
@@ -394,24 +433,22 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
         if (d < a) d = a;
         w = La_d1[e] / d;
     }
-    Wu[e] = w;
-    Wv[e] = w;
-    wz[2 * e] = w;
-    wz[2 * e + 1] = w;
+    W2[2 * e] = w;
+    W2[2 * e + 1] = w;
 }
 
 // metric of every vertex (ref :193-239 and :262-264)
 template <typename real>
 __global__ __launch_bounds__(256) void k_precond_vertex(
     int V, const int *__restrict__ ptr, const unsigned *__restrict__ idx,
-    const real *__restrict__ wz, const real *__restrict__ diag,
+    const real *__restrict__ W2, const real *__restrict__ diag,
     const real *__restrict__ La_l1, const R2<real> *__restrict__ xp,
     const Ctrl<real> *__restrict__ ctrl, int init, real condMin, real cap,
     const real *__restrict__ Ldiag, real *__restrict__ Ga,
     real *__restrict__ invAux, real *__restrict__ Th_l1) {
     __shared__ real lds[GatherCap<real>::v];
     const int v0 = blockIdx.x * kBlock;
-    const real s = gather_sum<real, GatherCap<real>::v>(V, v0, ptr, idx, wz, lds);
+    const real s = gather_sum<real, GatherCap<real>::v>(V, v0, ptr, idx, W2, lds);
     const int v = v0 + threadIdx.x;
     if (v >= V) return;
     real g = diag[v];
@@ -451,29 +488,36 @@ __global__ void k_precond_edge2(long E, const int *__restrict__ Eu,
                                 const real *__restrict__ invAux,
                                 const real *__restrict__ Ga,
                                 const real *__restrict__ La_d1,
-                                real *__restrict__ Wu, real *__restrict__ Wv,
+                                real *__restrict__ W2,
                                 real *__restrict__ Wd1u,
                                 real *__restrict__ Wd1v,
                                 real *__restrict__ Th, int recond,
                                 const R2<real> *__restrict__ xp,
                                 const real *__restrict__ grad,
-                                real *__restrict__ Zu, real *__restrict__ Zv) {
+                                real *__restrict__ Z2) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const int u = Eu[e], v = Ev[e];
-    const real wu = Wu[e] * invAux[u];
-    const real wv = Wv[e] * invAux[v];
-    Wu[e] = wu;
-    Wv[e] = wv;
+    const real wu = W2[2 * e] * invAux[u];
+    const real wv = W2[2 * e + 1] * invAux[v];
+    W2[2 * e] = wu;
+    W2[2 * e + 1] = wv;
     const real gu = Ga[u], gv = Ga[v];
     if (recond) {
-        Zu[e] = xp[u].x - gu * (grad[u] + Zu[e] / wu);
-        Zv[e] = xp[v].x - gv * (grad[v] + Zv[e] / wv);
+        Z2[2 * e] = xp[u].x - gu * (grad[u] + Z2[2 * e] / wu);
+        Z2[2 * e + 1] = xp[v].x - gv * (grad[v] + Z2[2 * e + 1] / wv);
     }
     const real a = wu / gu, b = wv / gv, s = a + b;
     Th[e] = La_d1[e] * s / (a * b);
     Wd1u[e] = a / s;
     Wd1v[e] = b / s;
+}
+
+// CSR position of every slot: pos2[idx[j]] = j
+__global__ void k_slot_positions(long n, const unsigned *__restrict__ idx,
+                                 unsigned *__restrict__ pos2) {
+    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) pos2[idx[j]] = (unsigned)j;
 }
 
 // gradient A X - Y of the identity / diagonal modes (ref :377-385, :441-445)
@@ -526,17 +570,23 @@ __device__ __forceinline__ void edge_update(const R2<real> &pu,
     }
 }
 
-template <typename real>
+// DR contributions W*Z: AVG_WZ writes them at wz[2e + side], AVG_SCATTER at
+// their CSR position wz[pos2[2e + side]], AVG_GATHER leaves them to the
+// vertex sweep
+template <typename real, int MODE>
 __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
-    const R2<real> *__restrict__ xp, real *__restrict__ Zu,
-    real *__restrict__ Zv, const real *__restrict__ Wd1u,
-    const real *__restrict__ Wd1v, const real *__restrict__ Th,
-    const real *__restrict__ Wu, const real *__restrict__ Wv,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl) {
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2,
+    const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
+    const real *__restrict__ Th, const real *__restrict__ W2,
+    real *__restrict__ wz, const unsigned *__restrict__ pos2, real rho,
+    const Ctrl<real> *ctrl, int nb, int xcd) {
+    constexpr bool WZ = MODE != AVG_GATHER;
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
-    const long e0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * EPT;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    const long e0 = ((long)blk * blockDim.x + threadIdx.x) * EPT;
     if (e0 >= E) return;
     if (e0 + EPT <= E) {
         const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
@@ -544,33 +594,48 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
         R2<real> pu[EPT], pv[EPT];
 #pragma unroll
         for (int j = 0; j < EPT; j++) { pu[j] = xp[iu.v[j]]; pv[j] = xp[iv.v[j]]; }
-        Pk<real, EPT> zu = ldv<real, EPT>(Zu + e0);
-        Pk<real, EPT> zv = ldv<real, EPT>(Zv + e0);
+        Pk<real, 2 * EPT> z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
         const Pk<real, EPT> a = ldv<real, EPT>(Wd1u + e0);
         const Pk<real, EPT> b = ldv<real, EPT>(Wd1v + e0);
         const Pk<real, EPT> t = ldv<real, EPT>(Th + e0);
-        const Pk<real, EPT> wu = ldv<real, EPT>(Wu + e0);
-        const Pk<real, EPT> wv = ldv<real, EPT>(Wv + e0);
-        Pk<real, 2 * EPT> out;
 #pragma unroll
-        for (int j = 0; j < EPT; j++) {
-            edge_update<real>(pu[j], pv[j], zu.v[j], zv.v[j], a.v[j], b.v[j],
+        for (int j = 0; j < EPT; j++)
+            edge_update<real>(pu[j], pv[j], z.v[2 * j], z.v[2 * j + 1], a.v[j], b.v[j],
                               t.v[j], rho);
-            out.v[2 * j] = wu.v[j] * zu.v[j];
-            out.v[2 * j + 1] = wv.v[j] * zv.v[j];
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
+        if (WZ) {
+            const Pk<real, 2 * EPT> w = ldv<real, 2 * EPT>(W2 + 2 * e0);
+            Pk<real, 2 * EPT> out;
+#pragma unroll
+            for (int j = 0; j < 2 * EPT; j++) out.v[j] = w.v[j] * z.v[j];
+            if (MODE == AVG_SCATTER) {
+                const Pk<unsigned, 2 * EPT> p = ldv<unsigned, 2 * EPT>(pos2 + 2 * e0);
+#pragma unroll
+                for (int j = 0; j < 2 * EPT; j++) wz[p.v[j]] = out.v[j];
+            } else if (MODE == AVG_SPLIT) {
+                Pk<real, EPT> ou, ov;
+#pragma unroll
+                for (int j = 0; j < EPT; j++) { ou.v[j] = out.v[2 * j]; ov.v[j] = out.v[2 * j + 1]; }
+                stv<real, EPT>(wz + e0, ou);
+                stv<real, EPT>(wz + E + e0, ov);
+            } else {
+                stv<real, 2 * EPT>(wz + 2 * e0, out);
+            }
         }
-        stv<real, EPT>(Zu + e0, zu);
-        stv<real, EPT>(Zv + e0, zv);
-        stv<real, 2 * EPT>(wz + 2 * e0, out);
     } else {
         for (long e = e0; e < E; e++) {
             const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
-            real zu = Zu[e], zv = Zv[e];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1];
             edge_update<real>(pu, pv, zu, zv, Wd1u[e], Wd1v[e], Th[e], rho);
-            Zu[e] = zu;
-            Zv[e] = zv;
-            wz[2 * e] = Wu[e] * zu;
-            wz[2 * e + 1] = Wv[e] * zv;
+            Z2[2 * e] = zu;
+            Z2[2 * e + 1] = zv;
+            if (WZ) {
+                long iu = (MODE == AVG_SCATTER) ? (long)pos2[2 * e] : 2 * e;
+                long iv = (MODE == AVG_SCATTER) ? (long)pos2[2 * e + 1] : 2 * e + 1;
+                if (MODE == AVG_SPLIT) { iu = e; iv = E + e; }
+                wz[iu] = W2[2 * e] * zu;
+                wz[iv] = W2[2 * e + 1] * zv;
+            }
         }
     }
 }
@@ -578,9 +643,12 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 template <typename real>
 struct VArgs {
     int V;
+    int nb, xcd;            // logical blocks, XCD-aware order
+    long E;
     const int *ptr;
     const unsigned *idx;
-    const real *wz;
+    const real *wz;         // W*Z per slot (WZ) or W2 (products formed here)
+    const real *z2;         // Z2 when the products are formed here
     R2<real> *xp;
     const real *Y, *A, *Ga, *Th_l1;
     int prox, positivity;
@@ -593,19 +661,29 @@ struct VArgs {
 
 // DR average (ordered), prox on the iterate, evolution partials, next
 // forward step (ref :491-529 then :355-464 of the next iteration)
-template <typename real>
+template <typename real, int MODE>
 __global__ __launch_bounds__(256) void k_vertex_sweep(VArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
-    const int v0 = blockIdx.x * kBlock;
-    real x = gather_sum<real, GatherCap<real>::v>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (blk >= a.nb) return;
+    const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
+    // per-vertex operands first: their latency hides under the gather
+    R2<real> q{};
+    real th = real(0), yv = real(0), gv = real(0), av = real(0);
+    if (v < a.V) {
+        q = a.xp[v];
+        if (a.prox == PROX_L1) th = a.Th_l1[v];
+        if (a.fwd) { yv = a.Y[v]; gv = a.Ga[v]; }
+        if (a.fwd == 2) av = a.A[v];
+    }
+    real x = gather_sum<real, GatherCap<real>::v, MODE>(a.V, v0, a.ptr, a.idx, a.wz, lds, a.z2, a.E);
     real num = real(0), den = real(0);
     if (v < a.V) {
         switch (a.prox) {
             case PROX_L1: {
-                const real th = a.Th_l1[v];
                 if (x > th) x -= th;
                 else if (!a.positivity && (x < -th)) x += th;
                 else x = real(0);
@@ -626,7 +704,6 @@ __global__ __launch_bounds__(256) void k_vertex_sweep(VArgs<real> a) {
             default:
                 break;
         }
-        R2<real> q = a.xp[v];
         if (a.track) {
             const real d = q.x - x;
             num = d * d;
@@ -634,9 +711,9 @@ __global__ __launch_bounds__(256) void k_vertex_sweep(VArgs<real> a) {
         }
         q.x = x;
         if (a.fwd) {
-            real p = (a.fwd == 2) ? a.A[v] * x : x;
-            p -= a.Y[v];
-            q.y = real(2) * x - a.Ga[v] * p;
+            real p = (a.fwd == 2) ? av * x : x;
+            p -= yv;
+            q.y = real(2) * x - gv * p;
         }
         a.xp[v] = q;
     }
@@ -644,8 +721,8 @@ __global__ __launch_bounds__(256) void k_vertex_sweep(VArgs<real> a) {
         num = block_sum(num, red[0]);
         den = block_sum(den, red[1]);
         if (threadIdx.x == 0) {
-            a.part[2 * blockIdx.x] = num;
-            a.part[2 * blockIdx.x + 1] = den;
+            a.part[2 * blk] = num;
+            a.part[2 * blk + 1] = den;
         }
     }
 }
@@ -811,7 +888,10 @@ class QuadSession final : public SessionBase {
     DevBuf<real> La_d1_, La_l1_, Y_, A_, L_;
     DevBuf<R2<real>> xp_;
     DevBuf<real> diag_, Ga_, invAux_, Th_l1_, absval_, grad_, pre_, xout_;
-    DevBuf<real> Zu_, Zv_, Wu_, Wv_, Wd1u_, Wd1v_, Th_, wz_;
+    DevBuf<real> Z2_, W2_, Wd1u_, Wd1v_, Th_, wz_;
+    int avg_ = AVG_SPLIT;  // how the DR contributions reach the vertex sweep
+    int xcd_e_ = 0, xcd_v_ = 1;  // XCD-aware block order (edge / vertex sweep)
+    DevBuf<unsigned> pos2_;
     DevBuf<real> R_, Rpart_, vpart_, opart_, Obj_, Dif_;
     DevBuf<int> cnt_part_;
     DevBuf<Ctrl<real>> ctrl_;
@@ -921,10 +1001,21 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         PFDR_HIP(hipStreamSynchronize(s));
     }
     // edge state and per-vertex metric
-    Zu_.alloc(E ? E : 1); Zv_.alloc(E ? E : 1);
-    Wu_.alloc(E ? E : 1); Wv_.alloc(E ? E : 1);
+    {
+        // tuning knobs for A/B runs: PFDR_AVERAGE = scatter | wz | gather,
+        // PFDR_XCD = <edge><vertex> bits, e.g. "01" (default)
+        const char *m = getenv("PFDR_AVERAGE");
+        if (m && strcmp(m, "wz") == 0) avg_ = AVG_WZ;
+        else if (m && strcmp(m, "split") == 0) avg_ = AVG_SPLIT;
+        else if (m && strcmp(m, "scatter") == 0) avg_ = AVG_SCATTER;
+        else if (m && strcmp(m, "gather") == 0) avg_ = AVG_GATHER;
+        const char *x = getenv("PFDR_XCD");
+        if (x && strlen(x) == 2) { xcd_e_ = x[0] == '1'; xcd_v_ = x[1] == '1'; }
+    }
+    Z2_.alloc(E ? 2 * E : 1);
+    W2_.alloc(E ? 2 * E : 1);
     Wd1u_.alloc(E ? E : 1); Wd1v_.alloc(E ? E : 1); Th_.alloc(E ? E : 1);
-    wz_.alloc(2 * E ? 2 * E : 1);
+    if (avg_ != AVG_GATHER) wz_.alloc(E ? 2 * E : 1);
     diag_.alloc(V); Ga_.alloc(V); invAux_.alloc(V); absval_.alloc(V);
     if (flavour_ == 0 && p->La_l1) Th_l1_.alloc(V);
     nbv_ = grid_for(V);
@@ -962,8 +1053,13 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     hctrl_->eps = (real(0) < difTol_ && difTol_ < Lim<real>::eps) ? difTol_ : Lim<real>::eps;
     push_ctrl();
 
-    // graph: ordered incidence CSR
+    // graph: ordered incidence CSR (+ the CSR position of every slot)
     build_incidence(Eu_.p, Ev_.p, V_, E_, inc_, s);
+    if (avg_ == AVG_SCATTER && E_) {
+        pos2_.alloc(2 * E);
+        k_slot_positions<<<grid_for(2 * E_), kBlock, 0, s>>>(2 * E_, inc_.idx.p, pos2_.p);
+        PFDR_HIP(hipGetLastError());
+    }
     // diagonal of A^tA
     if (mode_ == A_DIRECT) {
         ColArgs<real> ca{};
@@ -974,7 +1070,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
     PFDR_HIP(hipGetLastError());
     // Z = X at both ends, first preconditioning, first forward step
-    if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Zu_.p, Zv_.p);
+    if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p);
     precondition(true);
     if (mode_ == A_IDENT || mode_ == A_DIAG) {
         grad_.alloc(V);
@@ -993,10 +1089,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
-                            &pre_, &Zu_, &Zv_, &Wu_, &Wv_, &Wd1u_, &Wd1v_, &Th_, &wz_, &R_, &Rpart_,
+                            &pre_, &Z2_, &W2_, &Wd1u_, &Wd1v_, &Th_, &wz_, &R_, &Rpart_,
                             &vpart_, &opart_, &Obj_, &Dif_})
         acc(b->n * sizeof(real));
-    acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
+    acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4 + pos2_.n * 4);
 }
 
 template <typename real>
@@ -1091,17 +1187,17 @@ void QuadSession<real>::precondition(bool init) {
     if (!init) gradient();
     if (E_) {
         k_d1_weights<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, La_d1_.p, ctrl_.p, init ? 1 : 0,
-                                                   condMin_, xp_.p, Wu_.p, Wv_.p, wz_.p, Ga_.p,
-                                                   grad_.p, Zu_.p, Zv_.p);
+                                                   condMin_, xp_.p, W2_.p, Ga_.p,
+                                                   grad_.p, Z2_.p);
     }
-    k_precond_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, wz_.p, diag_.p,
+    k_precond_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, W2_.p, diag_.p,
                                                    La_l1_.p, xp_.p, ctrl_.p, init ? 1 : 0, condMin_,
                                                    cap_, Ldiag_ ? L_.p : nullptr, Ga_.p,
                                                    invAux_.p, Th_l1_.p);
     if (E_) {
         k_precond_edge2<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, invAux_.p, Ga_.p, La_d1_.p,
-                                                      Wu_.p, Wv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
-                                                      init ? 0 : 1, xp_.p, grad_.p, Zu_.p, Zv_.p);
+                                                      W2_.p, Wd1u_.p, Wd1v_.p, Th_.p,
+                                                      init ? 0 : 1, xp_.p, grad_.p, Z2_.p);
     }
     PFDR_HIP(hipGetLastError());
     if (!init) {
@@ -1147,18 +1243,32 @@ void QuadSession<real>::body() {
     constexpr int EPT = Vec<real>::kPer16B;
     if (E_) {
         ProfScope ps(prof, "edge_sweep", s);
-        k_edge_sweep<real><<<grid_for(E_, EPT), kBlock, 0, s>>>(
-            E_, Eu_.p, Ev_.p, xp_.p, Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p, Wu_.p, Wv_.p, wz_.p, rho_, c);
+        const int nb = grid_for(E_, EPT), g = xcd_grid(nb, xcd_e_);
+#define PFDR_EDGE(M) k_edge_sweep<real, M><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, \
+            Wd1u_.p, Wd1v_.p, Th_.p, W2_.p, wz_.p, pos2_.p, rho_, c, nb, xcd_e_)
+        if (avg_ == AVG_SCATTER) PFDR_EDGE(AVG_SCATTER);
+        else if (avg_ == AVG_WZ) PFDR_EDGE(AVG_WZ);
+        else if (avg_ == AVG_SPLIT) PFDR_EDGE(AVG_SPLIT);
+        else PFDR_EDGE(AVG_GATHER);
+#undef PFDR_EDGE
     }
     {
         VArgs<real> a{};
-        a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.wz = wz_.p; a.xp = xp_.p;
+        a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p;
+        a.wz = avg_ == AVG_GATHER ? W2_.p : wz_.p;
+        a.z2 = avg_ == AVG_GATHER ? Z2_.p : nullptr;
         a.Y = Y_.p; a.A = A_.p; a.Ga = Ga_.p; a.Th_l1 = Th_l1_.p;
         a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
         a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
         a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
+        a.nb = nbv_; a.xcd = xcd_v_;
+        const int g = xcd_grid(nbv_, xcd_v_);
         ProfScope ps(prof, "vertex_sweep", s);
-        k_vertex_sweep<real><<<nbv_, kBlock, 0, s>>>(a);
+        a.E = E_;
+        if (avg_ == AVG_SCATTER) k_vertex_sweep<real, AVG_SCATTER><<<g, kBlock, 0, s>>>(a);
+        else if (avg_ == AVG_WZ) k_vertex_sweep<real, AVG_WZ><<<g, kBlock, 0, s>>>(a);
+        else if (avg_ == AVG_SPLIT) k_vertex_sweep<real, AVG_SPLIT><<<g, kBlock, 0, s>>>(a);
+        else k_vertex_sweep<real, AVG_GATHER><<<g, kBlock, 0, s>>>(a);
     }
     if (gated) {
         k_finalize<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, ctrl_.p, rec_dif_ ? Dif_.p : nullptr,
