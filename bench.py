@@ -43,13 +43,18 @@ METRIC = "PFDR iter/s and Medge-updates/s, 10M-vertex 6-NN graph, 1/2/4/8 MI355X
 
 
 def headline_inputs(rank, nranks, dtype=np.float32):
-    """The headline graph (one independent replica per rank)."""
+    """Rank r's slab of the weak-scaled headline graph: the global jittered
+    grid is 250 x 200 x (200 * nranks), rank r owns the vertices of
+    z in [200 r, 200 r + 200) (10M) and the 60M edges they emit; edges
+    reaching the next slab are its halo.  nranks = 1: the headline graph."""
     from cp_pfdr_graph_d1_amd import pfdr
     nx, ny, nz = SHAPE
+    gshape = (nx, ny, nz * nranks)
     V = nx * ny * nz
-    Eu, Ev = pfdr.gen_knn_jitter_grid(SHAPE, KNN, GRAPH_SEED, 0.25)
-    Y = pfdr.gen_piecewise(nx, V, Y_SEED, dtype, 0.2)
-    return SHAPE, V, Eu, Ev, Y
+    v0 = rank * V
+    Eu, Ev = pfdr.gen_knn_jitter_grid(gshape, KNN, GRAPH_SEED, 0.25, (v0, v0 + V))
+    Y = pfdr.gen_piecewise(nx, V * nranks, Y_SEED, dtype, 0.2, (v0, v0 + V))
+    return gshape, V, Eu, Ev, Y
 
 
 # ------------------------------------------------------------ CPU baseline --
@@ -148,11 +153,17 @@ def main():
 
     gshape, V, Eu, Ev, Y = headline_inputs(rank, world)
     E = Eu.size
+    dist_kw = {}
+    if world > 1:  # 1-D vertex-range partition, RCCL halo exchange over xGMI
+        from cp_pfdr_graph_d1_amd import partition
+        comm = partition.comm_init(world, rank, lambda t: dist.broadcast(t, 0))
+        dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
+                       vtx_begin=rank * V, V_global=world * V, e_offset=rank * E)
     t = time.perf_counter()
     sess = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, E, Eu, Ev,
                         np.full(E, LA_D1, np.float32), np.zeros(V, np.float32), Y,
                         La_l1=np.full(V, LA_L1, np.float32), rho=RHO, condMin=COND_MIN,
-                        difTol=0.0, difRcd=0.0, itMax=args.warmup + args.steps)
+                        difTol=0.0, difRcd=0.0, itMax=args.warmup + args.steps, **dist_kw)
     setup_s = time.perf_counter() - t
     del Eu, Ev
     sess.run(args.warmup)
@@ -172,6 +183,7 @@ def main():
         el_max = float(tt.item())
     n_e, ms_e = sess.kernel_stats("edge_sweep")
     n_v, ms_v = sess.kernel_stats("vertex_sweep")
+    halo = {k: sess.kernel_stats(k)[1] for k in ("halo_pull", "halo_push")} if world > 1 else {}
     X, _, _, _ = sess.result()
     finite = bool(np.all(np.isfinite(X)))
     dev_bytes = sess.device_bytes()
@@ -205,7 +217,7 @@ def main():
                             SHAPE + (KNN, V, E)),
             "global_graph": "%dx%dx%d" % gshape,
             "V_per_gpu": V, "E_per_gpu": E,
-            "parallelism": "replicas" if world > 1 else "single",
+            "parallelism": "vertex-partition%d (RCCL halo)" % world if world > 1 else "single",
             "average": os.environ.get("PFDR_AVERAGE", "split"),
             "setup_s": round(setup_s, 3),
             "device_bytes": dev_bytes,
@@ -223,6 +235,7 @@ def main():
             "launches": n_e,
             "mean_ms": round(ms_e, 5),
             "vertex_sweep_mean_ms": round(ms_v, 5),
+            "halo_mean_ms": {k: round(v, 5) for k, v in halo.items()},
             "iteration_algorithmic_GBps": round(
                 (EDGE_BYTES * E + VERTEX_BYTES * V) / (ms_step * 1e-3) / 1e9, 1),
         },

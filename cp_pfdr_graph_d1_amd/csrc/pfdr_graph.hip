@@ -123,6 +123,42 @@ void build_incidence(const int *dEu, const int *dEv, int V, long E,
     PFDR_HIP(hipStreamSynchronize(s));
 }
 
+// Keyed CSR: entry i has key = (row << 32) | order and value = address of
+// its contribution.  Rows >= V (non-owned slots, key ~0) sort last and are
+// ignored.  ptr[v] = first sorted position of row v.
+__global__ void k_keyed_ptr(const unsigned long long *__restrict__ skey, long n, int V,
+                            int *__restrict__ ptr) {
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    long kp = (i == 0) ? -1 : (long)min((unsigned long long)V, skey[i - 1] >> 32);
+    long kc = (i == n) ? (long)V : (long)min((unsigned long long)V, skey[i] >> 32);
+    for (long v = kp + 1; v <= kc; v++) ptr[v] = (int)i;
+}
+
+void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int V,
+                           Incidence &inc, hipStream_t s) {
+    inc.V = V;
+    inc.n = n;
+    inc.ptr.alloc((size_t)V + 1);
+    inc.idx.alloc((size_t)(n > 0 ? n : 1));
+    if (n == 0) {
+        PFDR_HIP(hipMemsetAsync(inc.ptr.p, 0, sizeof(int) * (V + 1), s));
+        return;
+    }
+    unsigned vbits = 1;
+    while (vbits < 31 && ((1ull << vbits) <= (unsigned long long)V)) vbits++;
+    DevBuf<unsigned long long> skey(n);
+    size_t tmp_bytes = 0;
+    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, skey.p, vals, inc.idx.p,
+                                       (size_t)n, 0, 32 + vbits + 1, s));
+    DevBuf<char> tmp(tmp_bytes > 0 ? tmp_bytes : 1);
+    PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, keys, skey.p, vals, inc.idx.p,
+                                       (size_t)n, 0, 32 + vbits + 1, s));
+    k_keyed_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey.p, n, V, inc.ptr.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
 }  // namespace pfdr
 
 // ===================================================================== //

@@ -18,4 +18,11 @@ void check_endpoints(const int *dEu, const int *dEv, long E, int V, hipStream_t 
 void build_incidence(const int *dEu, const int *dEv, int V, long E,
                      Incidence &inc, hipStream_t s);
 
+// Keyed CSR (quadratic solvers): n entries, key = (row << 32) | order
+// (order = 2 e_global + side, the reference's summation order), value =
+// address of the entry's contribution; rows >= V are dropped.  keys/vals
+// are consumed (sorted out of place, then may be freed).
+void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int V,
+                           Incidence &inc, hipStream_t s);
+
 }  // namespace pfdr

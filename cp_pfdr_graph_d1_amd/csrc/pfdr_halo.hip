@@ -1,0 +1,595 @@
+// Partition plan, halo exchanges and the two transports (see pfdr_halo.hpp).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+
+#include "pfdr_halo.hpp"
+
+namespace pfdr {
+
+// ------------------------------------------------------------- kernels --
+template <int B>
+__global__ void k_pack(int n, const int *__restrict__ idx, const char *__restrict__ src,
+                       char *__restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    struct alignas(B) Blk { char b[B]; };
+    reinterpret_cast<Blk *>(dst)[i] = reinterpret_cast<const Blk *>(src)[idx[i]];
+}
+
+template <int B>
+__global__ void k_pack_u(int n, const unsigned *__restrict__ idx, const char *__restrict__ src,
+                         char *__restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    struct alignas(B) Blk { char b[B]; };
+    reinterpret_cast<Blk *>(dst)[i] = reinterpret_cast<const Blk *>(src)[idx[i]];
+}
+
+static void pack(int n, const int *idx, const void *src, void *dst, int eb, hipStream_t s) {
+    if (n <= 0) return;
+    const int g = grid_for(n);
+    switch (eb) {
+        case 4: k_pack<4><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
+        case 8: k_pack<8><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
+        case 16: k_pack<16><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
+        default: throw std::runtime_error("pack: element size");
+    }
+    PFDR_HIP(hipGetLastError());
+}
+
+static void pack_u(int n, const unsigned *idx, const void *src, void *dst, int eb, hipStream_t s) {
+    if (n <= 0) return;
+    const int g = grid_for(n);
+    switch (eb) {
+        case 4: k_pack_u<4><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
+        case 8: k_pack_u<8><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
+        default: throw std::runtime_error("pack: element size");
+    }
+    PFDR_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------ Transport --
+void Transport::allgather_i64(int64_t mine, std::vector<int64_t> &all, hipStream_t s) {
+    all.assign(nranks, 0);
+    all[rank] = mine;
+    if (nranks == 1) return;
+    DevBuf<int64_t> d(nranks);
+    PFDR_HIP(hipMemsetAsync(d.p, 0, sizeof(int64_t) * nranks, s));
+    PFDR_HIP(hipMemcpyAsync(d.p + rank, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    allreduce_sum(d.p, nranks, 2, s);
+    PFDR_HIP(hipMemcpyAsync(all.data(), d.p, sizeof(int64_t) * nranks, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
+                               std::vector<std::vector<int64_t>> &recv, hipStream_t s) {
+    const int n = nranks;
+    recv.assign(n, {});
+    // counts: everyone learns how much each peer sends it (allreduce of an n x n matrix)
+    DevBuf<int64_t> cnt((size_t)n * n);
+    std::vector<int64_t> hc((size_t)n * n, 0);
+    for (int q = 0; q < n; q++) hc[(size_t)rank * n + q] = (int64_t)send[q].size();
+    PFDR_HIP(hipMemcpyAsync(cnt.p, hc.data(), sizeof(int64_t) * n * n, hipMemcpyHostToDevice, s));
+    allreduce_sum(cnt.p, n * n, 2, s);
+    PFDR_HIP(hipMemcpyAsync(hc.data(), cnt.p, sizeof(int64_t) * n * n, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    std::vector<DevBuf<int64_t>> ds(n), dr(n);
+    std::vector<const void *> sp(n, nullptr);
+    std::vector<void *> rp(n, nullptr);
+    std::vector<size_t> sb(n, 0), rb(n, 0);
+    for (int q = 0; q < n; q++) {
+        if (q == rank) continue;
+        if (!send[q].empty()) {
+            ds[q].alloc(send[q].size());
+            PFDR_HIP(hipMemcpyAsync(ds[q].p, send[q].data(), sizeof(int64_t) * send[q].size(),
+                                    hipMemcpyHostToDevice, s));
+            sp[q] = ds[q].p;
+            sb[q] = sizeof(int64_t) * send[q].size();
+        }
+        const int64_t m = hc[(size_t)q * n + rank];
+        if (m > 0) {
+            dr[q].alloc(m);
+            rp[q] = dr[q].p;
+            rb[q] = sizeof(int64_t) * m;
+        }
+    }
+    exchange(sp, sb, rp, rb, s);
+    for (int q = 0; q < n; q++) {
+        if (q == rank) { recv[q] = send[q]; continue; }
+        recv[q].resize(rb[q] / sizeof(int64_t));
+        if (rb[q])
+            PFDR_HIP(hipMemcpyAsync(recv[q].data(), dr[q].p, rb[q], hipMemcpyDeviceToHost, s));
+    }
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+// ----------------------------------------------------------------- RCCL --
+class RcclTransport final : public Transport {
+    ncclComm_t comm_;
+    static void ck(ncclResult_t r, const char *what) {
+        if (r != ncclSuccess) {
+            char m[256];
+            snprintf(m, sizeof m, "RCCL %s: %s", what, ncclGetErrorString(r));
+            throw std::runtime_error(m);
+        }
+    }
+
+  public:
+    RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) { nranks = n; rank = r; }
+    void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
+                  const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
+                  hipStream_t s) override {
+        ck(ncclGroupStart(), "group start");
+        for (int q = 0; q < nranks; q++) {
+            if (q == rank) continue;
+            if (sbytes[q]) ck(ncclSend(send[q], sbytes[q], ncclChar, q, comm_, s), "send");
+            if (rbytes[q]) ck(ncclRecv(recv[q], rbytes[q], ncclChar, q, comm_, s), "recv");
+        }
+        ck(ncclGroupEnd(), "group end");
+    }
+    void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
+        ncclDataType_t t = dtype == PFDR_F32 ? ncclFloat32 : dtype == PFDR_F64 ? ncclFloat64 : ncclInt64;
+        ck(ncclAllReduce(dev, dev, n, t, ncclSum, comm_, s), "allreduce");
+    }
+    void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
+        if (rank > 0) ck(ncclRecv(dev, bytes, ncclChar, rank - 1, comm_, s), "chain recv");
+    }
+    void chain_send(const void *dev, size_t bytes, hipStream_t s) override {
+        if (rank + 1 < nranks) ck(ncclSend(dev, bytes, ncclChar, rank + 1, comm_, s), "chain send");
+    }
+    void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
+        ck(ncclBroadcast(dev, dev, bytes, ncclChar, root, comm_, s), "broadcast");
+    }
+};
+
+std::unique_ptr<Transport> make_rccl_transport(void *comm, int n, int r) {
+    return std::unique_ptr<Transport>(new RcclTransport(comm, n, r));
+}
+
+// ------------------------------------------------------------- Loopback --
+struct LoopHub {
+    int k;
+    std::mutex m;
+    std::condition_variable cv;
+    int count = 0;
+    long gen = 0;
+    struct Post {
+        std::vector<const void *> send;
+        std::vector<size_t> sbytes;
+        const void *ptr = nullptr;
+        hipEvent_t ready = nullptr, done = nullptr, chain = nullptr;
+        long chain_seq = 0;
+    };
+    std::vector<Post> post;
+    explicit LoopHub(int n) : k(n), post(n) {}
+    ~LoopHub() {
+        for (auto &p : post) {
+            if (p.ready) (void)hipEventDestroy(p.ready);
+            if (p.done) (void)hipEventDestroy(p.done);
+            if (p.chain) (void)hipEventDestroy(p.chain);
+        }
+    }
+    void barrier() {
+        std::unique_lock<std::mutex> l(m);
+        const long g = gen;
+        if (++count == k) {
+            count = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(l, [&] { return gen != g; });
+        }
+    }
+};
+
+template <typename T>
+__global__ void k_sum_ranks(int n, int k, const T *const *src, T *dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    T s = src[0][i];
+    for (int r = 1; r < k; r++) s += src[r][i];  // rank order: same result on every rank
+    dst[i] = s;
+}
+
+class LoopbackTransport final : public Transport {
+    LoopHub *hub_;
+    void ensure_events() {
+        auto &p = hub_->post[rank];
+        if (!p.ready) {
+            PFDR_HIP(hipEventCreateWithFlags(&p.ready, hipEventDisableTiming));
+            PFDR_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+            PFDR_HIP(hipEventCreateWithFlags(&p.chain, hipEventDisableTiming));
+        }
+    }
+
+  public:
+    LoopbackTransport(void *hub, int n, int r) : hub_((LoopHub *)hub) {
+        nranks = n;
+        rank = r;
+        if (hub_->k != n) throw std::runtime_error("loopback hub size differs from nranks");
+    }
+    void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
+                  const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
+                  hipStream_t s) override {
+        ensure_events();
+        auto &me = hub_->post[rank];
+        me.send = send;
+        me.sbytes = sbytes;
+        PFDR_HIP(hipEventRecord(me.ready, s));
+        hub_->barrier();
+        for (int q = 0; q < nranks; q++) {
+            if (q == rank || !rbytes[q]) continue;
+            auto &pq = hub_->post[q];
+            if (pq.sbytes[rank] != rbytes[q]) throw std::runtime_error("loopback exchange size mismatch");
+            PFDR_HIP(hipStreamWaitEvent(s, pq.ready, 0));
+            PFDR_HIP(hipMemcpyAsync(recv[q], pq.send[rank], rbytes[q], hipMemcpyDeviceToDevice, s));
+        }
+        PFDR_HIP(hipEventRecord(me.done, s));
+        hub_->barrier();
+        for (int q = 0; q < nranks; q++)
+            if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].done, 0));
+        hub_->barrier();  // nobody re-records `done` before every wait is enqueued
+    }
+    void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
+        ensure_events();
+        auto &me = hub_->post[rank];
+        me.ptr = dev;
+        PFDR_HIP(hipEventRecord(me.ready, s));
+        hub_->barrier();
+        for (int q = 0; q < nranks; q++)
+            if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].ready, 0));
+        const size_t eb = dtype == PFDR_F32 ? 4 : 8;
+        DevBuf<char> tmp((size_t)n * eb);
+        DevBuf<const void *> ptrs(nranks);
+        std::vector<const void *> hp(nranks);
+        for (int q = 0; q < nranks; q++) hp[q] = hub_->post[q].ptr;
+        PFDR_HIP(hipMemcpyAsync(ptrs.p, hp.data(), sizeof(void *) * nranks, hipMemcpyHostToDevice, s));
+        const int g = grid_for(n);
+        if (dtype == PFDR_F32)
+            k_sum_ranks<float><<<g, kBlock, 0, s>>>(n, nranks, (const float *const *)ptrs.p, (float *)tmp.p);
+        else if (dtype == PFDR_F64)
+            k_sum_ranks<double><<<g, kBlock, 0, s>>>(n, nranks, (const double *const *)ptrs.p, (double *)tmp.p);
+        else
+            k_sum_ranks<long long><<<g, kBlock, 0, s>>>(n, nranks, (const long long *const *)ptrs.p,
+                                                         (long long *)tmp.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipEventRecord(me.done, s));
+        hub_->barrier();
+        for (int q = 0; q < nranks; q++)
+            if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].done, 0));
+        PFDR_HIP(hipMemcpyAsync(dev, tmp.p, (size_t)n * eb, hipMemcpyDeviceToDevice, s));
+        PFDR_HIP(hipStreamSynchronize(s));  // tmp / ptrs die here
+        hub_->barrier();
+    }
+    void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
+        ensure_events();
+        if (rank == 0) return;
+        auto &prev = hub_->post[rank - 1];
+        auto &me = hub_->post[rank];
+        {
+            std::unique_lock<std::mutex> l(hub_->m);
+            hub_->cv.wait(l, [&] { return prev.chain_seq > me.chain_seq; });
+        }
+        PFDR_HIP(hipStreamWaitEvent(s, prev.chain, 0));
+        PFDR_HIP(hipMemcpyAsync(dev, prev.ptr, bytes, hipMemcpyDeviceToDevice, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+    void chain_send(const void *dev, size_t bytes, hipStream_t s) override {
+        ensure_events();
+        auto &me = hub_->post[rank];
+        (void)bytes;
+        if (rank + 1 < nranks) {
+            PFDR_HIP(hipEventRecord(me.chain, s));
+            PFDR_HIP(hipStreamSynchronize(s));
+            std::unique_lock<std::mutex> l(hub_->m);
+            me.ptr = dev;
+            me.chain_seq++;
+            hub_->cv.notify_all();
+        } else {
+            std::unique_lock<std::mutex> l(hub_->m);
+            me.chain_seq++;
+        }
+        hub_->barrier();  // keep dev alive until the successor copied it
+    }
+    void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
+        ensure_events();
+        auto &me = hub_->post[rank];
+        if (rank == root) {
+            me.ptr = dev;
+            PFDR_HIP(hipEventRecord(me.ready, s));
+        }
+        hub_->barrier();
+        if (rank != root) {
+            PFDR_HIP(hipStreamWaitEvent(s, hub_->post[root].ready, 0));
+            PFDR_HIP(hipMemcpyAsync(dev, hub_->post[root].ptr, bytes, hipMemcpyDeviceToDevice, s));
+        }
+        PFDR_HIP(hipStreamSynchronize(s));
+        hub_->barrier();
+    }
+};
+
+std::unique_ptr<Transport> make_loopback_transport(void *hub, int n, int r) {
+    return std::unique_ptr<Transport>(new LoopbackTransport(hub, n, r));
+}
+
+// ------------------------------------------------------------------ Halo --
+void Halo::pull(void *base, int eb, hipStream_t s) {
+    const int n = tr->nranks;
+    const int tot = pull_send_off[n];
+    if ((size_t)tot * eb > sendbuf.n) sendbuf.alloc((size_t)tot * eb);
+    pack(tot, pull_idx.p, base, sendbuf.p, eb, s);
+    std::vector<const void *> sp(n);
+    std::vector<void *> rp(n);
+    std::vector<size_t> sb(n), rb(n);
+    for (int q = 0; q < n; q++) {
+        sp[q] = sendbuf.p + (size_t)pull_send_off[q] * eb;
+        sb[q] = (size_t)pull_send_cnt[q] * eb;
+        rp[q] = (char *)base + ((size_t)V + ghost_off[q]) * eb;
+        rb[q] = (size_t)ghost_cnt[q] * eb;
+    }
+    tr->exchange(sp, sb, rp, rb, s);
+}
+
+void Halo::push(const void *wz, void *tail, int eb, hipStream_t s) {
+    const int n = tr->nranks;
+    const int tot = push_send_off[n];
+    if ((size_t)tot * eb > sendbuf.n) sendbuf.alloc((size_t)tot * eb);
+    pack_u(tot, push_addr.p, wz, sendbuf.p, eb, s);
+    std::vector<const void *> sp(n);
+    std::vector<void *> rp(n);
+    std::vector<size_t> sb(n), rb(n);
+    for (int q = 0; q < n; q++) {
+        sp[q] = sendbuf.p + (size_t)push_send_off[q] * eb;
+        sb[q] = (size_t)push_send_cnt[q] * eb;
+        rp[q] = (char *)tail + (size_t)push_recv_off[q] * eb;
+        rb[q] = (size_t)push_recv_cnt[q] * eb;
+    }
+    tr->exchange(sp, sb, rp, rb, s);
+}
+
+void plan_local(PlanHost &p, int nranks, int rank, const int64_t *off, long E, const int *Eu_g,
+                const int *Ev_g, const int64_t *e_global, int64_t e_offset) {
+    const int n = nranks;
+    p.nranks = n;
+    p.rank = rank;
+    p.E = E;
+    p.off.assign(off, off + n + 1);
+    for (int q = 0; q < n; q++)
+        if (p.off[q + 1] < p.off[q]) throw std::runtime_error("partition: offsets must increase");
+    p.lo = p.off[rank];
+    p.hi = p.off[rank + 1];
+    p.V = (int)(p.hi - p.lo);
+    const int64_t lo = p.lo, hi = p.hi, Vglob = p.off[n];
+    auto owner = [&](int64_t g) {
+        return (int)(std::upper_bound(p.off.begin(), p.off.end(), g) - p.off.begin()) - 1;
+    };
+    // ghosts: endpoints outside the owned range, sorted (hence grouped by owner)
+    std::vector<int64_t> &ghosts = p.ghosts;
+    ghosts.clear();
+    for (long e = 0; e < E; e++) {
+        const int64_t u = Eu_g[e], v = Ev_g[e];
+        if (u < 0 || u >= Vglob || v < 0 || v >= Vglob)
+            throw std::runtime_error("partition: edge endpoint outside [0, V_global)");
+        if (u < lo || u >= hi) ghosts.push_back(u);
+        if (v < lo || v >= hi) ghosts.push_back(v);
+    }
+    std::sort(ghosts.begin(), ghosts.end());
+    ghosts.erase(std::unique(ghosts.begin(), ghosts.end()), ghosts.end());
+    p.ghost_cnt.assign(n, 0);
+    for (int64_t g : ghosts) p.ghost_cnt[owner(g)]++;
+    p.ghost_off.assign(n + 1, 0);
+    for (int q = 0; q < n; q++) p.ghost_off[q + 1] = p.ghost_off[q] + p.ghost_cnt[q];
+    const int V = p.V;
+    auto local = [&](int64_t g) -> int {
+        if (g >= lo && g < hi) return (int)(g - lo);
+        return V + (int)(std::lower_bound(ghosts.begin(), ghosts.end(), g) - ghosts.begin());
+    };
+    p.Eu_l.resize(E);
+    p.Ev_l.resize(E);
+    p.req.assign(n, {});
+    p.items.assign(n, {});
+    p.addr.assign(n, {});
+    for (int q = 0; q < n; q++)
+        p.req[q].assign(ghosts.begin() + p.ghost_off[q], ghosts.begin() + p.ghost_off[q + 1]);
+    for (long e = 0; e < E; e++) {
+        const int64_t eg = e_global ? e_global[e] : e_offset + e;
+        if (eg < 0 || 2 * eg + 1 > 0xffffffffLL)
+            throw std::runtime_error("partition: global edge ids must lie in [0, 2^31)");
+        for (int side = 0; side < 2; side++) {
+            const int64_t g = side ? Ev_g[e] : Eu_g[e];
+            const int l = local(g);
+            (side ? p.Ev_l : p.Eu_l)[e] = l;
+            if (l >= V) {
+                const int q = owner(g);
+                p.items[q].push_back(g);
+                p.items[q].push_back(2 * eg + side);
+                p.addr[q].push_back((unsigned)(side * E + e));
+            }
+        }
+    }
+}
+
+void plan_finish(PlanHost &p, const std::vector<std::vector<int64_t>> &inreq,
+                 const std::vector<std::vector<int64_t>> &initems) {
+    const int n = p.nranks, me = p.rank;
+    const int64_t lo = p.lo, hi = p.hi;
+    p.pull_send_cnt.assign(n, 0);
+    p.pull_send_off.assign(n + 1, 0);
+    p.pull_idx.clear();
+    for (int q = 0; q < n; q++) {
+        if (q != me) {
+            for (int64_t g : inreq[q]) {
+                if (g < lo || g >= hi) throw std::runtime_error("partition: bad pull request");
+                p.pull_idx.push_back((int)(g - lo));
+            }
+            p.pull_send_cnt[q] = (int)inreq[q].size();
+        }
+        p.pull_send_off[q + 1] = p.pull_send_off[q] + p.pull_send_cnt[q];
+    }
+    p.push_send_cnt.assign(n, 0);
+    p.push_send_off.assign(n + 1, 0);
+    p.push_addr.clear();
+    for (int q = 0; q < n; q++) {
+        p.push_send_cnt[q] = (int)p.addr[q].size();
+        p.push_send_off[q + 1] = p.push_send_off[q] + p.push_send_cnt[q];
+        p.push_addr.insert(p.push_addr.end(), p.addr[q].begin(), p.addr[q].end());
+    }
+    p.push_recv_cnt.assign(n, 0);
+    p.push_recv_off.assign(n + 1, 0);
+    p.recv_keys.clear();
+    for (int q = 0; q < n; q++) {
+        if (q != me) {
+            const auto &it = initems[q];
+            for (size_t j = 0; j + 1 < it.size(); j += 2) {
+                const int64_t g = it[j];
+                if (g < lo || g >= hi) throw std::runtime_error("partition: bad push item");
+                p.recv_keys.push_back(((unsigned long long)(g - lo) << 32) |
+                                      (unsigned long long)it[j + 1]);
+            }
+            p.push_recv_cnt[q] = (int)(it.size() / 2);
+        }
+        p.push_recv_off[q + 1] = p.push_recv_off[q] + p.push_recv_cnt[q];
+    }
+}
+
+void build_halo(Halo &h, int V, int64_t vtx_begin, long E, const int *Eu_g, const int *Ev_g,
+                const int64_t *e_global, int64_t e_offset, std::vector<int> &Eu_l,
+                std::vector<int> &Ev_l, hipStream_t s) {
+    Transport &tr = *h.tr;
+    const int n = tr.nranks, me = tr.rank;
+    // global offsets (rank order must be vertex order)
+    std::vector<int64_t> cnt;
+    tr.allgather_i64(V, cnt, s);
+    std::vector<int64_t> off(n + 1, 0);
+    for (int q = 0; q < n; q++) off[q + 1] = off[q] + cnt[q];
+    if (off[me] != vtx_begin)
+        throw std::runtime_error("partition: vtx_begin must equal the sum of V over lower ranks");
+    PlanHost p;
+    plan_local(p, n, me, off.data(), E, Eu_g, Ev_g, e_global, e_offset);
+    std::vector<std::vector<int64_t>> inreq, initems;
+    tr.alltoallv_host(p.req, inreq, s);
+    tr.alltoallv_host(p.items, initems, s);
+    plan_finish(p, inreq, initems);
+    h.V = V;
+    h.E = E;
+    h.vtx_begin = vtx_begin;
+    h.off = off;
+    h.G = (int)p.ghosts.size();
+    h.ghost_cnt = p.ghost_cnt;
+    h.ghost_off = p.ghost_off;
+    h.pull_send_cnt = p.pull_send_cnt;
+    h.pull_send_off = p.pull_send_off;
+    h.push_send_cnt = p.push_send_cnt;
+    h.push_send_off = p.push_send_off;
+    h.push_recv_cnt = p.push_recv_cnt;
+    h.push_recv_off = p.push_recv_off;
+    h.R = (long)p.recv_keys.size();
+    h.pull_idx.alloc(p.pull_idx.size() ? p.pull_idx.size() : 1);
+    if (!p.pull_idx.empty())
+        PFDR_HIP(hipMemcpyAsync(h.pull_idx.p, p.pull_idx.data(), sizeof(int) * p.pull_idx.size(),
+                                hipMemcpyHostToDevice, s));
+    h.push_addr.alloc(p.push_addr.size() ? p.push_addr.size() : 1);
+    if (!p.push_addr.empty())
+        PFDR_HIP(hipMemcpyAsync(h.push_addr.p, p.push_addr.data(),
+                                sizeof(unsigned) * p.push_addr.size(), hipMemcpyHostToDevice, s));
+    h.recv_keys.alloc(p.recv_keys.size() ? p.recv_keys.size() : 1);
+    if (!p.recv_keys.empty())
+        PFDR_HIP(hipMemcpyAsync(h.recv_keys.p, p.recv_keys.data(),
+                                sizeof(unsigned long long) * p.recv_keys.size(),
+                                hipMemcpyHostToDevice, s));
+    Eu_l.swap(p.Eu_l);
+    Ev_l.swap(p.Ev_l);
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace pfdr
+
+extern "C" int pfdr_loopback_create(void **hub_out, int nranks) {
+    if (!hub_out || nranks < 1 || nranks > 64)
+        return pfdr::report_error("pfdr_loopback_create", "invalid arguments");
+    *hub_out = new pfdr::LoopHub(nranks);
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_loopback_destroy(void *hub) {
+    delete (pfdr::LoopHub *)hub;
+    return PFDR_OK;
+}
+
+// ---------------------------------------------- host planner (C ABI) --
+struct pfdr_plan {
+    pfdr::PlanHost p;
+    std::vector<std::vector<int64_t>> inreq, initems;
+};
+
+extern "C" int pfdr_plan_create(pfdr_plan **out, int nranks, int rank, const int64_t *offsets,
+                                int E, const int *Eu, const int *Ev, const int64_t *e_global,
+                                int64_t e_offset) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || !offsets || E < 0 ||
+        (E > 0 && (!Eu || !Ev)))
+        return pfdr::report_error("pfdr_plan_create", "invalid arguments");
+    try {
+        pfdr_plan *pl = new pfdr_plan();
+        pfdr::plan_local(pl->p, nranks, rank, offsets, E, Eu, Ev, e_global, e_offset);
+        pl->inreq.assign(nranks, {});
+        pl->initems.assign(nranks, {});
+        *out = pl;
+    } catch (const std::exception &ex) {
+        return pfdr::report_error("pfdr_plan_create", ex.what());
+    }
+    return PFDR_OK;
+}
+
+template <typename T>
+static int64_t copy_out(const std::vector<T> &v, void *out) {
+    if (out && !v.empty()) memcpy(out, v.data(), v.size() * sizeof(T));
+    return (int64_t)v.size();
+}
+
+extern "C" int64_t pfdr_plan_get(pfdr_plan *pl, int what, int peer, void *out) {
+    if (!pl) return -1;
+    const auto &p = pl->p;
+    if (peer < 0 || peer >= p.nranks) peer = 0;
+    switch (what) {
+        case PFDR_PLAN_GHOSTS: return copy_out(p.ghosts, out);
+        case PFDR_PLAN_EU_LOCAL: return copy_out(p.Eu_l, out);
+        case PFDR_PLAN_EV_LOCAL: return copy_out(p.Ev_l, out);
+        case PFDR_PLAN_PULL_REQUEST: return copy_out(p.req[peer], out);
+        case PFDR_PLAN_PUSH_ITEMS: return copy_out(p.items[peer], out);
+        case PFDR_PLAN_PUSH_ADDR: return copy_out(p.push_addr, out);
+        case PFDR_PLAN_PULL_INDEX: return copy_out(p.pull_idx, out);
+        case PFDR_PLAN_RECV_KEYS: return copy_out(p.recv_keys, out);
+        case PFDR_PLAN_GHOST_OFFSETS: return copy_out(p.ghost_off, out);
+        case PFDR_PLAN_PULL_OFFSETS: return copy_out(p.pull_send_off, out);
+        case PFDR_PLAN_PUSH_OFFSETS: return copy_out(p.push_send_off, out);
+        case PFDR_PLAN_RECV_OFFSETS: return copy_out(p.push_recv_off, out);
+        default: return -1;
+    }
+}
+
+extern "C" int pfdr_plan_set_incoming(pfdr_plan *pl, int peer, int what, int64_t n,
+                                      const int64_t *data) {
+    if (!pl || peer < 0 || peer >= pl->p.nranks || n < 0 || (n > 0 && !data))
+        return pfdr::report_error("pfdr_plan_set_incoming", "invalid arguments");
+    if (what == PFDR_PLAN_PULL_REQUEST) pl->inreq[peer].assign(data, data + n);
+    else if (what == PFDR_PLAN_PUSH_ITEMS) pl->initems[peer].assign(data, data + n);
+    else return pfdr::report_error("pfdr_plan_set_incoming", "what must be PULL_REQUEST or PUSH_ITEMS");
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_plan_finish(pfdr_plan *pl) {
+    if (!pl) return pfdr::report_error("pfdr_plan_finish", "null plan");
+    try {
+        pfdr::plan_finish(pl->p, pl->inreq, pl->initems);
+    } catch (const std::exception &ex) {
+        return pfdr::report_error("pfdr_plan_finish", ex.what());
+    }
+    return PFDR_OK;
+}
+
+extern "C" void pfdr_plan_destroy(pfdr_plan *pl) { delete pl; }

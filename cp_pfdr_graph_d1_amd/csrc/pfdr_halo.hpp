@@ -1,0 +1,117 @@
+// 1-D vertex-range partition of a PFDR graph across ranks (one GPU each),
+// SURVEY.md §8(e):
+//
+//   rank r owns the global vertices [off[r], off[r+1]) and the edges it was
+//   handed (normally those whose Eu it owns).  Per iteration:
+//     pull  : owners send (X, P) of their boundary vertices to the ranks that
+//             hold edges touching them (ghost copies), before the edge sweep;
+//     push  : each rank sends the DR contributions W*Z of edge ends whose
+//             vertex it does not own to that vertex's owner, after the edge
+//             sweep; the owner sums them in GLOBAL edge order, exactly where
+//             the single-GPU (and reference) summation puts them;
+//     reduce: iterate-evolution / objective partials (2-3 scalars).
+//   The preconditioner's amplitude c is a sequential sum in global vertex
+//   order, carried rank to rank (chain), so every rank gets the single-GPU c.
+//
+// Transport = RCCL (one process per GPU, grouped ncclSend/ncclRecv over
+// xGMI) or Loopback (k ranks as k host threads on one device, exchanges as
+// device-to-device copies) — the latter lets the whole partitioned path be
+// tested on one GPU against the unpartitioned solver.
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "pfdr_dev.hpp"
+
+namespace pfdr {
+
+class Transport {
+  public:
+    int nranks = 1, rank = 0;
+    virtual ~Transport() = default;
+    // point-to-point exchange with every peer (entries for this rank and
+    // zero sizes are skipped); enqueued on s
+    virtual void exchange(const std::vector<const void *> &send,
+                          const std::vector<size_t> &sbytes,
+                          const std::vector<void *> &recv,
+                          const std::vector<size_t> &rbytes, hipStream_t s) = 0;
+    // in-place sum over ranks of n values of dtype (PFDR_F32 / PFDR_F64) or
+    // int64 (dtype = 2), device memory
+    virtual void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) = 0;
+    // receive `bytes` from rank-1 into dev (rank 0: nothing)
+    virtual void chain_recv(void *dev, size_t bytes, hipStream_t s) = 0;
+    // send `bytes` from dev to rank+1 (last rank: nothing)
+    virtual void chain_send(const void *dev, size_t bytes, hipStream_t s) = 0;
+    virtual void broadcast(void *dev, size_t bytes, int root, hipStream_t s) = 0;
+    // host-level allgather of one int64 per rank (setup only)
+    void allgather_i64(int64_t mine, std::vector<int64_t> &all, hipStream_t s);
+    // variable-size all-to-all of host arrays (setup only)
+    void alltoallv_host(const std::vector<std::vector<int64_t>> &send,
+                        std::vector<std::vector<int64_t>> &recv, hipStream_t s);
+};
+
+std::unique_ptr<Transport> make_rccl_transport(void *comm, int nranks, int rank);
+std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
+
+// Partition plan of one rank plus its device-side exchange buffers.
+struct Halo {
+    std::unique_ptr<Transport> tr;
+    int V = 0;              // owned vertices (local ids [0, V))
+    int G = 0;              // ghost vertices (local ids [V, V + G)), grouped by owner
+    long E = 0;             // local edges
+    int64_t vtx_begin = 0;
+    std::vector<int64_t> off;          // nranks + 1 global vertex offsets
+    // pull: (X, P) of owned vertices to peers / into the ghost range
+    std::vector<int> pull_send_cnt, pull_send_off;  // per peer, into pull_idx
+    std::vector<int> ghost_cnt, ghost_off;          // per peer, into [V, V + G)
+    DevBuf<int> pull_idx;                           // owned local ids to send
+    // push: contributions of ghost-vertex slots to their owners
+    std::vector<int> push_send_cnt, push_send_off;  // per peer, into push_addr
+    std::vector<int> push_recv_cnt, push_recv_off;  // per peer, into the tail
+    long R = 0;                                     // received contributions
+    DevBuf<unsigned> push_addr;                     // local contribution addresses
+    // CSR keys of the received slots: (owned local vertex, 2 e_global + side)
+    DevBuf<unsigned long long> recv_keys;
+    // scratch send buffer (bytes)
+    DevBuf<char> sendbuf;
+
+    // gather elem-sized values at idx into sendbuf, exchange, land the
+    // peers' values in base + V (ghost range) — base holds Vg elements
+    void pull(void *base, int elem_bytes, hipStream_t s);
+    // contributions: gather wz[push_addr] (real) and land the peers' in tail
+    void push(const void *wz, void *tail, int elem_bytes, hipStream_t s);
+};
+
+// Host-only planning (no device needed; also exported through the C ABI so
+// the partition logic is testable on CPU with any transport).
+struct PlanHost {
+    int nranks = 1, rank = 0, V = 0;
+    long E = 0;
+    int64_t lo = 0, hi = 0;
+    std::vector<int64_t> off;                 // nranks + 1
+    std::vector<int64_t> ghosts;              // sorted global ids
+    std::vector<int> ghost_cnt, ghost_off;
+    std::vector<int> Eu_l, Ev_l;              // rank-local endpoint ids
+    std::vector<std::vector<int64_t>> req;    // pull requests to each owner (global ids)
+    std::vector<std::vector<int64_t>> items;  // push items to each owner: (g, 2 eg + side) pairs
+    std::vector<std::vector<unsigned>> addr;  // my contribution address of each item
+    // filled by plan_finish
+    std::vector<int> pull_idx, pull_send_cnt, pull_send_off;
+    std::vector<unsigned> push_addr;
+    std::vector<int> push_send_cnt, push_send_off, push_recv_cnt, push_recv_off;
+    std::vector<unsigned long long> recv_keys;
+};
+void plan_local(PlanHost &p, int nranks, int rank, const int64_t *off, long E, const int *Eu_g,
+                const int *Ev_g, const int64_t *e_global, int64_t e_offset);
+// inreq[q] / initems[q]: what peer q sent us (its req[rank] / items[rank])
+void plan_finish(PlanHost &p, const std::vector<std::vector<int64_t>> &inreq,
+                 const std::vector<std::vector<int64_t>> &initems);
+
+// Build the plan of this rank from its local edges (global endpoint ids and
+// global edge ids, host arrays), exchanging request lists with the peers.
+// Writes the rank-local endpoint ids (owned [0, V), ghosts [V, V + G)).
+void build_halo(Halo &h, int V, int64_t vtx_begin, long E, const int *Eu_g,
+                const int *Ev_g, const int64_t *e_global, int64_t e_offset,
+                std::vector<int> &Eu_l, std::vector<int> &Ev_l, hipStream_t s);
+
+}  // namespace pfdr

@@ -1,0 +1,851 @@
+// MI355X PFDR solver for
+//     F(x) = 1/2 ||y - A x||^2 + sum_e la_e |x_u - x_v| + sum_v la_v |x_v|
+//            (+ x >= 0)                              [flavour l1]
+//     F(x) = 1/2 ||y - A x||^2 + sum_e la_e |x_u - x_v| + i_[min,max](x)
+//                                                    [flavour bounds]
+// by preconditioned forward-Douglas-Rachford splitting, the algorithm of
+// reference src/PFDR_graph_quadratic_d1_l1.cpp:270-553 and
+// src/PFDR_graph_quadratic_d1_bounds.cpp:244-530, re-designed for gfx950:
+//
+//   per iteration (identity / diagonal A):
+//     k_edge_sweep   : TV prox of every edge + relaxed Z update + the two
+//                      DR contributions W*Z (one fused, fully coalesced
+//                      sweep over the edge arrays; (X, P) of both endpoints
+//                      gathered as one 8/16-byte pair)          ref :466-489
+//     k_vertex_sweep : ordered segmented DR average over the incidence CSR
+//                      (replaces the serial scatter :491-497), l1 / box
+//                      prox, iterate-evolution partials, and the NEXT
+//                      forward step P = 2X - Ga (A X - Y)      ref :491-529,
+//                                                                  :355-464
+//     k_finalize     : (only when dif is tracked / Obj recorded) evolution,
+//                      stop / recondition flags in device memory
+//   dense A adds a column-dot GEMV pair (N > 0) or one symmetric GEMV
+//   (N < 0) producing the forward step; they are HBM bound (M = 1), so they
+//   stream A with 16-byte loads instead of using MFMA.
+//
+// Arithmetic is written operation-for-operation as the reference and the
+// library is built with -ffp-contract=off, so the per-edge and per-vertex
+// updates round identically to it; the per-vertex sums run in the
+// reference's order (incidence CSR sorted by (e, side)).  Reductions (dif,
+// Obj, dense dot products) use fixed-shape trees.
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+
+#include "pfdr_graph.hpp"
+#include "pfdr_session.hpp"
+
+namespace pfdr {
+
+enum AMode : int { A_IDENT = 0, A_DIAG = 1, A_DIRECT = 2, A_ATA = 3 };
+enum Prox : int { PROX_NONE = 0, PROX_L1 = 1, PROX_POS = 2, PROX_BOX = 3,
+                  PROX_LO = 4, PROX_HI = 5 };
+// launch gates evaluated from the device control block
+enum Gate : int { GATE_NONE = 0, GATE_ACTIVE = 1, GATE_OBJ = 2,
+                  GATE_ACTIVE_OR_OBJ = 3 };
+
+template <typename real> using R2 = typename Vec<real>::v2;
+
+template <typename T, int N>
+struct alignas(sizeof(T) * N) Pk { T v[N]; };
+
+template <typename T, int N>
+__device__ __forceinline__ Pk<T, N> ldv(const T *p) {
+    return *reinterpret_cast<const Pk<T, N> *>(p);
+}
+template <typename T, int N>
+__device__ __forceinline__ void stv(T *p, const Pk<T, N> &x) {
+    *reinterpret_cast<Pk<T, N> *>(p) = x;
+}
+
+template <typename real>
+__device__ __forceinline__ bool gated(const Ctrl<real> *c, int gate) {
+    if (!c || gate == GATE_NONE) return false;
+    const bool halt = c->halt != 0;
+    const bool objdone = c->obj_it >= c->it;
+    if (gate == GATE_ACTIVE) return halt;
+    if (gate == GATE_OBJ) return objdone;
+    return halt && objdone;
+}
+
+// Ordered sum over the incidence CSR of the block's vertices.  The entries
+// of the block's contiguous vertex range (idx = address of each
+// contribution) are gathered cooperatively — all lanes busy whatever the
+// degrees, coalesced index reads, GB index loads then GB value gathers in
+// flight per lane — into LDS chunks; then each lane adds its own vertex's
+// entries in CSR order, i.e. in the reference's order (e, side).
+template <typename real, int CAP, int GB = 16>
+__device__ __forceinline__ real gather_sum(int V, int v0,
+                                           const int *__restrict__ ptr,
+                                           const unsigned *__restrict__ idx,
+                                           const real *__restrict__ wz,
+                                           real *lds) {
+    static_assert(CAP % (kBlock * GB) == 0, "chunk must be a whole batch");
+    const int tid = threadIdx.x;
+    const int v = v0 + tid;
+    const int vend = min(v0 + kBlock, V);
+    const long seg0 = ptr[v0], seg1 = ptr[vend];
+    const long my0 = (v < V) ? (long)ptr[v] : seg1;
+    const long my1 = (v < V) ? (long)ptr[v + 1] : seg1;
+    real s = real(0);
+    for (long c0 = seg0; c0 < seg1; c0 += CAP) {
+        const int n = (int)min((long)CAP, seg1 - c0);
+        for (int b = 0; b < n; b += kBlock * GB) {
+            unsigned id[GB];
+#pragma unroll
+            for (int u = 0; u < GB; u++) {
+                const int j = b + u * kBlock + tid;
+                id[u] = (j < n) ? idx[c0 + j] : 0u;
+            }
+            real w[GB];
+#pragma unroll
+            for (int u = 0; u < GB; u++) {
+                const int j = b + u * kBlock + tid;
+                w[u] = (j < n) ? wz[id[u]] : real(0);
+            }
+#pragma unroll
+            for (int u = 0; u < GB; u++) {
+                const int j = b + u * kBlock + tid;
+                if (j < n) lds[j] = w[u];
+            }
+        }
+        __syncthreads();
+        const long a = max(my0, c0), e = min(my1, c0 + (long)n);
+        for (long j = a; j < e; j++) s += lds[j - c0];
+        __syncthreads();
+    }
+    return s;
+}
+
+template <typename real> struct GatherCap;
+template <> struct GatherCap<float> { static constexpr int v = 4096; };
+template <> struct GatherCap<double> { static constexpr int v = 4096; };
+
+// ====================================================================== //
+//                                kernels                                  //
+// ====================================================================== //
+
+template <typename real>
+__global__ void k_xp_init(int V, const real *__restrict__ X, R2<real> *xp) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    R2<real> o;
+    o.x = X[v];
+    o.y = real(0);
+    xp[v] = o;
+}
+
+template <typename real>
+__global__ void k_x_extract(int V, const R2<real> *__restrict__ xp,
+                            real *__restrict__ X) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) X[v] = xp[v].x;
+}
+
+// Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324); half-edge layout Z2[2e + side]
+template <typename real>
+__global__ void k_z_init(long E, const int *__restrict__ Eu,
+                         const int *__restrict__ Ev,
+                         const R2<real> *__restrict__ xp,
+                         real *__restrict__ Z2) {
+    long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    Z2[2 * e] = xp[Eu[e]].x;
+    Z2[2 * e + 1] = xp[Ev[e]].x;
+}
+
+// diagonal of A^t A for the identity / diagonal / A^tA modes (ref :101-122)
+template <typename real>
+__global__ void k_diag(int V, int mode, const real *__restrict__ A,
+                       real *__restrict__ diag) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    real d = real(1);
+    if (mode == A_DIAG) d = A[v];
+    else if (mode == A_ATA) d = A[(size_t)(V + 1) * v];
+    diag[v] = d;
+}
+
+// --------------------------------------------------- dense column dots --
+enum ColEpi : int { EPI_STORE = 0, EPI_SELF = 1, EPI_DIV = 2,
+                    EPI_FWD_DIRECT = 3, EPI_FWD_ATA = 4,
+                    EPI_GRAD_DIRECT = 5, EPI_GRAD_ATA = 6 };
+
+template <typename real>
+struct ColArgs {
+    const real *A;        // column major, column c at A + len*c
+    int ncols, len;
+    const real *w;        // vector dotted with every column (len)
+    real *out;            // STORE/SELF/DIV/GRAD_*
+    const real *div;      // DIV
+    R2<real> *xp;         // FWD_*
+    const real *Ga, *Y;   // FWD_*, GRAD_ATA
+    const Ctrl<real> *ctrl;
+    int gate;
+};
+
+// One wave64 per column: 16-byte loads of the column (and of w, which
+// every wave re-reads from L2), wave-shuffle reduction, fused epilogue.
+// ref: diag of A^tA :102-110, pseudo-inverse :126-134, apply A^tA
+// :368-376, gradient -A^t R :432-440, forward :462-464.
+template <typename real, int EPI>
+__global__ __launch_bounds__(256) void k_col_dot(ColArgs<real> a) {
+    if (gated(a.ctrl, a.gate)) return;
+    const int lane = threadIdx.x & 63;
+    const long col = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (col >= a.ncols) return;
+    const real *c = a.A + (size_t)a.len * col;
+    const real *w = (EPI == EPI_SELF) ? c : a.w;
+    constexpr int VW = Vec<real>::kPer16B;
+    real acc = real(0);
+    if ((a.len % VW) == 0) {
+        const int nv = a.len / VW;
+        for (int i = lane; i < nv; i += 64) {
+            Pk<real, VW> x = ldv<real, VW>(c + (size_t)i * VW);
+            Pk<real, VW> y = ldv<real, VW>(w + (size_t)i * VW);
+#pragma unroll
+            for (int j = 0; j < VW; j++) acc += x.v[j] * y.v[j];
+        }
+    } else {
+        for (int i = lane; i < a.len; i += 64) acc += c[i] * w[i];
+    }
+    acc = wave_sum(acc);
+    if (lane != 0) return;
+    if (EPI == EPI_STORE || EPI == EPI_SELF) {
+        a.out[col] = acc;
+    } else if (EPI == EPI_DIV) {
+        a.out[col] = acc / a.div[col];
+    } else if (EPI == EPI_GRAD_DIRECT) {
+        a.out[col] = -acc;
+    } else if (EPI == EPI_GRAD_ATA) {
+        real p = acc;
+        p -= a.Y[col];
+        a.out[col] = p;
+    } else {
+        real p;
+        if (EPI == EPI_FWD_DIRECT) {
+            p = -acc;
+        } else {
+            p = acc;
+            p -= a.Y[col];
+        }
+        R2<real> q = a.xp[col];
+        q.y = real(2) * q.x - a.Ga[col] * p;
+        a.xp[col] = q;
+    }
+}
+
+// R partials: part[b][n] = sum_{v in block b} A[n + N v] X[v]
+// (column-major A streamed once, 16-byte loads, 4 columns in flight)
+template <typename real>
+__global__ __launch_bounds__(256) void k_rows_partial(
+    int N, int V, const real *__restrict__ A, const R2<real> *__restrict__ xp,
+    int cpb, real *__restrict__ part, const Ctrl<real> *ctrl, int gate) {
+    if (gated(ctrl, gate)) return;
+    const int b = blockIdx.x;
+    const int v0 = b * cpb, v1 = min(v0 + cpb, V);
+    constexpr int VW = Vec<real>::kPer16B;
+    if ((N % VW) == 0) {
+        for (int n0 = threadIdx.x * VW; n0 < N; n0 += kBlock * VW) {
+            real acc[VW];
+#pragma unroll
+            for (int j = 0; j < VW; j++) acc[j] = real(0);
+            int v = v0;
+            for (; v + 4 <= v1; v += 4) {
+                Pk<real, VW> c[4];
+                real x[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    c[q] = ldv<real, VW>(A + (size_t)N * (v + q) + n0);
+                    x[q] = xp[v + q].x;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int j = 0; j < VW; j++) acc[j] += c[q].v[j] * x[q];
+            }
+            for (; v < v1; v++) {
+                Pk<real, VW> c = ldv<real, VW>(A + (size_t)N * v + n0);
+                real x = xp[v].x;
+#pragma unroll
+                for (int j = 0; j < VW; j++) acc[j] += c.v[j] * x;
+            }
+#pragma unroll
+            for (int j = 0; j < VW; j++) part[(size_t)b * N + n0 + j] = acc[j];
+        }
+    } else {
+        for (int n = threadIdx.x; n < N; n += kBlock) {
+            real acc = real(0);
+            for (int v = v0; v < v1; v++) acc += A[(size_t)N * v + n] * xp[v].x;
+            part[(size_t)b * N + n] = acc;
+        }
+    }
+}
+
+// R[n] = Y[n] - sum_b part[b][n]   (ref :356-367)
+template <typename real>
+__global__ void k_rows_finish(int N, int nb, const real *__restrict__ part,
+                              const real *__restrict__ Y,
+                              real *__restrict__ R, const Ctrl<real> *ctrl,
+                              int gate) {
+    if (gated(ctrl, gate)) return;
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    real s = real(0);
+    int b = 0;
+    for (; b + 8 <= nb; b += 8) {
+        real t[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) t[q] = part[(size_t)(b + q) * N + n];
+#pragma unroll
+        for (int q = 0; q < 8; q++) s += t[q];
+    }
+    for (; b < nb; b++) s += part[(size_t)b * N + n];
+    R[n] = Y[n] - s;
+}
+
+// ---------------------------------------------------- preconditioning --
+// |amplitude| per vertex and block counts of nonzero amplitudes (ref
+// :124-153).  src 0: pseudo-inverse Y/diag (N <= 0); 1: precomputed (N > 0);
+// 2: current iterate (reconditioning).
+template <typename real>
+__global__ __launch_bounds__(256) void k_amp(int V, int src,
+                                             const real *__restrict__ Y,
+                                             const real *__restrict__ diag,
+                                             const real *__restrict__ pre,
+                                             const R2<real> *__restrict__ xp,
+                                             real *__restrict__ absval,
+                                             int *__restrict__ cnt_part) {
+    __shared__ int red[kBlock / kWave];
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    real a = real(0);
+    if (v < V) {
+        if (src == 0) {
+            real g = diag[v];
+            a = (g > real(0)) ? Y[v] / g : real(0);
+        } else if (src == 1) {
+            a = pre[v];
+        } else {
+            a = xp[v].x;
+        }
+        // c += a for a > 0, c -= a for a < 0 (identical to adding -a)
+        absval[v] = (a > real(0)) ? a : ((a < real(0)) ? -a : real(0));
+    }
+    int nz = (v < V) && (a > real(0) || a < real(0));
+    nz = block_sum(nz, red);
+    if (threadIdx.x == 0) cnt_part[blockIdx.x] = nz;
+}
+
+// Sum of |a| accumulated strictly sequentially in increasing v, seeded with
+// the running sum of the lower ranks — the reference's single-thread order
+// over the global vertex range — so the metric rounds exactly as the
+// reference's.  One workgroup: all lanes stage chunks in LDS (double
+// buffered), lane 0 adds them in order.  Also reduces the nonzero counts.
+template <typename real>
+__global__ __launch_bounds__(256) void k_seq_sum(int V, const real *__restrict__ absval,
+                                                 const real *__restrict__ seed,
+                                                 int nparts, const int *__restrict__ cnt_part,
+                                                 real *__restrict__ sum_out,
+                                                 long long *__restrict__ cnt_out) {
+    constexpr int CH = 4096;
+    __shared__ real buf[2][CH];
+    __shared__ long long red[kBlock / kWave];
+    long long cnt = 0;
+    for (int i = threadIdx.x; i < nparts; i += kBlock) cnt += cnt_part[i];
+    cnt = block_sum(cnt, red);
+    real s = seed ? *seed : real(0);
+    int cur = 0;
+    for (long j = threadIdx.x; j < min((long)CH, (long)V); j += kBlock) buf[0][j] = absval[j];
+    __syncthreads();
+    for (long c0 = 0; c0 < V; c0 += CH) {
+        const long n = min((long)CH, (long)V - c0);
+        const long nxt = c0 + CH;
+        if (threadIdx.x == 0) {
+            const real *b = buf[cur];
+            for (long j = 0; j < n; j++) s += b[j];
+        } else if (nxt < V) {
+            const long m = min((long)CH, (long)V - nxt);
+            for (long j = threadIdx.x - 1; j < m; j += kBlock - 1) buf[cur ^ 1][j] = absval[nxt + j];
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (threadIdx.x == 0) {
+        *sum_out = s;
+        *cnt_out = cnt;
+    }
+}
+
+// c = n / sum|a| (first call) or sum|a| / n (reconditioning) (ref :154)
+template <typename real>
+__global__ void k_set_c(const real *__restrict__ sum, const long long *__restrict__ cnt,
+                        int init, Ctrl<real> *ctrl) {
+    if (threadIdx.x != 0) return;
+    const real n = (real)(int)*cnt;
+    const real s = *sum;
+    ctrl->c = init ? n / s : s / n;
+    ctrl->cnt = (int)*cnt;
+}
+
+// d1 splitting weights (ref :156-192) into both half-edges W2[2e + side].
+// On reconditioning, first turn the auxiliary variables into subgradients
+// with the OLD weights and metric (ref :89-99).
+template <typename real>
+__global__ void k_d1_weights(long E, const int *__restrict__ Eu,
+                             const int *__restrict__ Ev,
+                             const real *__restrict__ La_d1,
+                             const Ctrl<real> *__restrict__ ctrl, int init,
+                             real condMin, const R2<real> *__restrict__ xp,
+                             real *__restrict__ W2, real *__restrict__ wz,
+                             const real *__restrict__ Ga,
+                             const real *__restrict__ grad,
+                             real *__restrict__ Z2) {
+    long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const real c = ctrl->c;
+    real w;
+    if (init) {
+        w = c * La_d1[e];
+    } else {
+        const int u = Eu[e], v = Ev[e];
+        const real xu = xp[u].x, xv = xp[v].x;
+        const real gu = Ga[u], gv = Ga[v];
+        Z2[2 * e] = (W2[2 * e] / gu) * (xu - gu * grad[u] - Z2[2 * e]);
+        Z2[2 * e + 1] = (W2[2 * e + 1] / gv) * (xv - gv * grad[v] - Z2[2 * e + 1]);
+        real a = xu, b = xv, d = a - b;
+        if (a < real(0)) a = -a;
+        if (b < real(0)) b = -b;
+        if (d < real(0)) d = -d;
+        if (a < b) a = b;
+        if (a < c) a = c;
+        a *= condMin;
+        if (d < a) d = a;
+        w = La_d1[e] / d;
+    }
+    W2[2 * e] = w;
+    W2[2 * e + 1] = w;
+    wz[e] = w;      // per-vertex sums go through the same CSR as the DR average
+    wz[E + e] = w;
+}
+
+// metric of every vertex (ref :193-239 and :262-264)
+template <typename real>
+__global__ __launch_bounds__(256) void k_precond_vertex(
+    int V, const int *__restrict__ ptr, const unsigned *__restrict__ idx,
+    const real *__restrict__ wz, const real *__restrict__ diag,
+    const real *__restrict__ La_l1, const R2<real> *__restrict__ xp,
+    const Ctrl<real> *__restrict__ ctrl, int init, real condMin, real cap,
+    const real *__restrict__ Ldiag, real *__restrict__ Ga,
+    real *__restrict__ invAux, real *__restrict__ Th_l1) {
+    __shared__ real lds[GatherCap<real>::v];
+    const int v0 = blockIdx.x * kBlock;
+    const real s = gather_sum<real, GatherCap<real>::v>(V, v0, ptr, idx, wz, lds);
+    const int v = v0 + threadIdx.x;
+    if (v >= V) return;
+    real g = diag[v];
+    g += s;
+    invAux[v] = real(1) / s;
+    if (La_l1) {
+        const real c = ctrl->c;
+        if (init) {
+            g += c * La_l1[v];
+        } else {
+            const real cm = c * condMin;
+            real d = xp[v].x;
+            if (d < real(0)) d = -d;
+            if (d < cm) d = cm;
+            g += La_l1[v] / d;
+        }
+    }
+    g = real(1) / g;
+    if (!Ldiag) {
+        if (g > cap) g = cap;
+    } else {
+        const real L = Ldiag[v];
+        if (L > real(0)) {
+            const real b = cap / L;
+            if (g > b) g = b;
+        }
+    }
+    Ga[v] = g;
+    if (La_l1) Th_l1[v] = g * La_l1[v];
+}
+
+// normalised splitting weights, prox weights and thresholds
+// (ref :196-203, :241-261)
+template <typename real>
+__global__ void k_precond_edge2(long E, const int *__restrict__ Eu,
+                                const int *__restrict__ Ev,
+                                const real *__restrict__ invAux,
+                                const real *__restrict__ Ga,
+                                const real *__restrict__ La_d1,
+                                real *__restrict__ W2,
+                                real *__restrict__ Wd1u,
+                                real *__restrict__ Wd1v,
+                                real *__restrict__ Th, int recond,
+                                const R2<real> *__restrict__ xp,
+                                const real *__restrict__ grad,
+                                real *__restrict__ Z2) {
+    long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int u = Eu[e], v = Ev[e];
+    const real wu = W2[2 * e] * invAux[u];
+    const real wv = W2[2 * e + 1] * invAux[v];
+    W2[2 * e] = wu;
+    W2[2 * e + 1] = wv;
+    const real gu = Ga[u], gv = Ga[v];
+    if (recond) {
+        Z2[2 * e] = xp[u].x - gu * (grad[u] + Z2[2 * e] / wu);
+        Z2[2 * e + 1] = xp[v].x - gv * (grad[v] + Z2[2 * e + 1] / wv);
+    }
+    const real a = wu / gu, b = wv / gv, s = a + b;
+    Th[e] = La_d1[e] * s / (a * b);
+    Wd1u[e] = a / s;
+    Wd1v[e] = b / s;
+}
+
+// CSR keys of the local slots: key = (vertex << 32) | (2 e_global + side),
+// value = address of the slot's contribution in the side-major wz; slots of
+// non-owned (ghost) vertices get key ~0 and are dropped by the CSR build.
+__global__ void k_slot_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                            int V, const unsigned *__restrict__ eg, long e_offset,
+                            unsigned long long *__restrict__ keys, unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const unsigned long long g = eg ? (unsigned long long)eg[e] : (unsigned long long)(e_offset + e);
+    const int u = Eu[e], v = Ev[e];
+    keys[e] = (u < V) ? (((unsigned long long)u << 32) | (2 * g)) : ~0ull;
+    keys[E + e] = (v < V) ? (((unsigned long long)v << 32) | (2 * g + 1)) : ~0ull;
+    vals[e] = (unsigned)e;
+    vals[E + e] = (unsigned)(E + e);
+}
+
+// gradient A X - Y of the identity / diagonal modes (ref :377-385, :441-445)
+template <typename real>
+__global__ void k_grad_vertex(int V, int mode, const real *__restrict__ A,
+                              const real *__restrict__ Y,
+                              const R2<real> *__restrict__ xp,
+                              real *__restrict__ grad) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const real x = xp[v].x;
+    real p = (mode == A_DIAG) ? A[v] * x : x;
+    p -= Y[v];
+    grad[v] = p;
+}
+
+// forward step from the gradient: P = 2 X - Ga grad   (ref :462-464)
+template <typename real>
+__global__ void k_forward_grad(int V, const real *__restrict__ Ga,
+                               const real *__restrict__ grad, R2<real> *xp) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    R2<real> q = xp[v];
+    q.y = real(2) * q.x - Ga[v] * grad[v];
+    xp[v] = q;
+}
+
+// ---------------------------------------------------------- iteration --
+// TV prox on every edge (ref :466-489) + the two DR contributions W*Z.
+// 16 bytes per lane on every edge stream: 4 (f32) / 2 (f64) edges per lane.
+template <typename real>
+__device__ __forceinline__ void edge_update(const R2<real> &pu,
+                                            const R2<real> &pv, real &zu,
+                                            real &zv, real wu, real wv,
+                                            real th, real rho) {
+    // pu.x = X[u], pu.y = P[u] (forward step)
+    const real a = wu * (pu.y - zu) + wv * (pv.y - zv);
+    real b = (pu.y - zu) - (pv.y - zv);
+    if (b > th) {
+        b -= th;
+        zu += rho * (a + wv * b - pu.x);
+        zv += rho * (a - wu * b - pv.x);
+    } else if (b < -th) {
+        b += th;
+        zu += rho * (a + wv * b - pu.x);
+        zv += rho * (a - wu * b - pv.x);
+    } else {
+        zu += rho * (a - pu.x);
+        zv += rho * (a - pv.x);
+    }
+}
+
+// Edge sweep; writes the DR contributions W*Z side-major: wz[e] (u end),
+// wz[E + e] (v end), so the u-side run of a vertex is contiguous.
+template <typename real>
+__global__ __launch_bounds__(256) void k_edge_sweep(
+    long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2,
+    const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
+    const real *__restrict__ Th, const real *__restrict__ W2,
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
+    if (ctrl && ctrl->halt) return;
+    constexpr int EPT = Vec<real>::kPer16B;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    const long e0 = ((long)blk * blockDim.x + threadIdx.x) * EPT;
+    if (e0 >= E) return;
+    if (e0 + EPT <= E) {
+        const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
+        const Pk<int, EPT> iv = ldv<int, EPT>(Ev + e0);
+        R2<real> pu[EPT], pv[EPT];
+#pragma unroll
+        for (int j = 0; j < EPT; j++) { pu[j] = xp[iu.v[j]]; pv[j] = xp[iv.v[j]]; }
+        Pk<real, 2 * EPT> z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
+        const Pk<real, EPT> a = ldv<real, EPT>(Wd1u + e0);
+        const Pk<real, EPT> b = ldv<real, EPT>(Wd1v + e0);
+        const Pk<real, EPT> t = ldv<real, EPT>(Th + e0);
+#pragma unroll
+        for (int j = 0; j < EPT; j++)
+            edge_update<real>(pu[j], pv[j], z.v[2 * j], z.v[2 * j + 1], a.v[j], b.v[j],
+                              t.v[j], rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
+        const Pk<real, 2 * EPT> w = ldv<real, 2 * EPT>(W2 + 2 * e0);
+        Pk<real, EPT> ou, ov;
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            ou.v[j] = w.v[2 * j] * z.v[2 * j];
+            ov.v[j] = w.v[2 * j + 1] * z.v[2 * j + 1];
+        }
+        stv<real, EPT>(wz + e0, ou);
+        stv<real, EPT>(wz + E + e0, ov);
+    } else {
+        for (long e = e0; e < E; e++) {
+            const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1];
+            edge_update<real>(pu, pv, zu, zv, Wd1u[e], Wd1v[e], Th[e], rho);
+            Z2[2 * e] = zu;
+            Z2[2 * e + 1] = zv;
+            wz[e] = W2[2 * e] * zu;
+            wz[E + e] = W2[2 * e + 1] * zv;
+        }
+    }
+}
+
+template <typename real>
+struct VArgs {
+    int V;
+    int nb, xcd;            // logical blocks, XCD-aware order
+    const int *ptr;
+    const unsigned *idx;
+    const real *wz;         // contributions (local side-major, then received)
+    R2<real> *xp;
+    const real *Y, *A, *Ga, *Th_l1;
+    int prox, positivity;
+    real lo, hi;
+    int fwd;        // 0: keep P (dense modes), 1: identity, 2: diagonal A
+    int track;      // iterate-evolution partials
+    real *part;     // 2 per block
+    const Ctrl<real> *ctrl;
+};
+
+// DR average (ordered), prox on the iterate, evolution partials, next
+// forward step (ref :491-529 then :355-464 of the next iteration)
+// occupancy target of the vertex sweep: 8 waves/SIMD in f32 (LDS allows 9
+// blocks per CU), 4 in f64 (32 KiB of LDS per block)
+template <typename real> struct VSweep;
+template <> struct VSweep<float> { static constexpr int waves = 8; };
+template <> struct VSweep<double> { static constexpr int waves = 4; };
+
+template <typename real, int GB>
+__global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real lds[GatherCap<real>::v];
+    __shared__ real red[2][kBlock / kWave];
+    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (blk >= a.nb) return;
+    const int v0 = blk * kBlock;
+    const int v = v0 + threadIdx.x;
+    // per-vertex operands first: their latency hides under the gather
+    R2<real> q{};
+    real th = real(0), yv = real(0), gv = real(0), av = real(0);
+    if (v < a.V) {
+        q = a.xp[v];
+        if (a.prox == PROX_L1) th = a.Th_l1[v];
+        if (a.fwd) { yv = a.Y[v]; gv = a.Ga[v]; }
+        if (a.fwd == 2) av = a.A[v];
+    }
+    real x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+    real num = real(0), den = real(0);
+    if (v < a.V) {
+        switch (a.prox) {
+            case PROX_L1: {
+                if (x > th) x -= th;
+                else if (!a.positivity && (x < -th)) x += th;
+                else x = real(0);
+            } break;
+            case PROX_POS:
+                if (x < real(0)) x = real(0);
+                break;
+            case PROX_BOX:
+                if (x < a.lo) x = a.lo;
+                else if (x > a.hi) x = a.hi;
+                break;
+            case PROX_LO:
+                if (x < a.lo) x = a.lo;
+                break;
+            case PROX_HI:
+                if (x > a.hi) x = a.hi;
+                break;
+            default:
+                break;
+        }
+        if (a.track) {
+            const real d = q.x - x;
+            num = d * d;
+            den = x * x;
+        }
+        q.x = x;
+        if (a.fwd) {
+            real p = (a.fwd == 2) ? av * x : x;
+            p -= yv;
+            q.y = real(2) * x - gv * p;
+        }
+        a.xp[v] = q;
+    }
+    if (a.track) {
+        num = block_sum(num, red[0]);
+        den = block_sum(den, red[1]);
+        if (threadIdx.x == 0) {
+            a.part[2 * blk] = num;
+            a.part[2 * blk + 1] = den;
+        }
+    }
+}
+
+// fixed-order sum of per-block partial pairs into out[0..1]
+template <typename real>
+__global__ __launch_bounds__(256) void k_reduce_pairs(int nparts, const real *__restrict__ part,
+                                                      real *__restrict__ out, int stride) {
+    __shared__ real red[2][kBlock / kWave];
+    real a = real(0), b = real(0);
+    for (int i = threadIdx.x; i < nparts; i += kBlock) {
+        a += part[2 * i];
+        b += part[2 * i + 1];
+    }
+    a = block_sum(a, red[0]);
+    b = block_sum(b, red[1]);
+    if (threadIdx.x == 0) { out[0] = a; out[stride] = b; }
+}
+
+// iterate evolution and loop control (ref :514-529, :424-429, :447-460);
+// red[0..1] = (sum (X - X_)^2, sum X^2) over all ranks
+template <typename real>
+__global__ void k_decide(Ctrl<real> *ctrl, const real *__restrict__ red,
+                         real *__restrict__ Dif, int track) {
+    if (threadIdx.x != 0 || ctrl->halt) return;
+    int it = ctrl->it;
+    if (track) {
+        const real num = red[0], den = red[1], eps = ctrl->eps;
+        const real dif = (den > eps) ? num / den : num / eps;
+        ctrl->dif = dif;
+        if (Dif) Dif[it] = dif;
+    }
+    it++;
+    ctrl->it = it;
+    const real dif = ctrl->dif;
+    if (it >= ctrl->itMax || dif < ctrl->difTol) {
+        ctrl->stop = 1;
+        ctrl->halt = 1;
+    } else if (dif < ctrl->difRcd) {
+        ctrl->recond = 1;
+        ctrl->halt = 1;
+    }
+}
+
+// ------------------------------------------------------------ objective --
+// partials: [0, nbv) data term, [nbv, 2 nbv) l1 term, [2 nbv, 2 nbv + nbe)
+// TV term, then the squared residual partials (direct mode).
+template <typename real>
+__global__ __launch_bounds__(256) void k_obj_vertex(
+    int V, int mode, const R2<real> *__restrict__ xp,
+    const real *__restrict__ A, const real *__restrict__ papp,
+    const real *__restrict__ Y, const real *__restrict__ La_l1,
+    real *__restrict__ part, int nbv, const Ctrl<real> *ctrl) {
+    if (gated(ctrl, GATE_OBJ)) return;
+    __shared__ real red[2][kBlock / kWave];
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    real dat = real(0), l1 = real(0);
+    if (v < V) {
+        const real x = xp[v].x;
+        if (mode != A_DIRECT) {
+            const real p = (mode == A_IDENT) ? x : (mode == A_DIAG ? A[v] * x : papp[v]);
+            dat = x * (real(0.5) * p - Y[v]);
+        }
+        if (La_l1) l1 = (x < real(0)) ? -(La_l1[v] * x) : La_l1[v] * x;
+    }
+    dat = block_sum(dat, red[0]);
+    l1 = block_sum(l1, red[1]);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = dat;
+        part[nbv + blockIdx.x] = l1;
+    }
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_obj_edge(
+    long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+    const R2<real> *__restrict__ xp, const real *__restrict__ La_d1,
+    real *__restrict__ part, const Ctrl<real> *ctrl) {
+    if (gated(ctrl, GATE_OBJ)) return;
+    __shared__ real red[kBlock / kWave];
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    real t = real(0);
+    if (e < E) {
+        const real b = xp[Eu[e]].x - xp[Ev[e]].x;
+        t = (b < real(0)) ? -(La_d1[e] * b) : La_d1[e] * b;
+    }
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_obj_rsq(int N,
+                                                 const real *__restrict__ R,
+                                                 real *__restrict__ part,
+                                                 const Ctrl<real> *ctrl) {
+    if (gated(ctrl, GATE_OBJ)) return;
+    __shared__ real red[kBlock / kWave];
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    real t = (n < N) ? R[n] * R[n] : real(0);
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+// objective partials -> red[0..2] = (data, l1, tv)
+template <typename real>
+__global__ __launch_bounds__(256) void k_obj_reduce(
+    const real *__restrict__ part, int nbv, int nbe, int nbn, int direct,
+    const Ctrl<real> *ctrl, real *__restrict__ red3) {
+    __shared__ real red[3][kBlock / kWave];
+    if (ctrl && ctrl->obj_it >= ctrl->it) return;
+    real dat = real(0), l1 = real(0), tv = real(0);
+    if (direct) {
+        for (int i = threadIdx.x; i < nbn; i += kBlock) dat += part[2 * nbv + nbe + i];
+    } else {
+        for (int i = threadIdx.x; i < nbv; i += kBlock) dat += part[i];
+    }
+    for (int i = threadIdx.x; i < nbv; i += kBlock) l1 += part[nbv + i];
+    for (int i = threadIdx.x; i < nbe; i += kBlock) tv += part[2 * nbv + i];
+    dat = block_sum(dat, red[0]);
+    l1 = block_sum(l1, red[1]);
+    tv = block_sum(tv, red[2]);
+    if (threadIdx.x == 0) { red3[0] = dat; red3[1] = l1; red3[2] = tv; }
+}
+
+template <typename real>
+__global__ void k_obj_write(const real *__restrict__ red3, int direct, int has_l1,
+                            Ctrl<real> *ctrl, real *__restrict__ Obj) {
+    if (threadIdx.x != 0) return;
+    if (ctrl && ctrl->obj_it >= ctrl->it) return;
+    real o = direct ? real(0.5) * red3[0] : red3[0];
+    o += red3[2];
+    if (has_l1) o += red3[1];
+    const int it = ctrl ? ctrl->it : 0;
+    Obj[it] = o;
+    if (ctrl) ctrl->obj_it = it;
+}
+
+}  // namespace pfdr

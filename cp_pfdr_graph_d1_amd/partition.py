@@ -1,0 +1,168 @@
+"""1-D vertex-range partition of a PFDR graph.
+
+* ``vertex_offsets`` / ``split_edges``: rank r owns global vertices
+  [off[r], off[r+1]) and the edges whose Eu it owns, keeping their global
+  edge ids (the per-vertex DR sums run in global edge order on every rank).
+* ``Plan``: the library's host-only planner (pfdr_plan_* in
+  include/pfdr_mi355x.h) — what a partitioned session runs at setup, drivable
+  over any transport (the CPU tests use torch.distributed/gloo).
+* ``solve_loopback``: k ranks as k threads on one GPU (loopback transport);
+  returns the concatenated result, which equals the unpartitioned solve.
+* ``comm_init``: RCCL communicator for one process per GPU, the id broadcast
+  over an existing torch.distributed process group.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import pfdr
+
+PLAN_GHOSTS, PLAN_EU_LOCAL, PLAN_EV_LOCAL = 0, 1, 2
+PLAN_PULL_REQUEST, PLAN_PUSH_ITEMS, PLAN_PUSH_ADDR = 3, 4, 5
+PLAN_PULL_INDEX, PLAN_RECV_KEYS = 6, 7
+PLAN_GHOST_OFFSETS, PLAN_PULL_OFFSETS, PLAN_PUSH_OFFSETS, PLAN_RECV_OFFSETS = 8, 9, 10, 11
+COMM_RCCL, COMM_LOOPBACK = 0, 1
+
+_PLAN_DTYPES = {PLAN_GHOSTS: np.int64, PLAN_EU_LOCAL: np.int32, PLAN_EV_LOCAL: np.int32,
+                PLAN_PULL_REQUEST: np.int64, PLAN_PUSH_ITEMS: np.int64,
+                PLAN_PUSH_ADDR: np.uint32, PLAN_PULL_INDEX: np.int32,
+                PLAN_RECV_KEYS: np.uint64, PLAN_GHOST_OFFSETS: np.int32,
+                PLAN_PULL_OFFSETS: np.int32, PLAN_PUSH_OFFSETS: np.int32,
+                PLAN_RECV_OFFSETS: np.int32}
+
+
+def vertex_offsets(V, k):
+    """Balanced contiguous vertex ranges, off[0] = 0, off[k] = V."""
+    return np.array([(V * r) // k for r in range(k + 1)], np.int64)
+
+
+def split_edges(Eu, off):
+    """Edge ids (ascending) owned by each rank: those whose Eu it owns."""
+    owner = np.searchsorted(off, np.asarray(Eu, np.int64), side="right") - 1
+    return [np.nonzero(owner == r)[0].astype(np.int64) for r in range(len(off) - 1)]
+
+
+class Plan:
+    def __init__(self, nranks, rank, off, Eu, Ev, e_global):
+        lib = pfdr.load()
+        lib.pfdr_plan_get.restype = C.c_int64
+        lib.pfdr_plan_get.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        lib.pfdr_plan_set_incoming.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64,
+                                               C.c_void_p]
+        lib.pfdr_plan_destroy.argtypes = [C.c_void_p]
+        self.lib = lib
+        self.nranks, self.rank = nranks, rank
+        self._off = np.ascontiguousarray(off, np.int64)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        eg = np.ascontiguousarray(e_global, np.int64)
+        h = C.c_void_p()
+        pfdr._check(lib.pfdr_plan_create(C.byref(h), C.c_int(nranks), C.c_int(rank),
+                                         C.c_void_p(self._off.ctypes.data), C.c_int(Eu.size),
+                                         C.c_void_p(Eu.ctypes.data), C.c_void_p(Ev.ctypes.data),
+                                         C.c_void_p(eg.ctypes.data), C.c_int64(0)),
+                    "pfdr_plan_create")
+        self.h = h
+
+    def get(self, what, peer=0):
+        n = self.lib.pfdr_plan_get(self.h, what, peer, None)
+        if n < 0:
+            raise pfdr.PFDRError("pfdr_plan_get(%d) failed" % what)
+        out = np.empty(n, _PLAN_DTYPES[what])
+        if n:
+            self.lib.pfdr_plan_get(self.h, what, peer, C.c_void_p(out.ctypes.data))
+        return out
+
+    def set_incoming(self, peer, what, data):
+        data = np.ascontiguousarray(data, np.int64)
+        pfdr._check(self.lib.pfdr_plan_set_incoming(self.h, peer, what, data.size,
+                                                    C.c_void_p(data.ctypes.data)),
+                    "pfdr_plan_set_incoming")
+
+    def finish(self):
+        pfdr._check(self.lib.pfdr_plan_finish(self.h), "pfdr_plan_finish")
+
+    def close(self):
+        if self.h:
+            self.lib.pfdr_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
+                   positivity=0, lo=-np.inf, hi=np.inf, Ltype=0, L=None, rho=1.5,
+                   condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=100, record_obj=False,
+                   record_dif=False, off=None):
+    """Partitioned solve with k ranks as k threads on the current GPU.
+    Returns (X, it, Obj, Dif, info) with X for all vertices."""
+    lib = pfdr.load()
+    V = np.asarray(X0).size
+    off = vertex_offsets(V, k) if off is None else np.asarray(off, np.int64)
+    parts = split_edges(Eu, off)
+    hub = C.c_void_p()
+    pfdr._check(lib.pfdr_loopback_create(C.byref(hub), C.c_int(k)), "pfdr_loopback_create")
+    results, errors = [None] * k, [None] * k
+
+    def rank_main(r):
+        try:
+            e = parts[r]
+            v0, v1 = int(off[r]), int(off[r + 1])
+            sl = slice(v0, v1)
+
+            def vsl(a):
+                if a is None:
+                    return None
+                a = np.asarray(a)
+                return a[sl] if a.size == V else a
+            s = pfdr.Session(kind, dtype, v1 - v0, e.size, np.asarray(Eu)[e],
+                             np.asarray(Ev)[e], np.asarray(La_d1)[e], vsl(X0), vsl(Y),
+                             A=vsl(A), La_l1=vsl(La_l1), positivity=positivity, lo=lo, hi=hi,
+                             Ltype=Ltype, L=vsl(L), rho=rho, condMin=condMin, difRcd=difRcd,
+                             difTol=difTol, itMax=itMax, record_obj=record_obj,
+                             record_dif=record_dif, nranks=k, rank=r, comm=hub.value,
+                             comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e)
+            s.run(itMax)
+            results[r] = s.result()
+            s.close()
+        except Exception as ex:  # reported by the caller
+            errors[r] = ex
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(k)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    lib.pfdr_loopback_destroy(hub)
+    for ex in errors:
+        if ex is not None:
+            raise ex
+    X = np.concatenate([res[0] for res in results])
+    its = {res[1] for res in results}
+    if len(its) != 1:
+        raise pfdr.PFDRError("ranks disagree on the iteration count: %s" % its)
+    it = its.pop()
+    return X, it, results[0][2], results[0][3], {"off": off, "edges": [p.size for p in parts]}
+
+
+def comm_init(nranks, rank, device_tensor_broadcast):
+    """RCCL communicator (one process per GPU).  ``device_tensor_broadcast``
+    broadcasts a uint8 torch tensor from rank 0 in place (e.g.
+    torch.distributed.broadcast)."""
+    import torch
+    lib = pfdr.load()
+    buf = (C.c_char * 128)()
+    if rank == 0:
+        pfdr._check(lib.pfdr_comm_unique_id(buf), "pfdr_comm_unique_id")
+    t = torch.tensor(list(bytes(buf)), dtype=torch.uint8, device="cuda")
+    device_tensor_broadcast(t)
+    raw = bytes(t.cpu().tolist())
+    idb = (C.c_char * 128).from_buffer_copy(raw)
+    comm = C.c_void_p()
+    pfdr._check(lib.pfdr_comm_init(C.byref(comm), nranks, rank, idb), "pfdr_comm_init")
+    return comm.value

@@ -39,7 +39,9 @@ EXPORTED = (
     "pfdr_session_kernel_stats", "pfdr_session_sync",
     "pfdr_session_device_bytes", "pfdr_session_destroy",
     "pfdr_comm_unique_id", "pfdr_comm_init", "pfdr_comm_destroy",
-    "pfdr_comm_allreduce_max_f64",
+    "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create",
+    "pfdr_loopback_destroy", "pfdr_plan_create", "pfdr_plan_get",
+    "pfdr_plan_set_incoming", "pfdr_plan_finish", "pfdr_plan_destroy",
     "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
     "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
 )
@@ -64,6 +66,7 @@ class Problem(C.Structure):
         ("itMax", C.c_int), ("verbose", C.c_int),
         ("record_obj", C.c_int), ("record_dif", C.c_int),
         ("nranks", C.c_int), ("rank", C.c_int), ("comm", C.c_void_p),
+        ("comm_kind", C.c_int),
         ("vtx_begin", C.c_int64), ("V_global", C.c_int64),
         ("e_global", C.c_void_p), ("e_offset", C.c_int64),
     ]
@@ -364,7 +367,9 @@ class Session:
                  La_l1=None, positivity=0, lo=-np.inf, hi=np.inf, K=0,
                  al=0.0, Ltype=SCAL, L=None, rho=1.5, condMin=1e-3,
                  difRcd=0.0, difTol=0.0, itMax=1000, record_obj=False,
-                 record_dif=False, verbose=0, device=False):
+                 record_dif=False, verbose=0, device=False, nranks=0, rank=0,
+                 comm=None, comm_kind=0, vtx_begin=0, V_global=0, e_global=None,
+                 e_offset=0):
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
@@ -390,6 +395,15 @@ class Session:
         p.rho, p.condMin, p.difRcd, p.difTol = rho, condMin, difRcd, difTol
         p.itMax, p.verbose = itMax, verbose
         p.record_obj, p.record_dif = int(record_obj), int(record_dif)
+        # 1-D vertex-range partition (see partition.py)
+        p.nranks, p.rank = nranks, rank
+        p.comm = comm
+        p.comm_kind = comm_kind
+        p.vtx_begin, p.V_global, p.e_offset = vtx_begin, V_global, e_offset
+        if e_global is not None:
+            eg = np.ascontiguousarray(e_global, np.int64)
+            self._keep.append(eg)
+            p.e_global = C.c_void_p(eg.ctypes.data)
         self.problem = p
         self.dtype = np.dtype(dtype)
         self.V, self.K = V, max(K, 1)

@@ -134,7 +134,8 @@ typedef struct pfdr_problem {
     int record_dif;       /* keep Dif[0..itMax-1] on the device */
     /* --- 1-D vertex-range partition (leave zero for one GPU) ------------ */
     int nranks, rank;     /* rank r owns global vertices [vtx_begin, vtx_begin+V) */
-    void *comm;           /* ncclComm_t created with pfdr_comm_init */
+    void *comm;           /* ncclComm_t (pfdr_comm_init) or loopback hub */
+    int comm_kind;        /* PFDR_COMM_RCCL or PFDR_COMM_LOOPBACK */
     int64_t vtx_begin;    /* first owned global vertex */
     int64_t V_global;     /* total vertices over all ranks */
     const int64_t *e_global; /* global id of each local edge; NULL: e_offset + e */
@@ -165,12 +166,51 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
 void pfdr_session_destroy(pfdr_session *s);
 
 /* ------------------------------------------------------ multi-GPU comm -- */
+/* Partitioned sessions (quadratic solvers, identity or diagonal A): every
+ * rank passes its owned vertices (V of them, global ids [vtx_begin,
+ * vtx_begin + V), ranks in vertex order) and its edges (global endpoint ids,
+ * global edge ids e_global or e_offset + e).  Creation and every run() are
+ * collective.  The result equals the unpartitioned solve bit for bit. */
+#define PFDR_COMM_RCCL 0      /* one process per GPU, ncclComm_t */
+#define PFDR_COMM_LOOPBACK 1  /* k ranks as k threads of one process, one GPU */
 #define PFDR_COMM_ID_BYTES 128
 /* rank 0 creates the id, the caller broadcasts it, every rank inits */
 int pfdr_comm_unique_id(void *id_out /* PFDR_COMM_ID_BYTES */);
 int pfdr_comm_init(void **comm_out, int nranks, int rank, const void *id);
 int pfdr_comm_destroy(void *comm);
 int pfdr_comm_allreduce_max_f64(void *comm, double *value);
+int pfdr_loopback_create(void **hub_out, int nranks);
+int pfdr_loopback_destroy(void *hub);
+
+/* Host-only partition planner (what the partitioned session runs at setup;
+ * exposed so the partition logic can be driven by any transport, e.g. the
+ * CPU tests).  Rank `rank` owns global vertices [offsets[rank],
+ * offsets[rank+1]); its E edges have global endpoints Eu/Ev and global ids
+ * e_global (or e_offset + e).  Flow: create -> get PULL_REQUEST/PUSH_ITEMS
+ * for every peer -> send them -> set_incoming what every peer sent ->
+ * finish -> get the results.  pfdr_plan_get returns the element count and
+ * copies the elements when out != NULL. */
+typedef struct pfdr_plan pfdr_plan;
+#define PFDR_PLAN_GHOSTS 0          /* int64 global ids of the ghost vertices */
+#define PFDR_PLAN_EU_LOCAL 1        /* int32 local endpoint ids (ghosts >= V) */
+#define PFDR_PLAN_EV_LOCAL 2
+#define PFDR_PLAN_PULL_REQUEST 3    /* int64 ghost ids owned by `peer` */
+#define PFDR_PLAN_PUSH_ITEMS 4      /* int64 (vertex, 2 e_global + side) pairs for `peer` */
+#define PFDR_PLAN_PUSH_ADDR 5       /* uint32 contribution address of every item sent */
+#define PFDR_PLAN_PULL_INDEX 6      /* int32 owned local ids to send, per peer */
+#define PFDR_PLAN_RECV_KEYS 7       /* uint64 (local vertex << 32 | order) of items received */
+#define PFDR_PLAN_GHOST_OFFSETS 8   /* int32 nranks + 1 */
+#define PFDR_PLAN_PULL_OFFSETS 9    /* int32 nranks + 1, into PULL_INDEX */
+#define PFDR_PLAN_PUSH_OFFSETS 10   /* int32 nranks + 1, into PUSH_ADDR */
+#define PFDR_PLAN_RECV_OFFSETS 11   /* int32 nranks + 1, into RECV_KEYS */
+int pfdr_plan_create(pfdr_plan **out, int nranks, int rank,
+    const int64_t *offsets, int E, const int *Eu, const int *Ev,
+    const int64_t *e_global, int64_t e_offset);
+int64_t pfdr_plan_get(pfdr_plan *plan, int what, int peer, void *out);
+int pfdr_plan_set_incoming(pfdr_plan *plan, int peer, int what, int64_t n,
+    const int64_t *data);
+int pfdr_plan_finish(pfdr_plan *plan);
+void pfdr_plan_destroy(pfdr_plan *plan);
 
 /* -------------------------------------------------- synthetic inputs -- */
 /* Host-side deterministic generators (no device needed), identical laws to
