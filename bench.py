@@ -1,22 +1,28 @@
 """Benchmark of the MI355X PFDR hot path (BASELINE.json metric).
 
-Workload (SURVEY.md §8(d) 'Headline'): PFDR_graph_quadratic_d1_l1<float>,
+Default workload (SURVEY.md §8(d) 'Headline'): PFDR_graph_quadratic_d1_l1<float>,
 identity A, La_d1 = 0.1, La_l1 = 0.01, rho = 1.5, on the jittered
 250x200x200 grid where every vertex emits its 6 nearest 26-neighbours:
 V = 10,000,000 vertices, E = 60,000,000 edges.  One "step" = one PFDR
-iteration over the whole graph (edge sweep + vertex sweep), inputs resident
-in HBM, difTol = difRcd = 0 and Obj = Dif = NULL as in the reference's
-per-iteration timing methodology (setup excluded, reported separately).
+iteration over the whole graph (halo pull, edge sweep, halo push, vertex
+sweep), inputs resident in HBM, difTol = difRcd = 0 and Obj = Dif = NULL as
+in the reference's per-iteration timing methodology (setup excluded,
+reported separately).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 
-N > 1 (launched by torch.distributed.run, one process per GPU): weak
-scaling — every rank owns a 10M-vertex slab;
+N > 1 (launched by torch.distributed.run, one process per GPU): every rank
+owns a z-slab of the graph (1-D vertex-range partition, RCCL halo exchange,
+DESIGN.md §6); the headline is weak-scaled (a 10M-vertex slab per GPU);
 ``value`` = all ranks' edge updates / max-over-ranks time.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
-(edge sweep, HIP events on the session stream over the timed region) and the
-reference CPU path timed on this host (bounded sample, its own process).
+(HIP events on the session stream over the timed region; PMC traffic from
+profiles/pmc_traffic.json) and the reference CPU path timed on this host
+(bounded sample, its own process, before this process touches the GPU).
+`--workload c1..c5` selects the other BASELINE.json configs
+(tools/workloads.py), measured for DESIGN.md; the driver's line is the
+default headline.
 """
 import argparse
 import json
@@ -29,32 +35,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-SHAPE = (250, 200, 200)
-KNN = 6
-GRAPH_SEED, Y_SEED = 6, 2
-LA_D1, LA_L1, RHO, COND_MIN = 0.1, 0.01, 1.5, 1e-3
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic bytes: per edge Eu, Ev (8) + Zu, Zv read and
-# write (16) + W_d1u, W_d1v, Th_d1 (12) + Wu, Wv (8) = 44 B; per vertex X,
-# Y, Ga, Th_l1 read + X write = 20 B (fp32)
-EDGE_BYTES, VERTEX_BYTES = 44, 20
-METRIC = "PFDR iter/s and Medge-updates/s, 10M-vertex 6-NN graph, 1/2/4/8 MI355X"
-
-
-def headline_inputs(rank, nranks, dtype=np.float32):
-    """Rank r's slab of the weak-scaled headline graph: the global jittered
-    grid is 250 x 200 x (200 * nranks), rank r owns the vertices of
-    z in [200 r, 200 r + 200) (10M) and the 60M edges they emit; edges
-    reaching the next slab are its halo.  nranks = 1: the headline graph."""
-    from cp_pfdr_graph_d1_amd import pfdr
-    nx, ny, nz = SHAPE
-    gshape = (nx, ny, nz * nranks)
-    V = nx * ny * nz
-    v0 = rank * V
-    Eu, Ev = pfdr.gen_knn_jitter_grid(gshape, KNN, GRAPH_SEED, 0.25, (v0, v0 + V))
-    Y = pfdr.gen_piecewise(nx, V * nranks, Y_SEED, dtype, 0.2, (v0, v0 + V))
-    return gshape, V, Eu, Ev, Y
 
 
 # ------------------------------------------------------------ CPU baseline --
@@ -66,17 +49,17 @@ def cpu_baseline_child(args):
     os.sched_setaffinity(0, cores)  # omp_get_num_procs honours the mask
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    from workloads import WORKLOADS
     kind = "reference" if oracle.available("ref_omp") else "port"
     lib = oracle.Oracle("ref_omp" if kind == "reference" else "port")
-    _, V, Eu, Ev, Y = headline_inputs(0, 1)
-    Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
-    La = np.full(Eu.size, LA_D1, np.float32)
-    L1 = np.full(V, LA_L1, np.float32)
+    inp = WORKLOADS["headline"].inputs(0, 1)
+    kw, V = inp["kw"], inp["V"]
+    Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
     times = {}
     for k in (args.cpu_k0, args.cpu_k1):
         t = time.perf_counter()
-        lib.quadratic_d1_l1(np.zeros(V, np.float32), Y, None, 0, Eu, Ev, La, L1, 0, 0, None,
-                            RHO, COND_MIN, 0.0, 0.0, k)
+        lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"], kw["La_l1"],
+                            0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
         times[k] = time.perf_counter() - t
     per_it = (times[args.cpu_k1] - times[args.cpu_k0]) / (args.cpu_k1 - args.cpu_k0)
     print(json.dumps({
@@ -101,16 +84,14 @@ def run_cpu_baseline(args):
         return {"value": None, "error": repr(ex)[:300]}
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the edge sweep from the committed rocprofv3
-    PMC summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
-    when it matches this workload; else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(kernel, E):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
+    when it was taken on this workload size; else None."""
     try:
-        d = json.load(open(path))
-        k = d["kernels"]["k_edge_sweep"]
-        if d.get("workload_E") == KNN * SHAPE[0] * SHAPE[1] * SHAPE[2]:
-            return k["hbm_bytes_per_launch"]
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        if d.get("workload_E") == E:
+            return d["kernels"]["k_" + kernel]["hbm_bytes_per_launch"]
     except Exception:
         pass
     return None
@@ -119,8 +100,9 @@ def pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-k0", type=int, default=2)
@@ -130,13 +112,16 @@ def main():
     if args.cpu_baseline_child:
         cpu_baseline_child(args)
         return
+    from workloads import WORKLOADS
+    wl = WORKLOADS[args.workload]
+    steps = args.steps if args.steps is not None else wl.steps
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first, in its own process, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and wl.name == "headline" and not args.no_cpu_baseline:
         cpu = run_cpu_baseline(args)
 
     import torch
@@ -151,99 +136,106 @@ def main():
         if world > 1:
             dist.barrier()
 
-    gshape, V, Eu, Ev, Y = headline_inputs(rank, world)
-    E = Eu.size
-    dist_kw = {}
-    if world > 1:  # 1-D vertex-range partition, RCCL halo exchange over xGMI
-        from cp_pfdr_graph_d1_amd import partition
-        comm = partition.comm_init(world, rank, lambda t: dist.broadcast(t, 0))
-        dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
-                       vtx_begin=rank * V, V_global=world * V, e_offset=rank * E)
     t = time.perf_counter()
-    sess = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, E, Eu, Ev,
-                        np.full(E, LA_D1, np.float32), np.zeros(V, np.float32), Y,
-                        La_l1=np.full(V, LA_L1, np.float32), rho=RHO, condMin=COND_MIN,
-                        difTol=0.0, difRcd=0.0, itMax=args.warmup + args.steps, **dist_kw)
+    inp = wl.inputs(rank, world)
+    gen_s = time.perf_counter() - t
+    V, E = inp["V"], inp["E"]
+    converge = bool(inp.get("converge", False))
+    kw = inp["kw"]
+    dist_kw, parallelism = {}, "single"
+    if world > 1 and wl.partitionable:  # 1-D vertex-range partition, RCCL halo over xGMI
+        from cp_pfdr_graph_d1_amd import partition
+        comm = partition.comm_init(world, rank, lambda x: dist.broadcast(x, 0))
+        dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
+                       vtx_begin=inp["vtx_begin"], e_offset=inp["e_offset"])
+        parallelism = "vertex-partition x%d (RCCL halo)" % world
+    elif world > 1:
+        parallelism = "independent replicas x%d" % world
+    warm = 0 if converge else args.warmup
+    itMax = steps if converge else warm + steps
+    t = time.perf_counter()
+    sess = pfdr.Session(wl.kind, wl.dtype, V, E, itMax=itMax, **kw, **dist_kw)
     setup_s = time.perf_counter() - t
-    del Eu, Ev
-    sess.run(args.warmup)
+    desc, graph = inp["desc"], inp["graph"]
+    del inp, kw
+    if warm:
+        sess.run(warm)
     sess.profile(True)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
-    it = sess.run(args.steps)
+    it = sess.run(steps)
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
-    assert it == args.warmup + args.steps, it
-    el_max = el
+    done = it - warm
+    assert converge or done == steps, (it, warm, steps)
+    el_max, E_all = el, E * world
     if world > 1:
-        tt = torch.tensor([el], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el_max = float(tt.item())
-    n_e, ms_e = sess.kernel_stats("edge_sweep")
-    n_v, ms_v = sess.kernel_stats("vertex_sweep")
-    halo = {k: sess.kernel_stats(k)[1] for k in ("halo_pull", "halo_push")} if world > 1 else {}
-    X, _, _, _ = sess.result()
-    finite = bool(np.all(np.isfinite(X)))
+        tt = torch.tensor([el, float(E)], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        el_max, E_all = float(tt[0].item()), int(tt[1].item())
+    names = (wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep", "sx_average",
+             "sx_project", "gemv_rows", "gemv_cols", "halo_pull", "halo_push")
+    stats = {k: sess.kernel_stats(k) for k in names}
+    res = sess.result()
+    finite = bool(np.all(np.isfinite(res[0])))
     dev_bytes = sess.device_bytes()
     sess.close()
+    if world > 1:
+        dist.destroy_process_group()
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
         return
-    total_edges = E * world
-    ms_step = el_max / args.steps * 1e3
-    value = total_edges * args.steps / el_max / 1e6
-    achieved = EDGE_BYTES * E / (ms_e * 1e-3) / 1e9 if ms_e > 0 else None
-    traffic = pmc_traffic()
+    ms_step = el_max / max(done, 1) * 1e3
+    n_dom, ms_dom = stats[wl.dominant]
+    alg = wl.dominant_bytes(V, E)
+    achieved = alg / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
     out = {
-        "metric": METRIC,
-        "value": round(value, 2),
+        "metric": wl.metric,
+        "value": round(E_all * done / el_max / 1e6, 2),
         "unit": "Medge-updates/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": done,
+        "warmup": warm,
         "ms_per_step": round(ms_step, 4),
         "iter_per_s": round(1e3 / ms_step, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl.scaling,
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64" if wl.dtype == np.float64 else "f32",
         "data": "synthetic",
         "config": {
-            "workload": "PFDR_graph_quadratic_d1_l1<float>, identity A, l1 + TV, "
-                        "jittered %dx%dx%d grid, %d-NN (V=%d, E=%d per GPU)" % (
-                            SHAPE + (KNN, V, E)),
-            "global_graph": "%dx%dx%d" % gshape,
+            "workload": desc,
+            "global_graph": graph,
             "V_per_gpu": V, "E_per_gpu": E,
-            "parallelism": "vertex-partition%d (RCCL halo)" % world if world > 1 else "single",
-            "average": os.environ.get("PFDR_AVERAGE", "split"),
+            "parallelism": parallelism,
             "setup_s": round(setup_s, 3),
+            "input_generation_s": round(gen_s, 3),
             "device_bytes": dev_bytes,
             "finite": finite,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_edge_sweep",
+            "kernel": "k_" + wl.dominant,
             "achieved": None if achieved is None else round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": EDGE_BYTES * E,
-            "launches": n_e,
-            "mean_ms": round(ms_e, 5),
-            "vertex_sweep_mean_ms": round(ms_v, 5),
-            "halo_mean_ms": {k: round(v, 5) for k, v in halo.items()},
-            "iteration_algorithmic_GBps": round(
-                (EDGE_BYTES * E + VERTEX_BYTES * V) / (ms_step * 1e-3) / 1e9, 1),
+            "traffic": pmc_traffic(wl.dominant, E),
+            "algorithmic_bytes_per_launch": int(alg),
+            "launches": n_dom,
+            "mean_ms": round(ms_dom, 5),
+            "kernels_mean_ms": {k: round(v[1], 5) for k, v in stats.items() if v[0]},
+            "iteration_algorithmic_GBps": round(wl.iteration_bytes(V, E) / (ms_step * 1e-3) / 1e9, 1),
         },
         "cpu_baseline": cpu,
     }
+    if converge:
+        out["converged_iterations"] = it
+        out["time_to_tolerance_s"] = round(el_max, 4)
+        out["final_dif"] = None if res[3] is None or res[1] < 1 else float(res[3][res[1] - 1])
     print(json.dumps(out))
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

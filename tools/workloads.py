@@ -1,0 +1,221 @@
+"""Benchmark workloads of bench.py: the headline graph and the five configs of
+BASELINE.json, restated concretely in SURVEY.md §8(d).
+
+Each workload builds the session arguments of one rank (inputs generated
+deterministically, natively where large) and states its algorithmic bytes
+ so bench.py can price the dominant kernel against the HBM
+roofline.  Only `headline` is the driver's bench line; the others are run
+with `python bench.py --workload cN` for DESIGN.md.
+"""
+import numpy as np
+
+from cp_pfdr_graph_d1_amd import pfdr
+
+
+class Workload:
+    name = ""
+    metric = ""
+    kind = pfdr.PFDR_KIND_L1
+    dtype = np.float32
+    scaling = "weak"
+    partitionable = True      # identity/diagonal quadratic: vertex partition
+    dominant = "edge_sweep"
+    edge_bytes = 44           # algorithmic bytes per edge per iteration
+    vertex_bytes = 20
+    steps = 50
+    itMax_extra = 0
+
+    def inputs(self, rank, world):
+        """-> dict(V, E, kw (pfdr.Session kwargs), vtx_begin, e_offset, desc,
+        graph[, converge])"""
+        raise NotImplementedError
+
+    def dominant_bytes(self, V, E):
+        """algorithmic HBM bytes of one launch of the dominant kernel"""
+        return self.edge_bytes * E
+
+    def iteration_bytes(self, V, E):
+        """algorithmic HBM bytes of one whole iteration"""
+        return self.edge_bytes * E + self.vertex_bytes * V
+
+
+def _grid_slab(shape3, rank, world, conn, strong):
+    """z-slab of a 3-D grid: weak scaling stacks `world` copies along z,
+    strong scaling splits the given grid."""
+    nx, ny, nz = shape3
+    if strong:
+        V_all = nx * ny * nz
+        g = (nx, ny, nz)
+        z0, z1 = (nz * rank) // world, (nz * (rank + 1)) // world
+    else:
+        g = (nx, ny, nz * world)
+        z0, z1 = nz * rank, nz * (rank + 1)
+        V_all = nx * ny * nz * world
+    v0, v1 = nx * ny * z0, nx * ny * z1
+    Eu, Ev = pfdr.gen_grid_edges(g, conn, (v0, v1))
+    return g, V_all, v0, v1, Eu, Ev
+
+
+class Headline(Workload):
+    name = "headline"
+    metric = "PFDR iter/s and Medge-updates/s, 10M-vertex 6-NN graph, 1/2/4/8 MI355X"
+    SHAPE = (250, 200, 200)
+
+    def inputs(self, rank, world):
+        nx, ny, nz = self.SHAPE
+        g = (nx, ny, nz * world)
+        V = nx * ny * nz
+        v0 = rank * V
+        Eu, Ev = pfdr.gen_knn_jitter_grid(g, 6, 6, 0.25, (v0, v0 + V))
+        Y = pfdr.gen_piecewise(nx, V * world, 2, np.float32, 0.2, (v0, v0 + V))
+        E = Eu.size
+        kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
+                  Y=Y, La_l1=np.full(V, 0.01, np.float32), rho=1.5, condMin=1e-3)
+        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=rank * E,
+                    desc="PFDR_graph_quadratic_d1_l1<float>, identity A, l1 + TV, jittered "
+                         "%dx%dx%d grid, 6-NN (V=%d, E=%d per GPU)" % (nx, ny, nz, V, E),
+                    graph="%dx%dx%d" % g)
+
+
+class C1(Workload):
+    """config 1: 256x256 4-NN, identity A (l22), fp64; time to tolerance"""
+    name = "c1"
+    metric = "PFDR_graph_quadratic_d1_l1<double> 256x256 4-NN l22: iterations/s to difTol 1e-6"
+    dtype = np.float64
+    edge_bytes, vertex_bytes = 80, 40
+    steps = 10000
+    partitionable = False
+
+    def inputs(self, rank, world):
+        from cp_pfdr_graph_d1_amd.graphs import grid_graph, uniform
+        Eu, Ev = grid_graph((256, 256), 4)
+        V = 65536
+        x = np.arange(V) % 256
+        Y = (np.where(x < 128, 1.0, -0.5) + (2 * uniform(1, np.arange(V)) - 1) * 0.2)
+        E = Eu.size
+        kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1), X0=np.zeros(V), Y=Y,
+                  La_l1=np.full(V, 0.01), rho=1.5, condMin=1e-3, difTol=1e-6,
+                  Ltype=pfdr.DIAG, record_dif=True)
+        return dict(V=V, E=E, kw=kw, vtx_begin=0, e_offset=0, converge=True,
+                    desc="C1: 256x256 4-NN, identity A, fp64, difTol 1e-6", graph="256x256")
+
+
+class C2(Workload):
+    """config 2: 256^3 6-NN grid, identity A, fp32 (weak: one 256^3 per GPU)"""
+    name = "c2"
+    metric = "PFDR_graph_quadratic_d1_l1<float> 256^3 6-NN: Medge-updates/s"
+
+    def inputs(self, rank, world):
+        g, V_all, v0, v1, Eu, Ev = _grid_slab((256, 256, 256), rank, world, 6, strong=False)
+        V = v1 - v0
+        Y = pfdr.gen_piecewise(256, V_all, 2, np.float32, 0.2, (v0, v1))
+        E = Eu.size
+        kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
+                  Y=Y, La_l1=np.full(V, 0.01, np.float32), rho=1.5, condMin=1e-3)
+        # edges are emitted per vertex in order: global ids are contiguous per rank
+        e0 = 0 if rank == 0 else pfdr.gen_grid_edges(g, 6, (0, v0))[0].size
+        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=e0,
+                    desc="C2: 256^3 6-NN grid (V=%d, E=%d per GPU), identity A, fp32" % (V, E),
+                    graph="%dx%dx%d" % g)
+
+
+class C3(Workload):
+    """config 3: dense A (N = 1024, V = 2M), fp32, single GPU (inputs on device)"""
+    name = "c3"
+    metric = "PFDR_graph_quadratic_d1_l1<float> dense A N=1024 V=2M: iterations/s"
+    partitionable = False
+    dominant = "gemv_cols"
+    steps = 20
+
+    def inputs(self, rank, world):
+        import torch
+        N, nx, ny = 1024, 2000, 1000
+        V = nx * ny
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3 + rank)
+        A = ((torch.rand((V, N), generator=g, device="cuda") - 0.5) * (12.0 / N) ** 0.5)
+        x0 = torch.zeros(V, device="cuda")
+        x0[: V // 3] = 1.0
+        x0[V // 3: 2 * V // 3] = -0.5
+        Y = torch.mv(A.t(), x0)
+        v = torch.rand(V, generator=g, device="cuda")
+        for _ in range(20):  # ||A||^2 by power iteration (the caller's L)
+            v = torch.mv(A.t().t(), torch.mv(A.t(), v))
+            v = v / v.norm()
+        L = torch.dot(torch.mv(A.t(), v), torch.mv(A.t(), v)).reshape(1) * 1.01
+        Eu, Ev = pfdr.gen_grid_edges((nx, ny), 4)
+        E = Eu.size
+        dev = lambda a, t=torch.float32: torch.as_tensor(a, dtype=t, device="cuda")
+        kw = dict(Eu=dev(Eu, torch.int32), Ev=dev(Ev, torch.int32),
+                  La_d1=torch.full((E,), 0.05, device="cuda"), X0=torch.zeros(V, device="cuda"),
+                  Y=Y.contiguous(), A=A.contiguous(), N=N,
+                  La_l1=torch.full((V,), 0.005, device="cuda"), L=L, Ltype=pfdr.SCAL,
+                  rho=1.5, condMin=1e-3, device=True)
+        self._keep = (A, Y, L, kw)
+        self.N = N
+        return dict(V=V, E=E, kw=kw, vtx_begin=0, e_offset=0,
+                    desc="C3: dense A N=1024 x V=2M fp32 (8.2 GB), 2000x1000 4-NN, direct (N>0) "
+                         "path (A^tA precomputed is V^2 = 4e12 entries: infeasible at V=2M)",
+                    graph="2000x1000")
+
+    def dominant_bytes(self, V, E):
+        # one pass over A (column dots P = -A^t R), + X, Ga, R
+        return 4 * self.N * V + 12 * V
+
+    def iteration_bytes(self, V, E):
+        # two passes over A (R = Y - A X, then P = -A^t R) + the graph
+        return 2 * 4 * self.N * V + self.edge_bytes * E + self.vertex_bytes * V
+
+
+class C4(Workload):
+    """config 4: simplex K = 10, KL al = 0.1, 2236^2 8-neighbour grid, fp32"""
+    name = "c4"
+    metric = "PFDR_graph_loss_d1_simplex<float> K=10 KL 5M-vertex 8-NN: Medge-updates/s"
+    kind = pfdr.PFDR_KIND_SIMPLEX
+    partitionable = False
+    dominant = "sx_edge_sweep"
+    K = 10
+    edge_bytes = 8 + 9 * 10 * 4
+    vertex_bytes = 10 * 4 * 4
+    steps = 20
+
+    def inputs(self, rank, world):
+        from cp_pfdr_graph_d1_amd.graphs import simplex_observation
+        n = 2236
+        V = n * n
+        Eu, Ev = pfdr.gen_grid_edges((n, n), 8)
+        v = np.arange(V)
+        lab = ((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)
+        Q = simplex_observation(V, self.K, 4, lab, np.float32)
+        E = Eu.size
+        kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32), X0=Q.copy(), Y=Q,
+                  K=self.K, al=0.1, rho=1.0, condMin=0.1)
+        return dict(V=V, E=E, kw=kw, vtx_begin=0, e_offset=0,
+                    desc="C4: 2236^2 8-neighbour grid (V=%d, E=%d), K=10, KL al=0.1, fp32" % (V, E),
+                    graph="2236x2236")
+
+
+class C5(Workload):
+    """config 5: bounds [0,1], 640^3 6-NN, fp32, split across the GPUs
+    (strong scaling: the 262M-vertex graph is fixed)"""
+    name = "c5"
+    metric = "PFDR_graph_quadratic_d1_bounds<float> 640^3 6-NN (1.6B directed edges): Medge-updates/s"
+    kind = pfdr.PFDR_KIND_BOUNDS
+    scaling = "strong"
+    vertex_bytes = 16
+    steps = 10
+
+    def inputs(self, rank, world):
+        g, V_all, v0, v1, Eu, Ev = _grid_slab((640, 640, 640), rank, world, 6, strong=True)
+        V = v1 - v0
+        Y = pfdr.gen_piecewise(640, V_all, 5, np.float32, 0.2, (v0, v1))
+        E = Eu.size
+        e0 = 0 if rank == 0 else pfdr.gen_grid_edges(g, 6, (0, v0))[0].size
+        kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
+                  Y=Y, lo=0.0, hi=1.0, rho=1.5, condMin=1e-3)
+        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=e0,
+                    desc="C5: 640^3 6-NN grid (V=262,144,000, E=785,203,200), bounds [0,1], fp32, "
+                         "%d GPU slab(s)" % world, graph="640x640x640")
+
+
+WORKLOADS = {w.name: w for w in (Headline(), C1(), C2(), C3(), C4(), C5())}
