@@ -176,7 +176,7 @@ def main():
         dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
         el_max, E_all = float(tt[0].item()), int(tt[1].item())
-    names = (wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep", "sx_average",
+    names = (wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep", "sx_vertex_sweep", "sx_average",
              "sx_project", "gemv_rows", "gemv_cols", "halo_pull", "halo_push")
     stats = {k: sess.kernel_stats(k) for k in names}
     res = sess.result()

@@ -634,13 +634,18 @@ static int quadratic_host(const char *fn, int kind, int V, int E, int N, real *X
     p.record_obj = Obj != nullptr;
     p.record_dif = Dif != nullptr;
     try {
+        CallTrace tr(fn);
         if (verbose) { printf("Initializing constants and variables... "); fflush(stdout); }
         std::unique_ptr<QuadSession<real>> s(new QuadSession<real>(&p));
         if (verbose) { printf("done.\nPreconditioned forward-Douglas-Rachford algorithm\n"); fflush(stdout); }
+        tr.setup_done();
         s->run(itMax);
+        tr.run_done();
         int its = 0;
         s->result(X, &its, Obj, Dif);
         if (it) *it = its;
+        s.reset();
+        tr.finish(V, E, N, 1, its);
     } catch (const HipError &h) {
         return report_error(fn, h);
     } catch (const std::exception &ex) {

@@ -1,5 +1,6 @@
 // Runtime pieces of libpfdr_mi355x.so that are not kernels: error state,
 // library stream, profiler, session C ABI dispatch.
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -20,6 +21,30 @@ static void set_error(const char *fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     g_last_error = buf;
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static bool trace_enabled() {
+    static const bool on = [] {
+        const char *v = getenv("PFDR_TRACE");
+        return v && v[0] && v[0] != '0';
+    }();
+    return on;
+}
+
+CallTrace::CallTrace(const char *name) : fn(name), on(trace_enabled()), t0(on ? now_ms() : 0) {}
+void CallTrace::setup_done() { if (on) t_setup = now_ms(); }
+void CallTrace::run_done() { if (on) t_run = now_ms(); }
+void CallTrace::finish(long V, long E, long N, int K, int it) {
+    if (!on) return;
+    const double t1 = now_ms();
+    fprintf(stderr, "[pfdr] %s V=%ld E=%ld N=%ld K=%d it=%d setup_ms=%.3f run_ms=%.3f "
+            "copy_ms=%.3f total_ms=%.3f\n", fn, V, E, N, K, it, t_setup - t0,
+            t_run - t_setup, t1 - t_run, t1 - t0);
 }
 
 int report_error(const char *fn, const HipError &h) {

@@ -57,6 +57,18 @@ class SessionBase {
     int device = 0;
 };
 
+// PFDR_TRACE=1: one stderr line per drop-in call (sizes, iterations, setup /
+// iteration / copy-back wall times) -- the view of a CP caller's inner loop.
+struct CallTrace {
+    const char *fn;
+    bool on;
+    double t0, t_setup = 0, t_run = 0;
+    explicit CallTrace(const char *name);
+    void setup_done();
+    void run_done();
+    void finish(long V, long E, long N, int K, int it);
+};
+
 }  // namespace pfdr
 
 struct pfdr_session {

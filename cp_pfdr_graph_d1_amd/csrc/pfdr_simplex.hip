@@ -7,13 +7,14 @@
 //   per iteration:
 //     k_sx_edge_sweep   : K-wide TV prox on every (edge, label) + relaxed Z
 //                         update + DR contributions W*Z      ref :589-634
-//     k_sx_average      : ordered per-(vertex, label) DR average over the
-//                         incidence CSR (the reference parallelises this
-//                         over labels only, :636-648)
-//     k_sx_project      : per-vertex metric simplex projection, evolution
+//     k_sx_vertex_sweep : (K <= 64) ordered per-(vertex, label) DR average
+//                         over the incidence CSR (the reference
+//                         parallelises it over labels only, :636-648),
+//                         per-vertex metric simplex projection, evolution
 //                         partials (l1 or label changes) and the NEXT
 //                         explicit step FP                  ref :651-691,
 //                                                               :567-587
+//     (K > 64: k_sx_average then k_sx_project, the same two halves)
 //     k_sx_finalize     : stop / recondition flags (when tracked)
 // Layouts: P, Q, Ga, GaQ, FP are K-by-V (index v*K + k) as in the reference;
 // edge state is K-by-E; the DR contributions are wz[side][e][k].
@@ -395,8 +396,16 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= EK) return;
     const int K = c.K;
-    const long e = i / K;
-    const int k = (int)(i - e * K);
+    long e;
+    int k;
+    if (EK <= 0xffffffffl) {  // 32-bit division (uniform branch)
+        const unsigned ue = (unsigned)i / (unsigned)K;
+        e = ue;
+        k = (int)((unsigned)i - ue * (unsigned)K);
+    } else {
+        e = i / K;
+        k = (int)(i - e * K);
+    }
     const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
     real a = FP[u] - Zu[i];
     const real b = FP[v] - Zv[i];
@@ -436,8 +445,10 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     }
     Zu[i] = zu;
     Zv[i] = zv;
-    wz[i] = Wu[i] * zu;
-    wz[EK + i] = Wv[i] * zv;
+    if (wz) {
+        wz[i] = Wu[i] * zu;
+        wz[EK + i] = Wv[i] * zv;
+    }
 }
 
 template <typename real>
@@ -496,6 +507,118 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
     if (a.track) {
         dif = block_sum(dif, red);
         if (threadIdx.x == 0) a.part[blockIdx.x] = dif;
+    }
+}
+
+// Fused vertex sweep (K <= 64): ordered DR average, metric projection,
+// evolution partials and the next explicit step in one pass.  A block owns
+// vb = floor(256 / K) consecutive vertices and gives each (vertex, label)
+// one lane: the lanes of a vertex read its incidence list together (one
+// broadcast load of the slot, then K contiguous contributions, so each
+// gathered edge costs one 4K-byte run instead of K scattered words), the
+// sums meet in LDS where one lane per vertex runs the projection of
+// ref src/proj_simplex_metric.cpp:41-80, and the lanes write P and FP back
+// coalesced.  Summation order per (v, k) is increasing slot 2e + side, as in
+// the reference's sequential average (ref :636-648).
+template <typename real>
+struct SxVArgs {
+    int V, vb;
+    long EK;
+    SxConst<real> c;
+    const int *ptr;
+    const unsigned *idx;
+    const real *wz, *Ga, *GaQ, *Q;
+    const real *Zu, *Zv, *Wu, *Wv;  // !WZ: contributions formed in the sweep
+    real *P, *FP, *lab;
+    int track;
+    real *part;
+    const Ctrl<real> *ctrl;
+};
+
+template <typename real, int NT, bool WZ>
+__global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real xs[NT], ms[NT];
+    __shared__ real red[NT / kWave];
+    const int K = a.c.K, vb = a.vb;
+    const int t = threadIdx.x;
+    const int vl = t / K;
+    const int k = t - vl * K;
+    const long v0 = (long)blockIdx.x * vb;
+    const long v = v0 + vl;
+    const bool live = vl < vb && v < a.V;
+    const long i = v * K + k;
+    if (live) {
+        const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
+        const real *__restrict__ wz = a.wz;
+        real s = real(0);
+        int j = j0;
+        // 8 slots, then 8 contributions in flight per lane; summed in order
+        for (; j + 8 <= j1; j += 8) {
+            unsigned sl[8];
+            real w[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
+            if (WZ) {
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    w[q] = wz[(long)(sl[q] & 1u) * a.EK + (long)(sl[q] >> 1) * K + k];
+            } else {  // W * Z formed here (the reference's product, same rounding)
+                real zq[8], wq[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const long o = (long)(sl[q] >> 1) * K + k;
+                    const bool sv = sl[q] & 1u;
+                    zq[q] = (sv ? a.Zv : a.Zu)[o];
+                    wq[q] = (sv ? a.Wv : a.Wu)[o];
+                }
+#pragma unroll
+                for (int q = 0; q < 8; q++) w[q] = wq[q] * zq[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) s += w[q];
+        }
+        for (; j < j1; j++) {
+            const unsigned slot = a.idx[j];
+            const long o = (long)(slot >> 1) * K + k;
+            if (WZ) s += wz[(long)(slot & 1u) * a.EK + o];
+            else s += (slot & 1u) ? a.Wv[o] * a.Zv[o] : a.Wu[o] * a.Zu[o];
+        }
+        xs[t] = s;
+        ms[t] = a.Ga[i];
+    }
+    __syncthreads();
+    real dif = real(0);
+    if (t < vb && v0 + t < a.V) {
+        real *x = xs + t * K;
+        proj_simplex_column<real, 1>(x, ms + t * K, K, real(1));
+        if (a.track == 2) {
+            real mx = x[0];
+            int l = 0;
+            for (int d = 1; d < K; d++) if (x[d] > mx) { mx = x[d]; l = d; }
+            const real fl = (real)l;
+            if (fl != a.lab[v0 + t]) { dif = real(1); a.lab[v0 + t] = fl; }
+        }
+    }
+    __syncthreads();
+    if (live) {
+        const real p = xs[t];
+        if (a.track == 1) {
+            real d = a.P[i] - p;
+            if (d < real(0)) d = -d;
+            dif += d;
+        }
+        a.P[i] = p;
+        a.FP[i] = sx_explicit(a.c, p, a.GaQ[i], a.Q[i]);
+    }
+    if (a.track) {
+        dif = wave_sum(dif);
+        if (NT > kWave) {
+            if ((t & (kWave - 1)) == 0) red[t / kWave] = dif;
+            __syncthreads();
+            if (t == 0) for (int q = 1; q < NT / kWave; q++) dif += red[q];
+        }
+        if (t == 0) a.part[blockIdx.x] = dif;
     }
 }
 
@@ -621,6 +744,12 @@ static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipS
 
 static int mask_words(int D) { return (D + 63) / 64; }
 
+// A/B switch: NAME=0 disables an optional fast path
+static bool env_flag_off(const char *name) {
+    const char *v = getenv(name);
+    return v && v[0] == '0';
+}
+
 template <typename real>
 static void launch_proj(real *X, const real *M, int D, int N, int nm,
                         const real *A, int na, hipStream_t s) {
@@ -655,6 +784,12 @@ class SimplexSession final : public SessionBase {
     Ctrl<real> *hctrl_ = nullptr;
     Incidence inc_;
     int nbv_, nbe_;
+    int vb_ = 0, nbs_ = 0, sx_nt_ = 256;  // fused vertex sweep: vertices, blocks, threads
+    // false (default): the vertex sweep forms W*Z from the gathered Z and W
+    // (K contiguous words per incidence), so the edge sweep neither reads W
+    // nor writes contributions: 28 instead of 44 streamed bytes per (e, k)
+    // (C4: 2.42 -> 2.17 ms/iteration)
+    bool sx_wz_ = false;
     int it_ = 0;
     bool stopped_ = false;
     int chunk_ = 32;
@@ -717,14 +852,24 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s);
     sx_copy_in(Q_, p->Y, VK_, mem, s);
     sx_copy_in(P_, p->X, VK_, mem, s);
-    FP_.alloc(VK_); Pavg_.alloc(VK_); Ga_.alloc(VK_); GaQ_.alloc(VK_); invAux_.alloc(VK_);
+    if (K_ <= 64 && !env_flag_off("PFDR_SX_FUSED")) {
+        const char *nt = getenv("PFDR_SX_NT");  // threads per block: 64 (default) or 256
+        sx_nt_ = (nt && atoi(nt) == 64) ? 64 : 256;
+        const char *wz = getenv("PFDR_SX_WZ");  // 1: edge sweep stores W*Z (A/B)
+        sx_wz_ = wz && wz[0] == '1';
+        vb_ = sx_nt_ / K_;
+        nbs_ = (int)((V_ + vb_ - 1) / vb_);
+    } else {
+        Pavg_.alloc(VK_);
+    }
+    FP_.alloc(VK_); Ga_.alloc(VK_); GaQ_.alloc(VK_); invAux_.alloc(VK_);
     const size_t EKn = EK_ ? EK_ : 1;
     Zu_.alloc(EKn); Zv_.alloc(EKn); Wu_.alloc(EKn); Wv_.alloc(EKn);
     if (c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn);
     nbv_ = grid_for(V_);
     nbe_ = grid_for(E_);
-    part_.alloc(nbv_);
+    part_.alloc(std::max(nbv_, nbs_));
     if (rec_obj_) { opart_.alloc((size_t)nbv_ + nbe_ + 1); Obj_.alloc((size_t)itMax_ + 1); }
     if (rec_dif_) Dif_.alloc(itMax_ > 0 ? itMax_ : 1);
     if (track_ == 2) {
@@ -801,14 +946,30 @@ void SimplexSession<real>::body() {
         ProfScope ps(prof, "sx_edge_sweep", s);
         k_sx_edge_sweep<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
                                                                Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               Wu_.p, Wv_.p, wz_.p, rho_, c);
+                                                               Wu_.p, Wv_.p,
+                                                               (vb_ && !sx_wz_) ? nullptr : wz_.p,
+                                                               rho_, c);
     }
-    {
-        ProfScope ps(prof, "sx_average", s);
-        k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, EK_, inc_.ptr.p, inc_.idx.p,
-                                                            wz_.p, Pavg_.p, c);
-    }
-    {
+    if (vb_) {
+        SxVArgs<real> a{};
+        a.V = V_; a.vb = vb_; a.EK = EK_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
+        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.FP = FP_.p;
+        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        ProfScope ps(prof, "sx_vertex_sweep", s);
+        a.Zu = Zu_.p; a.Zv = Zv_.p; a.Wu = Wu_.p; a.Wv = Wv_.p;
+        if (sx_nt_ == 256) {
+            if (sx_wz_) k_sx_vertex_sweep<real, 256, true><<<nbs_, 256, 0, s>>>(a);
+            else k_sx_vertex_sweep<real, 256, false><<<nbs_, 256, 0, s>>>(a);
+        } else {
+            if (sx_wz_) k_sx_vertex_sweep<real, 64, true><<<nbs_, 64, 0, s>>>(a);
+            else k_sx_vertex_sweep<real, 64, false><<<nbs_, 64, 0, s>>>(a);
+        }
+    } else {
+        {
+            ProfScope ps(prof, "sx_average", s);
+            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, EK_, inc_.ptr.p,
+                                                                inc_.idx.p, wz_.p, Pavg_.p, c);
+        }
         SxProjArgs<real> a{};
         a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
         a.P = P_.p; a.FP = FP_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
@@ -816,7 +977,7 @@ void SimplexSession<real>::body() {
         launch_project(a);
     }
     if (gated)
-        k_sx_finalize<real><<<1, kBlock, 0, s>>>(nbv_, part_.p, V_, track_, ctrl_.p,
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(vb_ ? nbs_ : nbv_, part_.p, V_, track_, ctrl_.p,
                                                  rec_dif_ ? Dif_.p : nullptr);
     PFDR_HIP(hipGetLastError());
     if (rec_obj_) objective();
@@ -902,13 +1063,18 @@ static int simplex_host(const char *fn, int K, int V, int E, real al, const real
     p.record_obj = Obj != nullptr;
     p.record_dif = Dif != nullptr;
     try {
+        CallTrace tr(fn);
         if (verbose) { printf("Initializing constants and variables... "); fflush(stdout); }
         std::unique_ptr<SimplexSession<real>> s(new SimplexSession<real>(&p));
         if (verbose) { printf("done.\nPreconditioned forward-Douglas-Rachford algorithm\n"); fflush(stdout); }
+        tr.setup_done();
         s->run(itMax);
+        tr.run_done();
         int its = 0;
         s->result(P, &its, Obj, Dif);
         if (it) *it = its;
+        s.reset();
+        tr.finish(V, E, 0, K, its);
     } catch (const HipError &h) {
         return report_error(fn, h);
     } catch (const std::exception &ex) {

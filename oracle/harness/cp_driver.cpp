@@ -11,7 +11,9 @@
  *        float64 CP_difTol, PFDR_difTol, rho, condMin,
  *        real Y[V], real A[V] (diagonal of A^tA), int32 Eu[E], Ev[E],
  *        real La_d1[E], real La_l1[V]
- *   out: int32 rV, CP_it, int32 Cv[V], real rX[rV] */
+ *   out: int32 rV, CP_it, int32 Cv[V], real rX[rV]
+ * stderr: the wall time of the CP call (cp_time_s=...) */
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -34,9 +36,12 @@ static int run(FILE *f, FILE *o, const int *h, const double *d) {
     int rV = 0, CP_it = 0;
     std::vector<int> Cv(V);
     real *rX = NULL;
+    const auto t0 = std::chrono::steady_clock::now();
     CP_PFDR_graph_quadratic_d1_l1<real>(V, E, 0, &rV, Cv.data(), &rX, Y.data(), A.data(),
         Eu.data(), Ev.data(), Ld.data(), Ll.data(), pos, (real)d[0], CP_itMax, &CP_it,
         (real)d[2], (real)d[3], (real)0, (real)d[1], PFDR_itMax, NULL, NULL, NULL, 0, NULL);
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "cp_time_s=%.6f rV=%d CP_it=%d\n", el, rV, CP_it);
     fwrite(&rV, 4, 1, o);
     fwrite(&CP_it, 4, 1, o);
     fwrite(Cv.data(), 4, V, o);
