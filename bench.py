@@ -182,6 +182,7 @@ def main():
     res = sess.result()
     finite = bool(np.all(np.isfinite(res[0])))
     dev_bytes = sess.device_bytes()
+    reordered = bool(sess.query("reordered"))
     sess.close()
     if world > 1:
         dist.destroy_process_group()
@@ -213,6 +214,7 @@ def main():
             "setup_s": round(setup_s, 3),
             "input_generation_s": round(gen_s, 3),
             "device_bytes": dev_bytes,
+            "relabelled": reordered,
             "finite": finite,
         },
         "roofline": {

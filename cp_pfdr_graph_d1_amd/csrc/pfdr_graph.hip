@@ -135,6 +135,11 @@ __global__ void k_keyed_ptr(const unsigned long long *__restrict__ skey, long n,
     for (long v = kp + 1; v <= kc; v++) ptr[v] = (int)i;
 }
 
+void keyed_rows(const unsigned long long *skey, long n, int V, int *ptr, hipStream_t s) {
+    k_keyed_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey, n, V, ptr);
+    PFDR_HIP(hipGetLastError());
+}
+
 void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int V,
                            Incidence &inc, hipStream_t s) {
     inc.V = V;

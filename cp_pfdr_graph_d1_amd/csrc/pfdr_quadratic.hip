@@ -3,9 +3,13 @@
 //  src/PFDR_graph_quadratic_d1_bounds.cpp:244-530), single GPU or one rank
 // of a 1-D vertex-range partition (pfdr_halo.hpp).  Kernels: see
 // pfdr_quadratic_kernels.hpp.
+#include <cstring>
 #include <stdexcept>
 
+#include <rocprim/rocprim.hpp>
+
 #include "pfdr_halo.hpp"
+#include "pfdr_order.hpp"
 #include "pfdr_quadratic_kernels.hpp"
 
 namespace pfdr {
@@ -22,6 +26,39 @@ static void copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStre
 
 template <typename real>
 static int dtype_of() { return sizeof(real) == 4 ? PFDR_F32 : PFDR_F64; }
+
+// d <- d[map] (map[i] = source index of element i)
+template <typename T>
+static void permute(DevBuf<T> &d, const int *map, size_t n, hipStream_t s) {
+    if (!d.p || !n) return;
+    DevBuf<T> t(n);
+    k_gather<T><<<grid_for(n), kBlock, 0, s>>>((long)n, d.p, map, t.p);
+    PFDR_HIP(hipGetLastError());
+    std::swap(d.p, t.p);
+    std::swap(d.n, t.n);
+}
+
+// edges sorted by their new u end (stable in the edge id): eorig[p] = the
+// original id of the edge now at position p; endpoints relabelled by where
+__global__ void k_edge_order_keys(long E, const int *__restrict__ Eu, const int *__restrict__ where,
+                                  unsigned long long *__restrict__ keys, unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    keys[e] = ((unsigned long long)where[Eu[e]] << 32) | (unsigned)e;
+    vals[e] = (unsigned)e;
+}
+
+__global__ void k_edge_relabel(long E, const unsigned *__restrict__ eorig,
+                               const int *__restrict__ Eu, const int *__restrict__ Ev,
+                               const int *__restrict__ where, int *__restrict__ nEu,
+                               int *__restrict__ nEv, int *__restrict__ emap) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const unsigned e = eorig[p];
+    nEu[p] = where[Eu[e]];
+    nEv[p] = where[Ev[e]];
+    emap[p] = (int)e;
+}
 
 template <typename real>
 class QuadSession final : public SessionBase {
@@ -47,6 +84,12 @@ class QuadSession final : public SessionBase {
     int xcd_e_ = 0, xcd_v_ = 1;  // XCD-aware block order (edge / vertex sweep)
     int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
+    // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
+    // emap_[edge position] = original edge id (setup only)
+    bool reordered_ = false;
+    DevBuf<int> order_, where_, emap_;
+    DevBuf<unsigned> eorig_;
+    DevBuf<real> amp_orig_;
     // device state
     DevBuf<int> Eu_, Ev_;
     DevBuf<real> La_d1_, La_l1_, Y_, A_, L_;
@@ -143,6 +186,14 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     const size_t asz = mode_ == A_DIRECT ? (size_t)N_ * V : mode_ == A_ATA ? V * V
                      : mode_ == A_DIAG ? V : 0;
     copy_in(A_, p->A, asz, mem, s);
+    if (reordered_) {  // inputs into the internal labels (identity / diagonal A only)
+        permute(La_d1_, emap_.p, E, s);
+        permute(La_l1_, order_.p, V, s);
+        permute(Y_, order_.p, V, s);
+        permute(A_, order_.p, V, s);
+        emap_.release();
+        amp_orig_.alloc(V);
+    }
     // scalar cap of the metric (ref :225-229), in `real` arithmetic like the reference
     real cap = real(1.9) * (real(2) - rho_);
     if (p->L && !Ldiag_) {
@@ -154,9 +205,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
     cap_ = cap;
     if (Ldiag_) copy_in(L_, p->L, V, mem, s);
+    if (reordered_ && Ldiag_) permute(L_, order_.p, V, s);
     {   // iterate (X, P) pairs, owned then ghost vertices
         DevBuf<real> X0;
         copy_in(X0, p->X, V, mem, s);
+        if (reordered_) permute(X0, order_.p, V, s);
         xp_.alloc(Vg);
         PFDR_HIP(hipMemsetAsync(xp_.p, 0, Vg * sizeof(R2<real>), s));
         k_xp_init<real><<<grid_for(V), kBlock, 0, s>>>(V_, X0.p, xp_.p);
@@ -239,6 +292,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_})
         acc(b->n * sizeof(real));
     acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
+    order_.release();  // inputs are in the internal labels now
+    acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
 
 // endpoints (local ids), partition plan, incidence CSR keyed by global edge id
@@ -250,6 +305,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     Eu_.alloc(E ? E : 1);
     Ev_.alloc(E ? E : 1);
     DevBuf<unsigned> eg;
+    const unsigned *eg_ptr = nullptr;  // original edge ids of a relabelled graph
     long e_offset = 0;
     if (p->nranks > 1 || p->comm) {
         if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks || !p->comm)
@@ -298,6 +354,32 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         }
     }
     check_endpoints(Eu_.p, Ev_.p, E_, Vg_, s);
+    if (!halo_ && E_ && (mode_ == A_IDENT || mode_ == A_DIAG) && p->reorder != PFDR_REORDER_OFF &&
+        (p->reorder == PFDR_REORDER_ON || labels_scattered(Eu_.p, Ev_.p, E_, V_, s)) &&
+        bfs_order(Eu_.p, Ev_.p, E_, V_, order_, where_, s)) {
+        // relabel the vertices and sort the edges by their new u end; the
+        // incidence keys keep the original edge ids (summation order)
+        reordered_ = true;
+        reordered = 1;
+        DevBuf<unsigned long long> k(E), ks(E);
+        DevBuf<unsigned> v(E);
+        eorig_.alloc(E);
+        k_edge_order_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, where_.p, k.p, v.p);
+        PFDR_HIP(hipGetLastError());
+        size_t tb = 0;
+        PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tb, k.p, ks.p, v.p, eorig_.p, E, 0, 64, s));
+        DevBuf<char> tmp(tb ? tb : 1);
+        PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tb, k.p, ks.p, v.p, eorig_.p, E, 0, 64, s));
+        DevBuf<int> nu(E), nv(E);
+        emap_.alloc(E);
+        k_edge_relabel<<<grid_for(E), kBlock, 0, s>>>(E_, eorig_.p, Eu_.p, Ev_.p, where_.p, nu.p,
+                                                      nv.p, emap_.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));
+        std::swap(Eu_.p, nu.p);
+        std::swap(Ev_.p, nv.p);
+        eg_ptr = eorig_.p;
+    }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
     const long n = 2 * E_ + R;
@@ -305,8 +387,8 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     DevBuf<unsigned long long> keys(n ? n : 1);
     DevBuf<unsigned> vals(n ? n : 1);
     if (E_) {
-        k_slot_keys<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, V_, eg.p, e_offset,
-                                                    keys.p, vals.p);
+        k_slot_keys<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, V_, eg_ptr ? eg_ptr : eg.p,
+                                                    e_offset, keys.p, vals.p);
         PFDR_HIP(hipGetLastError());
     }
     if (R) {
@@ -318,6 +400,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         PFDR_HIP(hipStreamSynchronize(s));
     }
     build_incidence_keyed(keys.p, vals.p, n, V_, inc_, s);
+    eorig_.release();
 }
 
 template <typename real>
@@ -405,7 +488,12 @@ void QuadSession<real>::amplitude(bool init) {
     PFDR_HIP(hipGetLastError());
     const bool seeded = halo_ && halo_->tr->rank > 0;
     if (halo_) halo_->tr->chain_recv(red_.p + 3, sizeof(real), s);
-    k_seq_sum<real><<<1, kBlock, 0, s>>>(V_, absval_.p, seeded ? red_.p + 3 : nullptr, nbv_,
+    const real *amp = absval_.p;
+    if (reordered_) {  // the reference's sequential sum runs in the caller's labels
+        k_gather<real><<<nbv_, kBlock, 0, s>>>(V_, absval_.p, where_.p, amp_orig_.p);
+        amp = amp_orig_.p;
+    }
+    k_seq_sum<real><<<1, kBlock, 0, s>>>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_,
                                          cnt_part_.p, csum_.p, ccnt_.p);
     PFDR_HIP(hipGetLastError());
     if (halo_) {
@@ -585,7 +673,10 @@ int QuadSession<real>::run(int iters) {
 template <typename real>
 void *QuadSession<real>::device_x() {
     if (xout_.n < (size_t)V_) xout_.alloc(V_);
-    k_x_extract<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xp_.p, xout_.p);
+    if (reordered_)
+        k_x_extract_perm<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xp_.p, where_.p, xout_.p);
+    else
+        k_x_extract<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xp_.p, xout_.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipStreamSynchronize(stream));
     return xout_.p;

@@ -144,6 +144,22 @@ __global__ void k_x_extract(int V, const R2<real> *__restrict__ xp,
     if (v < V) X[v] = xp[v].x;
 }
 
+// X in the caller's labels from a relabelled session: X[v] = xp[where[v]].x
+template <typename real>
+__global__ void k_x_extract_perm(int V, const R2<real> *__restrict__ xp,
+                                 const int *__restrict__ where, real *__restrict__ X) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) X[v] = xp[where[v]].x;
+}
+
+// dst[i] = src[map[i]] (relabelling gathers)
+template <typename T>
+__global__ void k_gather(long n, const T *__restrict__ src, const int *__restrict__ map,
+                         T *__restrict__ dst) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[map[i]];
+}
+
 // Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324); half-edge layout Z2[2e + side]
 template <typename real>
 __global__ void k_z_init(long E, const int *__restrict__ Eu,

@@ -152,7 +152,7 @@ using namespace pfdr;
     }
 
 extern "C" const char *pfdr_last_error(void) { return g_last_error.c_str(); }
-extern "C" int pfdr_abi_version(void) { return 1; }
+extern "C" int pfdr_abi_version(void) { return 2; }
 extern "C" int pfdr_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return -1;
@@ -223,6 +223,14 @@ extern "C" int pfdr_session_sync(pfdr_session *s) {
 
 extern "C" int64_t pfdr_session_device_bytes(pfdr_session *s) {
     return s ? s->impl->device_bytes : -1;
+}
+
+extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value) {
+    if (!s || !what || !value) return report_error("pfdr_session_query", "null argument");
+    if (!strcmp(what, "reordered")) *value = s->impl->reordered;
+    else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
+    else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
+    return PFDR_OK;
 }
 
 extern "C" void pfdr_session_destroy(pfdr_session *s) {

@@ -52,6 +52,7 @@ class SessionBase {
                         void *Dif_host) = 0;
     virtual void *device_x() = 0;
     int64_t device_bytes = 0;
+    int64_t reordered = 0;  // internal locality relabelling applied
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

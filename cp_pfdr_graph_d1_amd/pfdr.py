@@ -26,6 +26,8 @@ PFDR_F32, PFDR_F64 = 0, 1
 PFDR_MEM_HOST, PFDR_MEM_DEVICE = 0, 1
 PFDR_KIND_L1, PFDR_KIND_BOUNDS, PFDR_KIND_SIMPLEX = 0, 1, 2
 SCAL, DIAG = 0, 1
+REORDER_AUTO, REORDER_ON, REORDER_OFF = 0, 1, 2
+ABI_VERSION = 2  # pfdr_abi_version() of the matching library
 
 # every C entry point of include/pfdr_mi355x.h
 EXPORTED = (
@@ -37,7 +39,7 @@ EXPORTED = (
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
-    "pfdr_session_device_bytes", "pfdr_session_destroy",
+    "pfdr_session_device_bytes", "pfdr_session_query", "pfdr_session_destroy",
     "pfdr_comm_unique_id", "pfdr_comm_init", "pfdr_comm_destroy",
     "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create",
     "pfdr_loopback_destroy", "pfdr_plan_create", "pfdr_plan_get",
@@ -69,6 +71,7 @@ class Problem(C.Structure):
         ("comm_kind", C.c_int),
         ("vtx_begin", C.c_int64), ("V_global", C.c_int64),
         ("e_global", C.c_void_p), ("e_offset", C.c_int64),
+        ("reorder", C.c_int),
     ]
 
 
@@ -103,6 +106,9 @@ def load():
         lib.pfdr_comm_init.argtypes = [C.POINTER(C.c_void_p), C.c_int,
                                        C.c_int, C.c_void_p]
         lib.pfdr_comm_destroy.argtypes = [C.c_void_p]
+        if lib.pfdr_abi_version() != ABI_VERSION:
+            raise PFDRError("%s has ABI %d, this module expects %d: rebuild it" % (
+                LIB_PATH, lib.pfdr_abi_version(), ABI_VERSION))
         _LIB = lib
     return _LIB
 
@@ -369,7 +375,7 @@ class Session:
                  difRcd=0.0, difTol=0.0, itMax=1000, record_obj=False,
                  record_dif=False, verbose=0, device=False, nranks=0, rank=0,
                  comm=None, comm_kind=0, vtx_begin=0, V_global=0, e_global=None,
-                 e_offset=0):
+                 e_offset=0, reorder=REORDER_AUTO):
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
@@ -400,6 +406,7 @@ class Session:
         p.comm = comm
         p.comm_kind = comm_kind
         p.vtx_begin, p.V_global, p.e_offset = vtx_begin, V_global, e_offset
+        p.reorder = reorder
         if e_global is not None:
             eg = np.ascontiguousarray(e_global, np.int64)
             self._keep.append(eg)
@@ -433,6 +440,12 @@ class Session:
             self.h, name.encode(), C.byref(n), C.byref(ms)),
             "pfdr_session_kernel_stats")
         return n.value, ms.value
+
+    def query(self, what):
+        v = C.c_int64(0)
+        _check(self.lib.pfdr_session_query(self.h, what.encode(), C.byref(v)),
+               "pfdr_session_query")
+        return v.value
 
     def device_bytes(self):
         return int(self.lib.pfdr_session_device_bytes(self.h))

@@ -56,7 +56,7 @@ extern "C" {
 #define PFDR_LIPSCHITZ_DIAG 1
 
 const char *pfdr_last_error(void);
-int pfdr_abi_version(void);          /* 1 */
+int pfdr_abi_version(void);          /* 2 (pfdr_problem.reorder added) */
 int pfdr_device_count(void);         /* visible HIP devices, <0 on error */
 
 /* ------------------------------------------------------------------ l1 -- */
@@ -111,6 +111,15 @@ int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
 #define PFDR_MEM_HOST 0    /* pointers are host memory (copied in) */
 #define PFDR_MEM_DEVICE 1  /* pointers are device memory of the current device */
 
+/* Internal vertex relabelling for cache locality (breadth-first order,
+ * pfdr_order.hip): AUTO applies it when the labels look random (V >= 2^20 and
+ * over a quarter of the edges span more than V/64 labels).  Inputs and
+ * outputs stay in the caller's labels; the reference's summation orders are
+ * kept, so results do not change. */
+#define PFDR_REORDER_AUTO 0
+#define PFDR_REORDER_ON 1
+#define PFDR_REORDER_OFF 2
+
 typedef struct pfdr_problem {
     int kind;             /* PFDR_KIND_* */
     int dtype;            /* PFDR_F32 / PFDR_F64: type of every real array */
@@ -140,6 +149,8 @@ typedef struct pfdr_problem {
     int64_t V_global;     /* total vertices over all ranks */
     const int64_t *e_global; /* global id of each local edge; NULL: e_offset + e */
     int64_t e_offset;
+    /* --- internal locality reordering (quadratic solvers, one GPU) -------- */
+    int reorder;          /* PFDR_REORDER_*; results are identical either way */
 } pfdr_problem;
 
 typedef struct pfdr_session pfdr_session;
@@ -163,6 +174,9 @@ int pfdr_session_kernel_stats(pfdr_session *s, const char *kernel,
 int pfdr_session_sync(pfdr_session *s);
 /* Bytes of device memory held by the session. */
 int64_t pfdr_session_device_bytes(pfdr_session *s);
+/* Session facts by name: "reordered" (1 when the internal locality
+ * relabelling is active), "device_bytes". */
+int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 
 /* ------------------------------------------------------ multi-GPU comm -- */

@@ -77,6 +77,29 @@ class Headline(Workload):
                     graph="%dx%dx%d" % g)
 
 
+class HeadlineShuffled(Headline):
+    """SURVEY.md §8(d) headline ordering (ii): the same graph and data with a
+    random vertex relabelling and an edge shuffle (seed 7).  Single GPU: a
+    vertex-range partition of random labels has no locality to exploit."""
+    name = "headline_shuffled"
+    partitionable = False
+
+    def inputs(self, rank, world):
+        from cp_pfdr_graph_d1_amd.graphs import uniform
+        d = Headline.inputs(self, 0, 1)
+        kw, V, E = d["kw"], d["V"], d["E"]
+        new_of = np.empty(V, np.int64)
+        new_of[np.argsort(uniform(7, np.arange(V)), kind="stable")] = np.arange(V)
+        eperm = np.argsort(uniform(7 * 0x9E3779B9, np.arange(E)), kind="stable")
+        kw["Eu"] = new_of[kw["Eu"][eperm]].astype(np.int32)
+        kw["Ev"] = new_of[kw["Ev"][eperm]].astype(np.int32)
+        Y = np.empty_like(kw["Y"])
+        Y[new_of] = kw["Y"]
+        kw["Y"] = Y
+        d["desc"] = d["desc"].replace("6-NN", "6-NN, random vertex labels + edge shuffle (seed 7)")
+        return d
+
+
 class C1(Workload):
     """config 1: 256x256 4-NN, identity A (l22), fp64; time to tolerance"""
     name = "c1"
@@ -218,4 +241,4 @@ class C5(Workload):
                          "%d GPU slab(s)" % world, graph="640x640x640")
 
 
-WORKLOADS = {w.name: w for w in (Headline(), C1(), C2(), C3(), C4(), C5())}
+WORKLOADS = {w.name: w for w in (Headline(), HeadlineShuffled(), C1(), C2(), C3(), C4(), C5())}
