@@ -13,15 +13,6 @@ namespace pfdr {
 
 // ------------------------------------------------------------- kernels --
 template <int B>
-__global__ void k_pack(int n, const int *__restrict__ idx, const char *__restrict__ src,
-                       char *__restrict__ dst) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    struct alignas(B) Blk { char b[B]; };
-    reinterpret_cast<Blk *>(dst)[i] = reinterpret_cast<const Blk *>(src)[idx[i]];
-}
-
-template <int B>
 __global__ void k_pack_u(int n, const unsigned *__restrict__ idx, const char *__restrict__ src,
                          char *__restrict__ dst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -30,27 +21,43 @@ __global__ void k_pack_u(int n, const unsigned *__restrict__ idx, const char *__
     reinterpret_cast<Blk *>(dst)[i] = reinterpret_cast<const Blk *>(src)[idx[i]];
 }
 
-static void pack(int n, const int *idx, const void *src, void *dst, int eb, hipStream_t s) {
+// any element size that is a multiple of 4 bytes: one lane per word
+template <typename I>
+__global__ void k_pack_words(long n, int words, const I *__restrict__ idx,
+                             const unsigned *__restrict__ src, unsigned *__restrict__ dst) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * words) return;
+    const long i = t / words;
+    const int w = (int)(t - i * words);
+    dst[t] = src[(long)idx[i] * words + w];
+}
+
+template <typename I>
+static void pack_any(int n, const I *idx, const void *src, void *dst, int eb, hipStream_t s) {
     if (n <= 0) return;
     const int g = grid_for(n);
     switch (eb) {
-        case 4: k_pack<4><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
-        case 8: k_pack<8><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
-        case 16: k_pack<16><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
-        default: throw std::runtime_error("pack: element size");
+        case 4: k_pack_u<4><<<g, kBlock, 0, s>>>(n, (const unsigned *)idx, (const char *)src,
+                                                 (char *)dst); break;
+        case 8: k_pack_u<8><<<g, kBlock, 0, s>>>(n, (const unsigned *)idx, (const char *)src,
+                                                 (char *)dst); break;
+        case 16: k_pack_u<16><<<g, kBlock, 0, s>>>(n, (const unsigned *)idx, (const char *)src,
+                                                   (char *)dst); break;
+        default:
+            if (eb % 4) throw std::runtime_error("pack: element size");
+            k_pack_words<I><<<grid_for((long)n * (eb / 4)), kBlock, 0, s>>>(
+                n, eb / 4, idx, (const unsigned *)src, (unsigned *)dst);
     }
     PFDR_HIP(hipGetLastError());
 }
 
+static void pack(int n, const int *idx, const void *src, void *dst, int eb, hipStream_t s) {
+    // owned local ids are non-negative: the unsigned gather reads them alike
+    pack_any<int>(n, idx, src, dst, eb, s);
+}
+
 static void pack_u(int n, const unsigned *idx, const void *src, void *dst, int eb, hipStream_t s) {
-    if (n <= 0) return;
-    const int g = grid_for(n);
-    switch (eb) {
-        case 4: k_pack_u<4><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
-        case 8: k_pack_u<8><<<g, kBlock, 0, s>>>(n, idx, (const char *)src, (char *)dst); break;
-        default: throw std::runtime_error("pack: element size");
-    }
-    PFDR_HIP(hipGetLastError());
+    pack_any<unsigned>(n, idx, src, dst, eb, s);
 }
 
 // ------------------------------------------------------------ Transport --
@@ -336,15 +343,23 @@ void Halo::pull(void *base, int eb, hipStream_t s) {
 }
 
 void Halo::push(const void *wz, void *tail, int eb, hipStream_t s) {
+    pack_u(push_send_off[tr->nranks], push_addr.p, wz, push_buffer(eb), eb, s);
+    push_packed(sendbuf.p, tail, eb, s);
+}
+
+void *Halo::push_buffer(int eb) {
+    const size_t need = (size_t)push_send_off[tr->nranks] * eb;
+    if (need > sendbuf.n) sendbuf.alloc(need);
+    return sendbuf.p;
+}
+
+void Halo::push_packed(const void *packed, void *tail, int eb, hipStream_t s) {
     const int n = tr->nranks;
-    const int tot = push_send_off[n];
-    if ((size_t)tot * eb > sendbuf.n) sendbuf.alloc((size_t)tot * eb);
-    pack_u(tot, push_addr.p, wz, sendbuf.p, eb, s);
     std::vector<const void *> sp(n);
     std::vector<void *> rp(n);
     std::vector<size_t> sb(n), rb(n);
     for (int q = 0; q < n; q++) {
-        sp[q] = sendbuf.p + (size_t)push_send_off[q] * eb;
+        sp[q] = (const char *)packed + (size_t)push_send_off[q] * eb;
         sb[q] = (size_t)push_send_cnt[q] * eb;
         rp[q] = (char *)tail + (size_t)push_recv_off[q] * eb;
         rb[q] = (size_t)push_recv_cnt[q] * eb;
@@ -505,6 +520,85 @@ void build_halo(Halo &h, int V, int64_t vtx_begin, long E, const int *Eu_g, cons
     Eu_l.swap(p.Eu_l);
     Ev_l.swap(p.Ev_l);
     PFDR_HIP(hipStreamSynchronize(s));
+}
+
+void partition_setup(const pfdr_problem *p, int V, long E, std::unique_ptr<Halo> &halo,
+                     DevBuf<int> &Eu, DevBuf<int> &Ev, DevBuf<unsigned> &eg, long *e_offset,
+                     hipStream_t s) {
+    if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks || !p->comm)
+        throw std::runtime_error("distributed session needs nranks, rank and comm");
+    halo.reset(new Halo());
+    halo->tr = p->comm_kind == PFDR_COMM_LOOPBACK
+                   ? make_loopback_transport(p->comm, p->nranks, p->rank)
+                   : make_rccl_transport(p->comm, p->nranks, p->rank);
+    // the plan is built on the host from the global endpoint ids
+    std::vector<int> hu, hv, lu, lv;
+    std::vector<int64_t> heg;
+    const int *pu = p->Eu, *pv = p->Ev;
+    const int64_t *peg = p->e_global;
+    if (p->mem == PFDR_MEM_DEVICE) {
+        hu.resize(E); hv.resize(E);
+        PFDR_HIP(hipMemcpy(hu.data(), p->Eu, E * 4, hipMemcpyDeviceToHost));
+        PFDR_HIP(hipMemcpy(hv.data(), p->Ev, E * 4, hipMemcpyDeviceToHost));
+        pu = hu.data(); pv = hv.data();
+        if (peg) {
+            heg.resize(E);
+            PFDR_HIP(hipMemcpy(heg.data(), p->e_global, E * 8, hipMemcpyDeviceToHost));
+            peg = heg.data();
+        }
+    }
+    build_halo(*halo, V, p->vtx_begin, E, pu, pv, peg, p->e_offset, lu, lv, s);
+    Eu.alloc(E ? E : 1);
+    Ev.alloc(E ? E : 1);
+    if (E) {
+        PFDR_HIP(hipMemcpyAsync(Eu.p, lu.data(), E * 4, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemcpyAsync(Ev.p, lv.data(), E * 4, hipMemcpyHostToDevice, s));
+    }
+    *e_offset = 0;
+    if (peg) {
+        std::vector<unsigned> e32(E);
+        for (long e = 0; e < E; e++) e32[e] = (unsigned)peg[e];
+        eg.alloc(E ? E : 1);
+        PFDR_HIP(hipMemcpyAsync(eg.p, e32.data(), E * 4, hipMemcpyHostToDevice, s));
+    } else {
+        *e_offset = (long)p->e_offset;
+    }
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+// keys of the 2E local slots (rows >= V dropped: ghost ends are pushed)
+__global__ void k_slot_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                            int V, const unsigned *__restrict__ eg, long e_offset,
+                            unsigned long long *__restrict__ keys, unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const unsigned long long g = eg ? (unsigned long long)eg[e] : (unsigned long long)(e_offset + e);
+    const int u = Eu[e], v = Ev[e];
+    keys[e] = (u < V) ? (((unsigned long long)u << 32) | (2 * g)) : ~0ull;
+    keys[E + e] = (v < V) ? (((unsigned long long)v << 32) | (2 * g + 1)) : ~0ull;
+    vals[e] = (unsigned)e;
+    vals[E + e] = (unsigned)(E + e);
+}
+
+void contribution_incidence(const int *Eu, const int *Ev, long E, int V, const unsigned *eg,
+                            long e_offset, const Halo *halo, Incidence &inc, hipStream_t s) {
+    const long R = halo ? halo->R : 0;
+    const long n = 2 * E + R;
+    DevBuf<unsigned long long> keys(n ? n : 1);
+    DevBuf<unsigned> vals(n ? n : 1);
+    if (E) {
+        k_slot_keys<<<grid_for(E), kBlock, 0, s>>>(E, Eu, Ev, V, eg, e_offset, keys.p, vals.p);
+        PFDR_HIP(hipGetLastError());
+    }
+    if (R) {
+        PFDR_HIP(hipMemcpyAsync(keys.p + 2 * E, halo->recv_keys.p, R * sizeof(unsigned long long),
+                                hipMemcpyDeviceToDevice, s));
+        std::vector<unsigned> tail(R);
+        for (long j = 0; j < R; j++) tail[j] = (unsigned)(2 * E + j);
+        PFDR_HIP(hipMemcpyAsync(vals.p + 2 * E, tail.data(), R * 4, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+    build_incidence_keyed(keys.p, vals.p, n, V, inc, s);
 }
 
 }  // namespace pfdr

@@ -21,7 +21,7 @@
 #include <memory>
 #include <vector>
 
-#include "pfdr_dev.hpp"
+#include "pfdr_graph.hpp"
 
 namespace pfdr {
 
@@ -78,8 +78,14 @@ struct Halo {
     // gather elem-sized values at idx into sendbuf, exchange, land the
     // peers' values in base + V (ghost range) — base holds Vg elements
     void pull(void *base, int elem_bytes, hipStream_t s);
-    // contributions: gather wz[push_addr] (real) and land the peers' in tail
+    // contributions: gather wz[push_addr] (elem_bytes each) and land the
+    // peers' in tail
     void push(const void *wz, void *tail, int elem_bytes, hipStream_t s);
+    // the same exchange for contributions already packed in push_addr order
+    // (the caller formed them, e.g. the simplex's K-wide W*Z)
+    void push_packed(const void *packed, void *tail, int elem_bytes, hipStream_t s);
+    // scratch buffer for push_packed of n elements
+    void *push_buffer(int elem_bytes);
 };
 
 // Host-only planning (no device needed; also exported through the C ABI so
@@ -113,5 +119,21 @@ void plan_finish(PlanHost &p, const std::vector<std::vector<int64_t>> &inreq,
 void build_halo(Halo &h, int V, int64_t vtx_begin, long E, const int *Eu_g,
                 const int *Ev_g, const int64_t *e_global, int64_t e_offset,
                 std::vector<int> &Eu_l, std::vector<int> &Ev_l, hipStream_t s);
+
+// Partitioned session setup (both solvers): the transport from p->comm, the
+// plan of this rank from its global edges (host planner + exchanges), and
+// the rank-local endpoint ids in Eu / Ev (device, E each; owned [0, V),
+// ghosts [V, V + G)).  Global edge ids: eg (device, 32-bit) when
+// p->e_global is given, else *e_offset = p->e_offset.
+void partition_setup(const pfdr_problem *p, int V, long E, std::unique_ptr<Halo> &halo,
+                     DevBuf<int> &Eu, DevBuf<int> &Ev, DevBuf<unsigned> &eg, long *e_offset,
+                     hipStream_t s);
+
+// Contribution CSR of both solvers: the 2E local slots (address e = u end,
+// E + e = v end) keyed by (local vertex, 2 e_global + side) — the
+// reference's summation order — then the halo's received tail (addresses
+// 2E + j, keys from the plan).  eg: global edge ids or NULL (e_offset + e).
+void contribution_incidence(const int *Eu, const int *Ev, long E, int V, const unsigned *eg,
+                            long e_offset, const Halo *halo, Incidence &inc, hipStream_t s);
 
 }  // namespace pfdr

@@ -97,6 +97,8 @@ class QuadSession final : public SessionBase {
     DevBuf<real> diag_, Ga_, invAux_, Th_l1_, absval_, grad_, pre_, xout_;
     DevBuf<real> Z2_, W2_, Wd1u_, Wd1v_, Th_, wz_;
     DevBuf<real> R_, Rpart_, vpart_, opart_, Obj_, Dif_, red_, csum_;
+    DevBuf<real> Rsum_, xfull_;  // dense A on a partition: summed A X, gathered X
+    long v0_ = 0, Vglob_ = 0;
     DevBuf<long long> ccnt_;
     DevBuf<int> cnt_part_;
     DevBuf<Ctrl<real>> ctrl_;
@@ -120,6 +122,7 @@ class QuadSession final : public SessionBase {
     void pull_ctrl();
     void print_progress();
     void pull(void *base, int eb) { if (halo_) halo_->pull(base, eb, stream); }
+    const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
 };
 
 // ----------------------------------------------------------------- setup --
@@ -141,12 +144,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     else if (N_ < 0) mode_ = A_ATA;
     else mode_ = p->A ? A_DIAG : A_IDENT;
     if (mode_ == A_DIRECT && !p->A) throw std::runtime_error("N > 0 requires A");
-    if (mode_ == A_ATA && (!p->A || -N_ != V_))
-        throw std::runtime_error("N < 0 requires A = A^tA of size V-by-V and N = -V");
-    const bool dist = p->nranks > 1 || p->comm;
-    if (dist && (mode_ == A_DIRECT || mode_ == A_ATA))
-        throw std::runtime_error("the vertex partition supports identity and diagonal A "
-                                 "(dense A: one GPU)");
+    if (mode_ == A_ATA && !p->A) throw std::runtime_error("N < 0 requires A = A^tA");
     rho_ = (real)p->rho;
     condMin_ = (real)p->condMin;
     difTol_ = (real)p->difTol;
@@ -178,12 +176,19 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
 
     // graph, partition plan, incidence CSR
     setup_graph(p);
+    // dense A on a partition: this rank's columns (its vertices); A^tA columns
+    // have the global length
+    v0_ = halo_ ? (long)halo_->vtx_begin : 0;
+    Vglob_ = halo_ ? (long)halo_->off.back() : V_;
+    if (mode_ == A_ATA && -(long)N_ != Vglob_)
+        throw std::runtime_error("N < 0 requires A = A^tA (columns of the owned vertices, "
+                                 "length V) and N = -V (V over all ranks)");
     const int mem = p->mem;
     const size_t V = V_, E = E_, Vg = Vg_;
     copy_in(La_d1_, p->La_d1, E, mem, s);
     if (flavour_ == 0) copy_in(La_l1_, p->La_l1, V, mem, s);
     copy_in(Y_, p->Y, mode_ == A_DIRECT ? (size_t)N_ : V, mem, s);
-    const size_t asz = mode_ == A_DIRECT ? (size_t)N_ * V : mode_ == A_ATA ? V * V
+    const size_t asz = mode_ == A_DIRECT ? (size_t)N_ * V : mode_ == A_ATA ? (size_t)Vglob_ * V
                      : mode_ == A_DIAG ? V : 0;
     copy_in(A_, p->A, asz, mem, s);
     if (reordered_) {  // inputs into the internal labels (identity / diagonal A only)
@@ -244,7 +249,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         rows_nb_ = (V_ + rows_cpb_ - 1) / rows_cpb_;
         Rpart_.alloc((size_t)rows_nb_ * N_);
     }
-    if (mode_ == A_ATA) { pre_.alloc(V); xout_.alloc(V); }
+    if (mode_ == A_ATA) { pre_.alloc(V); xout_.alloc(V); xfull_.alloc(Vglob_); }
+    if (mode_ == A_DIRECT && halo_) Rsum_.alloc(N_);
 
     // control block
     ctrl_.alloc(1);
@@ -265,7 +271,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         ca.A = A_.p; ca.ncols = V_; ca.len = N_; ca.out = diag_.p;
         k_col_dot<real, EPI_SELF><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
     } else {
-        k_diag<real><<<grid_for(V), kBlock, 0, s>>>(V_, mode_, A_.p, diag_.p);
+        k_diag<real><<<grid_for(V), kBlock, 0, s>>>(V_, mode_, A_.p, Vglob_, v0_, diag_.p);
     }
     PFDR_HIP(hipGetLastError());
     // Z = X at both ends, first preconditioning, first forward step
@@ -289,7 +295,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
                             &pre_, &Z2_, &W2_, &Wd1u_, &Wd1v_, &Th_, &wz_, &R_, &Rpart_,
-                            &vpart_, &opart_, &Obj_, &Dif_, &xout_})
+                            &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_})
         acc(b->n * sizeof(real));
     acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     order_.release();  // inputs are in the internal labels now
@@ -308,44 +314,8 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     const unsigned *eg_ptr = nullptr;  // original edge ids of a relabelled graph
     long e_offset = 0;
     if (p->nranks > 1 || p->comm) {
-        if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks || !p->comm)
-            throw std::runtime_error("distributed session needs nranks, rank and comm");
-        halo_.reset(new Halo());
-        halo_->tr = p->comm_kind == PFDR_COMM_LOOPBACK
-                        ? make_loopback_transport(p->comm, p->nranks, p->rank)
-                        : make_rccl_transport(p->comm, p->nranks, p->rank);
-        // the plan is built on the host from the global endpoint ids
-        std::vector<int> hu, hv, lu, lv;
-        std::vector<int64_t> heg;
-        const int *pu = p->Eu, *pv = p->Ev;
-        const int64_t *peg = p->e_global;
-        if (p->mem == PFDR_MEM_DEVICE) {
-            hu.resize(E); hv.resize(E);
-            PFDR_HIP(hipMemcpy(hu.data(), p->Eu, E * 4, hipMemcpyDeviceToHost));
-            PFDR_HIP(hipMemcpy(hv.data(), p->Ev, E * 4, hipMemcpyDeviceToHost));
-            pu = hu.data(); pv = hv.data();
-            if (peg) {
-                heg.resize(E);
-                PFDR_HIP(hipMemcpy(heg.data(), p->e_global, E * 8, hipMemcpyDeviceToHost));
-                peg = heg.data();
-            }
-        }
-        build_halo(*halo_, V_, p->vtx_begin, E_, pu, pv, peg, p->e_offset, lu, lv, s);
+        partition_setup(p, V_, E_, halo_, Eu_, Ev_, eg, &e_offset, s);
         Vg_ = V_ + halo_->G;
-        if (E) {
-            PFDR_HIP(hipMemcpyAsync(Eu_.p, lu.data(), E * 4, hipMemcpyHostToDevice, s));
-            PFDR_HIP(hipMemcpyAsync(Ev_.p, lv.data(), E * 4, hipMemcpyHostToDevice, s));
-        }
-        if (peg) {
-            std::vector<unsigned> e32(E);
-            for (size_t e = 0; e < E; e++) e32[e] = (unsigned)peg[e];
-            eg.alloc(E ? E : 1);
-            PFDR_HIP(hipMemcpyAsync(eg.p, e32.data(), E * 4, hipMemcpyHostToDevice, s));
-            PFDR_HIP(hipStreamSynchronize(s));
-        } else {
-            e_offset = (long)p->e_offset;
-        }
-        PFDR_HIP(hipStreamSynchronize(s));
     } else {
         Vg_ = V_;
         if (E) {
@@ -382,24 +352,9 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
-    const long n = 2 * E_ + R;
-    wz_.alloc(n ? n : 1);
-    DevBuf<unsigned long long> keys(n ? n : 1);
-    DevBuf<unsigned> vals(n ? n : 1);
-    if (E_) {
-        k_slot_keys<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, V_, eg_ptr ? eg_ptr : eg.p,
-                                                    e_offset, keys.p, vals.p);
-        PFDR_HIP(hipGetLastError());
-    }
-    if (R) {
-        PFDR_HIP(hipMemcpyAsync(keys.p + 2 * E_, halo_->recv_keys.p, R * sizeof(unsigned long long),
-                                hipMemcpyDeviceToDevice, s));
-        std::vector<unsigned> tail(R);
-        for (long j = 0; j < R; j++) tail[j] = (unsigned)(2 * E_ + j);
-        PFDR_HIP(hipMemcpyAsync(vals.p + 2 * E_, tail.data(), R * 4, hipMemcpyHostToDevice, s));
-        PFDR_HIP(hipStreamSynchronize(s));
-    }
-    build_incidence_keyed(keys.p, vals.p, n, V_, inc_, s);
+    wz_.alloc(2 * E_ + R ? 2 * E_ + R : 1);
+    contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
+                           inc_, s);
     eorig_.release();
 }
 
@@ -420,8 +375,16 @@ void QuadSession<real>::gemv_rows(int gate) {
     ProfScope ps(prof, "gemv_rows", s);
     k_rows_partial<real><<<rows_nb_, kBlock, 0, s>>>(N_, V_, A_.p, xp_.p, rows_cpb_, Rpart_.p,
                                                     gate ? ctrl_.p : nullptr, gate);
-    k_rows_finish<real><<<grid_for(N_), kBlock, 0, s>>>(N_, rows_nb_, Rpart_.p, Y_.p, R_.p,
-                                                       gate ? ctrl_.p : nullptr, gate);
+    const Ctrl<real> *c = gate ? ctrl_.p : nullptr;
+    if (!halo_) {
+        k_rows_finish<real><<<grid_for(N_), kBlock, 0, s>>>(N_, rows_nb_, Rpart_.p, Y_.p, R_.p,
+                                                           c, gate);
+    } else {  // partial A X of this rank's columns, summed over the ranks
+        k_rows_finish<real><<<grid_for(N_), kBlock, 0, s>>>(N_, rows_nb_, Rpart_.p, nullptr,
+                                                           Rsum_.p, c, gate);
+        halo_->tr->allreduce_sum(Rsum_.p, N_, dtype_of<real>(), s);
+        k_rows_residual<real><<<grid_for(N_), kBlock, 0, s>>>(N_, Y_.p, Rsum_.p, R_.p, c, gate);
+    }
     PFDR_HIP(hipGetLastError());
 }
 
@@ -440,13 +403,33 @@ void QuadSession<real>::forward_dense(int gate) {
         ProfScope ps(prof, "gemv_cols", s);
         k_col_dot<real, EPI_FWD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
     } else {
-        ca.len = V_;
-        k_x_extract<real><<<grid_for(V_), kBlock, 0, s>>>(V_, xp_.p, xout_.p);
-        ca.w = xout_.p;
+        ca.len = (int)Vglob_;
+        ca.w = full_x();
         ProfScope ps(prof, "symv", s);
         k_col_dot<real, EPI_FWD_ATA><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
     }
     PFDR_HIP(hipGetLastError());
+}
+
+template <typename real>
+const real *QuadSession<real>::full_x() {
+    hipStream_t s = stream;
+    k_x_extract<real><<<grid_for(V_), kBlock, 0, s>>>(V_, xp_.p, xfull_.p + v0_);
+    PFDR_HIP(hipGetLastError());
+    if (halo_) {  // all-gather of the owned blocks
+        Transport &tr = *halo_->tr;
+        const int n = tr.nranks;
+        std::vector<const void *> sp(n, xfull_.p + v0_);
+        std::vector<size_t> sb(n, (size_t)V_ * sizeof(real));
+        std::vector<void *> rp(n);
+        std::vector<size_t> rb(n);
+        for (int q = 0; q < n; q++) {
+            rp[q] = xfull_.p + halo_->off[q];
+            rb[q] = (size_t)(halo_->off[q + 1] - halo_->off[q]) * sizeof(real);
+        }
+        tr.exchange(sp, sb, rp, rb, s);
+    }
+    return xfull_.p;
 }
 
 // gradient of the smooth part at the current X into grad_ (reconditioning)
@@ -464,9 +447,8 @@ void QuadSession<real>::gradient() {
             ca.len = N_; ca.w = R_.p;
             k_col_dot<real, EPI_GRAD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
         } else {
-            ca.len = V_;
-            k_x_extract<real><<<grid_for(V_), kBlock, 0, s>>>(V_, xp_.p, xout_.p);
-            ca.w = xout_.p;
+            ca.len = (int)Vglob_;
+            ca.w = full_x();
             k_col_dot<real, EPI_GRAD_ATA><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
         }
     }
@@ -556,19 +538,20 @@ void QuadSession<real>::objective() {
     pull(xp_.p, sizeof(R2<real>));  // TV of boundary edges needs the ghosts' X
     if (mode_ == A_ATA) {
         ColArgs<real> ca{};
-        ca.A = A_.p; ca.ncols = V_; ca.len = V_; ca.out = pre_.p;
+        ca.A = A_.p; ca.ncols = V_; ca.len = (int)Vglob_; ca.out = pre_.p;
         ca.ctrl = c; ca.gate = GATE_OBJ;
-        k_x_extract<real><<<grid_for(V_), kBlock, 0, s>>>(V_, xp_.p, xout_.p);
-        ca.w = xout_.p;
+        ca.w = full_x();
         k_col_dot<real, EPI_STORE><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
         papp = pre_.p;
     }
     k_obj_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, mode_, xp_.p, A_.p, papp, Y_.p,
                                                flavour_ == 0 ? La_l1_.p : nullptr, opart_.p, nbv_, c);
     if (E_) k_obj_edge<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, La_d1_.p, opart_.p + 2 * nbv_, c);
-    if (mode_ == A_DIRECT)
-        k_obj_rsq<real><<<nbn_, kBlock, 0, s>>>(N_, R_.p, opart_.p + 2 * nbv_ + nbe_, c);
-    k_obj_reduce<real><<<1, kBlock, 0, s>>>(opart_.p, nbv_, E_ ? nbe_ : 0, nbn_, mode_ == A_DIRECT,
+    // the residual is replicated on every rank: its norm counts once (rank 0)
+    const int nbn = (halo_ && halo_->tr->rank != 0) ? 0 : nbn_;
+    if (mode_ == A_DIRECT && nbn)
+        k_obj_rsq<real><<<nbn, kBlock, 0, s>>>(N_, R_.p, opart_.p + 2 * nbv_ + nbe_, c);
+    k_obj_reduce<real><<<1, kBlock, 0, s>>>(opart_.p, nbv_, E_ ? nbe_ : 0, nbn, mode_ == A_DIRECT,
                                             c, red_.p);
     if (halo_) halo_->tr->allreduce_sum(red_.p, 3, dtype_of<real>(), s);
     k_obj_write<real><<<1, 64, 0, s>>>(red_.p, mode_ == A_DIRECT,

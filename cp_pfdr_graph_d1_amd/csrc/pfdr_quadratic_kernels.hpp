@@ -173,14 +173,16 @@ __global__ void k_z_init(long E, const int *__restrict__ Eu,
 }
 
 // diagonal of A^t A for the identity / diagonal / A^tA modes (ref :101-122)
+// (A^tA: local column v of a column block starting at global row row0,
+// column length ld)
 template <typename real>
-__global__ void k_diag(int V, int mode, const real *__restrict__ A,
+__global__ void k_diag(int V, int mode, const real *__restrict__ A, long ld, long row0,
                        real *__restrict__ diag) {
     int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= V) return;
     real d = real(1);
     if (mode == A_DIAG) d = A[v];
-    else if (mode == A_ATA) d = A[(size_t)(V + 1) * v];
+    else if (mode == A_ATA) d = A[(size_t)ld * v + row0 + v];
     diag[v] = d;
 }
 
@@ -319,7 +321,16 @@ __global__ void k_rows_finish(int N, int nb, const real *__restrict__ part,
         for (int q = 0; q < 8; q++) s += t[q];
     }
     for (; b < nb; b++) s += part[(size_t)b * N + n];
-    R[n] = Y[n] - s;
+    R[n] = Y ? Y[n] - s : s;  // Y == NULL: this rank's partial A X (all-reduced next)
+}
+
+// R = Y - (A X summed over the ranks)
+template <typename real>
+__global__ void k_rows_residual(int N, const real *__restrict__ Y, const real *__restrict__ S,
+                                real *__restrict__ R, const Ctrl<real> *ctrl, int gate) {
+    if (gated(ctrl, gate)) return;
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < N) R[n] = Y[n] - S[n];
 }
 
 // ---------------------------------------------------- preconditioning --
@@ -520,22 +531,6 @@ __global__ void k_precond_edge2(long E, const int *__restrict__ Eu,
     Th[e] = La_d1[e] * s / (a * b);
     Wd1u[e] = a / s;
     Wd1v[e] = b / s;
-}
-
-// CSR keys of the local slots: key = (vertex << 32) | (2 e_global + side),
-// value = address of the slot's contribution in the side-major wz; slots of
-// non-owned (ghost) vertices get key ~0 and are dropped by the CSR build.
-__global__ void k_slot_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
-                            int V, const unsigned *__restrict__ eg, long e_offset,
-                            unsigned long long *__restrict__ keys, unsigned *__restrict__ vals) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    const unsigned long long g = eg ? (unsigned long long)eg[e] : (unsigned long long)(e_offset + e);
-    const int u = Eu[e], v = Ev[e];
-    keys[e] = (u < V) ? (((unsigned long long)u << 32) | (2 * g)) : ~0ull;
-    keys[E + e] = (v < V) ? (((unsigned long long)v << 32) | (2 * g + 1)) : ~0ull;
-    vals[e] = (unsigned)e;
-    vals[E + e] = (unsigned)(E + e);
 }
 
 // gradient A X - Y of the identity / diagonal modes (ref :377-385, :441-445)

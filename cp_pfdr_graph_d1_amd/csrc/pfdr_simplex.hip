@@ -24,6 +24,7 @@
 #include <memory>
 
 #include "pfdr_graph.hpp"
+#include "pfdr_halo.hpp"
 #include "pfdr_session.hpp"
 
 namespace pfdr {
@@ -217,28 +218,25 @@ __global__ void k_sx_d1_weights(long EK, int K, const int *__restrict__ Eu,
     wz[EK + i] = w;
 }
 
-// ordered per-(v, k) sum over the incidence CSR: slot s = 2e + side lives at
-// wz[side*EK + e*K + k]
+// ordered per-(v, k) sum over the contribution CSR (pfdr_halo.hpp): the
+// entry of address a (e: u end, E + e: v end, 2E + j: received) lives at
+// wz[a*K + k] — wz is [side][e][k] followed by the received tail
 template <typename real>
-__device__ __forceinline__ real sx_gather(long i, int K, long EK,
-                                          const int *__restrict__ ptr,
+__device__ __forceinline__ real sx_gather(long i, int K, const int *__restrict__ ptr,
                                           const unsigned *__restrict__ idx,
                                           const real *__restrict__ wz) {
     const long v = i / K;
     const int k = (int)(i - v * K);
     const int j0 = ptr[v], j1 = ptr[v + 1];
     real s = real(0);
-    for (int j = j0; j < j1; j++) {
-        const unsigned slot = idx[j];
-        s += wz[(long)(slot & 1u) * EK + (long)(slot >> 1) * K + k];
-    }
+    for (int j = j0; j < j1; j++) s += wz[(long)idx[j] * K + k];
     return s;
 }
 
 // metric of every (v, k), prox weights input and first-order information
 // (ref :192-285 per element, :307-335)
 template <typename real>
-__global__ void k_sx_precond_vertex(long VK, SxConst<real> c, long EK,
+__global__ void k_sx_precond_vertex(long VK, SxConst<real> c,
                                     const int *__restrict__ ptr,
                                     const unsigned *__restrict__ idx,
                                     const real *__restrict__ wz,
@@ -250,7 +248,7 @@ __global__ void k_sx_precond_vertex(long VK, SxConst<real> c, long EK,
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= VK) return;
     const int K = c.K;
-    const real s = sx_gather(i, K, EK, ptr, idx, wz);
+    const real s = sx_gather(i, K, ptr, idx, wz);
     real g;
     if (c.loss == LOSS_LINEAR) {
         // Ga itself accumulated the weights from zero, then was inverted
@@ -452,14 +450,14 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
 }
 
 template <typename real>
-__global__ void k_sx_average(long VK, int K, long EK, const int *__restrict__ ptr,
+__global__ void k_sx_average(long VK, int K, const int *__restrict__ ptr,
                              const unsigned *__restrict__ idx,
                              const real *__restrict__ wz,
                              real *__restrict__ Pavg, const Ctrl<real> *ctrl) {
     if (ctrl && ctrl->halt) return;
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= VK) return;
-    Pavg[i] = sx_gather(i, K, EK, ptr, idx, wz);
+    Pavg[i] = sx_gather(i, K, ptr, idx, wz);
 }
 
 template <typename real>
@@ -523,7 +521,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
 template <typename real>
 struct SxVArgs {
     int V, vb;
-    long EK;
+    long E;
     SxConst<real> c;
     const int *ptr;
     const unsigned *idx;
@@ -561,28 +559,33 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
             for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
             if (WZ) {
 #pragma unroll
-                for (int q = 0; q < 8; q++)
-                    w[q] = wz[(long)(sl[q] & 1u) * a.EK + (long)(sl[q] >> 1) * K + k];
+                for (int q = 0; q < 8; q++) w[q] = wz[(long)sl[q] * K + k];
             } else {  // W * Z formed here (the reference's product, same rounding)
                 real zq[8], wq[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
-                    const long o = (long)(sl[q] >> 1) * K + k;
-                    const bool sv = sl[q] & 1u;
-                    zq[q] = (sv ? a.Zv : a.Zu)[o];
-                    wq[q] = (sv ? a.Wv : a.Wu)[o];
+                    const long ad = sl[q];
+                    if (ad < 2 * a.E) {
+                        const bool sv = ad >= a.E;
+                        const long o = (sv ? ad - a.E : ad) * K + k;
+                        zq[q] = (sv ? a.Zv : a.Zu)[o];
+                        wq[q] = (sv ? a.Wv : a.Wu)[o];
+                    } else {  // received from the owner of the edge (already W*Z)
+                        zq[q] = wz[ad * K + k];
+                        wq[q] = real(1);
+                    }
                 }
 #pragma unroll
-                for (int q = 0; q < 8; q++) w[q] = wq[q] * zq[q];
+                for (int q = 0; q < 8; q++) w[q] = (sl[q] < 2 * a.E) ? wq[q] * zq[q] : zq[q];
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) s += w[q];
         }
         for (; j < j1; j++) {
-            const unsigned slot = a.idx[j];
-            const long o = (long)(slot >> 1) * K + k;
-            if (WZ) s += wz[(long)(slot & 1u) * a.EK + o];
-            else s += (slot & 1u) ? a.Wv[o] * a.Zv[o] : a.Wu[o] * a.Zu[o];
+            const long ad = a.idx[j];
+            if (WZ || ad >= 2 * a.E) s += wz[ad * K + k];
+            else if (ad >= a.E) s += a.Wv[(ad - a.E) * K + k] * a.Zv[(ad - a.E) * K + k];
+            else s += a.Wu[ad * K + k] * a.Zu[ad * K + k];
         }
         xs[t] = s;
         ms[t] = a.Ga[i];
@@ -622,18 +625,51 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     }
 }
 
+// K-wide W*Z of the pushed v ends (address E + e) / u ends (address e),
+// packed in the plan's push order
+template <typename real>
+__global__ void k_sx_pack_wz(long n, int K, long E, const unsigned *__restrict__ addr,
+                             const real *__restrict__ Wu, const real *__restrict__ Zu,
+                             const real *__restrict__ Wv, const real *__restrict__ Zv,
+                             real *__restrict__ out) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * K) return;
+    const long i = t / K;
+    const int k = (int)(t - i * K);
+    const long ad = addr[i];
+    out[t] = ad >= E ? Wv[(ad - E) * K + k] * Zv[(ad - E) * K + k]
+                     : Wu[ad * K + k] * Zu[ad * K + k];
+}
+
+// sum of the evolution partials (distributed: all-reduced before the decision)
+template <typename real>
+__global__ __launch_bounds__(256) void k_sx_partsum(int nparts, const real *__restrict__ part,
+                                                   const Ctrl<real> *ctrl, real *out) {
+    __shared__ real red[kBlock / kWave];
+    if (ctrl->halt) return;
+    real s = real(0);
+    for (int i = threadIdx.x; i < nparts; i += kBlock) s += part[i];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) *out = s;
+}
+
 template <typename real>
 __global__ __launch_bounds__(256) void k_sx_finalize(int nparts,
                                                      const real *__restrict__ part,
-                                                     int V, int track,
+                                                     long V, int track,
                                                      Ctrl<real> *ctrl,
-                                                     real *__restrict__ Dif) {
+                                                     real *__restrict__ Dif,
+                                                     const real *total) {
     __shared__ real red[kBlock / kWave];
     if (ctrl->halt) return;
     real s = real(0);
     if (track) {
-        for (int i = threadIdx.x; i < nparts; i += kBlock) s += part[i];
-        s = block_sum(s, red);
+        if (total) {
+            s = *total;
+        } else {
+            for (int i = threadIdx.x; i < nparts; i += kBlock) s += part[i];
+            s = block_sum(s, red);
+        }
     }
     if (threadIdx.x != 0) return;
     int it = ctrl->it;
@@ -719,7 +755,8 @@ template <typename real>
 __global__ __launch_bounds__(256) void k_sx_obj_finalize(const real *__restrict__ part,
                                                          int nbv, int nbe, int quad,
                                                          Ctrl<real> *ctrl,
-                                                         real *__restrict__ Obj) {
+                                                         real *__restrict__ Obj,
+                                                         real *__restrict__ sums) {
     __shared__ real red[2][kBlock / kWave];
     if (ctrl->obj_it >= ctrl->it) return;
     real l = real(0), tv = real(0);
@@ -728,8 +765,23 @@ __global__ __launch_bounds__(256) void k_sx_obj_finalize(const real *__restrict_
     l = block_sum(l, red[0]);
     tv = block_sum(tv, red[1]);
     if (threadIdx.x != 0) return;
+    if (sums) {  // distributed: all-reduced, then k_sx_obj_write
+        sums[0] = l;
+        sums[1] = tv;
+        return;
+    }
     if (quad) l *= real(0.5);
     Obj[ctrl->it] = l + tv;
+    ctrl->obj_it = ctrl->it;
+}
+
+template <typename real>
+__global__ void k_sx_obj_write(const real *__restrict__ sums, int quad, Ctrl<real> *ctrl,
+                               real *__restrict__ Obj) {
+    if (ctrl->obj_it >= ctrl->it) return;
+    real l = sums[0];
+    if (quad) l *= real(0.5);
+    Obj[ctrl->it] = l + sums[1];
     ctrl->obj_it = ctrl->it;
 }
 
@@ -773,7 +825,11 @@ class SimplexSession final : public SessionBase {
   private:
     SxConst<real> c_;
     int V_, K_, itMax_, verbose_;
-    long E_, EK_, VK_;
+    int Vg_;        // owned + ghost vertices (distributed)
+    long Vglob_;    // vertices over all ranks
+    long E_, EK_, VK_, R_ = 0;
+    std::unique_ptr<Halo> halo_;  // vertex partition (null on one GPU)
+    DevBuf<real> red_;            // all-reduced scalars
     real rho_, condMin_, difTol_, difRcd_, cap_;
     bool rec_obj_, rec_dif_;
     int track_;  // 0, 1 (l1 evolution), 2 (labels)
@@ -799,6 +855,11 @@ class SimplexSession final : public SessionBase {
     void objective();
     void body();
     void launch_project(const SxProjArgs<real> &a);
+    // K-wide ghost rows of a [Vg][K] array from their owners
+    void pullK(DevBuf<real> &b) {
+        if (halo_) halo_->pull(b.p, K_ * (int)sizeof(real), stream);
+    }
+    void push_wz();
 };
 
 template <typename real>
@@ -815,7 +876,6 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (p->K > 1024) throw std::runtime_error("K > 1024 labels is not supported");
     if (!p->X || !p->Y || !p->Eu || !p->Ev || !p->La_d1)
         throw std::runtime_error("P, Q, Eu, Ev and La_d1 are required");
-    if (p->nranks > 1) throw std::runtime_error("distributed simplex sessions are not supported yet");
     PFDR_HIP(hipGetDevice(&device));
     stream = lib_stream();
     hipStream_t s = stream;
@@ -843,15 +903,33 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
 
     const int mem = p->mem;
     const auto kind = mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    Eu_.alloc(E_ ? E_ : 1); Ev_.alloc(E_ ? E_ : 1);
-    if (E_) {
-        PFDR_HIP(hipMemcpyAsync(Eu_.p, p->Eu, E_ * sizeof(int), kind, s));
-        PFDR_HIP(hipMemcpyAsync(Ev_.p, p->Ev, E_ * sizeof(int), kind, s));
+    DevBuf<unsigned> eg;
+    long e_offset = 0;
+    if (p->nranks > 1 || p->comm) {  // vertex partition with K-wide halos
+        partition_setup(p, V_, E_, halo_, Eu_, Ev_, eg, &e_offset, s);
+        Vg_ = V_ + halo_->G;
+        R_ = halo_->R;
+        Vglob_ = (long)halo_->off.back();
+        red_.alloc(2);
+    } else {
+        Vg_ = V_;
+        Vglob_ = V_;
+        Eu_.alloc(E_ ? E_ : 1); Ev_.alloc(E_ ? E_ : 1);
+        if (E_) {
+            PFDR_HIP(hipMemcpyAsync(Eu_.p, p->Eu, E_ * sizeof(int), kind, s));
+            PFDR_HIP(hipMemcpyAsync(Ev_.p, p->Ev, E_ * sizeof(int), kind, s));
+        }
     }
+    check_endpoints(Eu_.p, Ev_.p, E_, Vg_, s);
+    contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg.p, e_offset, halo_.get(), inc_, s);
+    const size_t VgK = (size_t)Vg_ * K_;
     sx_copy_in(La_d1_, p->La_d1, E_, mem, s);
     if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s);
-    sx_copy_in(Q_, p->Y, VK_, mem, s);
-    sx_copy_in(P_, p->X, VK_, mem, s);
+    for (auto q : {std::make_pair(&Q_, p->Y), std::make_pair(&P_, (const void *)p->X)}) {
+        q.first->alloc(VgK);  // owned rows, then the ghosts' from their owners
+        PFDR_HIP(hipMemcpyAsync(q.first->p, q.second, VK_ * sizeof(real), kind, s));
+        pullK(*q.first);
+    }
     if (K_ <= 64 && !env_flag_off("PFDR_SX_FUSED")) {
         const char *nt = getenv("PFDR_SX_NT");  // threads per block: 64 (default) or 256
         sx_nt_ = (nt && atoi(nt) == 64) ? 64 : 256;
@@ -862,11 +940,11 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     } else {
         Pavg_.alloc(VK_);
     }
-    FP_.alloc(VK_); Ga_.alloc(VK_); GaQ_.alloc(VK_); invAux_.alloc(VK_);
+    FP_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
     const size_t EKn = EK_ ? EK_ : 1;
     Zu_.alloc(EKn); Zv_.alloc(EKn); Wu_.alloc(EKn); Wv_.alloc(EKn);
     if (c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
-    wz_.alloc(2 * EKn);
+    wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
     nbe_ = grid_for(E_);
     part_.alloc(std::max(nbv_, nbs_));
@@ -887,11 +965,11 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     hctrl_->difRcd = difRcd_;
     PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, s));
 
-    build_incidence(Eu_.p, Ev_.p, V_, E_, inc_, s);
     if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, Zv_.p);
     precondition(true);
     k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
     PFDR_HIP(hipGetLastError());
+    pullK(FP_);
     if (rec_obj_) objective();
     PFDR_HIP(hipStreamSynchronize(s));
     stopped_ = itMax_ <= 0;
@@ -910,14 +988,19 @@ void SimplexSession<real>::precondition(bool init) {
     const int gE = grid_for(EK_), gV = grid_for(VK_);
     if (!init) {
         k_sx_recover<real><<<nbv_, kBlock, 0, s>>>(V_, c_, La_f_.p, Q_.p, GaQ_.p, Ga_.p);
+        pullK(Ga_);
         if (EK_) k_sx_subgrad<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, P_.p, Q_.p, Ga_.p,
                                                           GaQ_.p, Wu_.p, Wv_.p, Zu_.p, Zv_.p);
     }
     k_sx_hessian<real><<<gV, kBlock, 0, s>>>(VK_, c_, La_f_.p, P_.p, Q_.p, Ga_.p);
     if (EK_) k_sx_d1_weights<real><<<gE, kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, La_d1_.p, init ? 1 : 0,
                                                          condMin_, P_.p, Wu_.p, Wv_.p, wz_.p);
-    k_sx_precond_vertex<real><<<gV, kBlock, 0, s>>>(VK_, c_, EK_, inc_.ptr.p, inc_.idx.p, wz_.p,
+    if (halo_) halo_->push(wz_.p, wz_.p + 2 * EK_, K_ * (int)sizeof(real), s);
+    k_sx_precond_vertex<real><<<gV, kBlock, 0, s>>>(VK_, c_, inc_.ptr.p, inc_.idx.p, wz_.p,
                                                     La_f_.p, Q_.p, cap_, Ga_.p, invAux_.p, GaQ_.p);
+    pullK(Ga_);
+    pullK(invAux_);
+    pullK(GaQ_);
     if (EK_) k_sx_precond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, La_d1_.p, invAux_.p,
                                                            Ga_.p, GaQ_.p, P_.p, Q_.p, Wu_.p, Wv_.p,
                                                            Wd1u_.p, Wd1v_.p, Th_.p, init ? 0 : 1,
@@ -933,7 +1016,12 @@ void SimplexSession<real>::objective() {
     if (E_) k_sx_obj_edge<real><<<nbe_, kBlock, 0, s>>>(E_, K_, Eu_.p, Ev_.p, La_d1_.p, P_.p,
                                                         opart_.p + nbv_, ctrl_.p);
     k_sx_obj_finalize<real><<<1, kBlock, 0, s>>>(opart_.p, nbv_, E_ ? nbe_ : 0,
-                                                 c_.loss == LOSS_QUAD, ctrl_.p, Obj_.p);
+                                                 c_.loss == LOSS_QUAD, ctrl_.p, Obj_.p,
+                                                 halo_ ? red_.p : nullptr);
+    if (halo_) {
+        halo_->tr->allreduce_sum(red_.p, 2, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
+        k_sx_obj_write<real><<<1, 1, 0, s>>>(red_.p, c_.loss == LOSS_QUAD, ctrl_.p, Obj_.p);
+    }
     PFDR_HIP(hipGetLastError());
 }
 
@@ -950,9 +1038,13 @@ void SimplexSession<real>::body() {
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
                                                                rho_, c);
     }
+    if (halo_) {
+        ProfScope ps(prof, "halo_push", s);
+        push_wz();
+    }
     if (vb_) {
         SxVArgs<real> a{};
-        a.V = V_; a.vb = vb_; a.EK = EK_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
+        a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
         a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.FP = FP_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
@@ -967,7 +1059,7 @@ void SimplexSession<real>::body() {
     } else {
         {
             ProfScope ps(prof, "sx_average", s);
-            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, EK_, inc_.ptr.p,
+            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, inc_.ptr.p,
                                                                 inc_.idx.p, wz_.p, Pavg_.p, c);
         }
         SxProjArgs<real> a{};
@@ -976,11 +1068,44 @@ void SimplexSession<real>::body() {
         ProfScope ps(prof, "sx_project", s);
         launch_project(a);
     }
-    if (gated)
-        k_sx_finalize<real><<<1, kBlock, 0, s>>>(vb_ ? nbs_ : nbv_, part_.p, V_, track_, ctrl_.p,
-                                                 rec_dif_ ? Dif_.p : nullptr);
+    if (halo_) {
+        ProfScope ps(prof, "halo_pull", s);
+        pullK(P_);
+        pullK(FP_);
+    }
+    const int nparts = vb_ ? nbs_ : nbv_;
+    if (gated && halo_) {
+        if (track_) {
+            k_sx_partsum<real><<<1, kBlock, 0, s>>>(nparts, part_.p, ctrl_.p, red_.p);
+            halo_->tr->allreduce_sum(red_.p, 1, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
+        }
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
+                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
+    } else if (gated) {
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(nparts, part_.p, Vglob_, track_, ctrl_.p,
+                                                 rec_dif_ ? Dif_.p : nullptr, nullptr);
+    }
     PFDR_HIP(hipGetLastError());
     if (rec_obj_) objective();
+}
+
+// K-wide DR contributions of ghost-vertex ends to their owners
+template <typename real>
+void SimplexSession<real>::push_wz() {
+    const int eb = K_ * (int)sizeof(real);
+    real *tail = wz_.p + 2 * EK_;
+    if (!vb_ || sx_wz_) {  // the edge sweep stored W*Z
+        halo_->push(wz_.p, tail, eb, stream);
+        return;
+    }
+    const long n = halo_->push_send_off[halo_->tr->nranks];
+    real *buf = (real *)halo_->push_buffer(eb);
+    if (n) {
+        k_sx_pack_wz<real><<<grid_for(n * K_), kBlock, 0, stream>>>(n, K_, E_, halo_->push_addr.p,
+                                                                    Wu_.p, Zu_.p, Wv_.p, Zv_.p, buf);
+        PFDR_HIP(hipGetLastError());
+    }
+    halo_->push_packed(buf, tail, eb, stream);
 }
 
 template <typename real>
@@ -1001,6 +1126,7 @@ int SimplexSession<real>::run(int iters) {
                 precondition(false);
                 k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
                 PFDR_HIP(hipGetLastError());
+                pullK(FP_);
                 difRcd_ *= real(0.1);  // ref :563
                 hctrl_->difRcd = difRcd_;
                 hctrl_->recond = 0;

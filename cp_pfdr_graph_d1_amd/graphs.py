@@ -149,9 +149,10 @@ def piecewise_observation(shape, seed, dtype=np.float64, noise=0.2):
     return (base + (2.0 * uniform(seed, v) - 1.0) * noise).astype(dtype)
 
 
-def simplex_observation(V, K, seed, block_labels, dtype=np.float64):
-    """Q = normalise(U(0,1) + 3*onehot(label)), column v = Q[v*K:(v+1)*K]."""
-    idx = np.arange(V * K, dtype=np.int64)
+def simplex_observation(V, K, seed, block_labels, dtype=np.float64, v0=0):
+    """Q = normalise(U(0,1) + 3*onehot(label)), column v = Q[v*K:(v+1)*K];
+    v0: first global vertex (the draws of a partition slab)."""
+    idx = int(v0) * K + np.arange(V * K, dtype=np.int64)
     Q = uniform(seed, idx).reshape(V, K)
     Q[np.arange(V), np.asarray(block_labels) % K] += 3.0
     Q /= Q.sum(1, keepdims=True)

@@ -98,11 +98,14 @@ class Plan:
 def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                    positivity=0, lo=-np.inf, hi=np.inf, Ltype=0, L=None, rho=1.5,
                    condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=100, record_obj=False,
-                   record_dif=False, off=None):
+                   record_dif=False, off=None, K=0, al=0.0, N=0):
     """Partitioned solve with k ranks as k threads on the current GPU.
-    Returns (X, it, Obj, Dif, info) with X for all vertices."""
+    Simplex (kind PFDR_KIND_SIMPLEX): X0 = P0 and Y = Q are K-by-V (v*K + k),
+    La_l1 = La_f.  Dense A: N > 0 (A is N-by-V column-major, each rank gets
+    its vertices' columns, Y stays whole) or N = -V (A^tA, column blocks).  Returns (X, it, Obj, Dif, info) with X for all vertices."""
     lib = pfdr.load()
-    V = np.asarray(X0).size
+    Kw = max(int(K), 1)
+    V = np.asarray(X0).size // Kw
     off = vertex_offsets(V, k) if off is None else np.asarray(off, np.int64)
     parts = split_edges(Eu, off)
     hub = C.c_void_p()
@@ -119,13 +122,21 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                 if a is None:
                     return None
                 a = np.asarray(a)
+                if Kw > 1 and a.size == V * Kw:
+                    return a[v0 * Kw:v1 * Kw]
                 return a[sl] if a.size == V else a
+            if N > 0:  # columns of the owned vertices; the data vector is whole
+                Ar, Yr = np.asarray(A).reshape(V, N)[v0:v1].ravel(), np.asarray(Y)
+            elif N < 0:
+                Ar, Yr = np.asarray(A).reshape(V, V)[v0:v1].ravel(), vsl(Y)
+            else:
+                Ar, Yr = vsl(A), vsl(Y)
             s = pfdr.Session(kind, dtype, v1 - v0, e.size, np.asarray(Eu)[e],
-                             np.asarray(Ev)[e], np.asarray(La_d1)[e], vsl(X0), vsl(Y),
-                             A=vsl(A), La_l1=vsl(La_l1), positivity=positivity, lo=lo, hi=hi,
+                             np.asarray(Ev)[e], np.asarray(La_d1)[e], vsl(X0), Yr, N=N,
+                             A=Ar, La_l1=vsl(La_l1), positivity=positivity, lo=lo, hi=hi,
                              Ltype=Ltype, L=vsl(L), rho=rho, condMin=condMin, difRcd=difRcd,
                              difTol=difTol, itMax=itMax, record_obj=record_obj,
-                             record_dif=record_dif, nranks=k, rank=r, comm=hub.value,
+                             record_dif=record_dif, K=K, al=al, nranks=k, rank=r, comm=hub.value,
                              comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e)
             s.run(itMax)
             results[r] = s.result()

@@ -506,6 +506,17 @@ def gen_grid_edges(shape, conn, v_range=None):
     return Eu, Ev
 
 
+def grid_edge_count(shape, conn, v_end):
+    """Edges gen_grid_edges emits for the vertices [0, v_end) (the global id
+    of a slab's first edge)."""
+    nx, ny = shape[0], shape[1]
+    nz = shape[2] if len(shape) > 2 else 1
+    n = load().pfdr_gen_grid_edges(nx, ny, nz, conn, 0, v_end, None, None)
+    if n < 0:
+        raise PFDRError("pfdr_gen_grid_edges: unsupported connectivity")
+    return int(n)
+
+
 def gen_piecewise(nx, V, seed, dtype=np.float32, noise=0.2, v_range=None):
     v0, v1 = (0, V) if v_range is None else v_range
     Y = np.empty(v1 - v0, dtype)

@@ -136,7 +136,7 @@ class C2(Workload):
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
                   Y=Y, La_l1=np.full(V, 0.01, np.float32), rho=1.5, condMin=1e-3)
         # edges are emitted per vertex in order: global ids are contiguous per rank
-        e0 = 0 if rank == 0 else pfdr.gen_grid_edges(g, 6, (0, v0))[0].size
+        e0 = pfdr.grid_edge_count(g, 6, v0)
         return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=e0,
                     desc="C2: 256^3 6-NN grid (V=%d, E=%d per GPU), identity A, fp32" % (V, E),
                     graph="%dx%dx%d" % g)
@@ -191,11 +191,11 @@ class C3(Workload):
 
 
 class C4(Workload):
-    """config 4: simplex K = 10, KL al = 0.1, 2236^2 8-neighbour grid, fp32"""
+    """config 4: simplex K = 10, KL al = 0.1, 2236^2 8-neighbour grid, fp32;
+    N > 1: weak scaling, each GPU a 2236^2 row slab (K-wide halos)"""
     name = "c4"
     metric = "PFDR_graph_loss_d1_simplex<float> K=10 KL 5M-vertex 8-NN: Medge-updates/s"
     kind = pfdr.PFDR_KIND_SIMPLEX
-    partitionable = False
     dominant = "sx_edge_sweep"
     K = 10
     edge_bytes = 8 + 9 * 10 * 4
@@ -206,16 +206,19 @@ class C4(Workload):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
         n = 2236
         V = n * n
-        Eu, Ev = pfdr.gen_grid_edges((n, n), 8)
+        g = (n, n * world)
+        v0 = rank * V
+        Eu, Ev = pfdr.gen_grid_edges(g, 8, (v0, v0 + V))
         v = np.arange(V)
         lab = ((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)
-        Q = simplex_observation(V, self.K, 4, lab, np.float32)
+        Q = simplex_observation(V, self.K, 4, lab, np.float32, v0=v0)
         E = Eu.size
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32), X0=Q.copy(), Y=Q,
                   K=self.K, al=0.1, rho=1.0, condMin=0.1)
-        return dict(V=V, E=E, kw=kw, vtx_begin=0, e_offset=0,
-                    desc="C4: 2236^2 8-neighbour grid (V=%d, E=%d), K=10, KL al=0.1, fp32" % (V, E),
-                    graph="2236x2236")
+        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=pfdr.grid_edge_count(g, 8, v0),
+                    desc="C4: 2236^2 8-neighbour grid (V=%d, E=%d per GPU), K=10, KL al=0.1, "
+                         "fp32" % (V, E),
+                    graph="%dx%d" % g)
 
 
 class C5(Workload):
@@ -233,7 +236,7 @@ class C5(Workload):
         V = v1 - v0
         Y = pfdr.gen_piecewise(640, V_all, 5, np.float32, 0.2, (v0, v1))
         E = Eu.size
-        e0 = 0 if rank == 0 else pfdr.gen_grid_edges(g, 6, (0, v0))[0].size
+        e0 = pfdr.grid_edge_count(g, 6, v0)
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
                   Y=Y, lo=0.0, hi=1.0, rho=1.5, condMin=1e-3)
         return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=e0,
