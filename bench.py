@@ -156,7 +156,7 @@ def main():
     t = time.perf_counter()
     sess = pfdr.Session(wl.kind, wl.dtype, V, E, itMax=itMax, **kw, **dist_kw)
     setup_s = time.perf_counter() - t
-    desc, graph = inp["desc"], inp["graph"]
+    desc, graph, extra = inp["desc"], inp["graph"], inp.get("extra")
     del inp, kw
     if warm:
         sess.run(warm)
@@ -233,6 +233,8 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if extra:
+        out["extra"] = extra
     if converge:
         out["converged_iterations"] = it
         out["time_to_tolerance_s"] = round(el_max, 4)

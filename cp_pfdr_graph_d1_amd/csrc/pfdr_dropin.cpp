@@ -5,7 +5,8 @@
 // reference's (src/PFDR_graph_quadratic_d1_l1.cpp:555-566,
 // src/PFDR_graph_quadratic_d1_bounds.cpp:532-543,
 // src/PFDR_graph_loss_d1_simplex.cpp:717-726,
-// src/proj_simplex_metric.cpp:85-89): same mangled names.
+// src/proj_simplex_metric.cpp:85-89, src/operator_norm_matrix.cpp:215-219):
+// same mangled names.
 #include <cstdio>
 #include <cstdlib>
 
@@ -13,6 +14,7 @@
 #include "../../include/PFDR_graph_quadratic_d1_bounds.hpp"
 #include "../../include/PFDR_graph_quadratic_d1_l1.hpp"
 #include "../../include/pfdr_mi355x.h"
+#include "../../include/operator_norm_matrix.hpp"
 #include "../../include/proj_simplex.hpp"
 
 namespace {
@@ -72,7 +74,22 @@ int pj(double *X, const double *M, int D, int N, int nm, const double *A, int na
     return pfdr_proj_simplex_metric_f64(X, M, D, N, nm, A, na);
 }
 
+int on(int M, int N, const float *A, float tol, int itMax, int nb, int vb, float *out) {
+    return pfdr_operator_norm_f32(M, N, A, PFDR_MEM_HOST, tol, itMax, nb, vb, out, nullptr);
+}
+int on(int M, int N, const double *A, double tol, int itMax, int nb, int vb, double *out) {
+    return pfdr_operator_norm_f64(M, N, A, PFDR_MEM_HOST, tol, itMax, nb, vb, out, nullptr);
+}
+
 }  // namespace
+
+template <typename real>
+real operator_norm_matrix(int M, int N, const real *A, const real nTol, const int itMax,
+                          int nbInit, const int verbose) {
+    real out = real(0);
+    check(on(M, N, A, nTol, itMax, nbInit, verbose, &out));
+    return out;
+}
 
 template <typename real>
 void PFDR_graph_quadratic_d1_l1(const int V, const int E, const int N, real *X, const real *Y,
@@ -141,3 +158,7 @@ template void proj_simplex_metric<float>(float *, const float *, const int, cons
     const int, const float *, const int);
 template void proj_simplex_metric<double>(double *, const double *, const int, const int,
     const int, const double *, const int);
+template float operator_norm_matrix<float>(int, int, const float *, const float, const int, int,
+                                           const int);
+template double operator_norm_matrix<double>(int, int, const double *, const double, const int,
+                                             int, const int);

@@ -1,0 +1,517 @@
+// Gram matrices on the matrix cores and the operator norm of a dense matrix
+// (the CP reduced-problem builder).
+//
+// Reference: src/operator_norm_matrix.cpp:87-212 — the squared operator norm
+// ||A||^2 by the power method on A^tA (or AA^t), from nbInit random starts,
+// after an optional explicit symmetrisation (:112-165).  CP calls it on every
+// reduced problem with a dense A (src/CP_PFDR_graph_quadratic_d1_l1.cpp:792,
+// :822), and forms the reduced Gram rA^t rA the same way (:688-702).
+//
+// MI355X design:
+//   * k_gram: G = L^t R for L = R = A (one matrix, two tiles), exact-f32
+//     MFMA (v_mfma_f32_32x32x2_f32) or f64 MFMA (v_mfma_f64_16x16x4_f64);
+//     256-thread blocks of 4 waves, a 2x2 grid of MFMA tiles per wave, K
+//     staged through LDS in BK slices; only the upper block triangle is
+//     computed, the epilogue mirrors it; the contraction is split into
+//     chunks (deterministic second pass) so that a 1024-wide Gram over two
+//     million columns still fills the 256 CUs.
+//   * the power method runs all starts at once: X is S-by-B, one apply is
+//     a skinny product (HBM-bound: each pass streams the matrix once for
+//     all B starts); each start keeps the reference's stopping rule
+//     (a - b)/b < nTol and result b.
+//   * symmetrise when the Gram's matrix-core time beats itMax * nbInit
+//     streaming passes over A on this GPU (the reference's rule counts CPU
+//     flops, :112).
+// Starts are deterministic (splitmix64), not time-seeded as in the
+// reference (:187): the estimate is reproducible.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "pfdr_graph.hpp"
+#include "pfdr_session.hpp"
+
+namespace pfdr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <typename real>
+struct Mfma;
+template <>
+struct Mfma<float> {
+    static constexpr int T = 32, KS = 2, NR = 16, BT = 128, BK = 32;
+    typedef f32x16 acc_t;
+    __device__ static acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    // C/D map of the 32x32 shapes
+    __device__ static int row(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+    __device__ static int col(int lane, int) { return lane & 31; }
+};
+template <>
+struct Mfma<double> {
+    static constexpr int T = 16, KS = 4, NR = 4, BT = 64, BK = 16;
+    typedef f64x4 acc_t;
+    __device__ static acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // f64 16x16x4 has its own C/D map (cdna_hip_programming.md §3)
+    __device__ static int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+    __device__ static int col(int lane, int) { return lane & 15; }
+};
+
+enum GramLayout : int {
+    GRAM_TN = 0,  // G = A^t A: A is K-by-P column-major (contraction index contiguous)
+    GRAM_NT = 1   // G = A A^t: A is P-by-K column-major (output index contiguous)
+};
+
+// element (i, k) of the operand: TN A[k + i*ld], NT A[i + k*ld]
+template <typename real, int LAYOUT>
+__device__ __forceinline__ real gram_elem(const real *A, long ld, long i, long k) {
+    return LAYOUT == GRAM_TN ? A[k + i * ld] : A[i + k * ld];
+}
+
+// One block = one BT x BT tile (bi <= bj) of the chunk [k0, k1) of the
+// contraction; output partial G (P x P, column-major) of this chunk.
+template <typename real, int LAYOUT>
+__global__ __launch_bounds__(256) void k_gram(int P, long K, const real *__restrict__ A, long ld,
+                                            long kchunk, real *__restrict__ Gpart) {
+    using M = Mfma<real>;
+    constexpr int BT = M::BT, BK = M::BK, T = M::T, WT = BT / 2, NT = WT / T;
+    const int bi = blockIdx.x, bj = blockIdx.y;
+    if (bi > bj) return;
+    const long k0 = (long)blockIdx.z * kchunk;
+    const long k1 = min(K, k0 + kchunk);
+    real *G = Gpart + (size_t)blockIdx.z * P * P;
+    __shared__ real Ls[BK][BT + 1], Rs[BK][BT + 1];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wi = w & 1, wj = w >> 1;
+    typename M::acc_t acc[NT][NT];
+#pragma unroll
+    for (int a = 0; a < NT; a++)
+#pragma unroll
+        for (int b = 0; b < NT; b++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) acc[a][b][r] = real(0);
+    const long i0 = (long)bi * BT, j0 = (long)bj * BT;
+    for (long kb = k0; kb < k1; kb += BK) {
+        // stage the two BT x BK operand tiles as [k][i]
+        for (int e = t; e < BT * BK; e += 256) {
+            int i, k;
+            if (LAYOUT == GRAM_TN) { i = e / BK; k = e - i * BK; }   // k fastest: coalesced columns
+            else { k = e / BT; i = e - k * BT; }                     // i fastest
+            const long kk = kb + k;
+            const bool kin = kk < k1;
+            Ls[k][i] = (kin && i0 + i < P) ? gram_elem<real, LAYOUT>(A, ld, i0 + i, kk) : real(0);
+            Rs[k][i] = (kin && j0 + i < P) ? gram_elem<real, LAYOUT>(A, ld, j0 + i, kk) : real(0);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int ks = 0; ks < BK; ks += M::KS) {
+            const int kr = ks + lane / T, c = lane % T;
+            real a[NT], b[NT];
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                a[q] = Ls[kr][wi * WT + q * T + c];
+                b[q] = Rs[kr][wj * WT + q * T + c];
+            }
+#pragma unroll
+            for (int x = 0; x < NT; x++)
+#pragma unroll
+                for (int y = 0; y < NT; y++) acc[x][y] = M::mma(a[x], b[y], acc[x][y]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int x = 0; x < NT; x++)
+#pragma unroll
+        for (int y = 0; y < NT; y++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) {
+                const long i = i0 + wi * WT + x * T + M::row(lane, r);
+                const long j = j0 + wj * WT + y * T + M::col(lane, r);
+                if (i < P && j < P) {
+                    G[i + j * P] = acc[x][y][r];
+                    if (bi != bj) G[j + i * P] = acc[x][y][r];
+                }
+            }
+}
+
+// G = sum of the chunk partials, in chunk order
+template <typename real>
+__global__ void k_gram_sum(long PP, int nchunk, const real *__restrict__ part,
+                           real *__restrict__ G) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= PP) return;
+    real s = part[i];
+    for (int c = 1; c < nchunk; c++) s += part[(size_t)c * PP + i];
+    G[i] = s;
+}
+
+// G (P x P) of A: which = 0 -> A^t A (A is K x P, ld >= K), 1 -> A A^t (A is
+// P x K, ld >= P).  Device pointers; G may not alias A.
+template <typename real>
+void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t s) {
+    using M = Mfma<real>;
+    if (P <= 0) return;
+    const int nb = (P + M::BT - 1) / M::BT;
+    const long tiles = (long)nb * (nb + 1) / 2;
+    long nchunk = std::max(1L, std::min((2048 + tiles - 1) / tiles, (K + 4 * M::BK - 1) / (4 * M::BK)));
+    long kchunk = (K + nchunk - 1) / nchunk;
+    kchunk = ((kchunk + M::BK - 1) / M::BK) * M::BK;
+    nchunk = K > 0 ? (K + kchunk - 1) / kchunk : 1;
+    if (nchunk > 65535) throw std::runtime_error("gram: contraction too long");
+    const size_t PP = (size_t)P * P;
+    DevBuf<real> part;
+    real *out = G;
+    if (nchunk > 1) { part.alloc(PP * nchunk); out = part.p; }
+    if (K == 0) { PFDR_HIP(hipMemsetAsync(G, 0, PP * sizeof(real), s)); return; }
+    dim3 grid(nb, nb, (unsigned)nchunk);
+    if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+    else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+    PFDR_HIP(hipGetLastError());
+    if (nchunk > 1) {
+        k_gram_sum<real><<<grid_for((long)PP), kBlock, 0, s>>>((long)PP, (int)nchunk, part.p, G);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));  // part is freed on return
+    }
+}
+
+// ------------------------------------------------------- power method --
+// Y (rows x B) = Mat (rows x K, column-major, ld) * X (K x B): one lane per
+// row, the B columns of X broadcast from LDS, the matrix streamed once.
+template <typename real, int B>
+__global__ __launch_bounds__(256) void k_apply_rows(int rows, long K, const real *__restrict__ Mat,
+                                                  long ld, const real *__restrict__ X,
+                                                  real *__restrict__ Y, int kchunk,
+                                                  real *__restrict__ part) {
+    __shared__ real xs[64][B];
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    const long kb0 = (long)blockIdx.y * kchunk, kb1 = min(K, kb0 + kchunk);
+    real acc[B];
+#pragma unroll
+    for (int c = 0; c < B; c++) acc[c] = real(0);
+    for (long k0 = kb0; k0 < kb1; k0 += 64) {
+        const int nk = (int)min(64L, kb1 - k0);
+        for (int e = threadIdx.x; e < 64 * B; e += 256) {
+            const int k = e / B, c = e - k * B;
+            xs[k][c] = k < nk ? X[(k0 + k) + (long)c * K] : real(0);
+        }
+        __syncthreads();
+        if (r < rows) {
+            for (int k = 0; k < nk; k++) {
+                const real m = Mat[r + (k0 + k) * ld];
+#pragma unroll
+                for (int c = 0; c < B; c++) acc[c] += m * xs[k][c];
+            }
+        }
+        __syncthreads();
+    }
+    if (r < rows) {
+        real *out = gridDim.y > 1 ? part + (size_t)blockIdx.y * rows * B : Y;
+#pragma unroll
+        for (int c = 0; c < B; c++) out[r + (long)c * rows] = acc[c];
+    }
+}
+
+template <typename real>
+__global__ void k_sum_parts(long n, int np, const real *__restrict__ part, real *__restrict__ Y) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    real s = part[i];
+    for (int c = 1; c < np; c++) s += part[(size_t)c * n + i];
+    Y[i] = s;
+}
+
+// Y (cols x B) = Mat^t X: Mat is rows x cols column-major; one wave per column
+template <typename real, int B>
+__global__ __launch_bounds__(256) void k_apply_cols(int rows, long cols, const real *__restrict__ Mat,
+                                                  long ld, const real *__restrict__ X,
+                                                  real *__restrict__ Y) {
+    const int lane = threadIdx.x & 63;
+    const long j = ((long)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (j >= cols) return;
+    const real *m = Mat + j * ld;
+    real acc[B];
+#pragma unroll
+    for (int c = 0; c < B; c++) acc[c] = real(0);
+    for (int i = lane; i < rows; i += 64) {
+        const real v = m[i];
+#pragma unroll
+        for (int c = 0; c < B; c++) acc[c] += v * X[i + (long)c * rows];
+    }
+#pragma unroll
+    for (int c = 0; c < B; c++) {
+        const real s = wave_sum(acc[c]);
+        if (lane == 0) Y[j + c * cols] = s;
+    }
+}
+
+// starting vectors: U[-1, 1) from splitmix64 (deterministic)
+template <typename real>
+__global__ void k_power_init(long n, int B, real *X) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * B) return;
+    unsigned long long z = (unsigned long long)i * 0xD1B54A32D192ED03ull + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    X[i] = (real)((double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0);
+}
+
+// per-column norms of X (n x B): one block per column
+template <typename real>
+__global__ __launch_bounds__(256) void k_col_norms(long n, const real *__restrict__ X,
+                                                 real *__restrict__ nrm) {
+    __shared__ real red[kBlock / kWave];
+    const real *x = X + (long)blockIdx.x * n;
+    real s = real(0);
+    for (long i = threadIdx.x; i < n; i += 256) s += x[i] * x[i];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) nrm[blockIdx.x] = std::sqrt(s);
+}
+
+// X[:, c] /= b[c]
+template <typename real>
+__global__ void k_col_scale(long n, int B, real *X, const real *__restrict__ b) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * B) return;
+    X[i] /= b[i / n];
+}
+
+// the reference's per-start stopping rule (:201-205): a = new norm, b = old;
+// state[c]: 0 running, 1 stopped; res[c] holds b
+template <typename real>
+__global__ void k_power_step(int B, const real *__restrict__ a, real *b, int *state, real nTol,
+                             int *running) {
+    const int c = threadIdx.x;
+    if (c >= B) return;
+    if (state[c]) return;
+    if ((a[c] - b[c]) / b[c] < nTol) { state[c] = 1; return; }
+    b[c] = a[c];
+    atomicAdd(running, 1);
+}
+
+template <typename real>
+static void apply_rows(int B, int rows, long K, const real *Mat, long ld, const real *X, real *Y,
+                       hipStream_t s) {
+    // split the contraction so that short-and-wide products fill the GPU
+    const int rb = (rows + 255) / 256;
+    int np = (int)std::max(1L, std::min(512L / rb, (K + 1023) / 1024));
+    const int kchunk = (int)((K + np - 1) / np);
+    np = (int)((K + kchunk - 1) / kchunk);
+    DevBuf<real> part;
+    if (np > 1) part.alloc((size_t)np * rows * B);
+    dim3 g(rb, np);
+#define PFDR_APPLY(BB) k_apply_rows<real, BB><<<g, 256, 0, s>>>(rows, K, Mat, ld, X, Y, kchunk, part.p)
+    if (B == 16) PFDR_APPLY(16);
+    else if (B == 32) PFDR_APPLY(32);
+    else PFDR_APPLY(64);
+#undef PFDR_APPLY
+    PFDR_HIP(hipGetLastError());
+    if (np > 1) {
+        k_sum_parts<real><<<grid_for((long)rows * B), kBlock, 0, s>>>((long)rows * B, np, part.p, Y);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+}
+
+template <typename real>
+static void apply_cols(int B, int rows, long cols, const real *Mat, long ld, const real *X, real *Y,
+                       hipStream_t s) {
+    const int g = grid_for(cols * 64);
+    if (B == 16) k_apply_cols<real, 16><<<g, 256, 0, s>>>(rows, cols, Mat, ld, X, Y);
+    else if (B == 32) k_apply_cols<real, 32><<<g, 256, 0, s>>>(rows, cols, Mat, ld, X, Y);
+    else k_apply_cols<real, 64><<<g, 256, 0, s>>>(rows, cols, Mat, ld, X, Y);
+    PFDR_HIP(hipGetLastError());
+}
+
+// squared operator norm of A (M x N column-major, device), or of the
+// symmetric S x S matrix A when M or N is 0 (ref :95-103)
+template <typename real>
+real operator_norm_device(int M, int N, const real *A, real nTol, int itMax, int nbInit,
+                          int verbose, hipStream_t s, double *gram_ms) {
+    if (gram_ms) *gram_ms = 0.0;
+    const int P = std::min(M, N);
+    int S;
+    const real *Mat = A;
+    DevBuf<real> G;
+    bool sym = false;
+    if (P == 0) {
+        S = std::max(M, N);
+        sym = true;
+    } else {
+        S = N;
+        // matrix-core Gram (2 M N P flops at ~1e14/s) vs itMax * nbInit
+        // streaming pass pairs over A (2 M N * sizeof(real) bytes at ~5e12/s)
+        const double t_gram = 2.0 * M * N * (double)P / 1e14;
+        const double t_pass = 2.0 * M * N * sizeof(real) / 5e12 * itMax * std::max(1, nbInit / 64 + 1);
+        if (t_gram < t_pass) {
+            sym = true;
+            S = P;
+            G.alloc((size_t)P * P);
+            hipEvent_t e0, e1;
+            if (gram_ms) {
+                PFDR_HIP(hipEventCreate(&e0));
+                PFDR_HIP(hipEventCreate(&e1));
+                PFDR_HIP(hipEventRecord(e0, s));
+            }
+            if (P == M) gram<real>(1, P, N, A, M, G.p, s);  // A A^t
+            else gram<real>(0, P, M, A, M, G.p, s);         // A^t A
+            if (gram_ms) {
+                float ms = 0.f;
+                PFDR_HIP(hipEventRecord(e1, s));
+                PFDR_HIP(hipEventSynchronize(e1));
+                PFDR_HIP(hipEventElapsedTime(&ms, e0, e1));
+                *gram_ms = ms;
+                (void)hipEventDestroy(e0);
+                (void)hipEventDestroy(e1);
+            }
+            Mat = G.p;
+        }
+    }
+    if (verbose) {
+        printf("compute matrix operator norm on %d initializations (%s)... ", nbInit,
+               sym ? "symmetrized" : "direct");
+        fflush(stdout);
+    }
+    const int n = S;               // length of the iterated vectors
+    const int B = nbInit <= 16 ? 16 : nbInit <= 32 ? 32 : 64;
+    real best = real(0);
+    for (int done = 0; done < std::max(nbInit, 1); done += B) {
+        DevBuf<real> X((size_t)n * B), Y((size_t)n * B), T(sym ? 0 : (size_t)M * B), a(B), b(B);
+        DevBuf<int> state(B), running(1);
+        PFDR_HIP(hipMemsetAsync(state.p, 0, B * sizeof(int), s));
+        k_power_init<real><<<grid_for((long)n * B), kBlock, 0, s>>>(n, B, X.p);
+        auto apply = [&](real *in, real *out) {  // out = Mat^t Mat in (or Mat in)
+            if (sym) {
+                apply_rows<real>(B, n, n, Mat, n, in, out, s);
+            } else {
+                apply_rows<real>(B, M, N, A, M, in, T.p, s);       // A X
+                apply_cols<real>(B, M, N, A, M, T.p, out, s);      // A^t (A X)
+            }
+        };
+        // b = ||X||; X /= b; X = A^tA X; b = ||X|| (ref :193-196)
+        k_col_norms<real><<<B, 256, 0, s>>>(n, X.p, b.p);
+        k_col_scale<real><<<grid_for((long)n * B), kBlock, 0, s>>>(n, B, X.p, b.p);
+        apply(X.p, Y.p);
+        k_col_norms<real><<<B, 256, 0, s>>>(n, Y.p, b.p);
+        std::swap(X.p, Y.p);
+        int *hrun = nullptr;
+        PFDR_HIP(hipHostMalloc(&hrun, sizeof(int), hipHostMallocDefault));
+        for (int it = 0; it < itMax; it++) {
+            k_col_scale<real><<<grid_for((long)n * B), kBlock, 0, s>>>(n, B, X.p, b.p);
+            apply(X.p, Y.p);
+            k_col_norms<real><<<B, 256, 0, s>>>(n, Y.p, a.p);
+            PFDR_HIP(hipMemsetAsync(running.p, 0, sizeof(int), s));
+            k_power_step<real><<<1, 64, 0, s>>>(B, a.p, b.p, state.p, nTol, running.p);
+            PFDR_HIP(hipGetLastError());
+            std::swap(X.p, Y.p);
+            PFDR_HIP(hipMemcpyAsync(hrun, running.p, sizeof(int), hipMemcpyDeviceToHost, s));
+            PFDR_HIP(hipStreamSynchronize(s));
+            if (*hrun == 0) break;
+        }
+        (void)hipHostFree(hrun);
+        std::vector<real> hb(B);
+        PFDR_HIP(hipMemcpyAsync(hb.data(), b.p, B * sizeof(real), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        const int use = std::min(B, std::max(nbInit, 1) - done);
+        for (int c = 0; c < use; c++)
+            if (hb[c] > best) best = hb[c];  // NaN-free starts only (ref :208)
+    }
+    if (verbose) { printf("done.\n"); fflush(stdout); }
+    return best;
+}
+
+template <typename real>
+static int opnorm_host(const char *fn, int M, int N, const real *A, int mem, real nTol, int itMax,
+                       int nbInit, int verbose, real *norm2, double *gram_ms) {
+    if (M < 0 || N < 0 || (M == 0 && N == 0) || !A || !norm2)
+        return report_error(fn, "invalid arguments");
+    try {
+        hipStream_t s = lib_stream();
+        const int P = std::min(M, N);
+        const size_t n = P == 0 ? (size_t)std::max(M, N) * std::max(M, N) : (size_t)M * N;
+        const real *dA = A;
+        DevBuf<real> buf;
+        if (mem != PFDR_MEM_DEVICE) {
+            buf.alloc(n);
+            PFDR_HIP(hipMemcpyAsync(buf.p, A, n * sizeof(real), hipMemcpyHostToDevice, s));
+            dA = buf.p;
+        }
+        *norm2 = operator_norm_device<real>(M, N, dA, nTol, itMax, nbInit, verbose, s, gram_ms);
+    } catch (const HipError &h) {
+        return report_error(fn, h);
+    } catch (const std::exception &ex) {
+        return report_error(fn, ex.what());
+    }
+    return PFDR_OK;
+}
+
+template <typename real>
+static int gram_host(const char *fn, int which, int M, int N, const real *A, int mem, real *G,
+                     double *ms) {
+    if (M < 0 || N < 0 || !A || !G || (which != 0 && which != 1))
+        return report_error(fn, "invalid arguments");
+    try {
+        hipStream_t s = lib_stream();
+        const int P = which == 0 ? N : M;
+        const long K = which == 0 ? M : N;
+        const size_t n = (size_t)M * N, PP = (size_t)P * P;
+        const real *dA = A;
+        real *dG = G;
+        DevBuf<real> bA, bG;
+        if (mem != PFDR_MEM_DEVICE) {
+            bA.alloc(n);
+            bG.alloc(PP);
+            PFDR_HIP(hipMemcpyAsync(bA.p, A, n * sizeof(real), hipMemcpyHostToDevice, s));
+            dA = bA.p;
+            dG = bG.p;
+        }
+        hipEvent_t e0, e1;
+        PFDR_HIP(hipEventCreate(&e0));
+        PFDR_HIP(hipEventCreate(&e1));
+        PFDR_HIP(hipEventRecord(e0, s));
+        gram<real>(which, P, K, dA, M, dG, s);
+        PFDR_HIP(hipEventRecord(e1, s));
+        PFDR_HIP(hipEventSynchronize(e1));
+        float t = 0.f;
+        PFDR_HIP(hipEventElapsedTime(&t, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (ms) *ms = t;
+        if (mem != PFDR_MEM_DEVICE)
+            PFDR_HIP(hipMemcpyAsync(G, dG, PP * sizeof(real), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    } catch (const HipError &h) {
+        return report_error(fn, h);
+    } catch (const std::exception &ex) {
+        return report_error(fn, ex.what());
+    }
+    return PFDR_OK;
+}
+
+}  // namespace pfdr
+
+extern "C" int pfdr_gram_f32(int which, int M, int N, const float *A, int mem, float *G,
+                             double *ms) {
+    return pfdr::gram_host<float>("pfdr_gram_f32", which, M, N, A, mem, G, ms);
+}
+extern "C" int pfdr_gram_f64(int which, int M, int N, const double *A, int mem, double *G,
+                             double *ms) {
+    return pfdr::gram_host<double>("pfdr_gram_f64", which, M, N, A, mem, G, ms);
+}
+extern "C" int pfdr_operator_norm_f32(int M, int N, const float *A, int mem, float nTol,
+                                      int itMax, int nbInit, int verbose, float *norm2,
+                                      double *gram_ms) {
+    return pfdr::opnorm_host<float>("pfdr_operator_norm_f32", M, N, A, mem, nTol, itMax, nbInit,
+                                    verbose, norm2, gram_ms);
+}
+extern "C" int pfdr_operator_norm_f64(int M, int N, const double *A, int mem, double nTol,
+                                      int itMax, int nbInit, int verbose, double *norm2,
+                                      double *gram_ms) {
+    return pfdr::opnorm_host<double>("pfdr_operator_norm_f64", M, N, A, mem, nTol, itMax, nbInit,
+                                     verbose, norm2, gram_ms);
+}

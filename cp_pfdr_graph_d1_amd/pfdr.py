@@ -36,6 +36,7 @@ EXPORTED = (
     "pfdr_quadratic_d1_bounds_f32", "pfdr_quadratic_d1_bounds_f64",
     "pfdr_loss_d1_simplex_f32", "pfdr_loss_d1_simplex_f64",
     "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
+    "pfdr_gram_f32", "pfdr_gram_f64", "pfdr_operator_norm_f32", "pfdr_operator_norm_f64",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -504,6 +505,65 @@ def gen_grid_edges(shape, conn, v_range=None):
     lib.pfdr_gen_grid_edges(nx, ny, nz, conn, v0, v1, Eu.ctypes.data,
                             Ev.ctypes.data)
     return Eu, Ev
+
+
+def gram(A, which=0, device=False):
+    """G = A^t A (which = 0) or A A^t (which = 1) on the matrix cores.
+    A: (M, N) numpy array (any order; treated as the matrix) or, with
+    device=True, a torch CUDA tensor holding the column-major M-by-N matrix
+    as a (N, M) contiguous tensor.  Returns (G, kernel_ms)."""
+    lib = load()
+    ms = C.c_double(0.0)
+    if device:
+        import torch
+        N, M = A.shape
+        P = N if which == 0 else M
+        G = torch.empty((P, P), dtype=A.dtype, device=A.device)
+        fn = lib.pfdr_gram_f32 if A.dtype == torch.float32 else lib.pfdr_gram_f64
+        _check(fn(which, M, N, C.c_void_p(A.data_ptr()), PFDR_MEM_DEVICE,
+                  C.c_void_p(G.data_ptr()), C.byref(ms)), "pfdr_gram")
+        return G, ms.value
+    A = np.asarray(A)
+    M, N = A.shape
+    Af = np.asfortranarray(A)
+    ct, sfx, _ = _real(Af.dtype)
+    P = N if which == 0 else M
+    G = np.empty((P, P), Af.dtype, order="F")
+    _check(getattr(lib, "pfdr_gram_" + sfx)(which, M, N, C.c_void_p(Af.ctypes.data),
+                                             PFDR_MEM_HOST, C.c_void_p(G.ctypes.data),
+                                             C.byref(ms)), "pfdr_gram")
+    return np.ascontiguousarray(G), ms.value
+
+
+def operator_norm(A, nTol=1e-3, itMax=100, nbInit=10, symmetric=False, device=False,
+                  M=None, N=None, verbose=0):
+    """||A||^2 (reference operator_norm_matrix).  symmetric=True: A is the
+    S-by-S A^tA / AA^t itself (the reference's M or N = 0).  device=True: A
+    is a torch CUDA tensor, column-major M-by-N stored as (N, M).  Returns
+    (norm2, gram_ms)."""
+    lib = load()
+    gms = C.c_double(0.0)
+    if device:
+        import torch
+        Nn, Mm = A.shape
+        if symmetric:
+            Mm, Nn = 0, Nn
+        ct = C.c_float if A.dtype == torch.float32 else C.c_double
+        fn = lib.pfdr_operator_norm_f32 if A.dtype == torch.float32 else lib.pfdr_operator_norm_f64
+        out = ct(0)
+        _check(fn(Mm, Nn, C.c_void_p(A.data_ptr()), PFDR_MEM_DEVICE, ct(nTol), itMax, nbInit,
+                  verbose, C.byref(out), C.byref(gms)), "pfdr_operator_norm")
+        return out.value, gms.value
+    A = np.asarray(A)
+    Af = np.asfortranarray(A)
+    ct, sfx, _ = _real(Af.dtype)
+    Mm, Nn = (0, A.shape[0]) if symmetric else A.shape
+    out = ct(0)
+    _check(getattr(lib, "pfdr_operator_norm_" + sfx)(Mm, Nn, C.c_void_p(Af.ctypes.data),
+                                                      PFDR_MEM_HOST, ct(nTol), itMax, nbInit,
+                                                      verbose, C.byref(out), C.byref(gms)),
+           "pfdr_operator_norm")
+    return out.value, gms.value
 
 
 def grid_edge_count(shape, conn, v_end):

@@ -179,6 +179,24 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 
+/* ------------------------------------------- dense matrices (CP builder) -- */
+/* Gram matrix on the matrix cores (exact-f32 / f64 MFMA, fixed-order
+ * reductions): which = 0 -> G = A^t A (N-by-N), 1 -> G = A A^t (M-by-M); A
+ * is M-by-N column major; mem = PFDR_MEM_HOST or _DEVICE for A and G.
+ * *ms (may be NULL) receives the kernel time.  Replaces the reference's
+ * symmetrisation loops (src/operator_norm_matrix.cpp:112-165,
+ * src/CP_PFDR_graph_quadratic_d1_l1.cpp:688-702). */
+int pfdr_gram_f32(int which, int M, int N, const float *A, int mem, float *G, double *ms);
+int pfdr_gram_f64(int which, int M, int N, const double *A, int mem, double *G, double *ms);
+/* Squared operator norm ||A||^2 by the power method (reference
+ * operator_norm_matrix<real>, include/operator_norm_matrix.hpp:12-14, same
+ * argument meaning; deterministic starts).  *gram_ms (may be NULL): time of
+ * the Gram step when the matrix was symmetrised first. */
+int pfdr_operator_norm_f32(int M, int N, const float *A, int mem, float nTol, int itMax,
+                           int nbInit, int verbose, float *norm2, double *gram_ms);
+int pfdr_operator_norm_f64(int M, int N, const double *A, int mem, double nTol, int itMax,
+                           int nbInit, int verbose, double *norm2, double *gram_ms);
+
 /* ------------------------------------------------------ multi-GPU comm -- */
 /* Partitioned sessions (quadratic solvers, identity or diagonal A): every
  * rank passes its owned vertices (V of them, global ids [vtx_begin,

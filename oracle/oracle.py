@@ -139,3 +139,17 @@ class Oracle:
         fn(_ptr(X, ct), _ptr(M, ct), C.c_int(D), C.c_int(N), C.c_int(nm),
            _ptr(A, ct), C.c_int(na))
         return X
+
+    # ------------------------------------------------- operator norm --
+    def operator_norm(self, A, M, N, nTol=1e-3, itMax=100, nbInit=10):
+        """The reference's operator_norm_matrix (OpenMP build only: its
+        source calls omp_* unguarded); A column-major M-by-N (M or N = 0:
+        symmetric).  Time-seeded starts: an estimate, not a fixed value."""
+        if self.kind != "ref_omp":
+            raise NotImplementedError("operator norm: reference OpenMP build only")
+        A = np.ascontiguousarray(A)
+        ct, sfx = _real(A.dtype)
+        fn = self._fn("operator_norm", sfx)
+        fn.restype = ct
+        return float(fn(C.c_int(M), C.c_int(N), _ptr(A, ct), ct(nTol), C.c_int(itMax),
+                        C.c_int(nbInit)))

@@ -25,6 +25,8 @@ REFERENCE_SYMBOLS = [
     "_Z26PFDR_graph_loss_d1_simplexIdEviiiT_PKS0_PS0_S2_PKiS5_S2_S0_S0_S0_S0_iPiS3_S3_i",
     "_Z19proj_simplex_metricIfEvPT_PKS0_iiiS3_i",
     "_Z19proj_simplex_metricIdEvPT_PKS0_iiiS3_i",
+    "_Z20operator_norm_matrixIfET_iiPKS0_S0_iii",
+    "_Z20operator_norm_matrixIdET_iiPKS0_S0_iii",
 ]
 
 
@@ -56,12 +58,12 @@ def test_dropin_cxx_symbols_exported():
 
 
 def test_dropin_symbols_equal_reference_build():
-    path = os.path.join(ROOT, "oracle", "_ref", "libpfdr_ref_seq.so")
+    path = os.path.join(ROOT, "oracle", "_ref", "libpfdr_ref_omp.so")
     if not os.path.exists(path):
         pytest.skip("reference build absent")
     def cxx(syms):
         return {s for s in syms if s.startswith("_Z") and
-                ("PFDR_graph" in s or "proj_simplex_metric" in s)}
+                ("PFDR_graph" in s or "proj_simplex_metric" in s or "operator_norm_matrix" in s)}
     ref, ours = cxx(_dynsyms(path)), cxx(_dynsyms(pfdr.LIB_PATH))
     assert ref == ours == set(REFERENCE_SYMBOLS)
 
