@@ -66,6 +66,8 @@ class QuadSession final : public SessionBase {
     explicit QuadSession(const pfdr_problem *p);
     ~QuadSession() override {
         if (hctrl_) (void)hipHostFree(hctrl_);
+        for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
+        if (comm_) (void)hipStreamDestroy(comm_);
     }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
@@ -122,6 +124,18 @@ class QuadSession final : public SessionBase {
     void pull_ctrl();
     void print_progress();
     void pull(void *base, int eb) { if (halo_) halo_->pull(base, eb, stream); }
+    // halo / compute overlap (partitioned sessions): the halo exchanges run
+    // on comm_ while the sweeps of interior edges [elo_, ehi_) and interior
+    // vertex blocks [blo_, bhi_) (no ghost endpoint, no received
+    // contribution) run on the session stream
+    hipStream_t comm_ = nullptr;
+    hipEvent_t ev_[4] = {};  // xp ready, pulled, boundary W*Z ready, pushed
+    long elo_ = 0, ehi_ = 0;
+    int blo_ = 0, bhi_ = 0;
+    bool overlap_ = false;
+    void plan_overlap();
+    void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name);
+    void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name);
     const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
 };
 
@@ -299,6 +313,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     order_.release();  // inputs are in the internal labels now
+    if (halo_) {
+        const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
+        if (!(o && o[0] == '0')) plan_overlap();
+    }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
 
@@ -560,36 +578,73 @@ void QuadSession<real>::objective() {
 }
 
 template <typename real>
+void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name) {
+    if (eend <= ebeg) return;
+    hipStream_t s = stream;
+    constexpr int EPT = Vec<real>::kPer16B;
+    ProfScope ps(prof, name, s);
+    const int nb = grid_for(eend - ebeg, EPT), g = xcd_grid(nb, xcd_e_);
+    k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, Wd1u_.p, Wd1v_.p,
+                                            Th_.p, W2_.p, wz_.p, rho_, c, nb, xcd_e_, ebeg, eend);
+}
+
+template <typename real>
+void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name) {
+    if (bend <= bbeg) return;
+    hipStream_t s = stream;
+    VArgs<real> a{};
+    a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p; a.wz = wz_.p;
+    a.Y = Y_.p; a.A = A_.p; a.Ga = Ga_.p; a.Th_l1 = Th_l1_.p;
+    a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
+    a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
+    a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
+    a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_v_;
+    ProfScope ps(prof, name, s);
+    if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, xcd_v_), kBlock, 0, s>>>(a);
+    else k_vertex_sweep<real, 16><<<xcd_grid(a.nb, xcd_v_), kBlock, 0, s>>>(a);
+}
+
+template <typename real>
 void QuadSession<real>::body() {
     hipStream_t s = stream;
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
-    constexpr int EPT = Vec<real>::kPer16B;
-    if (halo_) {
-        ProfScope ps(prof, "halo_pull", s);
-        halo_->pull(xp_.p, sizeof(R2<real>), s);
-    }
-    if (E_) {
-        ProfScope ps(prof, "edge_sweep", s);
-        const int nb = grid_for(E_, EPT), g = xcd_grid(nb, xcd_e_);
-        k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, Wd1u_.p, Wd1v_.p,
-                                                Th_.p, W2_.p, wz_.p, rho_, c, nb, xcd_e_);
-    }
-    if (halo_) {
-        ProfScope ps(prof, "halo_push", s);
-        halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), s);
-    }
-    {
-        VArgs<real> a{};
-        a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p; a.wz = wz_.p;
-        a.Y = Y_.p; a.A = A_.p; a.Ga = Ga_.p; a.Th_l1 = Th_l1_.p;
-        a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
-        a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
-        a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
-        a.nb = nbv_; a.xcd = xcd_v_;
-        ProfScope ps(prof, "vertex_sweep", s);
-        if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(nbv_, xcd_v_), kBlock, 0, s>>>(a);
-        else k_vertex_sweep<real, 16><<<xcd_grid(nbv_, xcd_v_), kBlock, 0, s>>>(a);
+    if (overlap_) {
+        // pull ghosts (comm) || interior edges; boundary edges; push (comm)
+        // || interior vertices; boundary vertices
+        PFDR_HIP(hipEventRecord(ev_[0], s));
+        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[0], 0));
+        {
+            ProfScope ps(prof, "halo_pull", comm_);
+            halo_->pull(xp_.p, sizeof(R2<real>), comm_);
+        }
+        PFDR_HIP(hipEventRecord(ev_[1], comm_));
+        edge_sweep(elo_, ehi_, c, "edge_sweep");
+        PFDR_HIP(hipStreamWaitEvent(s, ev_[1], 0));
+        edge_sweep(0, elo_, c, "edge_sweep_b");
+        edge_sweep(ehi_, E_, c, "edge_sweep_b");
+        PFDR_HIP(hipEventRecord(ev_[2], s));
+        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[2], 0));
+        {
+            ProfScope ps(prof, "halo_push", comm_);
+            halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), comm_);
+        }
+        PFDR_HIP(hipEventRecord(ev_[3], comm_));
+        vertex_sweep(blo_, bhi_, c, "vertex_sweep");
+        PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
+        vertex_sweep(0, blo_, c, "vertex_sweep_b");
+        vertex_sweep(bhi_, nbv_, c, "vertex_sweep_b");
+    } else {
+        if (halo_) {
+            ProfScope ps(prof, "halo_pull", s);
+            halo_->pull(xp_.p, sizeof(R2<real>), s);
+        }
+        edge_sweep(0, E_, c, "edge_sweep");
+        if (halo_) {
+            ProfScope ps(prof, "halo_push", s);
+            halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), s);
+        }
+        vertex_sweep(0, nbv_, c, "vertex_sweep");
     }
     if (gated) {
         if (track_) {
@@ -601,6 +656,54 @@ void QuadSession<real>::body() {
     PFDR_HIP(hipGetLastError());
     if (mode_ == A_DIRECT || mode_ == A_ATA) forward_dense(gated ? GATE_ACTIVE : GATE_NONE);
     if (rec_obj_) objective();
+}
+
+// interior edge range and vertex-block range of a partitioned session (the
+// longest runs without ghost endpoints / received contributions); edges
+// outside [elo_, ehi_) and blocks outside [blo_, bhi_) wait for the halo
+template <typename real>
+void QuadSession<real>::plan_overlap() {
+    hipStream_t s = stream;
+    constexpr int EPT = Vec<real>::kPer16B;
+    // edges: a ghost endpoint (u is always owned; v may be a ghost)
+    std::vector<int> hv(E_);
+    if (E_) PFDR_HIP(hipMemcpy(hv.data(), Ev_.p, E_ * 4, hipMemcpyDeviceToHost));
+    long best0 = 0, best1 = 0;
+    for (long e = 0; e < E_;) {
+        if (hv[e] >= V_) { e++; continue; }
+        long f = e;
+        while (f < E_ && hv[f] < V_) f++;
+        if (f - e > best1 - best0) { best0 = e; best1 = f; }
+        e = f;
+    }
+    // both cuts on the lane width: every launch starts vector-aligned
+    elo_ = ((best0 + EPT - 1) / EPT) * EPT;
+    ehi_ = std::max(elo_, (best1 / EPT) * EPT);
+    // vertex blocks: any CSR entry from the received tail
+    std::vector<int> ptr(V_ + 1);
+    std::vector<unsigned> idx(inc_.n);
+    PFDR_HIP(hipMemcpy(ptr.data(), inc_.ptr.p, (V_ + 1) * 4, hipMemcpyDeviceToHost));
+    if (inc_.n) PFDR_HIP(hipMemcpy(idx.data(), inc_.idx.p, inc_.n * 4, hipMemcpyDeviceToHost));
+    int b0 = 0, b1 = 0;
+    for (int b = 0; b < nbv_;) {
+        auto tailblk = [&](int q) {
+            const int v0 = q * kBlock, v1 = std::min(V_, v0 + kBlock);
+            for (int j = ptr[v0]; j < ptr[v1]; j++)
+                if (idx[j] >= (unsigned)(2 * E_)) return true;
+            return false;
+        };
+        if (tailblk(b)) { b++; continue; }
+        int f = b;
+        while (f < nbv_ && !tailblk(f)) f++;
+        if (f - b > b1 - b0) { b0 = b; b1 = f; }
+        b = f;
+    }
+    blo_ = b0;
+    bhi_ = b1;
+    PFDR_HIP(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    for (hipEvent_t &e : ev_) PFDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    overlap_ = true;
+    (void)s;
 }
 
 template <typename real>

@@ -583,7 +583,8 @@ __device__ __forceinline__ void edge_update(const R2<real> &pu,
     }
 }
 
-// Edge sweep; writes the DR contributions W*Z side-major: wz[e] (u end),
+// Edge sweep over the edges [ebeg, eend) (ebeg a multiple of the lane
+// width); writes the DR contributions W*Z side-major: wz[e] (u end),
 // wz[E + e] (v end), so the u-side run of a vertex is contiguous.
 template <typename real>
 __global__ __launch_bounds__(256) void k_edge_sweep(
@@ -591,14 +592,15 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     const R2<real> *__restrict__ xp, real *__restrict__ Z2,
     const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
     const real *__restrict__ Th, const real *__restrict__ W2,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd,
+    long ebeg, long eend) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     const int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;
-    const long e0 = ((long)blk * blockDim.x + threadIdx.x) * EPT;
-    if (e0 >= E) return;
-    if (e0 + EPT <= E) {
+    const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
+    if (e0 >= eend) return;
+    if (e0 + EPT <= eend) {
         const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
         const Pk<int, EPT> iv = ldv<int, EPT>(Ev + e0);
         R2<real> pu[EPT], pv[EPT];
@@ -623,7 +625,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
         stv<real, EPT>(wz + e0, ou);
         stv<real, EPT>(wz + E + e0, ov);
     } else {
-        for (long e = e0; e < E; e++) {
+        for (long e = e0; e < eend; e++) {
             const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
             real zu = Z2[2 * e], zv = Z2[2 * e + 1];
             edge_update<real>(pu, pv, zu, zv, Wd1u[e], Wd1v[e], Th[e], rho);
@@ -638,7 +640,8 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 template <typename real>
 struct VArgs {
     int V;
-    int nb, xcd;            // logical blocks, XCD-aware order
+    int nb, xcd;            // logical blocks of this launch, XCD-aware order
+    int bbeg;               // first block of this launch (vertex block bbeg*256)
     const int *ptr;
     const unsigned *idx;
     const real *wz;         // contributions (local side-major, then received)
@@ -665,8 +668,9 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
-    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
-    if (blk >= a.nb) return;
+    const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (lb >= a.nb) return;
+    const int blk = a.bbeg + lb;
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     // per-vertex operands first: their latency hides under the gather
