@@ -85,6 +85,7 @@ class QuadSession final : public SessionBase {
     bool rec_obj_, rec_dif_, track_;
     int xcd_e_ = 0, xcd_v_ = 1;  // XCD-aware block order (edge / vertex sweep)
     int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
+    bool rw_ = true;             // edge sweep recomputes the prox weights (prox_weights)
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
     // emap_[edge position] = original edge id (setup only)
@@ -173,6 +174,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (x && strlen(x) == 2) { xcd_e_ = x[0] == '1'; xcd_v_ = x[1] == '1'; }
         const char *g = getenv("PFDR_GB");  // 8 (default) or 16
         if (g && atoi(g) == 16) gb_ = 16;
+        // prox weights recomputed in every edge sweep (default; PFDR_EDGE_RW=0
+        // streams the stored Wd1u, Wd1v, Th instead): 12 -> 4 streamed bytes
+        // per edge, 12 bytes of HBM per edge freed; headline edge sweep
+        // 0.544 -> 0.525 ms, C2 0.465 -> 0.430 ms
+        const char *r = getenv("PFDR_EDGE_RW");
+        rw_ = !(r && r[0] == '0');
     }
     // prox selection (ref l1 :499-512, bounds :472-490)
     positivity_ = 0;
@@ -239,7 +246,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     // edge state and per-vertex metric
     const size_t En = E ? E : 1;
     Z2_.alloc(2 * En); W2_.alloc(2 * En);
-    Wd1u_.alloc(En); Wd1v_.alloc(En); Th_.alloc(En);
+    if (!rw_) { Wd1u_.alloc(En); Wd1v_.alloc(En); Th_.alloc(En); }
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
     if (flavour_ == 0 && p->La_l1) Th_l1_.alloc(V);
     nbv_ = grid_for(V);
@@ -584,8 +591,14 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     constexpr int EPT = Vec<real>::kPer16B;
     ProfScope ps(prof, name, s);
     const int nb = grid_for(eend - ebeg, EPT), g = xcd_grid(nb, xcd_e_);
-    k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, Wd1u_.p, Wd1v_.p,
-                                            Th_.p, W2_.p, wz_.p, rho_, c, nb, xcd_e_, ebeg, eend);
+    if (rw_)
+        k_edge_sweep<real, true><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, nullptr,
+                                                      nullptr, nullptr, W2_.p, wz_.p, rho_, c, nb,
+                                                      xcd_e_, ebeg, eend, Ga_.p, La_d1_.p);
+    else
+        k_edge_sweep<real, false><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, Wd1u_.p,
+                                                       Wd1v_.p, Th_.p, W2_.p, wz_.p, rho_, c, nb,
+                                                       xcd_e_, ebeg, eend, nullptr, nullptr);
 }
 
 template <typename real>
