@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "pfdr_graph.hpp"
+#include "pfdr_quadratic_kernels.hpp"
 #include "pfdr_session.hpp"
 
 namespace pfdr {
@@ -139,6 +140,114 @@ __global__ __launch_bounds__(256) void k_gram(int P, long K, const real *__restr
             }
 }
 
+// The same tile with 16-byte operand loads and a register prefetch of the
+// next K slice while the matrix cores work on the current one (needs
+// ld % (16 / sizeof(real)) == 0 and a 16-byte aligned A).
+template <typename real, int LAYOUT>
+__global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__restrict__ A, long ld,
+                                              long kchunk, real *__restrict__ Gpart) {
+    using M = Mfma<real>;
+    constexpr int BT = M::BT, BK = M::BK, T = M::T, WT = BT / 2, NT = WT / T;
+    constexpr int VW = 16 / sizeof(real);                 // reals per 16-byte load
+    constexpr int NL = BT * BK / (256 * VW);               // vector loads per operand per lane
+    const int bi = blockIdx.x, bj = blockIdx.y;
+    if (bi > bj) return;
+    const long k0 = (long)blockIdx.z * kchunk;
+    const long k1 = min(K, k0 + kchunk);
+    real *G = Gpart + (size_t)blockIdx.z * P * P;
+    __shared__ alignas(16) real Ls[BK][BT + VW], Rs[BK][BT + VW];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wi = w & 1, wj = w >> 1;
+    const long i0 = (long)bi * BT, j0 = (long)bj * BT;
+    typename M::acc_t acc[NT][NT];
+#pragma unroll
+    for (int a = 0; a < NT; a++)
+#pragma unroll
+        for (int b = 0; b < NT; b++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) acc[a][b][r] = real(0);
+    // lane's vector slots: NT layout (i, k) = (4 consecutive i, one k);
+    // TN layout (i, k) = (one i, VW consecutive k)
+    Pk<real, VW> lr[NL], rr[NL];
+    auto load = [&](long kb) {
+#pragma unroll
+        for (int q = 0; q < NL; q++) {
+            const int f = t + 256 * q;
+            int i, k;
+            if (LAYOUT == GRAM_NT) { k = f / (BT / VW); i = (f - k * (BT / VW)) * VW; }
+            else { i = f / (BK / VW); k = (f - i * (BK / VW)) * VW; }
+            const long kk = kb + k;
+            for (int side = 0; side < 2; side++) {
+                const long base = side ? j0 : i0;
+                Pk<real, VW> &o = side ? rr[q] : lr[q];
+                const bool full = LAYOUT == GRAM_NT ? (kk < k1 && base + i + VW <= P)
+                                                    : (kk + VW <= k1 && base + i < P);
+                if (full) {
+                    o = LAYOUT == GRAM_NT ? ldv<real, VW>(A + (base + i) + kk * ld)
+                                          : ldv<real, VW>(A + kk + (base + i) * ld);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < VW; u++) {
+                        const long ii = LAYOUT == GRAM_NT ? base + i + u : base + i;
+                        const long ku = LAYOUT == GRAM_NT ? kk : kk + u;
+                        o.v[u] = (ii < P && ku < k1) ? gram_elem<real, LAYOUT>(A, ld, ii, ku)
+                                                     : real(0);
+                    }
+                }
+            }
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int q = 0; q < NL; q++) {
+            const int f = t + 256 * q;
+            if (LAYOUT == GRAM_NT) {
+                const int k = f / (BT / VW), i = (f - k * (BT / VW)) * VW;
+                stv<real, VW>(&Ls[k][i], lr[q]);
+                stv<real, VW>(&Rs[k][i], rr[q]);
+            } else {
+                const int i = f / (BK / VW), k = (f - i * (BK / VW)) * VW;
+#pragma unroll
+                for (int u = 0; u < VW; u++) { Ls[k + u][i] = lr[q].v[u]; Rs[k + u][i] = rr[q].v[u]; }
+            }
+        }
+    };
+    if (k0 < k1) load(k0);
+    for (long kb = k0; kb < k1; kb += BK) {
+        store();
+        __syncthreads();
+        if (kb + BK < k1) load(kb + BK);  // in flight during the MFMAs below
+#pragma unroll 4
+        for (int ks = 0; ks < BK; ks += M::KS) {
+            const int kr = ks + lane / T, c = lane % T;
+            real a[NT], b[NT];
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                a[q] = Ls[kr][wi * WT + q * T + c];
+                b[q] = Rs[kr][wj * WT + q * T + c];
+            }
+#pragma unroll
+            for (int x = 0; x < NT; x++)
+#pragma unroll
+                for (int y = 0; y < NT; y++) acc[x][y] = M::mma(a[x], b[y], acc[x][y]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int x = 0; x < NT; x++)
+#pragma unroll
+        for (int y = 0; y < NT; y++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) {
+                const long i = i0 + wi * WT + x * T + M::row(lane, r);
+                const long j = j0 + wj * WT + y * T + M::col(lane, r);
+                if (i < P && j < P) {
+                    G[i + j * P] = acc[x][y][r];
+                    if (bi != bj) G[j + i * P] = acc[x][y][r];
+                }
+            }
+}
+
 // G = sum of the chunk partials, in chunk order
 template <typename real>
 __global__ void k_gram_sum(long PP, int nchunk, const real *__restrict__ part,
@@ -169,8 +278,15 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     if (nchunk > 1) { part.alloc(PP * nchunk); out = part.p; }
     if (K == 0) { PFDR_HIP(hipMemsetAsync(G, 0, PP * sizeof(real), s)); return; }
     dim3 grid(nb, nb, (unsigned)nchunk);
-    if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
-    else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+    const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0 &&
+                     !(getenv("PFDR_GRAM_SCALAR") && getenv("PFDR_GRAM_SCALAR")[0] == '1');
+    if (vec) {
+        if (which == 0) k_gram_v<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+        else k_gram_v<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+    } else {
+        if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+        else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+    }
     PFDR_HIP(hipGetLastError());
     if (nchunk > 1) {
         k_gram_sum<real><<<grid_for((long)PP), kBlock, 0, s>>>((long)PP, (int)nchunk, part.p, G);

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void k_seq_sum(int V, const real *__restrict__
                                                  real *__restrict__ sum_out,
                                                  long long *__restrict__ cnt_out) {
     constexpr int CH = 4096;
-    __shared__ real buf[2][CH];
+    __shared__ alignas(16) real buf[2][CH];
     __shared__ long long red[kBlock / kWave];
     long long cnt = 0;
     for (int i = threadIdx.x; i < nparts; i += kBlock) cnt += cnt_part[i];
@@ -390,8 +390,18 @@ __global__ __launch_bounds__(256) void k_seq_sum(int V, const real *__restrict__
         const long n = min((long)CH, (long)V - c0);
         const long nxt = c0 + CH;
         if (threadIdx.x == 0) {
+            // 16-byte LDS reads issued ahead of the dependent add chain
+            constexpr int W = Vec<real>::kPer16B;
             const real *b = buf[cur];
-            for (long j = 0; j < n; j++) s += b[j];
+            const int nw = (int)n / W * W;
+            int j = 0;
+#pragma unroll 4
+            for (; j < nw; j += W) {
+                const Pk<real, W> q = ldv<real, W>(b + j);
+#pragma unroll
+                for (int u = 0; u < W; u++) s += q.v[u];
+            }
+            for (; j < (int)n; j++) s += b[j];
         } else if (nxt < V) {
             const long m = min((long)CH, (long)V - nxt);
             for (long j = threadIdx.x - 1; j < m; j += kBlock - 1) buf[cur ^ 1][j] = absval[nxt + j];
