@@ -389,9 +389,11 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
     const real *__restrict__ Th, const real *__restrict__ Wu,
     const real *__restrict__ Wv, real *__restrict__ wz, real rho,
-    const Ctrl<real> *ctrl) {
+    const Ctrl<real> *ctrl, int nb, int xcd) {
     if (ctrl && ctrl->halt) return;
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    const long i = (long)blk * blockDim.x + threadIdx.x;
     if (i >= EK) return;
     const int K = c.K;
     long e;
@@ -521,6 +523,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
 template <typename real>
 struct SxVArgs {
     int V, vb;
+    int nb, xcd;  // blocks, XCD-aware order
     long E;
     SxConst<real> c;
     const int *ptr;
@@ -542,7 +545,9 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     const int t = threadIdx.x;
     const int vl = t / K;
     const int k = t - vl * K;
-    const long v0 = (long)blockIdx.x * vb;
+    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (blk >= a.nb) return;
+    const long v0 = (long)blk * vb;
     const long v = v0 + vl;
     const bool live = vl < vb && v < a.V;
     const long i = v * K + k;
@@ -561,31 +566,33 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) w[q] = wz[(long)sl[q] * K + k];
             } else {  // W * Z formed here (the reference's product, same rounding)
+                // branch-free: received entries (address 2E + j) sit in the
+                // tails of Zv / Wv (Zv: the sender's W*Z, Wv: 1), so all 16
+                // loads issue together
                 real zq[8], wq[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
                     const long ad = sl[q];
-                    if (ad < 2 * a.E) {
-                        const bool sv = ad >= a.E;
-                        const long o = (sv ? ad - a.E : ad) * K + k;
-                        zq[q] = (sv ? a.Zv : a.Zu)[o];
-                        wq[q] = (sv ? a.Wv : a.Wu)[o];
-                    } else {  // received from the owner of the edge (already W*Z)
-                        zq[q] = wz[ad * K + k];
-                        wq[q] = real(1);
-                    }
+                    const bool sv = ad >= a.E;
+                    const long o = (sv ? ad - a.E : ad) * K + k;
+                    zq[q] = (sv ? a.Zv : a.Zu)[o];
+                    wq[q] = (sv ? a.Wv : a.Wu)[o];
                 }
 #pragma unroll
-                for (int q = 0; q < 8; q++) w[q] = (sl[q] < 2 * a.E) ? wq[q] * zq[q] : zq[q];
+                for (int q = 0; q < 8; q++) w[q] = wq[q] * zq[q];
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) s += w[q];
         }
         for (; j < j1; j++) {
             const long ad = a.idx[j];
-            if (WZ || ad >= 2 * a.E) s += wz[ad * K + k];
-            else if (ad >= a.E) s += a.Wv[(ad - a.E) * K + k] * a.Zv[(ad - a.E) * K + k];
-            else s += a.Wu[ad * K + k] * a.Zu[ad * K + k];
+            if (WZ) {
+                s += wz[ad * K + k];
+            } else {
+                const bool sv = ad >= a.E;
+                const long o = (sv ? ad - a.E : ad) * K + k;
+                s += (sv ? a.Wv : a.Wu)[o] * (sv ? a.Zv : a.Zu)[o];
+            }
         }
         xs[t] = s;
         ms[t] = a.Ga[i];
@@ -621,8 +628,14 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
             __syncthreads();
             if (t == 0) for (int q = 1; q < NT / kWave; q++) dif += red[q];
         }
-        if (t == 0) a.part[blockIdx.x] = dif;
+        if (t == 0) a.part[blk] = dif;
     }
+}
+
+template <typename real>
+__global__ void k_fill(long n, real *p, real v) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 // K-wide W*Z of the pushed v ends (address E + e) / u ends (address e),
@@ -846,6 +859,7 @@ class SimplexSession final : public SessionBase {
     // nor writes contributions: 28 instead of 44 streamed bytes per (e, k)
     // (C4: 2.42 -> 2.17 ms/iteration)
     bool sx_wz_ = false;
+    int sx_xcd_e_ = 1, sx_xcd_v_ = 0;  // XCD-aware block order (PFDR_SX_XCD=<edge><vertex>; C4: edge on -2%)
     int it_ = 0;
     bool stopped_ = false;
     int chunk_ = 32;
@@ -933,6 +947,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64 && !env_flag_off("PFDR_SX_FUSED")) {
         const char *nt = getenv("PFDR_SX_NT");  // threads per block: 64 (default) or 256
         sx_nt_ = (nt && atoi(nt) == 64) ? 64 : 256;
+        const char *xc = getenv("PFDR_SX_XCD");
+        if (xc && strlen(xc) == 2) { sx_xcd_e_ = xc[0] == '1'; sx_xcd_v_ = xc[1] == '1'; }
         const char *wz = getenv("PFDR_SX_WZ");  // 1: edge sweep stores W*Z (A/B)
         sx_wz_ = wz && wz[0] == '1';
         vb_ = sx_nt_ / K_;
@@ -942,7 +958,11 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     }
     FP_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
     const size_t EKn = EK_ ? EK_ : 1;
-    Zu_.alloc(EKn); Zv_.alloc(EKn); Wu_.alloc(EKn); Wv_.alloc(EKn);
+    // Zv / Wv carry the received contributions after their E*K entries
+    // (Zv: the sender's W*Z, Wv: 1) for the fused vertex sweep
+    Zu_.alloc(EKn); Wu_.alloc(EKn);
+    Zv_.alloc(EKn + (size_t)R_ * K_); Wv_.alloc(EKn + (size_t)R_ * K_);
+    if (R_) k_fill<real><<<grid_for(R_ * K_), kBlock, 0, s>>>(R_ * K_, Wv_.p + EKn, real(1));
     if (c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
@@ -1032,11 +1052,12 @@ void SimplexSession<real>::body() {
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     if (EK_) {
         ProfScope ps(prof, "sx_edge_sweep", s);
-        k_sx_edge_sweep<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+        const int nb = grid_for(EK_);
+        k_sx_edge_sweep<real><<<xcd_grid(nb, sx_xcd_e_), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
                                                                Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
                                                                Wu_.p, Wv_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
-                                                               rho_, c);
+                                                               rho_, c, nb, sx_xcd_e_);
     }
     if (halo_) {
         ProfScope ps(prof, "halo_push", s);
@@ -1049,12 +1070,14 @@ void SimplexSession<real>::body() {
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.Wu = Wu_.p; a.Wv = Wv_.p;
+        a.nb = nbs_; a.xcd = sx_xcd_v_;
+        const int g = xcd_grid(nbs_, sx_xcd_v_);
         if (sx_nt_ == 256) {
-            if (sx_wz_) k_sx_vertex_sweep<real, 256, true><<<nbs_, 256, 0, s>>>(a);
-            else k_sx_vertex_sweep<real, 256, false><<<nbs_, 256, 0, s>>>(a);
+            if (sx_wz_) k_sx_vertex_sweep<real, 256, true><<<g, 256, 0, s>>>(a);
+            else k_sx_vertex_sweep<real, 256, false><<<g, 256, 0, s>>>(a);
         } else {
-            if (sx_wz_) k_sx_vertex_sweep<real, 64, true><<<nbs_, 64, 0, s>>>(a);
-            else k_sx_vertex_sweep<real, 64, false><<<nbs_, 64, 0, s>>>(a);
+            if (sx_wz_) k_sx_vertex_sweep<real, 64, true><<<g, 64, 0, s>>>(a);
+            else k_sx_vertex_sweep<real, 64, false><<<g, 64, 0, s>>>(a);
         }
     } else {
         {
@@ -1105,7 +1128,7 @@ void SimplexSession<real>::push_wz() {
                                                                     Wu_.p, Zu_.p, Wv_.p, Zv_.p, buf);
         PFDR_HIP(hipGetLastError());
     }
-    halo_->push_packed(buf, tail, eb, stream);
+    halo_->push_packed(buf, Zv_.p + EK_, eb, stream);  // the tail of Zv (vertex sweep)
 }
 
 template <typename real>

@@ -3,9 +3,11 @@
 Per MI355X_MICROARCH.md §HBM (gfx950): FETCH_SIZE (KiB) reads exactly half
 the bytes of a wide coalesced streaming read, so read bytes = 2 x FETCH_SIZE
 x 1024; WRITE_SIZE (KiB) reads the bytes of 16-B-per-lane streaming stores
-exactly.  The edge sweep streams 16 B per lane on every array (the xp
-gathers are 8 B and mostly cache hits), so the x2 correction applies to it.
-Usage: python tools/pmc_traffic.py <dir with fetch/ and write/ subdirs>
+exactly.  The sweeps stream 16 B per lane on every array, so the x2
+correction applies to their streams; gathers are uncalibrated (the guide:
+ratios between variants of one kernel are unaffected).  Infinity-Cache hits
+are counted by these counters, not excluded.
+Usage: python tools/pmc_traffic.py <dir with fetch/ and write/> [workload E V]
 """
 import csv
 import glob
@@ -13,8 +15,6 @@ import json
 import os
 import sys
 from collections import defaultdict
-
-KERNELS = {"k_edge_sweep": "k_edge_sweep", "k_vertex_sweep": "k_vertex_sweep"}
 
 
 def counter(dirname, name):
@@ -25,22 +25,23 @@ def counter(dirname, name):
             if r.get("Counter_Name") != name:
                 continue
             kn = r.get("Kernel_Name", "")
-            for short in KERNELS:
-                if short in kn:
-                    vals[short].append(float(r["Counter_Value"]))
+            short = kn.split("(")[0].split("<")[0].split("::")[-1].strip()
+            if short.startswith("void "):
+                short = short[5:]
+            vals[short].append(float(r["Counter_Value"]))
     return vals
 
 
-def main(root):
+def main(root, workload="headline", E=60000000, V=10000000):
     fetch = counter(os.path.join(root, "fetch"), "FETCH_SIZE")
     write = counter(os.path.join(root, "write"), "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                     "headline bench (V=10M, E=60M, fp32)",
-           "workload_E": 60000000, "workload_V": 10000000, "kernels": {}}
-    for k in KERNELS:
-        f, w = fetch.get(k, []), write.get(k, [])
-        if not f or not w:
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel "
+                     "trace only), bench.py --workload %s" % workload,
+           "workload": workload, "workload_E": E, "workload_V": V, "kernels": {}}
+    for k in sorted(set(fetch) & set(write)):
+        if not k.startswith("k_"):
             continue
+        f, w = fetch[k], write[k]
         fk, wk = sum(f) / len(f), sum(w) / len(w)
         rd = 2.0 * fk * 1024.0
         wr = wk * 1024.0
@@ -51,4 +52,5 @@ def main(root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    a = sys.argv[1:]
+    main(a[0], *(a[1:2] + [int(x) for x in a[2:4]]))
