@@ -609,6 +609,13 @@ static int gram_host(const char *fn, int which, int M, int N, const real *A, int
     return PFDR_OK;
 }
 
+template void gram<float>(int, int, long, const float *, long, float *, hipStream_t);
+template void gram<double>(int, int, long, const double *, long, double *, hipStream_t);
+template float operator_norm_device<float>(int, int, const float *, float, int, int, int,
+                                           hipStream_t, double *);
+template double operator_norm_device<double>(int, int, const double *, double, int, int, int,
+                                             hipStream_t, double *);
+
 }  // namespace pfdr
 
 extern "C" int pfdr_gram_f32(int which, int M, int N, const float *A, int mem, float *G,

@@ -37,6 +37,7 @@ EXPORTED = (
     "pfdr_loss_d1_simplex_f32", "pfdr_loss_d1_simplex_f64",
     "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
     "pfdr_gram_f32", "pfdr_gram_f64", "pfdr_operator_norm_f32", "pfdr_operator_norm_f64",
+    "pfdr_cp_reduce_f32", "pfdr_cp_reduce_f64",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -348,6 +349,70 @@ def PFDR_graph_loss_d1_simplex(Q, al, Eu, Ev, La_d1, rho, condMin, difRcd,
     return P.reshape(Q.shape, order="F"), it, Obj, Dif
 
 
+def PFDR_quadratic_l1(obs, source, target, edge_weight, A, l1_weight, positivity=0,
+                      PFDR_rho=1.0, PFDR_condMin=1e-3, PFDR_difRcd=0.0, PFDR_difTol=1e-4,
+                      PFDR_itMax=10000, verbose=0):
+    """PFDR front-end with the conventions of the reference's Python binding
+    (python/CP_quadratic_l1_py.cpp:7-56, 130-258, which wraps CP; this
+    entry solves the same functional F(x) = 1/2 ||A x - obs||^2 + sum_e
+    edge_weight |x_u - x_v| + sum_v l1_weight |x_v| directly with PFDR):
+      * A scalar -> identity (its value discarded); A of shape (N,) ->
+        diagonal, obs and A pre-multiplied (obs*A, A*A) as the binding does
+        (:121-132); A of shape (N, V) -> the design matrix;
+      * edge_weight / l1_weight: array, or scalar broadcast to every edge /
+        vertex (the binding's broadcast loops run to V for both, :134-145,
+        an out-of-range write for the edge weights when E > V; here each
+        fills its own length);
+      * source / target: any integer dtype (the binding reinterprets uint32
+        as int32, :228-258);
+      * defaults from :64-72 (PFDR_rho 1, condMin 1e-3, difRcd 0, difTol
+        1e-4, itMax 1e4).
+    Returns (x, iterations)."""
+    obs = np.asarray(obs)
+    if obs.dtype not in (np.float32, np.float64):
+        raise TypeError("Type unknown, must be float32, float64, f4, or f8.")
+    dt = obs.dtype
+    A = np.asarray(A, dt)
+    N = obs.size
+    Eu, Ev = _edges(source, target)
+    E = Eu.size
+    if A.ndim == 0 or A.size == 1 and A.ndim <= 1 and N != 1:
+        V, mode = N, "identity"
+    elif A.ndim == 1:
+        if A.size != N:
+            raise ValueError("A should be either a scalar, vector of size N, or a N-by-V matrix ")
+        V, mode = N, "diagonal"
+    elif A.ndim == 2:
+        if A.shape[0] != N:
+            raise ValueError("A should be either a scalar, a vector of size N, or a N-by-V matrix ")
+        V, mode = A.shape[1], "matrix"
+    else:
+        raise ValueError("A should be either a scalar, a vector of size N, or a N-by-V matrix ")
+    ew = np.asarray(edge_weight, dt).ravel()
+    ew = np.full(E, ew[0], dt) if ew.size == 1 else ew
+    lw = np.asarray(l1_weight, dt).ravel()
+    lw = np.full(V, lw[0], dt) if lw.size == 1 else lw
+    lib = Lib()
+    X0 = np.zeros(V, dt)
+    if mode == "identity":
+        X, it, _, _ = lib.quadratic_d1_l1(X0, obs, None, 0, Eu, Ev, ew, lw, positivity, SCAL,
+                                          None, PFDR_rho, PFDR_condMin, PFDR_difRcd,
+                                          PFDR_difTol, PFDR_itMax, verbose=verbose)
+    elif mode == "diagonal":
+        Yd = (obs * A).astype(dt)
+        Ad = (A * A).astype(dt)
+        X, it, _, _ = lib.quadratic_d1_l1(X0, Yd, Ad, 0, Eu, Ev, ew, lw, positivity, DIAG, Ad,
+                                          PFDR_rho, PFDR_condMin, PFDR_difRcd, PFDR_difTol,
+                                          PFDR_itMax, verbose=verbose)
+    else:
+        Af = np.asfortranarray(A)
+        L = np.array([operator_norm(Af)[0]], dt)
+        X, it, _, _ = lib.quadratic_d1_l1(X0, obs, Af.ravel(order="F"), N, Eu, Ev, ew, lw,
+                                          positivity, SCAL, L, PFDR_rho, PFDR_condMin,
+                                          PFDR_difRcd, PFDR_difTol, PFDR_itMax, verbose=verbose)
+    return X, it
+
+
 def proj_simplex_metric(X, M, A):
     """Column-wise metric simplex projection of the D-by-N array X
     (include/proj_simplex.hpp:33-35); M is D-by-nm, A has na entries."""
@@ -564,6 +629,36 @@ def operator_norm(A, nTol=1e-3, itMax=100, nbInit=10, symmetric=False, device=Fa
                                                       verbose, C.byref(out), C.byref(gms)),
            "pfdr_operator_norm")
     return out.value, gms.value
+
+
+def cp_reduce(N, A, Y, comp_ptr, comp_vertices, preAt=True, normTol=1e-3, normItMax=100,
+              normNbInit=10):
+    """CP reduced-problem builder (pfdr_cp_reduce_*): A is (N, V) for
+    N > 0 (or (V, V) A^tA for N < 0, length-V diagonal / None for N = 0),
+    comp_ptr (rV + 1) and comp_vertices (V) the components.  Returns dict
+    rA, rAA, rY, L, Leq (None where not formed)."""
+    Y = np.asarray(Y)
+    dt = Y.dtype
+    ct, sfx, _ = _real(dt)
+    ptr = np.ascontiguousarray(comp_ptr, np.int32)
+    Vc = np.ascontiguousarray(comp_vertices, np.int32)
+    rV, V = ptr.size - 1, Vc.size
+    Af = None
+    if A is not None:
+        Af = np.asfortranarray(np.asarray(A, dt)) if np.ndim(A) == 2 else np.ascontiguousarray(A, dt)
+    if N <= 0:
+        preAt = True
+    rA = np.zeros((rV, N), dt) if N > 0 else None        # column rv = rA[rv]
+    rAA = (np.zeros(rV, dt) if N == 0 else np.zeros((rV, rV), dt)) if preAt else None
+    rY = np.zeros(rV, dt) if preAt else None
+    L = np.zeros(rV, dt)
+    Leq = np.zeros(rV, dt) if N != 0 else None
+    p = lambda a: None if a is None else C.c_void_p(a.ctypes.data)
+    _check(getattr(load(), "pfdr_cp_reduce_" + sfx)(
+        C.c_int(N), C.c_int(V), p(Af), p(np.ascontiguousarray(Y)), C.c_int(rV), p(ptr), p(Vc),
+        C.c_int(int(preAt)), PFDR_MEM_HOST, ct(normTol), C.c_int(normItMax),
+        C.c_int(normNbInit), p(rA), p(rAA), p(rY), p(L), p(Leq)), "pfdr_cp_reduce")
+    return {"rA": None if rA is None else rA.T, "rAA": rAA, "rY": rY, "L": L, "Leq": Leq}
 
 
 def grid_edge_count(shape, conn, v_end):

@@ -197,6 +197,27 @@ int pfdr_operator_norm_f32(int M, int N, const float *A, int mem, float nTol, in
 int pfdr_operator_norm_f64(int M, int N, const double *A, int mem, double nTol, int itMax,
                            int nbInit, int verbose, double *norm2, double *gram_ms);
 
+/* Cut-pursuit reduced-problem builder (reference
+ * src/CP_PFDR_graph_quadratic_d1_l1.cpp:663-841).
+ * Components: rVc[rV + 1] offsets into the vertex list Vc[V].  A, Y as the
+ * CP caller's (N > 0: A N-by-V, Y length N; N = -V: A = A^tA, Y = A^tY;
+ * N = 0: A diagonal or NULL).  preAt (N > 0): also form rAA = rA^t rA and
+ * rY = rA^t Y (forced for N <= 0).  Outputs (host or device per mem): rA
+ * (N-by-rV, N > 0), rAA (rV-by-rV, or rV for N = 0), rY (rV; not formed
+ * for N > 0 without preAt: CP then passes the whole Y), L (rV: the
+ * Lipschitz metric l^2 c after Jacobi equilibration, c = squared norm of
+ * the equilibrated matrix by the power method with normTol / normItMax /
+ * normNbInit — CP uses 1e-3, 100, 10), Leq (rV, may be NULL: l).  All sums
+ * sequential in the reference's order (bit-identical to the restatement);
+ * only c depends on the (deterministic) starts. */
+int pfdr_cp_reduce_f32(int N, int V, const float *A, const float *Y, int rV, const int *rVc,
+                       const int *Vc, int preAt, int mem, float normTol, int normItMax,
+                       int normNbInit, float *rA, float *rAA, float *rY, float *L, float *Leq);
+int pfdr_cp_reduce_f64(int N, int V, const double *A, const double *Y, int rV, const int *rVc,
+                       const int *Vc, int preAt, int mem, double normTol, int normItMax,
+                       int normNbInit, double *rA, double *rAA, double *rY, double *L,
+                       double *Leq);
+
 /* ------------------------------------------------------ multi-GPU comm -- */
 /* Partitioned sessions (quadratic solvers, identity or diagonal A): every
  * rank passes its owned vertices (V of them, global ids [vtx_begin,

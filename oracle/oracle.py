@@ -153,3 +153,31 @@ class Oracle:
         fn.restype = ct
         return float(fn(C.c_int(M), C.c_int(N), _ptr(A, ct), ct(nTol), C.c_int(itMax),
                         C.c_int(nbInit)))
+
+    # ------------------------------------------- CP reduced problem --
+    def cp_reduce(self, N, A, Y, comp_ptr, comp_vertices, preAt=True):
+        """oracle/cp_reduce_body.h (port only): rA, rAA, rY, Leq as the
+        reference's CP forms them, without the operator norm."""
+        if self.kind != "port":
+            raise NotImplementedError("cp_reduce: C restatement only")
+        Y = np.ascontiguousarray(Y)
+        ct, sfx = _real(Y.dtype)
+        ptr = np.ascontiguousarray(comp_ptr, np.int32)
+        Vc = np.ascontiguousarray(comp_vertices, np.int32)
+        rV, V = ptr.size - 1, Vc.size
+        Af = None
+        if A is not None:
+            Af = (np.asfortranarray(np.asarray(A, Y.dtype)) if np.ndim(A) == 2
+                  else np.ascontiguousarray(A, Y.dtype))
+        if N <= 0:
+            preAt = True
+        rA = np.zeros((rV, N), Y.dtype) if N > 0 else None
+        rAA = (np.zeros(rV, Y.dtype) if N == 0 else np.zeros((rV, rV), Y.dtype)) if preAt else None
+        rY = np.zeros(rV, Y.dtype) if preAt else None
+        Leq = np.zeros(rV, Y.dtype)
+        fn = self._fn("cp_reduce", sfx)
+        fn(C.c_int(N), C.c_int(V), _ptr(Af, ct), _ptr(Y, ct), C.c_int(rV),
+           _ptr(ptr, C.c_int), _ptr(Vc, C.c_int), C.c_int(int(preAt)), _ptr(rA, ct),
+           _ptr(rAA, ct), _ptr(rY, ct), _ptr(Leq, ct))
+        return {"rA": None if rA is None else rA.T, "rAA": rAA, "rY": rY,
+                "Leq": Leq if N != 0 else None}

@@ -11,6 +11,8 @@
  *     oracle_pfdr_quadratic_d1_bounds_{f32,f64}
  *     oracle_pfdr_loss_d1_simplex_{f32,f64}
  *     oracle_proj_simplex_metric_{f32,f64}
+ *     oracle_cp_reduce_{f32,f64}   (cp_reduce_body.h: the CP reduced-problem
+ *                                   builder)
  * Argument lists follow the reference functions (Lipschtype passed as int,
  * no verbose flag).  Parity pinned against the reference itself: see the
  * header of pfdr_oracle_body.h.
@@ -28,6 +30,7 @@
  * from <cmath>), so the float objective accumulates a double product */
 #define ORACLE_LOG log
 #include "pfdr_oracle_body.h"
+#include "cp_reduce_body.h"
 #undef REAL
 #undef SFX
 #undef ORACLE_EPS
@@ -40,6 +43,7 @@
 #define ORACLE_HUGE HUGE_VAL
 #define ORACLE_LOG log
 #include "pfdr_oracle_body.h"
+#include "cp_reduce_body.h"
 #undef REAL
 #undef SFX
 #undef ORACLE_EPS
