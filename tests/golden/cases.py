@@ -146,6 +146,39 @@ def make_cases():
         cases["simplex_labels_" + nm] = dict(base, al=0.5, difTol=1.0,
                                            difRcd=8.0,
                                            P0=np.full(V * K, 1.0 / K, dt))
+    # --- edge cases of the graph as CP builds it: self-loops (CP links every
+    # isolated component to itself with weight eps,
+    # src/CP_PFDR_graph_quadratic_d1_l1.cpp:642-645) and repeated edges
+    # (reduced edges may repeat pairs; the headline graph keeps mirrored
+    # duplicates)
+    Eu = np.array([0, 0, 1, 2, 2, 3, 4, 5, 5, 6, 7], np.int32)
+    Ev = np.array([1, 0, 2, 3, 3, 4, 5, 6, 5, 7, 7], np.int32)
+    V = 8
+    for dt, nm in ((np.float64, "f64"), (np.float32, "f32")):
+        eps = np.finfo(dt).eps
+        La = np.array([0.2, eps, 0.3, 0.1, 0.15, 0.25, 0.2, 0.05, eps, 0.3, eps], dt)
+        Y = (np.array([1.0, 1.2, -0.5, 0.3, 2.0, 2.1, -1.0, 0.4]) * 1.5).astype(dt)
+        cases["l1_selfloops_" + nm] = dict(
+            solver="l1", X0=np.zeros(V, dt), Y=Y, A=None, N=0, Eu=Eu, Ev=Ev,
+            La_d1=La, La_l1=np.full(V, 0.05, dt), positivity=0, Ltype=0, L=None,
+            rho=1.5, condMin=1e-3, difRcd=1e-2, difTol=1e-7, itMax=5000)
+        cases["bounds_selfloops_" + nm] = dict(
+            solver="bounds", X0=np.zeros(V, dt), Y=Y, A=None, N=0, Eu=Eu, Ev=Ev,
+            La_d1=La, lo=-0.5, hi=1.5, Ltype=0, L=None, rho=1.5, condMin=1e-3,
+            difRcd=0.0, difTol=1e-7, itMax=5000)
+        # one component: CP's reduced problem of a constant solution
+        cases["l1_one_vertex_" + nm] = dict(
+            solver="l1", X0=np.zeros(1, dt), Y=np.array([0.7], dt), A=None, N=0,
+            Eu=np.array([0], np.int32), Ev=np.array([0], np.int32),
+            La_d1=np.array([eps], dt), La_l1=np.array([0.1], dt), positivity=1,
+            Ltype=0, L=None, rho=1.5, condMin=1e-3, difRcd=0.0, difTol=1e-8,
+            itMax=500)
+        Ks = 3
+        Qs = simplex_observation(V, Ks, 21, np.arange(V) % Ks, dt)
+        cases["simplex_selfloops_" + nm] = dict(
+            solver="simplex", K=Ks, P0=Qs.copy(), Q=Qs, Eu=Eu, Ev=Ev, La_d1=La,
+            La_f=(1.0 + np.arange(V) % 3).astype(dt), al=0.2, rho=1.0, condMin=0.1,
+            difRcd=0.0, difTol=1e-6, itMax=3000)
     # --- standalone metric simplex projection (D = 7, nm < N, na < N)
     for dt, nm in ((np.float32, "f32"), (np.float64, "f64")):
         D, N = 7, 300

@@ -1,0 +1,81 @@
+"""GPU parity at BASELINE.json's full sizes, through size-independent
+properties (the oracle would take minutes per iteration here):
+
+* the headline graph (V = 10M, E = 60M): a vertex-partitioned solve (2 and
+  4 loopback ranks, halo overlap on) and a relabelled solve both equal the
+  single-GPU solve bit for bit — the reference's summation order is kept in
+  every variant, so any difference is a bug;
+* C4 (simplex, K = 10, V = 5M, E = 20M): 2 ranks with K-wide halos equal
+  one GPU bit for bit;
+* every iterate finite and the objective lower after 40 iterations than
+  after 5 and than at the start (FDR is not a descent method step by step,
+  but it converges on these problems)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+ITS = 12
+
+
+def _single(wl_name, **extra):
+    from workloads import WORKLOADS
+    from cp_pfdr_graph_d1_amd import pfdr
+    wl = WORKLOADS[wl_name]
+    inp = wl.inputs(0, 1)
+    kw = dict(inp["kw"], **extra)
+    s = pfdr.Session(wl.kind, wl.dtype, inp["V"], inp["E"], itMax=ITS, **kw)
+    s.run(ITS)
+    X = s.result()[0]
+    rel = s.query("reordered")
+    s.close()
+    return inp, X, rel
+
+
+def _partitioned(wl, inp, k):
+    from cp_pfdr_graph_d1_amd import partition as P
+    kw = inp["kw"]
+    return P.solve_loopback(k, wl.kind, wl.dtype, kw["Eu"], kw["Ev"], kw["La_d1"], kw["X0"],
+                            kw["Y"], La_l1=kw.get("La_l1"), rho=kw["rho"],
+                            condMin=kw["condMin"], itMax=ITS, K=kw.get("K", 0),
+                            al=kw.get("al", 0.0))[0]
+
+
+def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
+    from workloads import WORKLOADS
+    from cp_pfdr_graph_d1_amd import pfdr
+    inp, X1, _ = _single("headline")
+    assert np.all(np.isfinite(X1))
+    for k in (2, 4):
+        Xk = _partitioned(WORKLOADS["headline"], inp, k)
+        assert np.array_equal(Xk, X1), "partitioned (%d ranks) differs" % k
+    _, Xr, rel = _single("headline", reorder=pfdr.REORDER_ON)
+    assert rel == 1
+    assert np.array_equal(Xr, X1)
+
+
+def test_c4_simplex_partitioned_equals_single(gpu_lib):
+    from workloads import WORKLOADS
+    inp, P1, _ = _single("c4")
+    assert np.all(np.isfinite(P1))
+    P2 = _partitioned(WORKLOADS["c4"], inp, 2)
+    assert np.array_equal(P2, P1)
+
+
+def test_headline_objective_decreases(gpu_lib):
+    from workloads import WORKLOADS
+    from cp_pfdr_graph_d1_amd import pfdr
+    wl = WORKLOADS["headline"]
+    inp = wl.inputs(0, 1)
+    s = pfdr.Session(wl.kind, wl.dtype, inp["V"], inp["E"], itMax=40, record_obj=True,
+                     **inp["kw"])
+    s.run(40)
+    X, it, Obj, _ = s.result()
+    s.close()
+    assert it == 40 and np.all(np.isfinite(Obj[: it + 1]))
+    assert Obj[40] < Obj[5] and Obj[40] < Obj[0]

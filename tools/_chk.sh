@@ -1,6 +1,6 @@
 set -u
-O=gpurun_out/cpr1
+O=gpurun_out/fs1
 mkdir -p $O
-timeout -k 10 600 python -m pytest tests/test_cp_reduce.py tests/test_frontend.py tests/test_abi.py -m gpu -q -x > $O/pytest.log 2>&1; rc=$?
-grep -E "passed|failed|Error|assert" $O/pytest.log | tail -20 | cut -c1-300
+timeout -k 10 1000 python -m pytest tests -m gpu -q -x --durations=8 > $O/pytest.log 2>&1; rc=$?
+grep -E "passed|failed|Error|assert|s call" $O/pytest.log | tail -20 | cut -c1-200
 exit $rc
