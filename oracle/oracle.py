@@ -181,3 +181,223 @@ class Oracle:
            _ptr(rAA, ct), _ptr(rY, ct), _ptr(Leq, ct))
         return {"rA": None if rA is None else rA.T, "rAA": rAA, "rY": rY,
                 "Leq": Leq if N != 0 else None}
+
+    # ------------------------------------------------ CP graph steps --
+    # oracle/cp_graph_body.h (port only), SURVEY.md §8(f) ranks 2-3.
+    def _port_only(self, what):
+        if self.kind != "port":
+            raise NotImplementedError("%s: C restatement only" % what)
+
+    def cp_components(self, V, Eu, Ev, active):
+        """:566-597 -> (Cv, Vc, rVc)"""
+        self._port_only("cp_components")
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        act = np.ascontiguousarray(active, np.uint8)
+        Cv = np.empty(V, np.int32)
+        Vc = np.empty(V, np.int32)
+        rVc = np.empty(V + 1, np.int32)
+        fn = self.lib.oracle_cp_components
+        fn.restype = C.c_int
+        rV = fn(C.c_int(V), C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+                _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int))
+        return Cv, Vc, rVc[:rV + 1].copy()
+
+    def cp_activate(self, Eu, Ev, segment, active):
+        """:430-440 / :521-556 -> (new active, count)"""
+        self._port_only("cp_activate")
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        seg = np.ascontiguousarray(segment, np.uint8)
+        act = np.array(active, np.uint8, copy=True)
+        fn = self.lib.oracle_cp_activate
+        fn.restype = C.c_int
+        w = fn(C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int), _ptr(seg, C.c_uint8),
+               _ptr(act, C.c_uint8))
+        return act, int(w)
+
+    def cp_reduced_graph(self, V, Eu, Ev, La_d1, La_l1, active, Cv, Vc, rVc, eps):
+        """:599-661 -> (rEu, rEv, rLa_d1, rLa_l1)"""
+        self._port_only("cp_reduced_graph")
+        La_d1 = np.ascontiguousarray(La_d1)
+        ct, sfx = _real(La_d1.dtype)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        L1 = None if La_l1 is None else np.ascontiguousarray(La_l1, La_d1.dtype)
+        act = np.ascontiguousarray(active, np.uint8)
+        Cv = np.ascontiguousarray(Cv, np.int32)
+        Vc = np.ascontiguousarray(Vc, np.int32)
+        rVc = np.ascontiguousarray(rVc, np.int32)
+        rV, E = rVc.size - 1, Eu.size
+        rEu = np.empty(E + rV, np.int32)
+        rEv = np.empty(E + rV, np.int32)
+        rLa = np.empty(E + rV, La_d1.dtype)
+        rL1 = None if L1 is None else np.empty(rV, La_d1.dtype)
+        fn = self._fn("cp_reduced_graph", sfx)
+        fn.restype = C.c_int
+        rE = fn(C.c_int(V), C.c_int(E), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int), _ptr(La_d1, ct),
+                _ptr(L1, ct), _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int),
+                _ptr(rVc, C.c_int), C.c_int(rV), ct(eps), _ptr(rEu, C.c_int), _ptr(rEv, C.c_int),
+                _ptr(rLa, ct), _ptr(rL1, ct))
+        return rEu[:rE].copy(), rEv[:rE].copy(), rLa[:rE].copy(), rL1
+
+    def cp_merge(self, Eu, Ev, Cv, rX, eps, difTol, active):
+        """:863-886 -> (new active, deactivated count)"""
+        self._port_only("cp_merge")
+        rX = np.ascontiguousarray(rX)
+        ct, sfx = _real(rX.dtype)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        Cv = np.ascontiguousarray(Cv, np.int32)
+        act = np.array(active, np.uint8, copy=True)
+        fn = self._fn("cp_merge", sfx)
+        fn.restype = C.c_int
+        n = fn(C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int), _ptr(Cv, C.c_int),
+               _ptr(rX, ct), ct(eps), ct(difTol), _ptr(act, C.c_uint8))
+        return act, int(n)
+
+    def cp_gradient(self, N, V, A, Y, R, Eu, Ev, La_d1, La_l1, active, Cv, Vc, rVc, rX):
+        """:339-400 -> DfS[V] (A: N-by-V for N > 0, V-by-V A^tA for N < 0,
+        diagonal or None for N = 0; all column major)"""
+        self._port_only("cp_gradient")
+        rX = np.ascontiguousarray(rX)
+        dt = rX.dtype
+        ct, sfx = _real(dt)
+        Af = None
+        if A is not None:
+            Af = (np.asfortranarray(np.asarray(A, dt)) if np.ndim(A) == 2
+                  else np.ascontiguousarray(A, dt))
+        Y = np.ascontiguousarray(Y, dt)
+        R = None if R is None else np.ascontiguousarray(R, dt)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        La_d1 = np.ascontiguousarray(La_d1, dt)
+        L1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+        act = np.ascontiguousarray(active, np.uint8)
+        Cv = np.ascontiguousarray(Cv, np.int32)
+        Vc = np.ascontiguousarray(Vc, np.int32)
+        rVc = np.ascontiguousarray(rVc, np.int32)
+        DfS = np.empty(V, dt)
+        self._fn("cp_gradient", sfx)(
+            C.c_int(N), C.c_int(V), C.c_int(Eu.size), _ptr(Af, ct), _ptr(Y, ct), _ptr(R, ct),
+            _ptr(Eu, C.c_int), _ptr(Ev, C.c_int), _ptr(La_d1, ct), _ptr(L1, ct),
+            _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int),
+            C.c_int(rVc.size - 1), _ptr(rX, ct), _ptr(DfS, ct))
+        return DfS
+
+    def cp_capacities(self, cut, La_d1, La_l1, positivity, active, Cv, rX, DfS):
+        """:402-535 -> (tr_cap[V], r_cap[E])"""
+        self._port_only("cp_capacities")
+        DfS = np.ascontiguousarray(DfS)
+        dt = DfS.dtype
+        ct, sfx = _real(dt)
+        La_d1 = np.ascontiguousarray(La_d1, dt)
+        L1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+        act = np.ascontiguousarray(active, np.uint8)
+        Cv = np.ascontiguousarray(Cv, np.int32)
+        rX = np.ascontiguousarray(rX, dt)
+        V, E = DfS.size, La_d1.size
+        tr = np.empty(V, dt)
+        rc = np.empty(E, dt)
+        self._fn("cp_capacities", sfx)(
+            C.c_int(cut), C.c_int(V), C.c_int(E), _ptr(La_d1, ct), _ptr(L1, ct),
+            C.c_int(int(positivity)), _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(rX, ct),
+            _ptr(DfS, ct), _ptr(tr, ct), _ptr(rc, ct))
+        return tr, rc
+
+
+class CPStepRef:
+    """The REFERENCE's cut-pursuit iteration (oracle/_ref/libcp_step_ref.so,
+    built from /root/reference/src by ``make -C oracle ref``; only where the
+    reference exists).  N = 0 (identity / diagonal A).  See
+    oracle/harness/cp_step.cpp."""
+
+    PATH = os.path.join(HERE, "_ref", "libcp_step_ref.so")
+
+    @staticmethod
+    def available():
+        return os.path.exists(CPStepRef.PATH)
+
+    def __init__(self):
+        if CPStepRef.PATH not in _CACHE:
+            _CACHE[CPStepRef.PATH] = C.CDLL(CPStepRef.PATH)
+        self.lib = _CACHE[CPStepRef.PATH]
+
+    def init(self, Y, A, Eu, Ev, La_d1, La_l1, positivity):
+        """rX0 of the reference's initialize() (one component)."""
+        Y = np.ascontiguousarray(Y)
+        ct, sfx = _real(Y.dtype)
+        A = None if A is None else np.ascontiguousarray(A, Y.dtype)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, Y.dtype)
+        La_d1 = np.ascontiguousarray(La_d1, Y.dtype)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        rX0 = np.zeros(1, Y.dtype)
+        getattr(self.lib, "cp_ref_init_" + sfx)(
+            C.c_int(Y.size), C.c_int(Eu.size), _ptr(Y, ct), _ptr(A, ct), _ptr(Eu, C.c_int),
+            _ptr(Ev, C.c_int), _ptr(La_d1, ct), _ptr(La_l1, ct), C.c_int(int(positivity)),
+            _ptr(rX0, ct))
+        return rX0
+
+    def step(self, Y, A, Eu, Ev, La_d1, La_l1, positivity, CP_difTol, state, rho=1.5,
+             condMin=1e-3, difRcd=0.0, difTol=1e-4, itMax=1000):
+        """One CP iteration from ``state`` (dict: active, Cv, Vc, rVc, rX);
+        returns the new state, the last cut's segments and the recorded
+        reduced problem (None when no edge was activated)."""
+        Y = np.ascontiguousarray(Y)
+        dt = Y.dtype
+        ct, sfx = _real(dt)
+        V, E = Y.size, Eu.size
+        A = None if A is None else np.ascontiguousarray(A, dt)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+        La_d1 = np.ascontiguousarray(La_d1, dt)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        act = np.array(state["active"], np.uint8, copy=True)
+        Cv = np.array(state["Cv"], np.int32, copy=True)
+        Vc = np.array(state["Vc"], np.int32, copy=True)
+        rV = C.c_int(int(state["rVc"].size - 1))
+        rVc = np.zeros(V + 1, np.int32)
+        rVc[:rV.value + 1] = state["rVc"]
+        rX = np.zeros(V, dt)
+        rX[:rV.value] = state["rX"]
+        seg = np.zeros(V, np.uint8)
+        called, rE = C.c_int(0), C.c_int(0)
+        rEu = np.zeros(E + V, np.int32)
+        rEv = np.zeros(E + V, np.int32)
+        rLa = np.zeros(E + V, dt)
+        rL1 = np.zeros(V, dt)
+        rY = np.zeros(V, dt)
+        rAA = np.zeros(V, dt)
+        getattr(self.lib, "cp_ref_step_" + sfx)(
+            C.c_int(V), C.c_int(E), _ptr(Y, ct), _ptr(A, ct), _ptr(Eu, C.c_int),
+            _ptr(Ev, C.c_int), _ptr(La_d1, ct), _ptr(La_l1, ct), C.c_int(int(positivity)),
+            ct(CP_difTol), ct(rho), ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax),
+            _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int),
+            C.byref(rV), _ptr(rX, ct), _ptr(seg, C.c_uint8), C.byref(called), C.byref(rE),
+            _ptr(rEu, C.c_int), _ptr(rEv, C.c_int), _ptr(rLa, ct), _ptr(rL1, ct), _ptr(rY, ct),
+            _ptr(rAA, ct))
+        n = rV.value
+        new = {"active": act, "Cv": Cv, "Vc": Vc, "rVc": rVc[:n + 1].copy(),
+               "rX": rX[:n].copy()}
+        red = None
+        if called.value:
+            m = rE.value
+            red = {"rEu": rEu[:m].copy(), "rEv": rEv[:m].copy(), "rLa_d1": rLa[:m].copy(),
+                   "rLa_l1": rL1[:n].copy() if La_l1 is not None else None,
+                   "rY": rY[:n].copy(), "rAA": rAA[:n].copy()}
+        return new, seg, red
+
+    def maxflow(self, Eu, Ev, tr_cap, r_cap):
+        """Segments (0 source, 1 sink) of the reference's BK maxflow."""
+        tr_cap = np.ascontiguousarray(tr_cap)
+        ct, sfx = _real(tr_cap.dtype)
+        r_cap = np.ascontiguousarray(r_cap, tr_cap.dtype)
+        Eu = np.ascontiguousarray(Eu, np.int32)
+        Ev = np.ascontiguousarray(Ev, np.int32)
+        seg = np.zeros(tr_cap.size, np.uint8)
+        fn = getattr(self.lib, "cp_ref_maxflow_" + sfx)
+        fn.restype = ct
+        fn(C.c_int(tr_cap.size), C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(tr_cap, ct), _ptr(r_cap, ct), _ptr(seg, C.c_uint8))
+        return seg

@@ -13,6 +13,10 @@
  *     oracle_proj_simplex_metric_{f32,f64}
  *     oracle_cp_reduce_{f32,f64}   (cp_reduce_body.h: the CP reduced-problem
  *                                   builder)
+ *     oracle_cp_components, oracle_cp_activate, oracle_cp_reduced_graph_*,
+ *     oracle_cp_merge_*, oracle_cp_gradient_*, oracle_cp_capacities_*
+ *                                  (cp_graph_body.h: the CP graph steps,
+ *                                   SURVEY.md §8(f) ranks 2-3)
  * Argument lists follow the reference functions (Lipschtype passed as int,
  * no verbose flag).  Parity pinned against the reference itself: see the
  * header of pfdr_oracle_body.h.
@@ -31,6 +35,7 @@
 #define ORACLE_LOG log
 #include "pfdr_oracle_body.h"
 #include "cp_reduce_body.h"
+#include "cp_graph_body.h"
 #undef REAL
 #undef SFX
 #undef ORACLE_EPS
@@ -44,6 +49,7 @@
 #define ORACLE_LOG log
 #include "pfdr_oracle_body.h"
 #include "cp_reduce_body.h"
+#include "cp_graph_body.h"
 #undef REAL
 #undef SFX
 #undef ORACLE_EPS

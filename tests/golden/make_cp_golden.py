@@ -1,0 +1,104 @@
+"""Generate the CP graph-step golden fixtures from the REFERENCE itself.
+
+For every case of cp_cases.py, run the reference's cut pursuit
+(oracle/_ref/libcp_step_ref.so: its CP_PFDR_graph_quadratic_d1_l1, graph
+and BK maxflow compiled from /root/reference/src without OpenMP) one
+iteration at a time from its own initial state, and store per iteration k:
+
+* ``k{k}_in_*``  : the state the iteration starts from (edge activity, Cv,
+                   Vc, rVc, rX);
+* ``k{k}_out_*`` : the state it produced (activity after the merge, Cv, Vc,
+                   rVc, rX) and ``k{k}_seg_last``, the segments of its last
+                   maxflow;
+* ``k{k}_red_*`` : the reduced problem CP handed to PFDR (rEu, rEv, rLa_d1,
+                   rLa_l1, rY, rAA);
+* ``k{k}_seg_first`` (two-cut iterations): the first cut's segments,
+                   DERIVED here (oracle capacities -> the reference's own BK
+                   maxflow) — the reference discards them — and accepted only
+                   because the whole derived chain reproduces the
+                   reference's outputs of that iteration bit for bit.
+
+Before saving, the script checks the oracle restatement
+(oracle/cp_graph_body.h) against every iteration: its capacities fed to the
+reference maxflow give the reference's last segments, and its activation,
+components, reduced graph and merge give the reference's state and reduced
+problem exactly.  Usage:  python tests/golden/make_cp_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+sys.path.insert(0, HERE)
+from oracle import CPStepRef, Oracle  # noqa: E402
+import cp_cases as CC  # noqa: E402
+
+
+def check_iteration(o, ref, c, state, new, seg_last, red):
+    """The oracle chain against one reference iteration; returns derived
+    first-cut segments (or None)."""
+    d = CC.cp_graph_iteration(o, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc), c,
+                              state, rX_new=new["rX"])
+    assert np.array_equal(d["segments"][-1], seg_last), "last cut segments"
+    if d["activated"] == 0:
+        assert red is None
+        for k in ("active", "Cv", "Vc", "rVc", "rX"):
+            assert np.array_equal(state[k], new[k]), k
+        return None
+    assert red is not None
+    assert np.array_equal(d["Cv"], new["Cv"]), "Cv"
+    assert np.array_equal(d["Vc"], new["Vc"]), "Vc"
+    assert np.array_equal(d["rVc"], new["rVc"]), "rVc"
+    rEu, rEv, rLa, rL1 = d["reduced"]
+    assert np.array_equal(rEu, red["rEu"]), "rEu"
+    assert np.array_equal(rEv, red["rEv"]), "rEv"
+    assert np.array_equal(rLa, red["rLa_d1"]), "rLa_d1"
+    if rL1 is not None:
+        assert np.array_equal(rL1, red["rLa_l1"]), "rLa_l1"
+    assert np.array_equal(d["active_post"], new["active"]), "active after merge"
+    return d["segments"][0] if len(d["segments"]) == 2 else None
+
+
+def main():
+    o = Oracle("port")
+    ref = CPStepRef()
+    for name, c in CC.make_cases().items():
+        out = {}
+        for k, v in c.items():
+            if v is not None:
+                out["in_" + k] = np.asarray(v)
+        V, E = c["Y"].size, c["Eu"].size
+        rX0 = ref.init(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                       c["positivity"])
+        state = {"active": np.zeros(E, np.uint8), "Cv": np.zeros(V, np.int32),
+                 "Vc": np.arange(V, dtype=np.int32), "rVc": np.array([0, V], np.int32),
+                 "rX": rX0}
+        hist = []
+        for k in range(CC.STEPS):
+            new, seg, red = ref.step(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                                     c["positivity"], c["CP_difTol"], state)
+            seg_first = check_iteration(o, ref, c, state, new, seg, red)
+            for key, val in state.items():
+                out["k%d_in_%s" % (k, key)] = val
+            for key, val in new.items():
+                out["k%d_out_%s" % (k, key)] = val
+            out["k%d_seg_last" % k] = seg
+            if seg_first is not None:
+                out["k%d_seg_first" % k] = seg_first
+            if red is not None:
+                for key, val in red.items():
+                    if val is not None:
+                        out["k%d_red_%s" % (k, key)] = val
+            hist.append("%d:%d/%s" % (new["rVc"].size - 1, int(new["active"].sum()),
+                                       "-" if red is None else red["rEu"].size))
+            state = new
+        out["meta_steps"] = np.int32(CC.STEPS)
+        out["meta_build"] = np.str_("g++ -O3 -ffp-contract=off, no OpenMP")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+        print("%-26s V=%d E=%d  rV:active/rE per iteration %s" % (name, V, E, " ".join(hist)))
+
+
+if __name__ == "__main__":
+    main()

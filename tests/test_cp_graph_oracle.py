@@ -1,0 +1,98 @@
+"""The oracle's CP graph steps (oracle/cp_graph_body.h, SURVEY.md §8(f)
+ranks 2-3) against the reference's own cut-pursuit iterations
+(tests/golden/cp_*.npz, made by tests/golden/make_cp_golden.py).
+
+Per recorded iteration: gradient -> capacities -> (the iteration's
+segments, from the fixture) -> activation -> components -> reduced graph
+-> merge with the iteration's PFDR values must reproduce the reference's
+state and reduced problem bit for bit; the reduced problem's rY / rAA
+(N = 0) must equal the CP builder restatement (cp_reduce_body.h).  Where
+the reference harness is built (this container), the oracle's capacities
+are also fed to the reference's BK maxflow, which must return the recorded
+segments.  CPU only.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import cp_cases as CC
+from oracle import CPStepRef
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+FILES = sorted(glob.glob(os.path.join(GOLDEN, "cp_*.npz")))
+NAMES = [os.path.basename(f)[:-4] for f in FILES if not f.endswith("cp_cases.npz")]
+
+
+def load_case(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    c = {k[3:]: d[k] for k in d.files if k.startswith("in_")}
+    for k in ("A", "La_l1"):
+        c.setdefault(k, None)
+    c["positivity"] = int(c["positivity"])
+    c["CP_difTol"] = float(c["CP_difTol"])
+    return c, d
+
+
+def iteration_state(d, k, io):
+    return {key: d["k%d_%s_%s" % (k, io, key)] for key in ("active", "Cv", "Vc", "rVc", "rX")}
+
+
+def test_fixtures_present():
+    assert len(NAMES) >= 10, NAMES
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_replays_reference_cp(oracle_port, name):
+    c, d = load_case(name)
+    o = oracle_port
+    for k in range(int(d["meta_steps"])):
+        st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
+        segs = [d["k%d_seg_first" % k]] if ("k%d_seg_first" % k) in d.files else []
+        segs.append(d["k%d_seg_last" % k])
+        it = iter(segs)
+        r = CC.cp_graph_iteration(o, lambda tr, rc: next(it), c, st, rX_new=new["rX"])
+        if r["activated"] == 0:
+            assert ("k%d_red_rEu" % k) not in d.files
+            continue
+        assert np.array_equal(r["Cv"], new["Cv"])
+        assert np.array_equal(r["Vc"], new["Vc"])
+        assert np.array_equal(r["rVc"], new["rVc"])
+        rEu, rEv, rLa, rL1 = r["reduced"]
+        assert np.array_equal(rEu, d["k%d_red_rEu" % k])
+        assert np.array_equal(rEv, d["k%d_red_rEv" % k])
+        assert np.array_equal(rLa, d["k%d_red_rLa_d1" % k])
+        if rL1 is not None:
+            assert np.array_equal(rL1, d["k%d_red_rLa_l1" % k])
+        assert np.array_equal(r["active_post"], new["active"])
+        # the reduced problem's rY / rAA: the CP builder restatement (N = 0)
+        red = o.cp_reduce(0, c["A"], c["Y"], new["rVc"], new["Vc"])
+        assert np.array_equal(red["rY"], d["k%d_red_rY" % k])
+        assert np.array_equal(red["rAA"], d["k%d_red_rAA" % k])
+
+
+@pytest.mark.skipif(not CPStepRef.available(), reason="reference harness not built here")
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_capacities_through_reference_maxflow(oracle_port, name):
+    c, d = load_case(name)
+    ref = CPStepRef()
+    for k in range(int(d["meta_steps"])):
+        st = iteration_state(d, k, "in")
+        r = CC.cp_graph_iteration(oracle_port, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc),
+                                  c, st)
+        assert np.array_equal(r["segments"][-1], d["k%d_seg_last" % k])
+        if ("k%d_seg_first" % k) in d.files:
+            assert np.array_equal(r["segments"][0], d["k%d_seg_first" % k])
+
+
+def test_isolated_selfloop_reattribution_is_pinned():
+    """The reference gives an isolated component's eps self-loop to the next
+    non-isolated component (rEc reset, :645-656): the disconnected case
+    holds such an edge (1, 0) at every iteration."""
+    for nm in ("f32", "f64"):
+        _, d = load_case("cp_disconnected_" + nm)
+        k = 0
+        u, v, w = d["k%d_red_rEu" % k], d["k%d_red_rEv" % k], d["k%d_red_rLa_d1" % k]
+        tiny = w < 1e-6
+        assert list(zip(u[tiny].tolist(), v[tiny].tolist())) == [(1, 0)]
