@@ -1,0 +1,1030 @@
+// Cut-pursuit graph steps on the GPU: the
+// full-graph work the reference's CP driver does around every reduced PFDR
+// solve, src/CP_PFDR_graph_quadratic_d1_l1.cpp:
+//
+//   gradient      DfS = smooth gradient at the piecewise-constant iterate +
+//                 the d1 and l1 directional terms                 :339-413
+//   capacities    source/sink capacities of the single (differentiable) or
+//                 the first / second cut, edge capacities         :402-535
+//   activate      activate the inactive edges a maxflow cut separates
+//                                                         :430-440, :519-556
+//   components    connected components of the graph minus its active edges,
+//                 in the reference's queue order (Cv, Vc, rVc)     :566-597
+//   reduced graph reduced edges (discovery order), summed TV weights, eps
+//                 self-loops of isolated components, summed l1 weights
+//                                                                  :599-661
+//   merge         deactivate edges between (relatively) equal components
+//                                                                  :863-886
+//
+// The maxflow itself (Boykov-Kolmogorov, sequential) stays with the caller
+// on the host: capacities go out, segments come back.
+//
+// Graph state lives in HBM for the whole CP run: endpoints, TV / l1
+// weights, the incidence CSR (arc ids 2e + side ascending per vertex, i.e.
+// the maxflow graph's adjacency lists REVERSED: include/graph.hpp:405-408
+// prepends), edge activity bytes, components.  Every result is identical
+// to the reference's (integer work exactly, and every floating sum in the
+// reference's order):
+//   * components: union-find gives each component's smallest vertex (the
+//     reference's root, its outer loop runs u = 0..V-1); then a
+//     level-synchronous BFS from all roots at once reproduces the
+//     reference's queue exactly: a vertex is claimed by the smallest
+//     (queue position of the parent, rank of the arc in the parent's list)
+//     with a 64-bit atomicMin, and the winners of each level are emitted in
+//     that order (count, scan, emit); a stable sort of the concatenated
+//     levels by component gives Vc.
+//   * reduced graph: candidate arcs are emitted in the reference's visiting
+//     order (Vc position, arc rank), stably sorted by (ru, rv), summed
+//     sequentially per group, and the groups ordered by (ru, first visit).
+#include <climits>
+#include <cstring>
+#include <memory>
+#include <vector>
+#include <rocprim/rocprim.hpp>
+#include <stdexcept>
+
+#include "pfdr_graph.hpp"
+
+namespace pfdr {
+
+// ------------------------------------------------------------- helpers --
+__device__ __forceinline__ int arc_head(unsigned a, const int *__restrict__ Eu,
+                                        const int *__restrict__ Ev) {
+    return (a & 1u) ? Eu[a >> 1] : Ev[a >> 1];
+}
+
+// grow-only temporary storage for rocPRIM calls
+struct Tmp {
+    DevBuf<char> b;
+    void *get(size_t n) {
+        if (n > b.n) b.alloc(n + (n >> 2) + 256);
+        return b.p;
+    }
+};
+
+template <typename T>
+static void excl_scan(Tmp &t, const T *in, T *out, long n, hipStream_t s) {
+    size_t bytes = 0;
+    PFDR_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(),
+                                     s));
+    void *p = t.get(bytes);
+    PFDR_HIP(rocprim::exclusive_scan(p, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), s));
+}
+
+template <typename K, typename V>
+static void sort_pairs(Tmp &t, K *kin, K *kout, V *vin, V *vout, long n, int bits,
+                       hipStream_t s) {
+    size_t bytes = 0;
+    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, bits, s));
+    void *p = t.get(bytes);
+    PFDR_HIP(rocprim::radix_sort_pairs(p, bytes, kin, kout, vin, vout, (size_t)n, 0, bits, s));
+}
+
+static int bits_for(long n) {  // smallest b with 2^b >= n (at least 1)
+    int b = 1;
+    while (b < 62 && (1L << b) < n) b++;
+    return b;
+}
+
+template <typename T>
+static T d2h_scalar(const T *p, hipStream_t s) {
+    T h;
+    PFDR_HIP(hipMemcpyAsync(&h, p, sizeof(T), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    return h;
+}
+
+// per-block partial count -> one atomicAdd (integer: order-free)
+__device__ __forceinline__ void block_count(int c, int *total) {
+    __shared__ int red[kBlock / kWave];
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < kBlock / kWave; i++) t += red[i];
+        if (t) atomicAdd(total, t);
+    }
+}
+
+// ------------------------------------------------ ordered segment sums --
+// out[g] = (((0 + x[o0]) + x[o0+1]) + ...) over [off[g], off[g+1]), with
+// x[i] = val[idx[i]] (idx may be null: x[i] = val[i]).  Short segments:
+// one lane each; long ones (> kWave entries) are appended to a list and
+// summed by one wave each (coalesced loads, the adds in order on one
+// lane's chain via readlane).
+constexpr int kSegShort = kWave;
+
+template <typename real>
+__global__ void k_segsum_short(int G, const int *__restrict__ off, const int *__restrict__ idx,
+                               const real *__restrict__ val, real *__restrict__ out,
+                               int *__restrict__ longs, int *__restrict__ nlong) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int a = off[g], b = off[g + 1];
+    if (b - a > kSegShort) {
+        longs[atomicAdd(nlong, 1)] = g;
+        return;
+    }
+    real s = real(0);
+    for (int i = a; i < b; i++) s += val[idx ? idx[i] : i];
+    out[g] = s;
+}
+
+template <typename real>
+__global__ __launch_bounds__(kBlock) void k_segsum_long(int n, const int *__restrict__ longs,
+                                                       const int *__restrict__ off,
+                                                       const int *__restrict__ idx,
+                                                       const real *__restrict__ val,
+                                                       real *__restrict__ out) {
+    const int w = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (w >= n) return;
+    const int g = longs[w];
+    const int a = off[g], b = off[g + 1];
+    real s = real(0);
+    for (int c = a; c < b; c += kWave) {
+        const int i = c + lane;
+        const real x = (i < b) ? val[idx ? idx[i] : i] : real(0);
+        const int m = min(kWave, b - c);
+        for (int k = 0; k < m; k++) s += __shfl(x, k, kWave);
+    }
+    if (lane == 0) out[g] = s;
+}
+
+template <typename real>
+static void segsum(int G, const int *off, const int *idx, const real *val, real *out,
+                   DevBuf<int> &longs, DevBuf<int> &nlong, hipStream_t s) {
+    if (G <= 0) return;
+    if (longs.n < (size_t)G) longs.alloc(G);
+    if (!nlong.p) nlong.alloc(1);
+    PFDR_HIP(hipMemsetAsync(nlong.p, 0, sizeof(int), s));
+    k_segsum_short<real><<<grid_for(G), kBlock, 0, s>>>(G, off, idx, val, out, longs.p, nlong.p);
+    const int nl = d2h_scalar(nlong.p, s);
+    if (nl) k_segsum_long<real><<<grid_for((long)nl * kWave), kBlock, 0, s>>>(nl, longs.p, off, idx,
+                                                                             val, out);
+    PFDR_HIP(hipGetLastError());
+}
+
+// ----------------------------------------------------------- components --
+__device__ __forceinline__ int uf_root(const int *parent, int v) {
+    for (;;) {
+        const int p = __hip_atomic_load(parent + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p == v) return v;
+        v = p;
+    }
+}
+
+__global__ void k_uf_init(int V, int *parent) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) parent[v] = v;
+}
+
+// union over the inactive edges: hook the larger root under the smaller one
+// by CAS on the root (a lost race retries from the new roots), so every
+// tree's root is its component's smallest vertex
+__global__ void k_uf_hook(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                          const uint8_t *__restrict__ active, int *parent) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x) {
+        if (active[e]) continue;
+        int a = Eu[e], b = Ev[e];
+        for (;;) {
+            a = uf_root(parent, a);
+            b = uf_root(parent, b);
+            if (a == b) break;
+            const int hi = max(a, b), lo = min(a, b);
+            if (atomicCAS(parent + hi, hi, lo) == hi) break;
+        }
+    }
+}
+
+__global__ void k_uf_flatten(int V, int *parent, int *is_root) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int r = uf_root(parent, v);
+    parent[v] = r;
+    is_root[v] = (r == v) ? 1 : 0;
+}
+
+// level 0: the roots in increasing order (= component order); Cv of every
+// other vertex -1 (unvisited), claims cleared
+__global__ void k_bfs_roots(int V, const int *__restrict__ is_root, const int *__restrict__ rid,
+                            int *__restrict__ L, int *__restrict__ Cv,
+                            unsigned long long *__restrict__ claim) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    claim[v] = ~0ull;
+    if (is_root[v]) {
+        L[rid[v]] = v;
+        Cv[v] = rid[v];
+    } else {
+        Cv[v] = -1;
+    }
+}
+
+__device__ __forceinline__ unsigned long long claim_key(int i, int j) {
+    return ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
+}
+
+// frontier L[lo, hi): every unvisited neighbour through an inactive edge is
+// claimed by its first visit in the reference's order (queue position i,
+// then the arc's rank j in the maxflow graph's list: slots descending)
+__global__ void k_bfs_claim(int lo, int hi, const int *__restrict__ L, const int *__restrict__ ptr,
+                            const unsigned *__restrict__ slot, const int *__restrict__ Eu,
+                            const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+                            const int *__restrict__ Cv, unsigned long long *claim) {
+    const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const int v = L[i];
+    const int b = ptr[v];
+    for (int k = ptr[v + 1] - 1, j = 0; k >= b; k--, j++) {
+        const unsigned a = slot[k];
+        if (active[a >> 1]) continue;
+        const int w = arc_head(a, Eu, Ev);
+        if (Cv[w] != -1) continue;
+        atomicMin(claim + w, claim_key(i, j));
+    }
+}
+
+// EMIT = false: cnt[i - lo] = claims won by L[i]; true: append them in order
+template <bool EMIT>
+__global__ void k_bfs_take(int lo, int hi, const int *__restrict__ ptr,
+                           const unsigned *__restrict__ slot, const int *__restrict__ Eu,
+                           const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+                           const unsigned long long *__restrict__ claim, int *__restrict__ cnt,
+                           int *L, int *Cv) {
+    const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const int v = L[i];
+    const int b = ptr[v];
+    int c = 0, base = 0, cv = 0;
+    if (EMIT) {
+        base = hi + cnt[i - lo];
+        cv = Cv[v];
+    }
+    for (int k = ptr[v + 1] - 1, j = 0; k >= b; k--, j++) {
+        const unsigned a = slot[k];
+        if (active[a >> 1]) continue;
+        const int w = arc_head(a, Eu, Ev);
+        if (claim[w] != claim_key(i, j)) continue;
+        if (EMIT) {
+            L[base + c] = w;
+            Cv[w] = cv;
+        }
+        c++;
+    }
+    if (!EMIT) cnt[i - lo] = c;
+}
+
+__global__ void k_gather_keys(int V, const int *__restrict__ L, const int *__restrict__ Cv,
+                              unsigned *__restrict__ key) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < V) key[i] = (unsigned)Cv[L[i]];
+}
+
+// rVc[c] = first position of component c in the sorted keys, rVc[rV] = V
+__global__ void k_comp_ptr(int V, int rV, const unsigned *__restrict__ skey, int *__restrict__ rVc) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > V) return;
+    if (i == V) { rVc[rV] = V; return; }
+    if (i == 0 || skey[i] != skey[i - 1]) rVc[skey[i]] = i;
+}
+
+// -------------------------------------------------------- reduced graph --
+// per Vc position s: candidate arcs of u = Vc[s] (active, nonzero weight,
+// neighbour component rv >= ru) in the reference's visiting order; any
+// active nonzero arc makes the component non-isolated (:626-633)
+template <typename real, bool EMIT>
+__global__ void k_rg_scan(int V, int rbits, const int *__restrict__ Vc, const int *__restrict__ Cv,
+                          const int *__restrict__ ptr, const unsigned *__restrict__ slot,
+                          const int *__restrict__ Eu, const int *__restrict__ Ev,
+                          const uint8_t *__restrict__ active, const real *__restrict__ La,
+                          int *__restrict__ cnt, uint8_t *__restrict__ nonIso,
+                          unsigned long long *__restrict__ key, unsigned *__restrict__ pos,
+                          int *__restrict__ cand_e) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= V) return;
+    const int u = Vc[s], ru = Cv[u];
+    const int b = ptr[u];
+    int c = 0, base = EMIT ? cnt[s] : 0;
+    bool any = false;
+    for (int k = ptr[u + 1] - 1; k >= b; k--) {
+        const unsigned a = slot[k];
+        const int e = (int)(a >> 1);
+        if (!active[e]) continue;
+        if (La[e] == real(0)) continue;
+        any = true;
+        const int rv = Cv[arc_head(a, Eu, Ev)];
+        if (rv < ru) continue;
+        if (EMIT) {
+            const int p = base + c;
+            key[p] = ((unsigned long long)ru << rbits) | (unsigned long long)rv;
+            pos[p] = (unsigned)p;
+            cand_e[p] = e;
+        }
+        c++;
+    }
+    if (!EMIT) {
+        cnt[s] = c;
+        if (any) nonIso[ru] = 1;
+    }
+}
+
+// group heads of the sorted (ru, rv) keys
+__global__ void k_rg_heads(long M, const unsigned long long *__restrict__ skey,
+                           int *__restrict__ head) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M) head[i] = (i == 0 || skey[i] != skey[i - 1]) ? 1 : 0;
+}
+
+// per group: start offset, (ru, rv); per entry: its weight in sorted order
+template <typename real>
+__global__ void k_rg_groups(long M, int rbits, const unsigned long long *__restrict__ skey,
+                            const unsigned *__restrict__ spos, const int *__restrict__ cand_e,
+                            const real *__restrict__ La, const int *__restrict__ head,
+                            const int *__restrict__ gid, int *__restrict__ goff,
+                            int *__restrict__ gru, int *__restrict__ grv,
+                            unsigned *__restrict__ gfirst, real *__restrict__ wsorted) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const unsigned p = spos[i];
+    wsorted[i] = La[cand_e[p]];
+    if (head[i]) {
+        const int g = gid[i];
+        const unsigned long long k = skey[i];
+        goff[g] = (int)i;
+        gru[g] = (int)(k >> rbits);
+        grv[g] = (int)(k & ((1ull << rbits) - 1));
+        gfirst[g] = p;  // stable sort: the group's first visit
+    }
+}
+
+// final order keys: groups by (ru, first visit); isolated components'
+// eps self-loop at (ru, 0) (they own no group)
+__global__ void k_rg_order_keys(int G, int rV, const int *__restrict__ gru,
+                                const unsigned *__restrict__ gfirst,
+                                const uint8_t *__restrict__ nonIso, const int *__restrict__ isoid,
+                                unsigned long long *__restrict__ key, int *__restrict__ val) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < G) {
+        key[i] = ((unsigned long long)gru[i] << 32) | gfirst[i];
+        val[i] = i;
+    } else if (i < G + rV) {
+        const int ru = i - G;
+        if (!nonIso[ru]) {
+            const int t = G + isoid[ru];
+            key[t] = (unsigned long long)ru << 32;
+            val[t] = -1 - ru;
+        }
+    }
+}
+
+// outputs; an isolated component's self-loop goes to the next non-isolated
+// component when there is one (the reference's rEc reset, :645-656)
+template <typename real>
+__global__ void k_rg_write(int rE, int nNI, const int *__restrict__ sval,
+                           const int *__restrict__ gru, const int *__restrict__ grv,
+                           const real *__restrict__ gw, const int *__restrict__ NI, real eps,
+                           int *__restrict__ rEu, int *__restrict__ rEv, real *__restrict__ rLa) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= rE) return;
+    const int g = sval[t];
+    if (g >= 0) {
+        rEu[t] = gru[g];
+        rEv[t] = grv[g];
+        rLa[t] = gw[g];
+        return;
+    }
+    const int ru = -1 - g;
+    int lo = 0, hi = nNI;  // first non-isolated component > ru
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (NI[m] > ru) hi = m; else lo = m + 1;
+    }
+    rEu[t] = (lo < nNI) ? NI[lo] : ru;
+    rEv[t] = ru;
+    rLa[t] = eps;
+}
+
+__global__ void k_flag_to_int(int n, const uint8_t *__restrict__ f, int neg, int *__restrict__ o) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o[i] = neg ? (f[i] ? 0 : 1) : (f[i] ? 1 : 0);
+}
+
+__global__ void k_compact_ids(int n, const uint8_t *__restrict__ f, const int *__restrict__ pos,
+                              int *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && f[i]) out[pos[i]] = i;
+}
+
+// -------------------------------------------------------------- merge --
+template <typename real>
+__global__ void k_cp_merge(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                           const int *__restrict__ Cv, const real *__restrict__ rX, real eps,
+                           real difTol, uint8_t *__restrict__ active, int *__restrict__ count) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (e < E && active[e]) {
+        real a = rX[Cv[Eu[e]]], b = rX[Cv[Ev[e]]], d = a - b;
+        if (a < real(0)) a = -a;
+        if (b < real(0)) b = -b;
+        if (d < real(0)) d = -d;
+        if (a < b) a = b;
+        d = (a > eps) ? d / a : d / eps;
+        if (d <= difTol) {
+            active[e] = 0;
+            c = 1;
+        }
+    }
+    block_count(c, count);
+}
+
+// ------------------------------------------------------------ gradient --
+// DfS base of the N = 0 modes (:369-376), then the d1 term over the active
+// arcs in the maxflow graph's order and the l1 term (:379-413); N != 0:
+// the base is already in DfS
+template <typename real>
+__global__ void k_cp_grad(int V, int base_mode, const real *__restrict__ A,
+                          const real *__restrict__ Y, const int *__restrict__ ptr,
+                          const unsigned *__restrict__ slot, const int *__restrict__ Eu,
+                          const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+                          const real *__restrict__ La, const real *__restrict__ L1,
+                          const int *__restrict__ Cv, const real *__restrict__ rX,
+                          real *__restrict__ DfS) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= V) return;
+    const real xu = rX[Cv[u]];
+    real g;
+    if (base_mode == 1) g = A[u] * xu - Y[u];
+    else if (base_mode == 0) g = xu - Y[u];
+    else g = DfS[u];
+    const int b = ptr[u];
+    for (int k = ptr[u + 1] - 1; k >= b; k--) {
+        const unsigned a = slot[k];
+        const int e = (int)(a >> 1);
+        if (!active[e]) continue;
+        const real d = xu - rX[Cv[arc_head(a, Eu, Ev)]];
+        if (d > real(0)) g += La[e];
+        else if (d < real(0)) g -= La[e];
+    }
+    if (L1) {
+        if (xu > real(0)) g += L1[u];
+        else if (xu < real(0)) g -= L1[u];
+    }
+    DfS[u] = g;
+}
+
+// N > 0: DfS[v] = -(sum_n A[n, v] R[n]) in n order (:342-352).  One wave
+// per 64 columns: 64 x 64 tiles staged through LDS (coalesced column
+// reads), then each lane adds its column's entries in order.
+template <typename real>
+__global__ __launch_bounds__(kWave) void k_cp_grad_direct(int N, int V, const real *__restrict__ A,
+                                                         const real *__restrict__ R,
+                                                         real *__restrict__ DfS) {
+    __shared__ real t[kWave][kWave + 1];
+    const int lane = threadIdx.x;
+    const int v0 = blockIdx.x * kWave;
+    real s = real(0);
+    for (int n0 = 0; n0 < N; n0 += kWave) {
+        const int n = n0 + lane;
+        const real r = (n < N) ? R[n] : real(0);
+        for (int c = 0; c < kWave; c++) {
+            const int v = v0 + c;
+            t[c][lane] = (v < V && n < N) ? A[(size_t)N * v + n] * r : real(0);
+        }
+        __syncthreads();
+        const int m = min(kWave, N - n0);
+        for (int k = 0; k < m; k++) s += t[lane][k];
+        __syncthreads();
+    }
+    if (v0 + lane < V) DfS[v0 + lane] = -s;
+}
+
+// N < 0: DfS[u] = sum over components with rX != 0 of (component sum of
+// column u of A^tA, in Vc order) * rX, minus Y[u] (:353-368); one lane per u
+template <typename real>
+__global__ void k_cp_grad_ata(int V, int rV, const real *__restrict__ A, const real *__restrict__ Y,
+                              const int *__restrict__ Vc, const int *__restrict__ rVc,
+                              const real *__restrict__ rX, real *__restrict__ DfS) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= V) return;
+    const real *Av = A + (size_t)V * u;
+    real b = real(0);
+    for (int rv = 0; rv < rV; rv++) {
+        const real x = rX[rv];
+        if (x == real(0)) continue;
+        real a = real(0);
+        for (int s = rVc[rv], t = rVc[rv + 1]; s < t; s++) a += Av[Vc[s]];
+        b += a * x;
+    }
+    DfS[u] = b - Y[u];
+}
+
+// ---------------------------------------------------------- capacities --
+template <typename real>
+__global__ void k_cp_trcap(int V, int cut, int positivity, const real *__restrict__ L1,
+                           const int *__restrict__ Cv, const real *__restrict__ rX,
+                           const real *__restrict__ DfS, real *__restrict__ tr) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const bool zero = rX[Cv[v]] == real(0);
+    real t = DfS[v];
+    if (cut == 1 && L1 && zero) t = DfS[v] + L1[v];
+    else if (cut == 2 && zero) t = positivity ? -Lim<real>::huge : DfS[v] - L1[v];
+    tr[v] = t;
+}
+
+template <typename real>
+__global__ void k_cp_rcap(long E, const uint8_t *__restrict__ active, const real *__restrict__ La,
+                          real *__restrict__ rc) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < E) rc[e] = active[e] ? real(0) : La[e];
+}
+
+__global__ void k_cp_activate(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                              const uint8_t *__restrict__ seg, uint8_t *__restrict__ active,
+                              int *__restrict__ count) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (e < E && seg[Eu[e]] != seg[Ev[e]] && !active[e]) {
+        active[e] = 1;
+        c = 1;
+    }
+    block_count(c, count);
+}
+
+// ================================================================ state --
+struct CpGraphBase {
+    virtual ~CpGraphBase() = default;
+    int V = 0;
+    long E = 0;
+    int dtype = PFDR_F32;
+    hipStream_t s = nullptr;
+    DevBuf<int> Eu, Ev;
+    Incidence inc;
+    DevBuf<uint8_t> active;
+    DevBuf<int> Cv, Vc, rVc;
+    int rV = 0, rE = 0;
+    DevBuf<int> rEu, rEv;
+    DevBuf<int> count;
+    Tmp tmp;
+    double last_ms = 0;
+    // scratch
+    DevBuf<int> i0, i1, i2, L;
+    DevBuf<unsigned long long> claim;
+    DevBuf<int> longs, nlong;
+
+    void components();
+    virtual void reduced_graph(double eps) = 0;
+    virtual int merge(double eps, double difTol) = 0;
+    virtual void gradient(int N, const void *A, const void *Y, const void *R, int mem) = 0;
+    virtual void capacities(int cut, int positivity, void *tr, void *rc, int mem) = 0;
+    virtual void set_values(const void *rX, int mem) = 0;
+    virtual void get_reduced(int *rEu_o, int *rEv_o, void *rLa_o, void *rL1_o, int mem) = 0;
+    virtual void get_dfs(void *out, int mem) = 0;
+    int activate(const uint8_t *seg, int mem);
+};
+
+static hipMemcpyKind kind_in(int mem) {
+    return mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+}
+static hipMemcpyKind kind_out(int mem) {
+    return mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+}
+
+void CpGraphBase::components() {
+    const int Vn = V;
+    i0.alloc(Vn);  // parent
+    i1.alloc(Vn + 1);  // is_root, then scratch
+    i2.alloc(Vn + 1);  // root ids
+    L.alloc(Vn);
+    claim.alloc(Vn);
+    Cv.alloc(Vn);
+    k_uf_init<<<grid_for(Vn), kBlock, 0, s>>>(Vn, i0.p);
+    if (E > 0)
+        k_uf_hook<<<std::min(grid_for(E), 8192), kBlock, 0, s>>>(E, Eu.p, Ev.p, active.p, i0.p);
+    k_uf_flatten<<<grid_for(Vn), kBlock, 0, s>>>(Vn, i0.p, i1.p);
+    PFDR_HIP(hipMemsetAsync(i1.p + Vn, 0, sizeof(int), s));
+    excl_scan(tmp, i1.p, i2.p, Vn + 1, s);
+    rV = d2h_scalar(i2.p + Vn, s);
+    k_bfs_roots<<<grid_for(Vn), kBlock, 0, s>>>(Vn, i1.p, i2.p, L.p, Cv.p, claim.p);
+    PFDR_HIP(hipGetLastError());
+    // levels; i1/i2 reused as per-frontier counts / offsets
+    int lo = 0, hi = rV;
+    while (hi > lo && hi < Vn) {
+        const int n = hi - lo;
+        k_bfs_claim<<<grid_for(n), kBlock, 0, s>>>(lo, hi, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+                                                   active.p, Cv.p, claim.p);
+        k_bfs_take<false><<<grid_for(n), kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+                                                         active.p, claim.p, i1.p, L.p, Cv.p);
+        PFDR_HIP(hipMemsetAsync(i1.p + n, 0, sizeof(int), s));
+        excl_scan(tmp, i1.p, i2.p, n + 1, s);
+        const int add = d2h_scalar(i2.p + n, s);
+        if (add == 0) break;
+        if (add > Vn - hi) throw std::runtime_error("components: BFS overflow");
+        k_bfs_take<true><<<grid_for(n), kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+                                                        active.p, claim.p, i2.p, L.p, Cv.p);
+        PFDR_HIP(hipGetLastError());
+        lo = hi;
+        hi += add;
+    }
+    if (hi != Vn) throw std::runtime_error("components: BFS did not reach every vertex");
+    // Vc = the concatenated levels stably sorted by component
+    DevBuf<unsigned> key(Vn), skey(Vn);
+    Vc.alloc(Vn);
+    rVc.alloc(Vn + 1);
+    k_gather_keys<<<grid_for(Vn), kBlock, 0, s>>>(Vn, L.p, Cv.p, key.p);
+    sort_pairs(tmp, key.p, skey.p, L.p, Vc.p, Vn, bits_for(rV), s);
+    k_comp_ptr<<<grid_for(Vn + 1), kBlock, 0, s>>>(Vn, rV, skey.p, rVc.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+int CpGraphBase::activate(const uint8_t *seg, int mem) {
+    DevBuf<uint8_t> bs;
+    const uint8_t *ds = seg;
+    if (mem != PFDR_MEM_DEVICE) {
+        bs.alloc(V);
+        PFDR_HIP(hipMemcpyAsync(bs.p, seg, V, hipMemcpyHostToDevice, s));
+        ds = bs.p;
+    }
+    if (!count.p) count.alloc(1);
+    PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
+    if (E > 0) k_cp_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, ds, active.p, count.p);
+    PFDR_HIP(hipGetLastError());
+    return d2h_scalar(count.p, s);
+}
+
+template <typename real>
+struct CpGraph : CpGraphBase {
+    DevBuf<real> La, L1, rX, DfS, rLa, rL1, gw, ws;
+    bool has_l1 = false;
+
+    void set_values(const void *x, int mem) override {
+        if (rV <= 0) throw std::runtime_error("set_values: no components");
+        rX.alloc(rV);
+        PFDR_HIP(hipMemcpyAsync(rX.p, x, sizeof(real) * rV, kind_in(mem), s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void reduced_graph(double eps_d) override {
+        const real eps = (real)eps_d;
+        const int Vn = V;
+        const int rbits = bits_for(rV);
+        DevBuf<uint8_t> nonIso(rV);
+        PFDR_HIP(hipMemsetAsync(nonIso.p, 0, rV, s));
+        i1.alloc(Vn + 1);
+        i2.alloc(Vn + 1);
+        k_rg_scan<real, false><<<grid_for(Vn), kBlock, 0, s>>>(
+            Vn, rbits, Vc.p, Cv.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p, La.p, i1.p,
+            nonIso.p, nullptr, nullptr, nullptr);
+        PFDR_HIP(hipMemsetAsync(i1.p + Vn, 0, sizeof(int), s));
+        excl_scan(tmp, i1.p, i2.p, Vn + 1, s);
+        const long M = d2h_scalar(i2.p + Vn, s);
+        DevBuf<unsigned long long> key(M + 1), skey(M + 1);
+        DevBuf<unsigned> pos(M + 1), spos(M + 1);
+        DevBuf<int> cand_e(M + 1);
+        if (M > 0) {
+            k_rg_scan<real, true><<<grid_for(Vn), kBlock, 0, s>>>(
+                Vn, rbits, Vc.p, Cv.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p, La.p, i2.p,
+                nonIso.p, key.p, pos.p, cand_e.p);
+            sort_pairs(tmp, key.p, skey.p, pos.p, spos.p, M, 2 * rbits, s);
+        }
+        // groups
+        DevBuf<int> head(M + 1), gid(M + 1);
+        int G = 0;
+        if (M > 0) {
+            k_rg_heads<<<grid_for(M), kBlock, 0, s>>>(M, skey.p, head.p);
+            PFDR_HIP(hipMemsetAsync(head.p + M, 0, sizeof(int), s));
+            excl_scan(tmp, head.p, gid.p, M + 1, s);
+            G = d2h_scalar(gid.p + M, s);
+        }
+        DevBuf<int> goff(G + 1), gru(G + 1), grv(G + 1);
+        DevBuf<unsigned> gfirst(G + 1);
+        gw.alloc(G + 1);
+        ws.alloc(M + 1);
+        if (G > 0) {
+            k_rg_groups<real><<<grid_for(M), kBlock, 0, s>>>(M, rbits, skey.p, spos.p, cand_e.p,
+                                                             La.p, head.p, gid.p, goff.p, gru.p,
+                                                             grv.p, gfirst.p, ws.p);
+            // (M fits an int: at most 2E candidates)
+            const int Mi = (int)M;
+            PFDR_HIP(hipMemcpyAsync(goff.p + G, &Mi, sizeof(int), hipMemcpyHostToDevice, s));
+            segsum<real>(G, goff.p, nullptr, ws.p, gw.p, longs, nlong, s);
+        }
+        // isolated components, non-isolated list
+        DevBuf<int> fl(rV + 1), isoid(rV + 1), niid(rV + 1), NI(rV + 1);
+        k_flag_to_int<<<grid_for(rV), kBlock, 0, s>>>(rV, nonIso.p, 1, fl.p);
+        PFDR_HIP(hipMemsetAsync(fl.p + rV, 0, sizeof(int), s));
+        excl_scan(tmp, fl.p, isoid.p, rV + 1, s);
+        k_flag_to_int<<<grid_for(rV), kBlock, 0, s>>>(rV, nonIso.p, 0, fl.p);
+        excl_scan(tmp, fl.p, niid.p, rV + 1, s);
+        k_compact_ids<<<grid_for(rV), kBlock, 0, s>>>(rV, nonIso.p, niid.p, NI.p);
+        const int nIso = d2h_scalar(isoid.p + rV, s);
+        const int nNI = d2h_scalar(niid.p + rV, s);
+        rE = G + nIso;
+        DevBuf<unsigned long long> okey(rE + 1), oskey(rE + 1);
+        DevBuf<int> oval(rE + 1), osval(rE + 1);
+        k_rg_order_keys<<<grid_for(G + rV), kBlock, 0, s>>>(G, rV, gru.p, gfirst.p, nonIso.p,
+                                                            isoid.p, okey.p, oval.p);
+        if (rE > 0) sort_pairs(tmp, okey.p, oskey.p, oval.p, osval.p, rE, 32 + rbits, s);
+        rEu.alloc(rE + 1);
+        rEv.alloc(rE + 1);
+        rLa.alloc(rE + 1);
+        if (rE > 0)
+            k_rg_write<real><<<grid_for(rE), kBlock, 0, s>>>(rE, nNI, osval.p, gru.p, grv.p, gw.p,
+                                                             NI.p, eps, rEu.p, rEv.p, rLa.p);
+        // l1 weights: component sums in Vc order (:611-613)
+        if (has_l1) {
+            rL1.alloc(rV);
+            segsum<real>(rV, rVc.p, Vc.p, L1.p, rL1.p, longs, nlong, s);
+        }
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void get_reduced(int *rEu_o, int *rEv_o, void *rLa_o, void *rL1_o, int mem) override {
+        const auto k = kind_out(mem);
+        if (rEu_o && rE) PFDR_HIP(hipMemcpyAsync(rEu_o, rEu.p, sizeof(int) * rE, k, s));
+        if (rEv_o && rE) PFDR_HIP(hipMemcpyAsync(rEv_o, rEv.p, sizeof(int) * rE, k, s));
+        if (rLa_o && rE) PFDR_HIP(hipMemcpyAsync(rLa_o, rLa.p, sizeof(real) * rE, k, s));
+        if (rL1_o && has_l1 && rL1.p)
+            PFDR_HIP(hipMemcpyAsync(rL1_o, rL1.p, sizeof(real) * rV, k, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    int merge(double eps, double difTol) override {
+        if (!rX.p) throw std::runtime_error("merge: set the component values first");
+        if (!count.p) count.alloc(1);
+        PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
+        if (E > 0)
+            k_cp_merge<real><<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Cv.p, rX.p, (real)eps,
+                                                            (real)difTol, active.p, count.p);
+        PFDR_HIP(hipGetLastError());
+        return d2h_scalar(count.p, s);
+    }
+
+    void gradient(int N, const void *A, const void *Y, const void *R, int mem) override {
+        if (!rX.p) throw std::runtime_error("gradient: set the component values first");
+        DfS.alloc(V);
+        const size_t asz = N > 0 ? (size_t)N * V : N < 0 ? (size_t)V * V : (size_t)V;
+        const size_t ysz = (size_t)V;
+        DevBuf<real> bA, bY, bR;
+        auto in = [&](DevBuf<real> &b, const void *h, size_t n) -> const real * {
+            if (!h) return nullptr;
+            if (mem == PFDR_MEM_DEVICE) return (const real *)h;
+            b.alloc(n);
+            PFDR_HIP(hipMemcpyAsync(b.p, h, sizeof(real) * n, hipMemcpyHostToDevice, s));
+            return b.p;
+        };
+        const real *dA = in(bA, A, asz);
+        const real *dY = in(bY, Y, N > 0 ? 0 : ysz);
+        const real *dR = in(bR, R, N > 0 ? (size_t)N : 0);
+        int mode = 0;
+        if (N > 0) {
+            if (!dA || !dR) throw std::runtime_error("gradient: N > 0 needs A and R");
+            k_cp_grad_direct<real><<<(V + kWave - 1) / kWave, kWave, 0, s>>>(N, V, dA, dR, DfS.p);
+            mode = 2;
+        } else if (N < 0) {
+            if (-N != V || !dA || !dY) throw std::runtime_error("gradient: N < 0 needs A^tA, A^tY");
+            k_cp_grad_ata<real><<<grid_for(V), kBlock, 0, s>>>(V, rV, dA, dY, Vc.p, rVc.p, rX.p,
+                                                               DfS.p);
+            mode = 2;
+        } else {
+            if (!dY) throw std::runtime_error("gradient: Y required");
+            mode = dA ? 1 : 0;
+        }
+        k_cp_grad<real><<<grid_for(V), kBlock, 0, s>>>(V, mode, dA, dY, inc.ptr.p, inc.idx.p, Eu.p,
+                                                       Ev.p, active.p, La.p,
+                                                       has_l1 ? L1.p : nullptr, Cv.p, rX.p, DfS.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void get_dfs(void *out, int mem) override {
+        if (!DfS.p) throw std::runtime_error("no gradient computed");
+        PFDR_HIP(hipMemcpyAsync(out, DfS.p, sizeof(real) * V, kind_out(mem), s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void capacities(int cut, int positivity, void *tr, void *rc, int mem) override {
+        if (!DfS.p) throw std::runtime_error("capacities: compute the gradient first");
+        if (cut == 2 && !positivity && !has_l1)
+            throw std::runtime_error("capacities: cut 2 without positivity needs La_l1");
+        DevBuf<real> btr, brc;
+        real *dtr = (real *)tr, *drc = (real *)rc;
+        if (mem != PFDR_MEM_DEVICE) {
+            btr.alloc(V);
+            brc.alloc(E > 0 ? E : 1);
+            dtr = btr.p;
+            drc = brc.p;
+        }
+        if (tr)
+            k_cp_trcap<real><<<grid_for(V), kBlock, 0, s>>>(V, cut, positivity,
+                                                            has_l1 ? L1.p : nullptr, Cv.p, rX.p,
+                                                            DfS.p, dtr);
+        if (rc && E > 0) k_cp_rcap<real><<<grid_for(E), kBlock, 0, s>>>(E, active.p, La.p, drc);
+        PFDR_HIP(hipGetLastError());
+        if (mem != PFDR_MEM_DEVICE) {
+            if (tr) PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost, s));
+            if (rc && E > 0)
+                PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
+        }
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+};
+
+}  // namespace pfdr
+
+struct pfdr_cpgraph {
+    pfdr::CpGraphBase *g;
+};
+
+using pfdr::report_error;
+
+#define CPG_TRY(fn, body)                                  \
+    try {                                                  \
+        body;                                              \
+    } catch (const pfdr::HipError &h) {                    \
+        return report_error(fn, h);                        \
+    } catch (const std::exception &ex) {                   \
+        return report_error(fn, ex.what());                \
+    }                                                      \
+    return PFDR_OK;
+
+template <typename real>
+static pfdr::CpGraphBase *cpg_new(int V, int E, const int *Eu, const int *Ev, const void *La_d1,
+                                  const void *La_l1, int mem) {
+    using namespace pfdr;
+    auto *g = new CpGraph<real>();
+    std::unique_ptr<CpGraph<real>> hold(g);
+    g->V = V;
+    g->E = E;
+    g->dtype = sizeof(real) == 4 ? PFDR_F32 : PFDR_F64;
+    g->s = lib_stream();
+    const auto k = kind_in(mem);
+    g->Eu.alloc(E > 0 ? E : 1);
+    g->Ev.alloc(E > 0 ? E : 1);
+    g->La.alloc(E > 0 ? E : 1);
+    if (E > 0) {
+        PFDR_HIP(hipMemcpyAsync(g->Eu.p, Eu, sizeof(int) * E, k, g->s));
+        PFDR_HIP(hipMemcpyAsync(g->Ev.p, Ev, sizeof(int) * E, k, g->s));
+        PFDR_HIP(hipMemcpyAsync(g->La.p, La_d1, sizeof(real) * E, k, g->s));
+    }
+    g->has_l1 = La_l1 != nullptr;
+    if (La_l1) {
+        g->L1.alloc(V);
+        PFDR_HIP(hipMemcpyAsync(g->L1.p, La_l1, sizeof(real) * V, k, g->s));
+    }
+    build_incidence(g->Eu.p, g->Ev.p, V, E, g->inc, g->s);  // validates the endpoints
+    g->active.alloc(E > 0 ? E : 1);
+    PFDR_HIP(hipMemsetAsync(g->active.p, 0, E > 0 ? E : 1, g->s));
+    // CP's initial state: one component, Vc = 0..V-1 (:181-187)
+    g->rV = 1;
+    g->Cv.alloc(V);
+    g->Vc.alloc(V);
+    g->rVc.alloc(V + 1);
+    PFDR_HIP(hipMemsetAsync(g->Cv.p, 0, sizeof(int) * V, g->s));
+    {
+        std::vector<int> iota(V);
+        for (int v = 0; v < V; v++) iota[v] = v;
+        PFDR_HIP(hipMemcpyAsync(g->Vc.p, iota.data(), sizeof(int) * V, hipMemcpyHostToDevice, g->s));
+        const int r[2] = {0, V};
+        PFDR_HIP(hipMemcpyAsync(g->rVc.p, r, sizeof r, hipMemcpyHostToDevice, g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
+    }
+    hold.release();
+    return g;
+}
+
+extern "C" int pfdr_cpgraph_create(pfdr_cpgraph **out, int dtype, int V, int E, const int *Eu,
+                                   const int *Ev, const void *La_d1, const void *La_l1, int mem) {
+    const char *fn = "pfdr_cpgraph_create";
+    if (!out || V <= 0 || E < 0 || (E > 0 && (!Eu || !Ev || !La_d1)) ||
+        (dtype != PFDR_F32 && dtype != PFDR_F64))
+        return report_error(fn, "invalid arguments");
+    if ((long)E * 2 >= (1L << 31)) return report_error(fn, "E must be < 2^30");
+    *out = nullptr;
+    CPG_TRY(fn, {
+        pfdr::CpGraphBase *g = dtype == PFDR_F32
+                                   ? cpg_new<float>(V, E, Eu, Ev, La_d1, La_l1, mem)
+                                   : cpg_new<double>(V, E, Eu, Ev, La_d1, La_l1, mem);
+        *out = new pfdr_cpgraph{g};
+    })
+}
+
+extern "C" void pfdr_cpgraph_destroy(pfdr_cpgraph *g) {
+    if (!g) return;
+    delete g->g;
+    delete g;
+}
+
+extern "C" int pfdr_cpgraph_set_active(pfdr_cpgraph *h, const uint8_t *active, int mem) {
+    if (!h || !active) return report_error("pfdr_cpgraph_set_active", "null argument");
+    CPG_TRY("pfdr_cpgraph_set_active", {
+        auto *g = h->g;
+        if (g->E > 0)
+            PFDR_HIP(hipMemcpyAsync(g->active.p, active, g->E, pfdr::kind_in(mem), g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
+    })
+}
+
+extern "C" int pfdr_cpgraph_get_active(pfdr_cpgraph *h, uint8_t *active, int mem) {
+    if (!h || !active) return report_error("pfdr_cpgraph_get_active", "null argument");
+    CPG_TRY("pfdr_cpgraph_get_active", {
+        auto *g = h->g;
+        if (g->E > 0)
+            PFDR_HIP(hipMemcpyAsync(active, g->active.p, g->E, pfdr::kind_out(mem), g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
+    })
+}
+
+extern "C" int pfdr_cpgraph_set_components(pfdr_cpgraph *h, int rV, const int *Cv, const int *Vc,
+                                           const int *rVc, int mem) {
+    const char *fn = "pfdr_cpgraph_set_components";
+    if (!h || !Cv || !Vc || !rVc || rV <= 0 || rV > h->g->V)
+        return report_error(fn, "invalid arguments");
+    CPG_TRY(fn, {
+        auto *g = h->g;
+        const auto k = pfdr::kind_in(mem);
+        g->rV = rV;
+        PFDR_HIP(hipMemcpyAsync(g->Cv.p, Cv, sizeof(int) * g->V, k, g->s));
+        PFDR_HIP(hipMemcpyAsync(g->Vc.p, Vc, sizeof(int) * g->V, k, g->s));
+        PFDR_HIP(hipMemcpyAsync(g->rVc.p, rVc, sizeof(int) * (rV + 1), k, g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
+    })
+}
+
+extern "C" int pfdr_cpgraph_get_components(pfdr_cpgraph *h, int *rV, int *Cv, int *Vc, int *rVc,
+                                           int mem) {
+    if (!h) return report_error("pfdr_cpgraph_get_components", "null graph");
+    CPG_TRY("pfdr_cpgraph_get_components", {
+        auto *g = h->g;
+        const auto k = pfdr::kind_out(mem);
+        if (rV) *rV = g->rV;
+        if (Cv) PFDR_HIP(hipMemcpyAsync(Cv, g->Cv.p, sizeof(int) * g->V, k, g->s));
+        if (Vc) PFDR_HIP(hipMemcpyAsync(Vc, g->Vc.p, sizeof(int) * g->V, k, g->s));
+        if (rVc) PFDR_HIP(hipMemcpyAsync(rVc, g->rVc.p, sizeof(int) * (g->rV + 1), k, g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
+    })
+}
+
+extern "C" int pfdr_cpgraph_set_values(pfdr_cpgraph *h, const void *rX, int mem) {
+    if (!h || !rX) return report_error("pfdr_cpgraph_set_values", "null argument");
+    CPG_TRY("pfdr_cpgraph_set_values", h->g->set_values(rX, mem))
+}
+
+extern "C" int pfdr_cpgraph_components(pfdr_cpgraph *h, int *rV) {
+    if (!h) return report_error("pfdr_cpgraph_components", "null graph");
+    CPG_TRY("pfdr_cpgraph_components", {
+        h->g->components();
+        if (rV) *rV = h->g->rV;
+    })
+}
+
+extern "C" int pfdr_cpgraph_reduced_graph(pfdr_cpgraph *h, double eps, int *rE) {
+    if (!h) return report_error("pfdr_cpgraph_reduced_graph", "null graph");
+    CPG_TRY("pfdr_cpgraph_reduced_graph", {
+        h->g->reduced_graph(eps);
+        if (rE) *rE = h->g->rE;
+    })
+}
+
+extern "C" int pfdr_cpgraph_get_reduced(pfdr_cpgraph *h, int *rEu, int *rEv, void *rLa_d1,
+                                        void *rLa_l1, int mem) {
+    if (!h) return report_error("pfdr_cpgraph_get_reduced", "null graph");
+    CPG_TRY("pfdr_cpgraph_get_reduced", h->g->get_reduced(rEu, rEv, rLa_d1, rLa_l1, mem))
+}
+
+extern "C" int pfdr_cpgraph_merge(pfdr_cpgraph *h, double eps, double difTol, int *deactivated) {
+    if (!h) return report_error("pfdr_cpgraph_merge", "null graph");
+    CPG_TRY("pfdr_cpgraph_merge", {
+        const int n = h->g->merge(eps, difTol);
+        if (deactivated) *deactivated = n;
+    })
+}
+
+extern "C" int pfdr_cpgraph_gradient(pfdr_cpgraph *h, int N, const void *A, const void *Y,
+                                     const void *R, int mem, void *DfS) {
+    if (!h) return report_error("pfdr_cpgraph_gradient", "null graph");
+    CPG_TRY("pfdr_cpgraph_gradient", {
+        h->g->gradient(N, A, Y, R, mem);
+        if (DfS) h->g->get_dfs(DfS, mem);
+    })
+}
+
+extern "C" int pfdr_cpgraph_capacities(pfdr_cpgraph *h, int cut, int positivity, void *tr_cap,
+                                       void *r_cap, int mem) {
+    if (!h || cut < 0 || cut > 2) return report_error("pfdr_cpgraph_capacities", "invalid arguments");
+    CPG_TRY("pfdr_cpgraph_capacities", h->g->capacities(cut, positivity, tr_cap, r_cap, mem))
+}
+
+extern "C" int pfdr_cpgraph_activate(pfdr_cpgraph *h, const uint8_t *segment, int mem,
+                                     int *activated) {
+    if (!h || !segment) return report_error("pfdr_cpgraph_activate", "null argument");
+    CPG_TRY("pfdr_cpgraph_activate", {
+        const int n = h->g->activate(segment, mem);
+        if (activated) *activated = n;
+    })
+}

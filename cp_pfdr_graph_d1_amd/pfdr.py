@@ -38,6 +38,11 @@ EXPORTED = (
     "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
     "pfdr_gram_f32", "pfdr_gram_f64", "pfdr_operator_norm_f32", "pfdr_operator_norm_f64",
     "pfdr_cp_reduce_f32", "pfdr_cp_reduce_f64",
+    "pfdr_cpgraph_create", "pfdr_cpgraph_destroy", "pfdr_cpgraph_set_active",
+    "pfdr_cpgraph_get_active", "pfdr_cpgraph_set_components", "pfdr_cpgraph_get_components",
+    "pfdr_cpgraph_set_values", "pfdr_cpgraph_components", "pfdr_cpgraph_reduced_graph",
+    "pfdr_cpgraph_get_reduced", "pfdr_cpgraph_merge", "pfdr_cpgraph_gradient",
+    "pfdr_cpgraph_capacities", "pfdr_cpgraph_activate",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -659,6 +664,128 @@ def cp_reduce(N, A, Y, comp_ptr, comp_vertices, preAt=True, normTol=1e-3, normIt
         C.c_int(int(preAt)), PFDR_MEM_HOST, ct(normTol), C.c_int(normItMax),
         C.c_int(normNbInit), p(rA), p(rAA), p(rY), p(L), p(Leq)), "pfdr_cp_reduce")
     return {"rA": None if rA is None else rA.T, "rAA": rAA, "rY": rY, "L": L, "Leq": Leq}
+
+
+class CPGraph:
+    """Device-resident cut-pursuit graph (pfdr_cpgraph_*, SURVEY.md §8(f)
+    ranks 2-3): the full-graph steps of every CP iteration of
+    src/CP_PFDR_graph_quadratic_d1_l1.cpp with the reference's results and
+    orders.  Arrays in and out are numpy (host); the maxflow between
+    ``capacities`` and ``activate`` is the caller's."""
+
+    def __init__(self, V, Eu, Ev, La_d1, La_l1=None):
+        La_d1 = np.asarray(La_d1)
+        self.dtype = La_d1.dtype
+        self.ct, _, code = _real(self.dtype)
+        self.V = int(V)
+        Eu, Ev = _edges(Eu, Ev)
+        self.E = Eu.size
+        La_d1 = _arr(La_d1, self.dtype)
+        La_l1 = _arr(La_l1, self.dtype)
+        self._keep = (Eu, Ev, La_d1, La_l1)
+        self.h = C.c_void_p()
+        p = lambda a: None if a is None else C.c_void_p(a.ctypes.data)
+        _check(load().pfdr_cpgraph_create(C.byref(self.h), code, C.c_int(self.V),
+                                          C.c_int(self.E), p(Eu), p(Ev), p(La_d1), p(La_l1),
+                                          PFDR_MEM_HOST), "pfdr_cpgraph_create")
+        self.has_l1 = La_l1 is not None
+        self.rV = 1
+
+    @staticmethod
+    def _p(a):
+        return None if a is None else C.c_void_p(a.ctypes.data)
+
+    def _call(self, name, *args):
+        _check(getattr(load(), name)(self.h, *args), name)
+
+    def set_active(self, active):
+        a = np.ascontiguousarray(active, np.uint8)
+        self._call("pfdr_cpgraph_set_active", self._p(a), PFDR_MEM_HOST)
+
+    def active(self):
+        a = np.empty(self.E, np.uint8)
+        self._call("pfdr_cpgraph_get_active", self._p(a), PFDR_MEM_HOST)
+        return a
+
+    def set_components(self, Cv, Vc, rVc):
+        Cv, Vc, rVc = (np.ascontiguousarray(x, np.int32) for x in (Cv, Vc, rVc))
+        self.rV = rVc.size - 1
+        self._call("pfdr_cpgraph_set_components", C.c_int(self.rV), self._p(Cv), self._p(Vc),
+                   self._p(rVc), PFDR_MEM_HOST)
+
+    def components(self):
+        """:566-597 -> (Cv, Vc, rVc)"""
+        rV = C.c_int()
+        self._call("pfdr_cpgraph_components", C.byref(rV))
+        self.rV = rV.value
+        Cv = np.empty(self.V, np.int32)
+        Vc = np.empty(self.V, np.int32)
+        rVc = np.empty(self.rV + 1, np.int32)
+        self._call("pfdr_cpgraph_get_components", None, self._p(Cv), self._p(Vc), self._p(rVc),
+                   PFDR_MEM_HOST)
+        return Cv, Vc, rVc
+
+    def set_values(self, rX):
+        x = np.ascontiguousarray(rX, self.dtype)
+        self._call("pfdr_cpgraph_set_values", self._p(x), PFDR_MEM_HOST)
+
+    def reduced_graph(self, eps):
+        """:599-661 -> (rEu, rEv, rLa_d1, rLa_l1 or None)"""
+        rE = C.c_int()
+        self._call("pfdr_cpgraph_reduced_graph", C.c_double(eps), C.byref(rE))
+        n = rE.value
+        rEu = np.empty(n, np.int32)
+        rEv = np.empty(n, np.int32)
+        rLa = np.empty(n, self.dtype)
+        rL1 = np.empty(self.rV, self.dtype) if self.has_l1 else None
+        self._call("pfdr_cpgraph_get_reduced", self._p(rEu), self._p(rEv), self._p(rLa),
+                   self._p(rL1), PFDR_MEM_HOST)
+        return rEu, rEv, rLa, rL1
+
+    def merge(self, eps, difTol):
+        """:863-886 -> number of deactivated edges"""
+        n = C.c_int()
+        self._call("pfdr_cpgraph_merge", C.c_double(eps), C.c_double(difTol), C.byref(n))
+        return n.value
+
+    def gradient(self, N=0, A=None, Y=None, R=None):
+        """:339-413 -> DfS[V]"""
+        Af = None
+        if A is not None:
+            Af = (np.asfortranarray(np.asarray(A, self.dtype)) if np.ndim(A) == 2
+                  else np.ascontiguousarray(A, self.dtype))
+        Y = _arr(Y, self.dtype)
+        R = _arr(R, self.dtype)
+        DfS = np.empty(self.V, self.dtype)
+        self._call("pfdr_cpgraph_gradient", C.c_int(N), self._p(Af), self._p(Y), self._p(R),
+                   PFDR_MEM_HOST, self._p(DfS))
+        return DfS
+
+    def capacities(self, cut, positivity=0):
+        """:402-535 -> (tr_cap[V], r_cap[E]) of cut 0 (differentiable), 1 or 2"""
+        tr = np.empty(self.V, self.dtype)
+        rc = np.empty(self.E, self.dtype)
+        self._call("pfdr_cpgraph_capacities", C.c_int(cut), C.c_int(int(positivity)),
+                   self._p(tr), self._p(rc), PFDR_MEM_HOST)
+        return tr, rc
+
+    def activate(self, segment):
+        """activate the inactive edges the cut separates -> how many"""
+        seg = np.ascontiguousarray(segment, np.uint8)
+        n = C.c_int()
+        self._call("pfdr_cpgraph_activate", self._p(seg), PFDR_MEM_HOST, C.byref(n))
+        return n.value
+
+    def close(self):
+        if self.h:
+            load().pfdr_cpgraph_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def grid_edge_count(shape, conn, v_end):

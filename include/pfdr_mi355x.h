@@ -218,6 +218,57 @@ int pfdr_cp_reduce_f64(int N, int V, const double *A, const double *Y, int rV, c
                        int normNbInit, double *rA, double *rAA, double *rY, double *L,
                        double *Leq);
 
+/* ------------------------------------------- cut-pursuit graph steps -- */
+/* The full-graph work of every cut-pursuit iteration around the reduced
+ * PFDR solve, on a device-resident graph
+ * (reference src/CP_PFDR_graph_quadratic_d1_l1.cpp; the maxflow stays with
+ * the caller: capacities out, segments 0 = SOURCE / 1 = SINK back).  The
+ * graph holds the endpoints, TV weights La_d1[E], l1 weights La_l1[V] (or
+ * NULL), the activity of every edge (CP's is_active, initially none), the
+ * components (Cv[V], Vc[V], rVc[rV + 1], initially one) and the component
+ * values rX[rV].  Every result equals the reference's, including its
+ * orders (queue order of Vc, visiting order of the reduced edges) and its
+ * floating sums.  dtype PFDR_F32 / PFDR_F64 fixes the real type of every
+ * void* below; mem = PFDR_MEM_HOST / _DEVICE for the caller's arrays. */
+typedef struct pfdr_cpgraph pfdr_cpgraph;
+int pfdr_cpgraph_create(pfdr_cpgraph **out, int dtype, int V, int E,
+    const int *Eu, const int *Ev, const void *La_d1, const void *La_l1, int mem);
+void pfdr_cpgraph_destroy(pfdr_cpgraph *g);
+int pfdr_cpgraph_set_active(pfdr_cpgraph *g, const uint8_t *active, int mem);
+int pfdr_cpgraph_get_active(pfdr_cpgraph *g, uint8_t *active, int mem);
+int pfdr_cpgraph_set_components(pfdr_cpgraph *g, int rV, const int *Cv,
+    const int *Vc, const int *rVc, int mem);
+/* any output may be NULL */
+int pfdr_cpgraph_get_components(pfdr_cpgraph *g, int *rV, int *Cv, int *Vc,
+    int *rVc, int mem);
+/* rX[rV]: the values of the current components */
+int pfdr_cpgraph_set_values(pfdr_cpgraph *g, const void *rX, int mem);
+/* connected components of the graph minus its active edges (:566-597) */
+int pfdr_cpgraph_components(pfdr_cpgraph *g, int *rV);
+/* reduced edges and weights of the current components (:599-661); eps is
+ * CP's (:236-251), the weight of an isolated component's self-loop */
+int pfdr_cpgraph_reduced_graph(pfdr_cpgraph *g, double eps, int *rE);
+/* rEu, rEv, rLa_d1 [rE], rLa_l1 [rV] (when La_l1); any may be NULL */
+int pfdr_cpgraph_get_reduced(pfdr_cpgraph *g, int *rEu, int *rEv,
+    void *rLa_d1, void *rLa_l1, int mem);
+/* deactivate the active edges whose components' values differ by at most
+ * CP_difTol relatively (:863-886) */
+int pfdr_cpgraph_merge(pfdr_cpgraph *g, double eps, double CP_difTol, int *deactivated);
+/* DfS[V] (kept on the device; copied out when DfS != NULL) at the current
+ * values (:339-413): N > 0: A N-by-V, R[N] the residual Y - A X; N = -V:
+ * A = A^tA, Y = A^tY; N = 0: A diagonal or NULL, Y = A^tY */
+int pfdr_cpgraph_gradient(pfdr_cpgraph *g, int N, const void *A, const void *Y,
+    const void *R, int mem, void *DfS);
+/* cut 0: the single cut of the differentiable case (La_l1 NULL, no
+ * positivity); 1 / 2: directions +1_U / -1_U (:402-535).  tr_cap[V]
+ * (source > 0 / sink < 0), r_cap[E] (both arcs of an edge), from the
+ * activity BEFORE this cut's activations; either may be NULL */
+int pfdr_cpgraph_capacities(pfdr_cpgraph *g, int cut, int positivity,
+    void *tr_cap, void *r_cap, int mem);
+/* activate the inactive edges whose ends lie in different segments[V] */
+int pfdr_cpgraph_activate(pfdr_cpgraph *g, const uint8_t *segment, int mem,
+    int *activated);
+
 /* ------------------------------------------------------ multi-GPU comm -- */
 /* Partitioned sessions (quadratic solvers, identity or diagonal A): every
  * rank passes its owned vertices (V of them, global ids [vtx_begin,

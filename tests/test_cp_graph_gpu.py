@@ -1,0 +1,228 @@
+"""GPU parity of the cut-pursuit graph steps (pfdr_cpgraph_*, SURVEY.md
+§8(f) ranks 2-3) through the C ABI.
+
+* Golden replay: every recorded iteration of the reference's own cut
+  pursuit (tests/golden/cp_*.npz) — gradient and capacities against the
+  oracle (itself pinned to the reference), activation with the iteration's
+  segments, components (Cv, Vc queue order, rVc), reduced graph and merge
+  against the reference's outputs: all bit for bit.
+* Larger graphs against the oracle (bit for bit): 3-D grids, a k-NN
+  multigraph, a long chain (thousands of BFS levels), an edgeless graph,
+  random activity patterns; dense gradients (N > 0, N = -V).
+"""
+import numpy as np
+import pytest
+
+import cp_cases as CC
+from test_cp_graph_oracle import NAMES, iteration_state, load_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cpgraph_cls(gpu_lib):
+    from cp_pfdr_graph_d1_amd.pfdr import CPGraph
+    return CPGraph
+
+
+def _eq(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if a.dtype.kind == "f":
+        assert np.array_equal(a.view(np.uint8), np.ascontiguousarray(b, a.dtype).view(np.uint8)), \
+            (what, np.flatnonzero(a != b)[:5])
+    else:
+        assert np.array_equal(a, b), (what, np.flatnonzero(a != b)[:5])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_replays_reference_cp(cpgraph_cls, oracle_port, name):
+    c, d = load_case(name)
+    o = oracle_port
+    dt = c["Y"].dtype
+    eps = CC.cp_eps(dt, c["CP_difTol"])
+    g = cpgraph_cls(c["Y"].size, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"])
+    two_cuts = c["La_l1"] is not None or c["positivity"]
+    for k in range(int(d["meta_steps"])):
+        st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
+        g.set_active(st["active"])
+        g.set_components(st["Cv"], st["Vc"], st["rVc"])
+        g.set_values(st["rX"])
+        DfS = g.gradient(0, c["A"], c["Y"])
+        oD = o.cp_gradient(0, c["Y"].size, c["A"], c["Y"], None, c["Eu"], c["Ev"], c["La_d1"],
+                           c["La_l1"], st["active"], st["Cv"], st["Vc"], st["rVc"], st["rX"])
+        _eq(DfS, oD, "DfS")
+        cuts = (1, 2) if two_cuts else (0,)
+        caps = {}
+        for cut in cuts:
+            tr, rc = g.capacities(cut, c["positivity"])
+            otr, orc = o.cp_capacities(cut, c["La_d1"], c["La_l1"], c["positivity"],
+                                       st["active"], st["Cv"], st["rX"], oD)
+            _eq(tr, otr, "tr_cap cut %d" % cut)
+            _eq(rc, orc, "r_cap cut %d" % cut)
+            caps[cut] = (tr, rc)
+        segs = ([d["k%d_seg_first" % k]] if two_cuts else []) + [d["k%d_seg_last" % k]]
+        w = sum(g.activate(s) for s in segs)
+        act = st["active"]
+        ow = 0
+        for s in segs:
+            act, n = o.cp_activate(c["Eu"], c["Ev"], s, act)
+            ow += n
+        assert w == ow
+        _eq(g.active(), act, "active before merge")
+        if w == 0:
+            continue
+        Cv, Vc, rVc = g.components()
+        _eq(Cv, new["Cv"], "Cv")
+        _eq(Vc, new["Vc"], "Vc")
+        _eq(rVc, new["rVc"], "rVc")
+        rEu, rEv, rLa, rL1 = g.reduced_graph(eps)
+        _eq(rEu, d["k%d_red_rEu" % k], "rEu")
+        _eq(rEv, d["k%d_red_rEv" % k], "rEv")
+        _eq(rLa, d["k%d_red_rLa_d1" % k], "rLa_d1")
+        if rL1 is not None:
+            _eq(rL1, d["k%d_red_rLa_l1" % k], "rLa_l1")
+        g.set_values(new["rX"])
+        g.merge(eps, c["CP_difTol"])
+        _eq(g.active(), new["active"], "active after merge")
+    g.close()
+
+
+# ------------------------------------------------------- larger graphs --
+def _graph(kind):
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, knn_jitter_grid
+    if kind == "grid3d":
+        Eu, Ev = grid_graph((40, 36, 30), 6)
+        return 40 * 36 * 30, Eu, Ev
+    if kind == "knn":
+        Eu, Ev = knn_jitter_grid((30, 28, 24), k=6, seed=21)
+        return 30 * 28 * 24, Eu, Ev
+    if kind == "chain":
+        V = 6000
+        return V, np.arange(V - 1, dtype=np.int32), np.arange(1, V, dtype=np.int32)
+    if kind == "grid2d8":
+        Eu, Ev = grid_graph((300, 200), 8)
+        return 300 * 200, Eu, Ev
+    raise ValueError(kind)
+
+
+def _activity(kind, V, Eu, Ev, seed):
+    """cut-like activity: edges between random blobs, plus random extras"""
+    rng = np.random.default_rng(seed)
+    lab = (np.arange(V) // max(1, V // 37) * 7919 + rng.integers(0, 3, V) // 2) % 11
+    act = (lab[Eu] != lab[Ev]).astype(np.uint8)
+    act[rng.random(Eu.size) < 0.05] = 1
+    if kind == "chain":
+        act[:] = 0
+        act[rng.choice(Eu.size, 5, replace=False)] = 1
+    return act
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("kind", ["grid3d", "knn", "chain", "grid2d8"])
+def test_gpu_graph_steps_match_oracle(cpgraph_cls, oracle_port, kind, dt):
+    o = oracle_port
+    V, Eu, Ev = _graph(kind)
+    rng = np.random.default_rng(5)
+    La = (0.01 + rng.random(Eu.size)).astype(dt)
+    La[rng.random(Eu.size) < 0.02] = 0
+    L1 = (0.02 * rng.random(V)).astype(dt)
+    act = _activity(kind, V, Eu, Ev, 7)
+    g = cpgraph_cls(V, Eu, Ev, La, L1)
+    g.set_active(act)
+    Cv, Vc, rVc = g.components()
+    oCv, oVc, orVc = o.cp_components(V, Eu, Ev, act)
+    _eq(Cv, oCv, "Cv")
+    _eq(Vc, oVc, "Vc")
+    _eq(rVc, orVc, "rVc")
+    eps = float(np.finfo(dt).eps)
+    red = g.reduced_graph(eps)
+    ored = o.cp_reduced_graph(V, Eu, Ev, La, L1, act, oCv, oVc, orVc, eps)
+    for a, b, nm in zip(red, ored, ("rEu", "rEv", "rLa_d1", "rLa_l1")):
+        _eq(a, b, nm)
+    rV = rVc.size - 1
+    rX = np.round(rng.standard_normal(rV), 2).astype(dt)  # ties -> merges
+    rX[rng.random(rV) < 0.2] = 0
+    g.set_values(rX)
+    Y = rng.standard_normal(V).astype(dt)
+    A = (0.5 + rng.random(V)).astype(dt)
+    for AA in (None, A):
+        D = g.gradient(0, AA, Y)
+        oD = o.cp_gradient(0, V, AA, Y, None, Eu, Ev, La, L1, act, oCv, oVc, orVc, rX)
+        _eq(D, oD, "DfS")
+        for cut, pos in ((0, 0), (1, 0), (2, 0), (2, 1)):
+            tr, rc = g.capacities(cut, pos)
+            otr, orc = o.cp_capacities(cut, La, L1, pos, act, oCv, rX, oD)
+            _eq(tr, otr, "tr")
+            _eq(rc, orc, "rc")
+    seg = (rng.random(V) < 0.5).astype(np.uint8)
+    n = g.activate(seg)
+    oact, on = o.cp_activate(Eu, Ev, seg, act)
+    assert n == on
+    _eq(g.active(), oact, "activate")
+    m = g.merge(eps, 1e-3)
+    oact2, om = o.cp_merge(Eu, Ev, oCv, rX, eps, 1e-3, oact)
+    assert m == om
+    _eq(g.active(), oact2, "merge")
+    g.close()
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_gpu_edgeless_and_all_active(cpgraph_cls, oracle_port, dt):
+    o = oracle_port
+    V = 1000
+    Eu = np.zeros(0, np.int32)
+    g = cpgraph_cls(V, Eu, Eu, np.zeros(0, dt))
+    Cv, Vc, rVc = g.components()
+    assert rVc.size == V + 1 and np.array_equal(Cv, np.arange(V))
+    rEu, rEv, rLa, _ = g.reduced_graph(1e-7)
+    oEu, oEv, oLa, _ = o.cp_reduced_graph(V, Eu, Eu, np.zeros(0, dt), None, np.zeros(0, np.uint8),
+                                          Cv, Vc, rVc, 1e-7)
+    _eq(rEu, oEu, "rEu")
+    _eq(rEv, oEv, "rEv")
+    _eq(rLa, oLa, "rLa")
+    g.close()
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    Eu, Ev = grid_graph((50, 40), 4)
+    La = np.full(Eu.size, 0.1, dt)
+    act = np.ones(Eu.size, np.uint8)
+    g = cpgraph_cls(2000, Eu, Ev, La)
+    g.set_active(act)
+    Cv, Vc, rVc = g.components()
+    oCv, oVc, orVc = o.cp_components(2000, Eu, Ev, act)
+    _eq(Vc, oVc, "Vc")
+    red = g.reduced_graph(1e-7)
+    ored = o.cp_reduced_graph(2000, Eu, Ev, La, None, act, oCv, oVc, orVc, 1e-7)
+    for a, b, nm in zip(red[:3], ored[:3], ("rEu", "rEv", "rLa")):
+        _eq(a, b, nm)
+    g.close()
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_gpu_dense_gradients_match_oracle(cpgraph_cls, oracle_port, dt):
+    o = oracle_port
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    rng = np.random.default_rng(9)
+    Eu, Ev = grid_graph((20, 15), 4)
+    V = 300
+    La = np.full(Eu.size, 0.05, dt)
+    act = _activity("grid2d8", V, Eu, Ev, 3)
+    g = cpgraph_cls(V, Eu, Ev, La)
+    g.set_active(act)
+    Cv, Vc, rVc = g.components()
+    rX = rng.standard_normal(rVc.size - 1).astype(dt)
+    rX[::3] = 0
+    g.set_values(rX)
+    for N in (37, 200):  # direct: A N-by-V, R the residual
+        A = rng.standard_normal((N, V)).astype(dt)
+        R = rng.standard_normal(N).astype(dt)
+        D = g.gradient(N, A, None, R)
+        oD = o.cp_gradient(N, V, A, np.zeros(V, dt), R, Eu, Ev, La, None, act, Cv, Vc, rVc, rX)
+        _eq(D, oD, "DfS N=%d" % N)
+    B = rng.standard_normal((V, V)).astype(dt)
+    AtA = (B + B.T).astype(dt)
+    AtY = rng.standard_normal(V).astype(dt)
+    D = g.gradient(-V, AtA, AtY)
+    oD = o.cp_gradient(-V, V, AtA, AtY, None, Eu, Ev, La, None, act, Cv, Vc, rVc, rX)
+    _eq(D, oD, "DfS N=-V")
+    g.close()
