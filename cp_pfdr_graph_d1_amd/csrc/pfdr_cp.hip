@@ -37,7 +37,16 @@ __global__ void k_cp_colsum(int N, int rV, const real *__restrict__ A, const int
     if (n >= N) return;
     for (int rv = blockIdx.y; rv < rV; rv += gridDim.y) {
         real a = real(0);
-        for (int s = rVc[rv], t = rVc[rv + 1]; s < t; s++) a += A[(size_t)N * Vc[s] + n];
+        int s = rVc[rv];
+        const int t = rVc[rv + 1];
+        for (; s + 8 <= t; s += 8) {  // 8 column loads in flight, adds in order
+            real x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = A[(size_t)N * Vc[s + u] + n];
+#pragma unroll
+            for (int u = 0; u < 8; u++) a += x[u];
+        }
+        for (; s < t; s++) a += A[(size_t)N * Vc[s] + n];
         rA[(size_t)N * rv + n] = a;
     }
 }
@@ -69,24 +78,11 @@ __global__ void k_cp_rY_dot(int N, int rV, const real *__restrict__ rA, const re
     rY[rv] = s;
 }
 
-// rY[rv] = component sum of Y; diag: rAA[rv] = component sum of A or size (:715-759)
+// identity (:756-758): rAA[rv] = component size
 template <typename real>
-__global__ void k_cp_compsum(int rV, const real *__restrict__ Y, const real *__restrict__ A,
-                             int diag, const int *__restrict__ rVc, const int *__restrict__ Vc,
-                             real *__restrict__ rY, real *__restrict__ rAA) {
+__global__ void k_cp_sizes(int rV, const int *__restrict__ rVc, real *__restrict__ rAA) {
     const int rv = blockIdx.x * blockDim.x + threadIdx.x;
-    if (rv >= rV) return;
-    real a = real(0);
-    for (int s = rVc[rv], t = rVc[rv + 1]; s < t; s++) a += Y[Vc[s]];
-    rY[rv] = a;
-    if (!diag) return;
-    if (A) {
-        real d = real(0);
-        for (int s = rVc[rv], t = rVc[rv + 1]; s < t; s++) d += A[Vc[s]];
-        rAA[rv] = d;
-    } else {
-        rAA[rv] = (real)(rVc[rv + 1] - rVc[rv]);
-    }
+    if (rv < rV) rAA[rv] = (real)(rVc[rv + 1] - rVc[rv]);
 }
 
 // upper triangle of the double component sums of A^tA (:724-741)
@@ -234,7 +230,12 @@ static int cp_reduce_host(const char *fn, int N, int V, const real *A, const rea
                 k_cp_rY_dot<real><<<gV, b1, 0, s>>>(N, rV, drA, dY, drY);
             }
         } else {
-            k_cp_compsum<real><<<gV, b1, 0, s>>>(rV, dY, dA, N == 0 ? 1 : 0, dptr, dVc, drY, drAA);
+            // rY = component sums of Y (:715-723); N = 0: rAA = component sums
+            // of the diagonal (:744-755) or the sizes (:756-758) — each sum in
+            // Vc order, giant components by one LDS-staged workgroup
+            ordered_segment_sums<real>(rV, dptr, dVc, dY, drY, s);
+            if (N == 0 && dA) ordered_segment_sums<real>(rV, dptr, dVc, dA, drAA, s);
+            else if (N == 0) k_cp_sizes<real><<<gV, b1, 0, s>>>(rV, dptr, drAA);
             if (N < 0) {
                 k_cp_ata<real><<<gVV, b1, 0, s>>>(V, rV, dA, dptr, dVc, drAA);
                 k_cp_mirror<real><<<gVV, b1, 0, s>>>(rV, drAA);

@@ -111,8 +111,7 @@ __device__ __forceinline__ void block_count(int c, int *total) {
 // out[g] = (((0 + x[o0]) + x[o0+1]) + ...) over [off[g], off[g+1]), with
 // x[i] = val[idx[i]] (idx may be null: x[i] = val[i]).  Short segments:
 // one lane each; long ones (> kWave entries) are appended to a list and
-// summed by one wave each (coalesced loads, the adds in order on one
-// lane's chain via readlane).
+// summed by one workgroup each (k_segsum_long).
 constexpr int kSegShort = kWave;
 
 template <typename real>
@@ -131,25 +130,56 @@ __global__ void k_segsum_short(int G, const int *__restrict__ off, const int *__
     out[g] = s;
 }
 
-template <typename real>
+// one workgroup per long segment: waves 1-3 stage the next chunk in LDS
+// (double buffered, coalesced / gathered loads) while lane 0 of wave 0 adds
+// the current one in order, 16-byte LDS reads issued ahead of its chain
+template <typename real, bool GATHER>
 __global__ __launch_bounds__(kBlock) void k_segsum_long(int n, const int *__restrict__ longs,
                                                        const int *__restrict__ off,
                                                        const int *__restrict__ idx,
                                                        const real *__restrict__ val,
                                                        real *__restrict__ out) {
-    const int w = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-    const int lane = threadIdx.x & (kWave - 1);
-    if (w >= n) return;
-    const int g = longs[w];
-    const int a = off[g], b = off[g + 1];
+    constexpr int CH = 4096;
+    __shared__ alignas(16) real buf[2][CH];
+    if ((int)blockIdx.x >= n) return;
+    const int g = longs[blockIdx.x];
+    const long a = off[g], b = off[g + 1];
+    const int t = threadIdx.x;
+    // loaders (waves 1-3): 16 independent loads in flight per lane
+    // (indices clamped into the chunk, so every load is unconditional)
+    auto load = [&](int which, long c0) {
+        constexpr int B = 16, NL = kBlock - kWave;
+        const int m = (int)min((long)CH, b - c0);
+        for (int j0 = t - kWave; j0 < m; j0 += B * NL) {
+            int id[B];
+            real x[B];
+#pragma unroll
+            for (int u = 0; u < B; u++) {
+                const long j = c0 + min(j0 + u * NL, m - 1);
+                id[u] = GATHER ? idx[j] : (int)j;
+            }
+#pragma unroll
+            for (int u = 0; u < B; u++) x[u] = val[id[u]];
+#pragma unroll
+            for (int u = 0; u < B; u++)
+                if (j0 + u * NL < m) buf[which][j0 + u * NL] = x[u];
+        }
+    };
     real s = real(0);
-    for (int c = a; c < b; c += kWave) {
-        const int i = c + lane;
-        const real x = (i < b) ? val[idx ? idx[i] : i] : real(0);
-        const int m = min(kWave, b - c);
-        for (int k = 0; k < m; k++) s += __shfl(x, k, kWave);
+    int cur = 0;
+    if (t >= kWave) load(0, a);
+    __syncthreads();
+    for (long c0 = a; c0 < b; c0 += CH) {
+        const int m = (int)min((long)CH, b - c0);
+        if (t == 0) {
+            s = ordered_add(s, buf[cur], m);
+        } else if (t >= kWave && c0 + CH < b) {
+            load(cur ^ 1, c0 + CH);
+        }
+        __syncthreads();
+        cur ^= 1;
     }
-    if (lane == 0) out[g] = s;
+    if (t == 0) out[g] = s;
 }
 
 template <typename real>
@@ -161,10 +191,22 @@ static void segsum(int G, const int *off, const int *idx, const real *val, real 
     PFDR_HIP(hipMemsetAsync(nlong.p, 0, sizeof(int), s));
     k_segsum_short<real><<<grid_for(G), kBlock, 0, s>>>(G, off, idx, val, out, longs.p, nlong.p);
     const int nl = d2h_scalar(nlong.p, s);
-    if (nl) k_segsum_long<real><<<grid_for((long)nl * kWave), kBlock, 0, s>>>(nl, longs.p, off, idx,
-                                                                             val, out);
+    if (nl && idx) k_segsum_long<real, true><<<nl, kBlock, 0, s>>>(nl, longs.p, off, idx, val, out);
+    else if (nl) k_segsum_long<real, false><<<nl, kBlock, 0, s>>>(nl, longs.p, off, idx, val, out);
     PFDR_HIP(hipGetLastError());
 }
+
+template <typename real>
+void ordered_segment_sums(int G, const int *off, const int *idx, const real *val, real *out,
+                          hipStream_t s) {
+    DevBuf<int> longs, nlong;
+    segsum<real>(G, off, idx, val, out, longs, nlong, s);
+    PFDR_HIP(hipStreamSynchronize(s));  // scratch freed at scope exit
+}
+template void ordered_segment_sums<float>(int, const int *, const int *, const float *, float *,
+                                          hipStream_t);
+template void ordered_segment_sums<double>(int, const int *, const int *, const double *,
+                                           double *, hipStream_t);
 
 // ----------------------------------------------------------- components --
 __device__ __forceinline__ int uf_root(const int *parent, int v) {
@@ -227,6 +269,12 @@ __device__ __forceinline__ unsigned long long claim_key(int i, int j) {
     return ((unsigned long long)(unsigned)i << 32) | (unsigned)j;
 }
 
+// A frontier vertex's arcs are handled by a subgroup of kSub lanes (arc j
+// by lane j mod kSub), so the dependent gathers of an arc (slot, activity,
+// endpoint, component) run for up to kSub arcs at once instead of one
+// after the other.
+constexpr int kSub = 16;
+
 // frontier L[lo, hi): every unvisited neighbour through an inactive edge is
 // claimed by its first visit in the reference's order (queue position i,
 // then the arc's rank j in the maxflow graph's list: slots descending)
@@ -234,12 +282,13 @@ __global__ void k_bfs_claim(int lo, int hi, const int *__restrict__ L, const int
                             const unsigned *__restrict__ slot, const int *__restrict__ Eu,
                             const int *__restrict__ Ev, const uint8_t *__restrict__ active,
                             const int *__restrict__ Cv, unsigned long long *claim) {
-    const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    const long gt = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = lo + (int)(gt / kSub), l = (int)(gt % kSub);
     if (i >= hi) return;
     const int v = L[i];
-    const int b = ptr[v];
-    for (int k = ptr[v + 1] - 1, j = 0; k >= b; k--, j++) {
-        const unsigned a = slot[k];
+    const int top = ptr[v + 1] - 1, deg = top + 1 - ptr[v];
+    for (int j = l; j < deg; j += kSub) {
+        const unsigned a = slot[top - j];
         if (active[a >> 1]) continue;
         const int w = arc_head(a, Eu, Ev);
         if (Cv[w] != -1) continue;
@@ -247,34 +296,46 @@ __global__ void k_bfs_claim(int lo, int hi, const int *__restrict__ L, const int
     }
 }
 
-// EMIT = false: cnt[i - lo] = claims won by L[i]; true: append them in order
+// EMIT = false: cnt[i - lo] = claims won by L[i]; true: append them in
+// arc order at hi + cnt[i - lo] (the exclusive scan of the counts)
 template <bool EMIT>
 __global__ void k_bfs_take(int lo, int hi, const int *__restrict__ ptr,
                            const unsigned *__restrict__ slot, const int *__restrict__ Eu,
                            const int *__restrict__ Ev, const uint8_t *__restrict__ active,
                            const unsigned long long *__restrict__ claim, int *__restrict__ cnt,
                            int *L, int *Cv) {
-    const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    const long gt = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = lo + (int)(gt / kSub), l = (int)(gt % kSub);
+    const int sh = (threadIdx.x & (kWave - 1)) & ~(kSub - 1);  // subgroup's first lane
     if (i >= hi) return;
     const int v = L[i];
-    const int b = ptr[v];
+    const int top = ptr[v + 1] - 1, deg = top + 1 - ptr[v];
     int c = 0, base = 0, cv = 0;
     if (EMIT) {
         base = hi + cnt[i - lo];
         cv = Cv[v];
     }
-    for (int k = ptr[v + 1] - 1, j = 0; k >= b; k--, j++) {
-        const unsigned a = slot[k];
-        if (active[a >> 1]) continue;
-        const int w = arc_head(a, Eu, Ev);
-        if (claim[w] != claim_key(i, j)) continue;
-        if (EMIT) {
-            L[base + c] = w;
+    for (int j0 = 0; j0 < deg; j0 += kSub) {
+        const int j = j0 + l;
+        bool win = false;
+        int w = 0;
+        if (j < deg) {
+            const unsigned a = slot[top - j];
+            if (!active[a >> 1]) {
+                w = arc_head(a, Eu, Ev);
+                win = claim[w] == claim_key(i, j);
+            }
+        }
+        const unsigned long long m = __ballot(win);
+        const unsigned mine = (unsigned)(m >> sh) & ((1u << kSub) - 1);
+        if (EMIT && win) {
+            const int p = base + c + __builtin_popcount(mine & ((1u << l) - 1));
+            L[p] = w;
             Cv[w] = cv;
         }
-        c++;
+        c += __builtin_popcount(mine);
     }
-    if (!EMIT) cnt[i - lo] = c;
+    if (!EMIT && l == 0) cnt[i - lo] = c;
 }
 
 __global__ void k_gather_keys(int V, const int *__restrict__ L, const int *__restrict__ Cv,
@@ -614,16 +675,17 @@ void CpGraphBase::components() {
     int lo = 0, hi = rV;
     while (hi > lo && hi < Vn) {
         const int n = hi - lo;
-        k_bfs_claim<<<grid_for(n), kBlock, 0, s>>>(lo, hi, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+        const int gb = grid_for((long)n * kSub);
+        k_bfs_claim<<<gb, kBlock, 0, s>>>(lo, hi, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
                                                    active.p, Cv.p, claim.p);
-        k_bfs_take<false><<<grid_for(n), kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+        k_bfs_take<false><<<gb, kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
                                                          active.p, claim.p, i1.p, L.p, Cv.p);
         PFDR_HIP(hipMemsetAsync(i1.p + n, 0, sizeof(int), s));
         excl_scan(tmp, i1.p, i2.p, n + 1, s);
         const int add = d2h_scalar(i2.p + n, s);
         if (add == 0) break;
         if (add > Vn - hi) throw std::runtime_error("components: BFS overflow");
-        k_bfs_take<true><<<grid_for(n), kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
+        k_bfs_take<true><<<gb, kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
                                                         active.p, claim.p, i2.p, L.p, Cv.p);
         PFDR_HIP(hipGetLastError());
         lo = hi;

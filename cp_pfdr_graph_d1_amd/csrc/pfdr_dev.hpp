@@ -103,6 +103,44 @@ __device__ __forceinline__ T block_sum(T v, T *lds /* >= kBlock/64 */) {
     return s;
 }
 
+// packed vector of N T (16-byte accesses)
+template <typename T, int N>
+struct alignas(sizeof(T) * N) Pk { T v[N]; };
+
+// s + q[0] + q[1] + ... + q[m-1], left to right, from LDS.  Two register
+// sets A / B of U x 16 bytes: the reads of one set are in flight while the
+// other set's values are added, so the dependent add chain (one v_add per
+// element) never waits for LDS (LDS ops complete in order: waiting for A
+// leaves B's U reads outstanding).
+template <typename real>
+__device__ __forceinline__ real ordered_add(real s, const real *q, int m) {
+    constexpr int W = Vec<real>::kPer16B, U = 8, S = W * U;
+    using P = Pk<real, W>;
+    const int ns = m / S;  // whole sets
+    P A[U], B[U];
+    auto ld = [&](P *r, int set) {
+#pragma unroll
+        for (int u = 0; u < U; u++) r[u] = *reinterpret_cast<const P *>(q + set * S + u * W);
+    };
+    auto add = [&](const P *r) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int k = 0; k < W; k++) s += r[u].v[k];
+    };
+    if (ns > 0) ld(A, 0);
+    int i = 0;
+    for (; i + 1 < ns; i += 2) {
+        ld(B, i + 1);
+        add(A);
+        if (i + 2 < ns) ld(A, i + 2);
+        add(B);
+    }
+    if (i < ns) add(A);
+    for (int j = ns * S; j < m; j++) s += q[j];
+    return s;
+}
+
 // XCD-aware block order: the dispatcher deals blocks round-robin over the 8
 // XCDs (blocks b, b+8, ... share one L2), so give each XCD a CONTIGUOUS range
 // of logical blocks: neighbouring blocks, which gather the same neighbour

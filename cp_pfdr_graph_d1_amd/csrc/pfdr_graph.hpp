@@ -28,4 +28,12 @@ void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int
 // Row offsets ptr[0..V] of n keys sorted by row (row = key >> 32).
 void keyed_rows(const unsigned long long *skey, long n, int V, int *ptr, hipStream_t s);
 
+// out[g] = ((0 + x[off[g]]) + x[off[g] + 1]) + ... over [off[g], off[g+1]),
+// x[i] = val[idx[i]] (idx may be null: val[i]), each sum in that exact
+// order (pfdr_cpgraph.hip: one lane per short segment, one LDS-staged
+// workgroup per long one).  Synchronises the stream.
+template <typename real>
+void ordered_segment_sums(int G, const int *off, const int *idx, const real *val, real *out,
+                          hipStream_t s);
+
 }  // namespace pfdr

@@ -49,9 +49,6 @@ enum Gate : int { GATE_NONE = 0, GATE_ACTIVE = 1, GATE_OBJ = 2,
 template <typename real> using R2 = typename Vec<real>::v2;
 
 template <typename T, int N>
-struct alignas(sizeof(T) * N) Pk { T v[N]; };
-
-template <typename T, int N>
 __device__ __forceinline__ Pk<T, N> ldv(const T *p) {
     return *reinterpret_cast<const Pk<T, N> *>(p);
 }
@@ -390,21 +387,19 @@ __global__ __launch_bounds__(256) void k_seq_sum(int V, const real *__restrict__
         const long n = min((long)CH, (long)V - c0);
         const long nxt = c0 + CH;
         if (threadIdx.x == 0) {
-            // 16-byte LDS reads issued ahead of the dependent add chain
-            constexpr int W = Vec<real>::kPer16B;
-            const real *b = buf[cur];
-            const int nw = (int)n / W * W;
-            int j = 0;
-#pragma unroll 4
-            for (; j < nw; j += W) {
-                const Pk<real, W> q = ldv<real, W>(b + j);
+            s = ordered_add(s, buf[cur], (int)n);
+        } else if (threadIdx.x >= kWave && nxt < V) {
+            // waves 1-3 stage the next chunk, 16 loads in flight per lane
+            constexpr int B = 16, NL = kBlock - kWave;
+            const int m = (int)min((long)CH, (long)V - nxt);
+            for (int j0 = threadIdx.x - kWave; j0 < m; j0 += B * NL) {
+                real x[B];
 #pragma unroll
-                for (int u = 0; u < W; u++) s += q.v[u];
+                for (int u = 0; u < B; u++) x[u] = absval[nxt + min(j0 + u * NL, m - 1)];
+#pragma unroll
+                for (int u = 0; u < B; u++)
+                    if (j0 + u * NL < m) buf[cur ^ 1][j0 + u * NL] = x[u];
             }
-            for (; j < (int)n; j++) s += b[j];
-        } else if (nxt < V) {
-            const long m = min((long)CH, (long)V - nxt);
-            for (long j = threadIdx.x - 1; j < m; j += kBlock - 1) buf[cur ^ 1][j] = absval[nxt + j];
         }
         __syncthreads();
         cur ^= 1;
