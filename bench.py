@@ -189,6 +189,7 @@ def main():
     finite = bool(np.all(np.isfinite(res[0])))
     dev_bytes = sess.device_bytes()
     reordered = bool(sess.query("reordered"))
+    split_blocks = sess.query("split_blocks") if wl.kind != pfdr.PFDR_KIND_SIMPLEX else 0
     sess.close()
     if world > 1:
         dist.destroy_process_group()
@@ -221,6 +222,7 @@ def main():
             "input_generation_s": round(gen_s, 3),
             "device_bytes": dev_bytes,
             "relabelled": reordered,
+            "split_incidence_blocks": split_blocks,
             "finite": finite,
         },
         "roofline": {

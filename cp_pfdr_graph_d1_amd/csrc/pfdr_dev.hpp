@@ -142,16 +142,25 @@ __device__ __forceinline__ real ordered_add(real s, const real *q, int m) {
 }
 
 // XCD-aware block order: the dispatcher deals blocks round-robin over the 8
-// XCDs (blocks b, b+8, ... share one L2), so give each XCD a CONTIGUOUS range
-// of logical blocks: neighbouring blocks, which gather the same neighbour
-// bands of the graph, then share an L2.  Placement is a speed hint only.
-// Launch xcd_grid(nb) blocks; a block whose logical id is >= nb returns.
-__device__ __forceinline__ int xcd_block(int b, int nb, int on) {
-    if (!on) return b;
-    const int per = (nb + 7) >> 3;
-    return (b & 7) * per + (b >> 3);
+// XCDs (blocks b, b+8, ... share one L2).  mode 0: identity; 1: each XCD
+// gets a CONTIGUOUS eighth of the logical blocks (neighbouring blocks, which
+// gather the same neighbour bands of the graph, share an L2); C >= 2: runs
+// of C consecutive logical blocks per XCD, the 8 XCDs side by side on a
+// window of 8C blocks.  Placement is a speed hint only.  Launch
+// xcd_grid(nb, mode) blocks; a block whose logical id is >= nb returns.
+__device__ __forceinline__ int xcd_block(int b, int nb, int mode) {
+    if (mode == 0) return b;
+    if (mode == 1) {
+        const int per = (nb + 7) >> 3;
+        return (b & 7) * per + (b >> 3);
+    }
+    const int r = b >> 3;
+    return ((r / mode) * 8 + (b & 7)) * mode + r % mode;
 }
-inline int xcd_grid(int nb, int on) { return on ? ((nb + 7) >> 3) << 3 : nb; }
+inline int xcd_grid(int nb, int mode) {
+    const int q = mode <= 1 ? 8 : 8 * mode;
+    return mode ? (nb + q - 1) / q * q : nb;
+}
 
 inline int grid_for(long n, int per_thread = 1) {
     long t = (n + per_thread - 1) / per_thread;

@@ -106,6 +106,11 @@ class QuadSession final : public SessionBase {
     DevBuf<int> cnt_part_;
     DevBuf<Ctrl<real>> ctrl_;
     Incidence inc_;
+    // split incidence (edges sorted by u): u-run offsets, per-vertex order
+    // masks, addresses of the other entries, per-block path flag
+    DevBuf<int> uptr_, blkok_;
+    DevBuf<unsigned> mask_, oidx_;
+    void build_split();
     Ctrl<real> *hctrl_ = nullptr;  // pinned mirror
     int nbv_, nbe_, nbn_, rows_nb_, rows_cpb_;
     int it_ = 0;
@@ -172,6 +177,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     {   // tuning knob for A/B runs: PFDR_XCD = <edge bit><vertex bit>, default "01"
         const char *x = getenv("PFDR_XCD");
         if (x && strlen(x) == 2) { xcd_e_ = x[0] == '1'; xcd_v_ = x[1] == '1'; }
+        const char *xc = getenv("PFDR_XCD_CHUNK");  // edge sweep: runs of C blocks per XCD
+        if (xc && atoi(xc) >= 2) xcd_e_ = atoi(xc);
+        const char *xv = getenv("PFDR_XCD_CHUNK_V");  // vertex sweep: idem
+        if (xv && atoi(xv) >= 2) xcd_v_ = atoi(xv);
         const char *g = getenv("PFDR_GB");  // 8 (default) or 16
         if (g && atoi(g) == 16) gb_ = 16;
         // prox weights recomputed in every edge sweep (default; PFDR_EDGE_RW=0
@@ -319,6 +328,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_})
         acc(b->n * sizeof(real));
     acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
+    acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
     order_.release();  // inputs are in the internal labels now
     if (halo_) {
         const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
@@ -381,6 +391,44 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
+    build_split();
+}
+
+// Split incidence for the vertex sweep (split_sum): when the edges are
+// sorted by their u end (natural emission order, relabelled sessions), each
+// vertex's u-end contributions are a contiguous run of wz and need no
+// address.  Blocks that do not qualify keep the CSR gather.
+template <typename real>
+void QuadSession<real>::build_split() {
+    const char *sp = getenv("PFDR_SPLIT");  // A/B: PFDR_SPLIT=0 keeps the CSR gather everywhere
+    if ((sp && sp[0] == '0') || !E_) return;
+    hipStream_t s = stream;
+    DevBuf<unsigned long long> bad(1);
+    PFDR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
+    k_u_order_check<<<grid_for(E_), kBlock, 0, s>>>(E_, V_, Eu_.p, bad.p);
+    PFDR_HIP(hipGetLastError());
+    unsigned long long nbad = 0;
+    PFDR_HIP(hipMemcpyAsync(&nbad, bad.p, sizeof(nbad), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    if (nbad) return;
+    const int nb = grid_for(V_);
+    const long ototal = inc_.n - E_;  // every local edge's u end is an owned row
+    if (ototal < 0) return;
+    uptr_.alloc((size_t)V_ + 1);
+    mask_.alloc(V_);
+    oidx_.alloc(ototal ? ototal : 1);
+    blkok_.alloc(nb);
+    k_uptr<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, V_, Eu_.p, uptr_.p);
+    k_split_build<<<nb, kBlock, 0, s>>>(V_, E_, inc_.ptr.p, inc_.idx.p, uptr_.p, ototal, mask_.p,
+                                        oidx_.p, blkok_.p, GatherCap<real>::v / 2);
+    PFDR_HIP(hipGetLastError());
+    std::vector<int> h(nb);
+    PFDR_HIP(hipMemcpyAsync(h.data(), blkok_.p, nb * sizeof(int), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    long n = 0;
+    for (int x : h) n += x;
+    split_blocks = n;
+    if (!n) { uptr_.release(); mask_.release(); oidx_.release(); blkok_.release(); }
 }
 
 template <typename real>
@@ -607,6 +655,7 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
     hipStream_t s = stream;
     VArgs<real> a{};
     a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p; a.wz = wz_.p;
+    a.uptr = uptr_.p; a.mask = mask_.p; a.oidx = oidx_.p; a.blkok = blkok_.p;
     a.Y = Y_.p; a.A = A_.p; a.Ga = Ga_.p; a.Th_l1 = Th_l1_.p;
     a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);

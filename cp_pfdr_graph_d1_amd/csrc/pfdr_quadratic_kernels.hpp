@@ -120,6 +120,130 @@ template <typename real> struct GatherCap;
 template <> struct GatherCap<float> { static constexpr int v = 4096; };
 template <> struct GatherCap<double> { static constexpr int v = 4096; };
 
+// Split incidence of a graph whose edges are sorted by their u end (see
+// k_split_build): the u-end contributions of vertex v are the contiguous
+// run wz[uptr[v] .. uptr[v+1]) (side-major wz, u ends first), so only the
+// OTHER entries (v ends and received contributions) need an address,
+// oidx[ptr[v] - uptr[v] ...], and a 32-bit mask per vertex says, entry by
+// entry in the reference's order, which list the next term comes from.
+// The block's u-runs are staged with coalesced loads (no index, no
+// pointer chase), the others gathered; both lists meet in LDS and each
+// lane adds its vertex's terms in the reference's (e, side) order.
+// Valid for a block whose runs fit the LDS halves (checked at setup).
+template <typename real, int GB>
+__device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__restrict__ ptr,
+                                          const int *__restrict__ uptr,
+                                          const unsigned *__restrict__ mask,
+                                          const unsigned *__restrict__ oidx,
+                                          const real *__restrict__ wz, real *lds) {
+    constexpr int CU = GatherCap<real>::v / 2;
+    const int tid = threadIdx.x;
+    const int vend = min(v0 + kBlock, V);
+    // per-lane bookkeeping first: its latency hides under the staging
+    int p0 = 0, p1 = 0, u0 = 0;
+    unsigned m = 0u;
+    if (v < V) { p0 = ptr[v]; p1 = ptr[v + 1]; u0 = uptr[v]; m = mask[v]; }
+    const int ua = uptr[v0], ub = uptr[vend];
+    const int oa = ptr[v0] - ua, ob = ptr[vend] - ub;
+    const int nu = ub - ua, no = ob - oa;
+    const int nmax = max(nu, no);
+    for (int b = 0; b < nmax; b += kBlock * GB) {
+        unsigned id[GB];
+        real wu[GB], wo[GB];
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            const int j = b + u * kBlock + tid;
+            id[u] = (j < no) ? oidx[oa + j] : 0u;
+            wu[u] = (j < nu) ? wz[ua + j] : real(0);
+        }
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            const int j = b + u * kBlock + tid;
+            wo[u] = (j < no) ? wz[id[u]] : real(0);
+        }
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            const int j = b + u * kBlock + tid;
+            if (j < nu) lds[j] = wu[u];
+            if (j < no) lds[CU + j] = wo[u];
+        }
+    }
+    __syncthreads();
+    real s = real(0);
+    if (v < V) {
+        int pu = u0 - ua, po = CU + (p0 - u0) - oa;
+        for (int i = p0; i < p1; i++) {
+            const bool own = m & 1u;
+            s += lds[own ? pu : po];
+            pu += own;
+            po += !own;
+            m >>= 1;
+        }
+    }
+    return s;
+}
+
+// ------------------------------------------------ split incidence setup --
+// counts edges out of u order or with a u end outside [0, V)
+static __global__ void k_u_order_check(long E, int V, const int *__restrict__ Eu,
+                                unsigned long long *__restrict__ bad) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int u = Eu[e];
+    if (u < 0 || u >= V || (e + 1 < E && u > Eu[e + 1])) atomicAdd(bad, 1ull);
+}
+
+// uptr[v] = first edge whose u end is >= v, v in [0, V] (Eu sorted)
+static __global__ void k_uptr(long E, int V, const int *__restrict__ Eu, int *__restrict__ uptr) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e > E) return;
+    const int lo = e == 0 ? 0 : Eu[e - 1] + 1;
+    const int hi = e == E ? V : Eu[e];
+    for (int v = lo; v <= hi; v++) uptr[v] = (int)e;
+}
+
+// One lane per vertex: mask (bit i: the i-th CSR entry is the vertex's next
+// own u-run contribution) and the other entries' addresses in CSR order.
+// blkok[b] = 1 when every vertex of block b has <= 32 entries with its
+// u-run in edge order, and the block's runs fit the LDS halves (cap).
+static __global__ __launch_bounds__(256) void k_split_build(int V, long E, const int *__restrict__ ptr,
+                                                     const unsigned *__restrict__ idx,
+                                                     const int *__restrict__ uptr, long ototal,
+                                                     unsigned *__restrict__ mask,
+                                                     unsigned *__restrict__ oidx,
+                                                     int *__restrict__ blkok, int cap) {
+    const int v0 = blockIdx.x * kBlock;
+    const int v = v0 + threadIdx.x;
+    int ok = 1;
+    if (v < V) {
+        const int p0 = ptr[v], p1 = ptr[v + 1], u0 = uptr[v], u1 = uptr[v + 1];
+        const long o0 = (long)p0 - u0;
+        unsigned m = 0u;
+        int cu = 0, co = 0;
+        if (p1 - p0 > 32) ok = 0;
+        for (int j = p0; j < p1; j++) {
+            const unsigned id = idx[j];
+            if ((long)id < E) {
+                if ((long)id != (long)u0 + cu) ok = 0;
+                if (j - p0 < 32) m |= 1u << (j - p0);
+                cu++;
+            } else {
+                if (o0 + co >= 0 && o0 + co < ototal) oidx[o0 + co] = id;
+                co++;
+            }
+        }
+        if (cu != u1 - u0) ok = 0;
+        mask[v] = m;
+    }
+    const int all = __syncthreads_and(ok);
+    if (threadIdx.x == 0) {
+        const int vend = min(v0 + kBlock, V);
+        const int nu = uptr[vend] - uptr[v0];
+        const int no = (ptr[vend] - uptr[vend]) - (ptr[v0] - uptr[v0]);
+        blkok[blockIdx.x] = (all && nu <= cap && no >= 0 && no <= cap) ? 1 : 0;
+    }
+}
+
 // ====================================================================== //
 //                                kernels                                  //
 // ====================================================================== //
@@ -626,14 +750,18 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
         const Pk<int, EPT> iv = ldv<int, EPT>(Ev + e0);
         R2<real> pu[EPT], pv[EPT];
 #pragma unroll
-        for (int j = 0; j < EPT; j++) { pu[j] = xp[iu.v[j]]; pv[j] = xp[iv.v[j]]; }
+        for (int j = 0; j < EPT; j++) {
+            pu[j] = xp[iu.v[j]]; pv[j] = xp[iv.v[j]];
+        }
         Pk<real, 2 * EPT> z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
         const Pk<real, 2 * EPT> w = ldv<real, 2 * EPT>(W2 + 2 * e0);
         Pk<real, EPT> a, b, t;
         if (RW) {
             real gu[EPT], gv[EPT];
 #pragma unroll
-            for (int j = 0; j < EPT; j++) { gu[j] = Ga[iu.v[j]]; gv[j] = Ga[iv.v[j]]; }
+            for (int j = 0; j < EPT; j++) {
+                gu[j] = Ga[iu.v[j]]; gv[j] = Ga[iv.v[j]];
+            }
             const Pk<real, EPT> la = ldv<real, EPT>(La_d1 + e0);
 #pragma unroll
             for (int j = 0; j < EPT; j++)
@@ -684,6 +812,9 @@ struct VArgs {
     int bbeg;               // first block of this launch (vertex block bbeg*256)
     const int *ptr;
     const unsigned *idx;
+    const int *uptr;        // split incidence (null: CSR gather everywhere)
+    const unsigned *mask, *oidx;
+    const int *blkok;       // per block: 1 = split path
     const real *wz;         // contributions (local side-major, then received)
     R2<real> *xp;
     const real *Y, *A, *Ga, *Th_l1;
@@ -722,7 +853,11 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
         if (a.fwd) { yv = a.Y[v]; gv = a.Ga[v]; }
         if (a.fwd == 2) av = a.A[v];
     }
-    real x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+    real x;
+    if (a.blkok && a.blkok[blk])  // block-uniform
+        x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds);
+    else
+        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
     real num = real(0), den = real(0);
     if (v < a.V) {
         switch (a.prox) {

@@ -53,6 +53,7 @@ class SessionBase {
     virtual void *device_x() = 0;
     int64_t device_bytes = 0;
     int64_t reordered = 0;  // internal locality relabelling applied
+    int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

@@ -1,0 +1,117 @@
+"""GPU: the split incidence of the vertex sweep (csrc/pfdr_quadratic_kernels.hpp
+split_sum).  When the edges are sorted by their u end, each vertex's u-end
+contributions are a contiguous run and only the other entries are gathered;
+a per-vertex mask keeps the reference's (e, side) summation order.  The
+split and the plain CSR gather must give the same iterates bit for bit, and
+both must match the restatement of the reference (oracle)."""
+import os
+
+import numpy as np
+import pytest
+
+from cp_pfdr_graph_d1_amd import pfdr
+from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, uniform
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(split, V, Eu, Ev, Y, dt, it, reorder=pfdr.REORDER_OFF, **kw):
+    old = os.environ.get("PFDR_SPLIT")
+    os.environ["PFDR_SPLIT"] = "1" if split else "0"
+    try:
+        s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                         np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3,
+                         itMax=it, reorder=reorder, **kw)
+    finally:
+        if old is None:
+            del os.environ["PFDR_SPLIT"]
+        else:
+            os.environ["PFDR_SPLIT"] = old
+    nsplit = s.query("split_blocks")
+    s.run(it)
+    X, its, _, Dif = s.result()
+    s.close()
+    return X, its, Dif, nsplit
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_split_equals_gather_natural_grid(gpu_lib, dt):
+    """3-D 6-neighbour grid in emission order: every block takes the split
+    path; with reconditioning and a tolerance the two paths agree bit for bit
+    (iterates, iteration count, Dif)."""
+    shape = (48, 40, 24)
+    Eu, Ev = grid_graph(shape, 6)
+    V = int(np.prod(shape))
+    Y = piecewise_observation(shape, 3, dt)
+    kw = dict(difRcd=1e-1, difTol=1e-5, record_dif=True)
+    Xs, its, Ds, ns = _solve(True, V, Eu, Ev, Y, dt, 400, **kw)
+    Xg, itg, Dg, ng = _solve(False, V, Eu, Ev, Y, dt, 400, **kw)
+    assert ns == (V + 255) // 256 and ng == 0
+    assert its == itg
+    assert np.array_equal(Xs, Xg)
+    assert np.array_equal(Ds[:its], Dg[:itg])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_split_mixed_blocks_with_hubs(gpu_lib, oracle_port, dt):
+    """A 2-D grid plus hub vertices of degree > 32 and zero-out-degree runs:
+    the hubs' blocks fall back to the CSR gather, the others split; results
+    equal the plain gather and the oracle bit for bit at a fixed k."""
+    shape = (96, 80)
+    V = int(np.prod(shape))
+    Eu0, Ev0 = grid_graph(shape, 8)
+    rng_t = uniform(5, np.arange(4000))
+    hubs = np.array([17, 3000, 3001, 7000], np.int64)
+    extra_u = np.repeat(hubs, 40)
+    extra_v = (rng_t[: extra_u.size] * V).astype(np.int64)
+    extra_v[extra_v == extra_u] += 1
+    Eu = np.concatenate([Eu0.astype(np.int64), extra_u])
+    Ev = np.concatenate([Ev0.astype(np.int64), extra_v % V])
+    # drop the out-edges of a band of vertices (zero out-degree runs)
+    keep = ~((Eu >= 5000) & (Eu < 5400))
+    Eu, Ev = Eu[keep], Ev[keep]
+    order = np.argsort(Eu, kind="stable")
+    Eu, Ev = Eu[order].astype(np.int32), Ev[order].astype(np.int32)
+    Y = piecewise_observation(shape, 4, dt)
+    k = 25
+    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, dt, k)
+    Xg, _, _, _ = _solve(False, V, Eu, Ev, Y, dt, k)
+    nb = (V + 255) // 256
+    assert 0 < ns < nb
+    assert np.array_equal(Xs, Xg)
+    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
+                                                np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
+                                                0, 0, None, 1.5, 1e-3, 0.0, 0.0, k)
+    assert ito == k
+    assert np.array_equal(Xs, Xo)
+
+
+def test_split_unsorted_edges_keep_the_gather(gpu_lib):
+    """Edges out of u order: no split blocks, same results as sorted input
+    handled by the gather (the summation order is the edge order)."""
+    shape = (64, 64)
+    Eu, Ev = grid_graph(shape, 4)
+    V = int(np.prod(shape))
+    p = np.argsort(uniform(9, np.arange(Eu.size)), kind="stable")
+    Eu, Ev = Eu[p].astype(np.int32), Ev[p].astype(np.int32)
+    Y = piecewise_observation(shape, 6, np.float32)
+    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, np.float32, 10)
+    Xg, _, _, _ = _solve(False, V, Eu, Ev, Y, np.float32, 10)
+    assert ns == 0
+    assert np.array_equal(Xs, Xg)
+
+
+def test_split_after_relabelling(gpu_lib):
+    """Randomly labelled grid: the relabelled session sorts its edges by the
+    new u end, so it splits, and stays bit-identical to the plain solve."""
+    shape = (128, 128, 64)
+    Eu, Ev = grid_graph(shape, 6)
+    V = int(np.prod(shape))
+    new_of = np.empty(V, np.int64)
+    new_of[np.argsort(uniform(11, np.arange(V)), kind="stable")] = np.arange(V)
+    Eu, Ev = new_of[Eu].astype(np.int32), new_of[Ev].astype(np.int32)
+    Y = piecewise_observation(shape, 7, np.float32)
+    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_ON)
+    Xg, _, _, ng = _solve(False, V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_OFF)
+    assert ns > 0 and ng == 0
+    assert np.array_equal(Xs, Xg)
