@@ -91,7 +91,7 @@ def pmc_traffic(kernel, E):
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
         if d.get("workload_E") == E:
-            return d["kernels"]["k_" + kernel]["hbm_bytes_per_launch"]
+            return d["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         pass
     return None
@@ -189,7 +189,12 @@ def main():
     finite = bool(np.all(np.isfinite(res[0])))
     dev_bytes = sess.device_bytes()
     reordered = bool(sess.query("reordered"))
-    split_blocks = sess.query("split_blocks") if wl.kind != pfdr.PFDR_KIND_SIMPLEX else 0
+    quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
+    split_blocks = sess.query("split_blocks") if quad else 0
+    # the edge sweep's kernel: u ends staged in LDS for u-sorted edges
+    kname = "k_" + wl.dominant
+    if wl.dominant == "edge_sweep" and quad and sess.query("ustaged"):
+        kname = "k_edge_sweep_us"
     sess.close()
     if world > 1:
         dist.destroy_process_group()
@@ -227,12 +232,12 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_" + wl.dominant,
+            "kernel": kname,
             "achieved": None if achieved is None else round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(wl.dominant, E),
+            "traffic": pmc_traffic(kname, E),
             "algorithmic_bytes_per_launch": int(alg),
             "launches": n_dom,
             "mean_ms": round(ms_dom, 5),

@@ -86,6 +86,7 @@ class QuadSession final : public SessionBase {
     int xcd_e_ = 0, xcd_v_ = 1;  // XCD-aware block order (edge / vertex sweep)
     int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
     bool rw_ = true;             // edge sweep recomputes the prox weights (prox_weights)
+    bool us_ = true;             // edge sweep stages the u ends of u-sorted edges
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
     // emap_[edge position] = original edge id (setup only)
@@ -189,6 +190,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         // 0.544 -> 0.525 ms, C2 0.465 -> 0.430 ms
         const char *r = getenv("PFDR_EDGE_RW");
         rw_ = !(r && r[0] == '0');
+        // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us)
+        const char *u = getenv("PFDR_USTAGE");
+        us_ = !(u && u[0] == '0');
     }
     // prox selection (ref l1 :499-512, bounds :472-490)
     positivity_ = 0;
@@ -400,8 +404,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
 // address.  Blocks that do not qualify keep the CSR gather.
 template <typename real>
 void QuadSession<real>::build_split() {
-    const char *sp = getenv("PFDR_SPLIT");  // A/B: PFDR_SPLIT=0 keeps the CSR gather everywhere
-    if ((sp && sp[0] == '0') || !E_) return;
+    if (!E_) return;
     hipStream_t s = stream;
     DevBuf<unsigned long long> bad(1);
     PFDR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
@@ -415,10 +418,14 @@ void QuadSession<real>::build_split() {
     const long ototal = inc_.n - E_;  // every local edge's u end is an owned row
     if (ototal < 0) return;
     uptr_.alloc((size_t)V_ + 1);
+    k_uptr<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, V_, Eu_.p, uptr_.p);
+    PFDR_HIP(hipGetLastError());
+    ustaged = (rw_ && us_) ? 1 : 0;
+    const char *sp = getenv("PFDR_SPLIT");  // A/B: PFDR_SPLIT=0 keeps the CSR gather everywhere
+    if (sp && sp[0] == '0') return;
     mask_.alloc(V_);
     oidx_.alloc(ototal ? ototal : 1);
     blkok_.alloc(nb);
-    k_uptr<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, V_, Eu_.p, uptr_.p);
     k_split_build<<<nb, kBlock, 0, s>>>(V_, E_, inc_.ptr.p, inc_.idx.p, uptr_.p, ototal, mask_.p,
                                         oidx_.p, blkok_.p, GatherCap<real>::v / 2);
     PFDR_HIP(hipGetLastError());
@@ -428,7 +435,8 @@ void QuadSession<real>::build_split() {
     long n = 0;
     for (int x : h) n += x;
     split_blocks = n;
-    if (!n) { uptr_.release(); mask_.release(); oidx_.release(); blkok_.release(); }
+    if (!n) { mask_.release(); oidx_.release(); blkok_.release(); }  // uptr_ serves the edge sweep
+    ustaged = (rw_ && us_) ? 1 : 0;
 }
 
 template <typename real>
@@ -639,7 +647,11 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     constexpr int EPT = Vec<real>::kPer16B;
     ProfScope ps(prof, name, s);
     const int nb = grid_for(eend - ebeg, EPT), g = xcd_grid(nb, xcd_e_);
-    if (rw_)
+    if (rw_ && us_ && uptr_.p)
+        k_edge_sweep_us<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, W2_.p,
+                                                   wz_.p, rho_, c, nb, xcd_e_, ebeg, eend, Ga_.p,
+                                                   La_d1_.p);
+    else if (rw_)
         k_edge_sweep<real, true><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, nullptr,
                                                       nullptr, nullptr, W2_.p, wz_.p, rho_, c, nb,
                                                       xcd_e_, ebeg, eend, Ga_.p, La_d1_.p);

@@ -805,6 +805,123 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     }
 }
 
+// Edge sweep of a graph whose edges are sorted by their u end (uptr: first
+// edge of each u, see k_uptr), prox weights recomputed (RW).  The u ends of
+// a block's edges are a short vertex range [ua, ub]: the block stages their
+// edge offsets, (X, P) pairs and metric in LDS with coalesced loads, so the
+// Eu stream (4 bytes per edge) is not read and only the v ends are
+// gathered; each lane finds the u end of its edges by a binary search of
+// the staged offsets.  A block whose u range exceeds the LDS cap reads Eu.
+template <typename real> struct USpan { static constexpr int v = 1024; };
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_edge_sweep_us(
+    long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+    const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
+    const real *__restrict__ W2, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
+    int nb, int xcd, long ebeg, long eend, const real *__restrict__ Ga,
+    const real *__restrict__ La_d1) {
+    if (ctrl && ctrl->halt) return;
+    constexpr int EPT = Vec<real>::kPer16B;
+    constexpr int CAP = USpan<real>::v;
+    __shared__ int s_ptr[CAP + 1];
+    __shared__ R2<real> s_xp[CAP];
+    __shared__ real s_ga[CAP];
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;  // whole block
+    const int tid = threadIdx.x;
+    const long eb = ebeg + (long)blk * kBlock * EPT;
+    const long el = min(eb + (long)kBlock * EPT, eend) - 1;  // block's last edge
+    const int ua = Eu[eb], ub = Eu[el];
+    const int span = ub - ua + 1;
+    const bool staged = span <= CAP;  // block-uniform
+    const long e0 = eb + (long)tid * EPT;
+    const bool full = e0 + EPT <= eend;
+    // streams first: their latency hides under the staging
+    Pk<int, EPT> iv{};
+    Pk<real, 2 * EPT> z{}, w{};
+    Pk<real, EPT> la{};
+    R2<real> pu[EPT], pv[EPT];
+    real gu[EPT], gv[EPT];
+    if (full) {
+        iv = ldv<int, EPT>(Ev + e0);
+        z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
+        w = ldv<real, 2 * EPT>(W2 + 2 * e0);
+        la = ldv<real, EPT>(La_d1 + e0);
+        // v-end gathers before the staging: the two round trips overlap
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            pv[j] = xp[iv.v[j]];
+            gv[j] = Ga[iv.v[j]];
+        }
+    }
+    if (staged) {
+        for (int i = tid; i <= span; i += kBlock) s_ptr[i] = uptr[ua + i];
+        for (int i = tid; i < span; i += kBlock) {
+            s_xp[i] = xp[ua + i];
+            s_ga[i] = Ga[ua + i];
+        }
+    }
+    __syncthreads();
+    if (e0 >= eend) return;
+    if (full) {
+        int ku[EPT];
+        if (staged) {
+            int lo = 0, hi = span - 1;  // largest k with s_ptr[k] <= e0
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((long)s_ptr[mid] <= e0) lo = mid;
+                else hi = mid - 1;
+            }
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                while (lo + 1 < span && (long)s_ptr[lo + 1] <= e0 + j) lo++;
+                ku[j] = lo;
+            }
+        } else {
+            const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
+#pragma unroll
+            for (int j = 0; j < EPT; j++) ku[j] = iu.v[j];
+        }
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            if (staged) { pu[j] = s_xp[ku[j]]; gu[j] = s_ga[ku[j]]; }
+            else { pu[j] = xp[ku[j]]; gu[j] = Ga[ku[j]]; }
+        }
+        Pk<real, EPT> a, b, t;
+#pragma unroll
+        for (int j = 0; j < EPT; j++)
+            prox_weights<real>(w.v[2 * j], w.v[2 * j + 1], gu[j], gv[j], la.v[j], a.v[j], b.v[j],
+                               t.v[j]);
+#pragma unroll
+        for (int j = 0; j < EPT; j++)
+            edge_update<real>(pu[j], pv[j], z.v[2 * j], z.v[2 * j + 1], a.v[j], b.v[j], t.v[j],
+                              rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
+        Pk<real, EPT> ou, ov;
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            ou.v[j] = w.v[2 * j] * z.v[2 * j];
+            ov.v[j] = w.v[2 * j + 1] * z.v[2 * j + 1];
+        }
+        stv<real, EPT>(wz + e0, ou);
+        stv<real, EPT>(wz + E + e0, ov);
+    } else {
+        for (long e = e0; e < eend; e++) {
+            const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1];
+            real du, dv, th;
+            prox_weights<real>(W2[2 * e], W2[2 * e + 1], Ga[Eu[e]], Ga[Ev[e]], La_d1[e], du, dv,
+                               th);
+            edge_update<real>(pu, pv, zu, zv, du, dv, th, rho);
+            Z2[2 * e] = zu;
+            Z2[2 * e + 1] = zv;
+            wz[e] = W2[2 * e] * zu;
+            wz[E + e] = W2[2 * e + 1] * zv;
+        }
+    }
+}
+
 template <typename real>
 struct VArgs {
     int V;

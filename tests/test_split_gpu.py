@@ -1,5 +1,5 @@
 """GPU: the split incidence of the vertex sweep (csrc/pfdr_quadratic_kernels.hpp
-split_sum).  When the edges are sorted by their u end, each vertex's u-end
+split_sum) and the u-staged edge sweep (k_edge_sweep_us).  When the edges are sorted by their u end, each vertex's u-end
 contributions are a contiguous run and only the other entries are gathered;
 a per-vertex mask keeps the reference's (e, side) summation order.  The
 split and the plain CSR gather must give the same iterates bit for bit, and
@@ -15,18 +15,25 @@ from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, unifo
 pytestmark = pytest.mark.gpu
 
 
+KNOBS = ("PFDR_SPLIT", "PFDR_USTAGE")
+
+
 def _solve(split, V, Eu, Ev, Y, dt, it, reorder=pfdr.REORDER_OFF, **kw):
-    old = os.environ.get("PFDR_SPLIT")
-    os.environ["PFDR_SPLIT"] = "1" if split else "0"
+    """split: True = split vertex sweep and u-staged edge sweep (defaults),
+    False = CSR gather and Eu stream everywhere."""
+    old = {k: os.environ.get(k) for k in KNOBS}
+    for k in KNOBS:
+        os.environ[k] = "1" if split else "0"
     try:
         s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
                          np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3,
                          itMax=it, reorder=reorder, **kw)
     finally:
-        if old is None:
-            del os.environ["PFDR_SPLIT"]
-        else:
-            os.environ["PFDR_SPLIT"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     nsplit = s.query("split_blocks")
     s.run(it)
     X, its, _, Dif = s.result()
@@ -67,8 +74,9 @@ def test_split_mixed_blocks_with_hubs(gpu_lib, oracle_port, dt):
     extra_v[extra_v == extra_u] += 1
     Eu = np.concatenate([Eu0.astype(np.int64), extra_u])
     Ev = np.concatenate([Ev0.astype(np.int64), extra_v % V])
-    # drop the out-edges of a band of vertices (zero out-degree runs)
-    keep = ~((Eu >= 5000) & (Eu < 5400))
+    # drop the out-edges of a band of vertices (a zero out-degree run longer
+    # than the edge sweep's staged u span: those blocks read Eu)
+    keep = ~((Eu >= 5000) & (Eu < 6500))
     Eu, Ev = Eu[keep], Ev[keep]
     order = np.argsort(Eu, kind="stable")
     Eu, Ev = Eu[order].astype(np.int32), Ev[order].astype(np.int32)
