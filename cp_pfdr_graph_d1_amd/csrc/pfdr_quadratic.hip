@@ -85,7 +85,6 @@ class QuadSession final : public SessionBase {
     bool rec_obj_, rec_dif_, track_;
     int xcd_e_ = 0, xcd_v_ = 1;  // XCD-aware block order (edge / vertex sweep)
     int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
-    bool rw_ = true;             // edge sweep recomputes the prox weights (prox_weights)
     bool us_ = true;             // edge sweep stages the u ends of u-sorted edges
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
@@ -99,7 +98,12 @@ class QuadSession final : public SessionBase {
     DevBuf<real> La_d1_, La_l1_, Y_, A_, L_;
     DevBuf<R2<real>> xp_;
     DevBuf<real> diag_, Ga_, invAux_, Th_l1_, absval_, grad_, pre_, xout_;
-    DevBuf<real> Z2_, W2_, Wd1u_, Wd1v_, Th_, wz_;
+    DevBuf<real> Z2_, wz_;
+    // splitting weights as factors (k_d1_weights): a_e = cw_ La_d1[e] until the
+    // first reconditioning, then A1_[e]; (Ga, invAux) pairs of every vertex
+    DevBuf<real> A1_;
+    DevBuf<R2<real>> gi_;
+    real cw_ = real(0);
     DevBuf<real> R_, Rpart_, vpart_, opart_, Obj_, Dif_, red_, csum_;
     DevBuf<real> Rsum_, xfull_;  // dense A on a partition: summed A X, gathered X
     long v0_ = 0, Vglob_ = 0;
@@ -184,12 +188,6 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (xv && atoi(xv) >= 2) xcd_v_ = atoi(xv);
         const char *g = getenv("PFDR_GB");  // 8 (default) or 16
         if (g && atoi(g) == 16) gb_ = 16;
-        // prox weights recomputed in every edge sweep (default; PFDR_EDGE_RW=0
-        // streams the stored Wd1u, Wd1v, Th instead): 12 -> 4 streamed bytes
-        // per edge, 12 bytes of HBM per edge freed; headline edge sweep
-        // 0.544 -> 0.525 ms, C2 0.465 -> 0.430 ms
-        const char *r = getenv("PFDR_EDGE_RW");
-        rw_ = !(r && r[0] == '0');
         // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us)
         const char *u = getenv("PFDR_USTAGE");
         us_ = !(u && u[0] == '0');
@@ -258,8 +256,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
     // edge state and per-vertex metric
     const size_t En = E ? E : 1;
-    Z2_.alloc(2 * En); W2_.alloc(2 * En);
-    if (!rw_) { Wd1u_.alloc(En); Wd1v_.alloc(En); Th_.alloc(En); }
+    Z2_.alloc(2 * En);
+    gi_.alloc(Vg);
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
     if (flavour_ == 0 && p->La_l1) Th_l1_.alloc(V);
     nbv_ = grid_for(V);
@@ -322,16 +320,18 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
     if (rec_obj_) objective();  // Obj[0]
     PFDR_HIP(hipStreamSynchronize(s));
+    // c of the first conditioning: a_e = cw_ La_d1[e] in the edge sweeps
+    PFDR_HIP(hipMemcpy(&cw_, &ctrl_.p->c, sizeof(real), hipMemcpyDeviceToHost));
     stopped_ = (itMax_ <= 0);
 
     device_bytes = 0;
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
-                            &pre_, &Z2_, &W2_, &Wd1u_, &Wd1v_, &Th_, &wz_, &R_, &Rpart_,
+                            &pre_, &Z2_, &A1_, &wz_, &R_, &Rpart_,
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_})
         acc(b->n * sizeof(real));
-    acc(xp_.n * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
+    acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
     order_.release();  // inputs are in the internal labels now
     if (halo_) {
@@ -420,7 +420,7 @@ void QuadSession<real>::build_split() {
     uptr_.alloc((size_t)V_ + 1);
     k_uptr<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, V_, Eu_.p, uptr_.p);
     PFDR_HIP(hipGetLastError());
-    ustaged = (rw_ && us_) ? 1 : 0;
+    ustaged = us_ ? 1 : 0;
     const char *sp = getenv("PFDR_SPLIT");  // A/B: PFDR_SPLIT=0 keeps the CSR gather everywhere
     if (sp && sp[0] == '0') return;
     mask_.alloc(V_);
@@ -436,7 +436,7 @@ void QuadSession<real>::build_split() {
     for (int x : h) n += x;
     split_blocks = n;
     if (!n) { mask_.release(); oidx_.release(); blkok_.release(); }  // uptr_ serves the edge sweep
-    ustaged = (rw_ && us_) ? 1 : 0;
+    ustaged = us_ ? 1 : 0;
 }
 
 template <typename real>
@@ -581,10 +581,13 @@ void QuadSession<real>::precondition(bool init) {
         pull(xp_.p, sizeof(R2<real>));  // X at the ghosts
         pull(grad_.p, sizeof(real));
     }
+    const bool first_recond = !init && !A1_.p;
+    if (first_recond) A1_.alloc(E_ ? E_ : 1);  // a_e leave cw La_d1 for good
     if (E_) {
         k_d1_weights<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, La_d1_.p, ctrl_.p, init ? 1 : 0,
-                                                   condMin_, xp_.p, W2_.p, wz_.p, Ga_.p,
-                                                   grad_.p, Z2_.p);
+                                                   condMin_, xp_.p, first_recond ? nullptr : A1_.p,
+                                                   cw_, invAux_.p, A1_.p, wz_.p, Ga_.p, grad_.p,
+                                                   Z2_.p);
         PFDR_HIP(hipGetLastError());
     }
     if (halo_) halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), s);
@@ -595,11 +598,11 @@ void QuadSession<real>::precondition(bool init) {
     PFDR_HIP(hipGetLastError());
     pull(Ga_.p, sizeof(real));
     pull(invAux_.p, sizeof(real));
-    if (E_) {
-        k_precond_edge2<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, invAux_.p, Ga_.p, La_d1_.p,
-                                                      W2_.p, Wd1u_.p, Wd1v_.p, Th_.p,
-                                                      init ? 0 : 1, xp_.p, grad_.p, Z2_.p);
+    if (E_ && !init) {
+        k_recond_edge<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, A1_.p, invAux_.p, Ga_.p,
+                                                    xp_.p, grad_.p, Z2_.p);
     }
+    k_gi_pack<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, Ga_.p, invAux_.p, gi_.p);
     PFDR_HIP(hipGetLastError());
     if (!init) {
         // forward step with the new metric from the gradient taken before
@@ -647,18 +650,13 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     constexpr int EPT = Vec<real>::kPer16B;
     ProfScope ps(prof, name, s);
     const int nb = grid_for(eend - ebeg, EPT), g = xcd_grid(nb, xcd_e_);
-    if (rw_ && us_ && uptr_.p)
-        k_edge_sweep_us<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, W2_.p,
-                                                   wz_.p, rho_, c, nb, xcd_e_, ebeg, eend, Ga_.p,
-                                                   La_d1_.p);
-    else if (rw_)
-        k_edge_sweep<real, true><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, nullptr,
-                                                      nullptr, nullptr, W2_.p, wz_.p, rho_, c, nb,
-                                                      xcd_e_, ebeg, eend, Ga_.p, La_d1_.p);
+    if (us_ && uptr_.p)
+        k_edge_sweep_us<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p,
+                                                   cw_, gi_.p, La_d1_.p, wz_.p, rho_, c, nb,
+                                                   xcd_e_, ebeg, eend);
     else
-        k_edge_sweep<real, false><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, Wd1u_.p,
-                                                       Wd1v_.p, Th_.p, W2_.p, wz_.p, rho_, c, nb,
-                                                       xcd_e_, ebeg, eend, nullptr, nullptr);
+        k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
+                                                La_d1_.p, wz_.p, rho_, c, nb, xcd_e_, ebeg, eend);
 }
 
 template <typename real>

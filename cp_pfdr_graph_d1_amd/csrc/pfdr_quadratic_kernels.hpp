@@ -545,16 +545,32 @@ __global__ void k_set_c(const real *__restrict__ sum, const long long *__restric
     ctrl->cnt = (int)*cnt;
 }
 
-// d1 splitting weights (ref :156-192) into both half-edges W2[2e + side].
-// On reconditioning, first turn the auxiliary variables into subgradients
-// with the OLD weights and metric (ref :89-99).
+// Splitting weights.  The reference stores Wu[e] = a_e Aux[u]^-1 and
+// Wv[e] = a_e Aux[v]^-1 (ref :156-203), a_e = c La_d1[e] at the first
+// conditioning, La_d1[e] / d_e at a reconditioning.  This build keeps only
+// the factors: a_e is recomputed from La_d1 and the scalar c of the first
+// conditioning (cw), or read from A1 after a reconditioning; invAux per
+// vertex (with Ga in the packed gi pair).  Every product a_e * invAux is
+// the reference's own operation, so the weights are identical bit for bit.
+template <typename real>
+__device__ __forceinline__ real edge_a(long e, const real *__restrict__ A1,
+                                       const real *__restrict__ La_d1, real cw) {
+    return A1 ? A1[e] : cw * La_d1[e];
+}
+
+// d1 contributions a_e to the per-vertex sums (both ends through the CSR,
+// like the DR average; ref :156-192).  On reconditioning, first turn the
+// auxiliary variables into subgradients with the OLD weights and metric
+// (ref :89-99), then store the new a_e in A1 (A1old: null while the old
+// a_e are still cw La_d1).
 template <typename real>
 __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
                              const int *__restrict__ Ev,
                              const real *__restrict__ La_d1,
                              const Ctrl<real> *__restrict__ ctrl, int init,
                              real condMin, const R2<real> *__restrict__ xp,
-                             real *__restrict__ W2, real *__restrict__ wz,
+                             const real *A1old, real cw, const real *__restrict__ invAux,
+                             real *A1, real *__restrict__ wz,
                              const real *__restrict__ Ga,
                              const real *__restrict__ grad,
                              real *__restrict__ Z2) {
@@ -568,8 +584,10 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
         const int u = Eu[e], v = Ev[e];
         const real xu = xp[u].x, xv = xp[v].x;
         const real gu = Ga[u], gv = Ga[v];
-        Z2[2 * e] = (W2[2 * e] / gu) * (xu - gu * grad[u] - Z2[2 * e]);
-        Z2[2 * e + 1] = (W2[2 * e + 1] / gv) * (xv - gv * grad[v] - Z2[2 * e + 1]);
+        const real a0 = edge_a(e, A1old, La_d1, cw);
+        const real wu = a0 * invAux[u], wv = a0 * invAux[v];
+        Z2[2 * e] = (wu / gu) * (xu - gu * grad[u] - Z2[2 * e]);
+        Z2[2 * e + 1] = (wv / gv) * (xv - gv * grad[v] - Z2[2 * e + 1]);
         real a = xu, b = xv, d = a - b;
         if (a < real(0)) a = -a;
         if (b < real(0)) b = -b;
@@ -579,14 +597,12 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
         a *= condMin;
         if (d < a) d = a;
         w = La_d1[e] / d;
+        A1[e] = w;
     }
-    W2[2 * e] = w;
-    W2[2 * e + 1] = w;
     wz[e] = w;      // per-vertex sums go through the same CSR as the DR average
     wz[E + e] = w;
 }
 
-// metric of every vertex (ref :193-239 and :262-264)
 template <typename real>
 __global__ __launch_bounds__(256) void k_precond_vertex(
     int V, const int *__restrict__ ptr, const unsigned *__restrict__ idx,
@@ -629,44 +645,40 @@ __global__ __launch_bounds__(256) void k_precond_vertex(
     if (La_l1) Th_l1[v] = g * La_l1[v];
 }
 
-// normalised splitting weights, prox weights and thresholds
-// (ref :196-203, :241-261)
+// reconditioning: auxiliary variables back from subgradients with the new
+// weights and metric (ref :241-250)
 template <typename real>
-__global__ void k_precond_edge2(long E, const int *__restrict__ Eu,
-                                const int *__restrict__ Ev,
-                                const real *__restrict__ invAux,
-                                const real *__restrict__ Ga,
-                                const real *__restrict__ La_d1,
-                                real *__restrict__ W2,
-                                real *__restrict__ Wd1u,
-                                real *__restrict__ Wd1v,
-                                real *__restrict__ Th, int recond,
-                                const R2<real> *__restrict__ xp,
-                                const real *__restrict__ grad,
-                                real *__restrict__ Z2) {
+__global__ void k_recond_edge(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                              const real *__restrict__ A1, const real *__restrict__ invAux,
+                              const real *__restrict__ Ga, const R2<real> *__restrict__ xp,
+                              const real *__restrict__ grad, real *__restrict__ Z2) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const int u = Eu[e], v = Ev[e];
-    const real wu = W2[2 * e] * invAux[u];
-    const real wv = W2[2 * e + 1] * invAux[v];
-    W2[2 * e] = wu;
-    W2[2 * e + 1] = wv;
+    const real wu = A1[e] * invAux[u];
+    const real wv = A1[e] * invAux[v];
     const real gu = Ga[u], gv = Ga[v];
-    if (recond) {
-        Z2[2 * e] = xp[u].x - gu * (grad[u] + Z2[2 * e] / wu);
-        Z2[2 * e + 1] = xp[v].x - gv * (grad[v] + Z2[2 * e + 1] / wv);
-    }
-    if (!Th) return;  // prox weights recomputed by the edge sweep (prox_weights)
-    const real a = wu / gu, b = wv / gv, s = a + b;
-    Th[e] = La_d1[e] * s / (a * b);
-    Wd1u[e] = a / s;
-    Wd1v[e] = b / s;
+    Z2[2 * e] = xp[u].x - gu * (grad[u] + Z2[2 * e] / wu);
+    Z2[2 * e + 1] = xp[v].x - gv * (grad[v] + Z2[2 * e + 1] / wv);
+}
+
+// (Ga, invAux) pairs of owned and ghost vertices: one 8/16-byte gather per
+// edge end in the edge sweeps
+template <typename real>
+__global__ void k_gi_pack(int n, const real *__restrict__ Ga, const real *__restrict__ invAux,
+                          R2<real> *__restrict__ gi) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    R2<real> q;
+    q.x = Ga[v];
+    q.y = invAux[v];
+    gi[v] = q;
 }
 
 // the prox weights and threshold of an edge from its splitting weights,
-// the metric of its ends and its TV weight — the operations of
-// k_precond_edge2 (ref :252-259), so recomputing them in every edge sweep
-// gives the stored values bit for bit
+// the metric of its ends and its TV weight — the operations of the
+// reference's precomputation (ref :252-259), recomputed in every edge sweep
+// (bit for bit the values the reference stores in W_d1u, W_d1v, Th_d1)
 template <typename real>
 __device__ __forceinline__ void prox_weights(real wu, real wv, real gu, real gv, real la,
                                              real &du, real &dv, real &th) {
@@ -726,19 +738,33 @@ __device__ __forceinline__ void edge_update(const R2<real> &pu,
     }
 }
 
+// one edge: splitting weights from a_e and the ends' invAux, prox weights
+// from them and the ends' metric, TV prox + relaxed Z update, the two DR
+// contributions W*Z
+template <typename real>
+__device__ __forceinline__ void edge_full(const R2<real> &pu, const R2<real> &pv,
+                                          const R2<real> &giu, const R2<real> &giv, real a,
+                                          real la, real &zu, real &zv, real &ou, real &ov,
+                                          real rho) {
+    const real wu = a * giu.y, wv = a * giv.y;
+    real du, dv, th;
+    prox_weights<real>(wu, wv, giu.x, giv.x, la, du, dv, th);
+    edge_update<real>(pu, pv, zu, zv, du, dv, th, rho);
+    ou = wu * zu;
+    ov = wv * zv;
+}
+
 // Edge sweep over the edges [ebeg, eend) (ebeg a multiple of the lane
 // width); writes the DR contributions W*Z side-major: wz[e] (u end),
-// wz[E + e] (v end), so the u-side run of a vertex is contiguous.
-// RW: the prox weights are recomputed from W2, the gathered metric and
-// La_d1 (prox_weights) instead of streamed: 4 instead of 12 bytes per edge.
-template <typename real, bool RW>
+// wz[E + e] (v end), so the u-side run of a vertex is contiguous.  Streams
+// per edge: Eu, Ev, Z (r/w), La_d1, the two contributions (+ A1 after a
+// reconditioning); gathers (X, P) and (Ga, invAux) of both ends.
+template <typename real>
 __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
-    const R2<real> *__restrict__ xp, real *__restrict__ Z2,
-    const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
-    const real *__restrict__ Th, const real *__restrict__ W2,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd,
-    long ebeg, long eend, const real *__restrict__ Ga, const real *__restrict__ La_d1) {
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
+    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
+    real rho, const Ctrl<real> *ctrl, int nb, int xcd, long ebeg, long eend) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     const int blk = xcd_block(blockIdx.x, nb, xcd);
@@ -748,85 +774,67 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     if (e0 + EPT <= eend) {
         const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
         const Pk<int, EPT> iv = ldv<int, EPT>(Ev + e0);
-        R2<real> pu[EPT], pv[EPT];
+        R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             pu[j] = xp[iu.v[j]]; pv[j] = xp[iv.v[j]];
+            gu[j] = gi[iu.v[j]]; gv[j] = gi[iv.v[j]];
         }
         Pk<real, 2 * EPT> z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        const Pk<real, 2 * EPT> w = ldv<real, 2 * EPT>(W2 + 2 * e0);
-        Pk<real, EPT> a, b, t;
-        if (RW) {
-            real gu[EPT], gv[EPT];
+        const Pk<real, EPT> la = ldv<real, EPT>(La_d1 + e0);
+        Pk<real, EPT> a;
+        if (A1) a = ldv<real, EPT>(A1 + e0);
+        else {
 #pragma unroll
-            for (int j = 0; j < EPT; j++) {
-                gu[j] = Ga[iu.v[j]]; gv[j] = Ga[iv.v[j]];
-            }
-            const Pk<real, EPT> la = ldv<real, EPT>(La_d1 + e0);
-#pragma unroll
-            for (int j = 0; j < EPT; j++)
-                prox_weights<real>(w.v[2 * j], w.v[2 * j + 1], gu[j], gv[j], la.v[j], a.v[j],
-                                   b.v[j], t.v[j]);
-        } else {
-            a = ldv<real, EPT>(Wd1u + e0);
-            b = ldv<real, EPT>(Wd1v + e0);
-            t = ldv<real, EPT>(Th + e0);
+            for (int j = 0; j < EPT; j++) a.v[j] = cw * la.v[j];
         }
-#pragma unroll
-        for (int j = 0; j < EPT; j++)
-            edge_update<real>(pu[j], pv[j], z.v[2 * j], z.v[2 * j + 1], a.v[j], b.v[j],
-                              t.v[j], rho);
-        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
         Pk<real, EPT> ou, ov;
 #pragma unroll
-        for (int j = 0; j < EPT; j++) {
-            ou.v[j] = w.v[2 * j] * z.v[2 * j];
-            ov.v[j] = w.v[2 * j + 1] * z.v[2 * j + 1];
-        }
+        for (int j = 0; j < EPT; j++)
+            edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
+                            z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
         stv<real, EPT>(wz + e0, ou);
         stv<real, EPT>(wz + E + e0, ov);
     } else {
         for (long e = e0; e < eend; e++) {
-            const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
-            real zu = Z2[2 * e], zv = Z2[2 * e + 1];
-            real du, dv, th;
-            if (RW) {
-                prox_weights<real>(W2[2 * e], W2[2 * e + 1], Ga[Eu[e]], Ga[Ev[e]], La_d1[e], du,
-                                   dv, th);
-            } else {
-                du = Wd1u[e]; dv = Wd1v[e]; th = Th[e];
-            }
-            edge_update<real>(pu, pv, zu, zv, du, dv, th, rho);
+            const int u = Eu[e], v = Ev[e];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            edge_full<real>(xp[u], xp[v], gi[u], gi[v], edge_a(e, A1, La_d1, cw), La_d1[e], zu,
+                            zv, ou, ov, rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
-            wz[e] = W2[2 * e] * zu;
-            wz[E + e] = W2[2 * e + 1] * zv;
+            wz[e] = ou;
+            wz[E + e] = ov;
         }
     }
 }
 
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
-// edge of each u, see k_uptr), prox weights recomputed (RW).  The u ends of
-// a block's edges are a short vertex range [ua, ub]: the block stages their
-// edge offsets, (X, P) pairs and metric in LDS with coalesced loads, so the
-// Eu stream (4 bytes per edge) is not read and only the v ends are
-// gathered; each lane finds the u end of its edges by a binary search of
-// the staged offsets.  A block whose u range exceeds the LDS cap reads Eu.
+// edge of each u, see k_uptr).  The u ends of a block's edges are a short
+// vertex range [ua, ub]: the block stages their edge offsets, (X, P) and
+// (Ga, invAux) pairs in LDS with coalesced loads, so the Eu stream is not
+// read and only the v ends are gathered (issued before the staging, so
+// the two round trips overlap); each lane finds the u end of its edges by
+// a binary search of the staged offsets.  A block whose u range exceeds
+// the LDS cap reads Eu.
 template <typename real> struct USpan { static constexpr int v = 1024; };
-
+// Occupancy: 86 VGPRs (f32) = 5 waves/SIMD.  Forcing 6 (80 VGPRs) or 7 (68)
+// waves was slower on the headline (0.442 -> 0.450 / 0.462 ms): more loads
+// in flight per SIMD only adds cache pressure here.
 template <typename real>
 __global__ __launch_bounds__(256) void k_edge_sweep_us(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
-    const real *__restrict__ W2, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
-    int nb, int xcd, long ebeg, long eend, const real *__restrict__ Ga,
-    const real *__restrict__ La_d1) {
+    const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
+    const real *__restrict__ La_d1, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
+    int nb, int xcd, long ebeg, long eend) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int CAP = USpan<real>::v;
     __shared__ int s_ptr[CAP + 1];
     __shared__ R2<real> s_xp[CAP];
-    __shared__ real s_ga[CAP];
+    __shared__ R2<real> s_gi[CAP];
     const int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
     const int tid = threadIdx.x;
@@ -837,35 +845,32 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     const bool staged = span <= CAP;  // block-uniform
     const long e0 = eb + (long)tid * EPT;
     const bool full = e0 + EPT <= eend;
-    // streams first: their latency hides under the staging
+    // streams and v-end gathers first: their latency hides under the staging
     Pk<int, EPT> iv{};
-    Pk<real, 2 * EPT> z{}, w{};
-    Pk<real, EPT> la{};
-    R2<real> pu[EPT], pv[EPT];
-    real gu[EPT], gv[EPT];
+    Pk<real, 2 * EPT> z{};
+    Pk<real, EPT> la{}, a{};
+    R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
     if (full) {
         iv = ldv<int, EPT>(Ev + e0);
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        w = ldv<real, 2 * EPT>(W2 + 2 * e0);
         la = ldv<real, EPT>(La_d1 + e0);
-        // v-end gathers before the staging: the two round trips overlap
+        if (A1) a = ldv<real, EPT>(A1 + e0);
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             pv[j] = xp[iv.v[j]];
-            gv[j] = Ga[iv.v[j]];
+            gv[j] = gi[iv.v[j]];
         }
     }
     if (staged) {
         for (int i = tid; i <= span; i += kBlock) s_ptr[i] = uptr[ua + i];
         for (int i = tid; i < span; i += kBlock) {
             s_xp[i] = xp[ua + i];
-            s_ga[i] = Ga[ua + i];
+            s_gi[i] = gi[ua + i];
         }
     }
     __syncthreads();
     if (e0 >= eend) return;
     if (full) {
-        int ku[EPT];
         if (staged) {
             int lo = 0, hi = span - 1;  // largest k with s_ptr[k] <= e0
             while (lo < hi) {
@@ -876,48 +881,39 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
 #pragma unroll
             for (int j = 0; j < EPT; j++) {
                 while (lo + 1 < span && (long)s_ptr[lo + 1] <= e0 + j) lo++;
-                ku[j] = lo;
+                pu[j] = s_xp[lo];
+                gu[j] = s_gi[lo];
             }
         } else {
             const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
 #pragma unroll
-            for (int j = 0; j < EPT; j++) ku[j] = iu.v[j];
+            for (int j = 0; j < EPT; j++) {
+                pu[j] = xp[iu.v[j]];
+                gu[j] = gi[iu.v[j]];
+            }
         }
+        if (!A1) {
 #pragma unroll
-        for (int j = 0; j < EPT; j++) {
-            if (staged) { pu[j] = s_xp[ku[j]]; gu[j] = s_ga[ku[j]]; }
-            else { pu[j] = xp[ku[j]]; gu[j] = Ga[ku[j]]; }
+            for (int j = 0; j < EPT; j++) a.v[j] = cw * la.v[j];
         }
-        Pk<real, EPT> a, b, t;
-#pragma unroll
-        for (int j = 0; j < EPT; j++)
-            prox_weights<real>(w.v[2 * j], w.v[2 * j + 1], gu[j], gv[j], la.v[j], a.v[j], b.v[j],
-                               t.v[j]);
-#pragma unroll
-        for (int j = 0; j < EPT; j++)
-            edge_update<real>(pu[j], pv[j], z.v[2 * j], z.v[2 * j + 1], a.v[j], b.v[j], t.v[j],
-                              rho);
-        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
         Pk<real, EPT> ou, ov;
 #pragma unroll
-        for (int j = 0; j < EPT; j++) {
-            ou.v[j] = w.v[2 * j] * z.v[2 * j];
-            ov.v[j] = w.v[2 * j + 1] * z.v[2 * j + 1];
-        }
+        for (int j = 0; j < EPT; j++)
+            edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
+                            z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
         stv<real, EPT>(wz + e0, ou);
         stv<real, EPT>(wz + E + e0, ov);
     } else {
         for (long e = e0; e < eend; e++) {
-            const R2<real> pu = xp[Eu[e]], pv = xp[Ev[e]];
-            real zu = Z2[2 * e], zv = Z2[2 * e + 1];
-            real du, dv, th;
-            prox_weights<real>(W2[2 * e], W2[2 * e + 1], Ga[Eu[e]], Ga[Ev[e]], La_d1[e], du, dv,
-                               th);
-            edge_update<real>(pu, pv, zu, zv, du, dv, th, rho);
+            const int u = Eu[e], v = Ev[e];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            edge_full<real>(xp[u], xp[v], gi[u], gi[v], edge_a(e, A1, La_d1, cw), La_d1[e], zu,
+                            zv, ou, ov, rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
-            wz[e] = W2[2 * e] * zu;
-            wz[E + e] = W2[2 * e + 1] * zv;
+            wz[e] = ou;
+            wz[E + e] = ov;
         }
     }
 }

@@ -92,7 +92,8 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise PFDRError("%s is missing: build it with "
                             "`make -C cp_pfdr_graph_d1_amd/csrc`" % LIB_PATH)
-        lib = C.CDLL(LIB_PATH)
+        # PFDR_LIB_PATH: A/B of compile-time variants of the same library
+        lib = C.CDLL(os.environ.get("PFDR_LIB_PATH") or LIB_PATH)
         lib.pfdr_last_error.restype = C.c_char_p
         lib.pfdr_session_device_x.restype = C.c_void_p
         lib.pfdr_session_device_bytes.restype = C.c_int64
