@@ -157,6 +157,13 @@ __device__ __forceinline__ int xcd_block(int b, int nb, int mode) {
     const int r = b >> 3;
     return ((r / mode) * 8 + (b & 7)) * mode + r % mode;
 }
+// chunked mode C of a launch of nb blocks: halved until every XCD gets at
+// least 4 runs (small launches must still spread over all 8 XCDs)
+inline int xcd_fit(int nb, int mode) {
+    if (mode < 2) return mode;
+    while (mode >= 2 && nb < 32 * mode) mode >>= 1;
+    return mode >= 2 ? mode : 0;
+}
 inline int xcd_grid(int nb, int mode) {
     const int q = mode <= 1 ? 8 : 8 * mode;
     return mode ? (nb + q - 1) / q * q : nb;

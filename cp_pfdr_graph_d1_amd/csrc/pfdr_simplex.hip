@@ -859,7 +859,9 @@ class SimplexSession final : public SessionBase {
     // nor writes contributions: 28 instead of 44 streamed bytes per (e, k)
     // (C4: 2.42 -> 2.17 ms/iteration)
     bool sx_wz_ = false;
-    int sx_xcd_e_ = 1, sx_xcd_v_ = 0;  // XCD-aware block order (PFDR_SX_XCD=<edge><vertex>; C4: edge on -2%)
+    // XCD-aware block order (PFDR_SX_XCD=<edge><vertex>, PFDR_SX_XCD_CHUNK[_V]):
+    // runs of 64 edge blocks per XCD (C4 edge sweep 1.275 -> 1.244 ms, r1zm)
+    int sx_xcd_e_ = 64, sx_xcd_v_ = 0;
     int it_ = 0;
     bool stopped_ = false;
     int chunk_ = 32;
@@ -949,6 +951,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         sx_nt_ = (nt && atoi(nt) == 64) ? 64 : 256;
         const char *xc = getenv("PFDR_SX_XCD");
         if (xc && strlen(xc) == 2) { sx_xcd_e_ = xc[0] == '1'; sx_xcd_v_ = xc[1] == '1'; }
+        const char *xe = getenv("PFDR_SX_XCD_CHUNK");  // runs of C blocks per XCD (edge sweep)
+        if (xe && atoi(xe) >= 2) sx_xcd_e_ = atoi(xe);
+        const char *xv = getenv("PFDR_SX_XCD_CHUNK_V");  // idem, vertex sweep
+        if (xv && atoi(xv) >= 2) sx_xcd_v_ = atoi(xv);
         const char *wz = getenv("PFDR_SX_WZ");  // 1: edge sweep stores W*Z (A/B)
         sx_wz_ = wz && wz[0] == '1';
         vb_ = sx_nt_ / K_;
@@ -1053,11 +1059,12 @@ void SimplexSession<real>::body() {
     if (EK_) {
         ProfScope ps(prof, "sx_edge_sweep", s);
         const int nb = grid_for(EK_);
-        k_sx_edge_sweep<real><<<xcd_grid(nb, sx_xcd_e_), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+        const int xm = xcd_fit(nb, sx_xcd_e_);
+        k_sx_edge_sweep<real><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
                                                                Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
                                                                Wu_.p, Wv_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
-                                                               rho_, c, nb, sx_xcd_e_);
+                                                               rho_, c, nb, xm);
     }
     if (halo_) {
         ProfScope ps(prof, "halo_push", s);
@@ -1070,8 +1077,8 @@ void SimplexSession<real>::body() {
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.Wu = Wu_.p; a.Wv = Wv_.p;
-        a.nb = nbs_; a.xcd = sx_xcd_v_;
-        const int g = xcd_grid(nbs_, sx_xcd_v_);
+        a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
+        const int g = xcd_grid(nbs_, a.xcd);
         if (sx_nt_ == 256) {
             if (sx_wz_) k_sx_vertex_sweep<real, 256, true><<<g, 256, 0, s>>>(a);
             else k_sx_vertex_sweep<real, 256, false><<<g, 256, 0, s>>>(a);
