@@ -38,6 +38,30 @@ struct SxConst {
     real alK, al1, alKal1;
 };
 
+template <typename real> using SxR2 = typename Vec<real>::v2;
+
+// Splitting weights as factors (ref :199-239): Wu[e*K+k] = a * Aux[u]^-1,
+// a = La_d1[e] at the first conditioning, La_d1[e] / d at a
+// reconditioning.  Only a (A1, one real per (e, k), after a
+// reconditioning) and the per-(v, k) (Ga, 1/Aux) pairs (GI, Ga before its
+// normalisation by the vertex maximum, ref :360-369) are kept; every
+// product a * invAux is the reference's own operation.
+template <typename real>
+__device__ __forceinline__ real sx_a(long i, long e, const real *__restrict__ A1,
+                                     const real *__restrict__ La_d1) {
+    return A1 ? A1[i] : La_d1[e];
+}
+
+// prox weights and threshold (ref :287-306), operation for operation
+template <typename real>
+__device__ __forceinline__ void sx_prox_weights(real wu, real wv, real gu, real gv, real la,
+                                                real &du, real &dv, real &th) {
+    const real a = wu / gu, b = wv / gv, s = a + b;
+    th = la * s / (a * b);
+    du = a / s;
+    dv = b / s;
+}
+
 // ------------------------------------------------ metric projection ----
 // Projection of x (D values, stride 1) onto {x >= 0, sum x = a} in the
 // metric diag(1/m): active-set sweep of ref src/proj_simplex_metric.cpp:41-80,
@@ -144,6 +168,7 @@ __global__ void k_sx_recover(int V, SxConst<real> c, const real *__restrict__ La
 }
 
 // reconditioning, step 2: auxiliary variables -> subgradients (ref :136-156)
+// with the OLD weights a * invAux (A1old null: a = La_d1)
 template <typename real>
 __global__ void k_sx_subgrad(long EK, SxConst<real> c, const int *__restrict__ Eu,
                              const int *__restrict__ Ev,
@@ -151,8 +176,9 @@ __global__ void k_sx_subgrad(long EK, SxConst<real> c, const int *__restrict__ E
                              const real *__restrict__ Q,
                              const real *__restrict__ Ga,
                              const real *__restrict__ GaQ,
-                             const real *__restrict__ Wu,
-                             const real *__restrict__ Wv,
+                             const real *__restrict__ A1old,
+                             const real *__restrict__ La_d1,
+                             const real *__restrict__ invAux,
                              real *__restrict__ Zu, real *__restrict__ Zv) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= EK) return;
@@ -160,15 +186,17 @@ __global__ void k_sx_subgrad(long EK, SxConst<real> c, const int *__restrict__ E
     const long e = i / K;
     const int k = (int)(i - e * K);
     const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    const real a0 = sx_a(i, e, A1old, La_d1);
+    const real wu = a0 * invAux[u], wv = a0 * invAux[v];
     if (c.loss == LOSS_LINEAR) {
-        Zu[i] = (Wu[i] / Ga[u]) * (P[u] + GaQ[u] - Zu[i]);
-        Zv[i] = (Wv[i] / Ga[v]) * (P[v] + GaQ[v] - Zv[i]);
+        Zu[i] = (wu / Ga[u]) * (P[u] + GaQ[u] - Zu[i]);
+        Zv[i] = (wv / Ga[v]) * (P[v] + GaQ[v] - Zv[i]);
     } else if (c.loss == LOSS_QUAD) {
-        Zu[i] = (Wu[i] / Ga[u]) * (P[u] - GaQ[u] * (P[u] - Q[u]) - Zu[i]);
-        Zv[i] = (Wv[i] / Ga[v]) * (P[v] - GaQ[v] * (P[v] - Q[v]) - Zv[i]);
+        Zu[i] = (wu / Ga[u]) * (P[u] - GaQ[u] * (P[u] - Q[u]) - Zu[i]);
+        Zv[i] = (wv / Ga[v]) * (P[v] - GaQ[v] * (P[v] - Q[v]) - Zv[i]);
     } else {
-        Zu[i] = (Wu[i] / Ga[u]) * (P[u] + GaQ[u] / (c.alKal1 + P[u]) - Zu[i]);
-        Zv[i] = (Wv[i] / Ga[v]) * (P[v] + GaQ[v] / (c.alKal1 + P[v]) - Zv[i]);
+        Zu[i] = (wu / Ga[u]) * (P[u] + GaQ[u] / (c.alKal1 + P[u]) - Zu[i]);
+        Zv[i] = (wv / Ga[v]) * (P[v] + GaQ[v] / (c.alKal1 + P[v]) - Zv[i]);
     }
 }
 
@@ -191,14 +219,14 @@ __global__ void k_sx_hessian(long VK, SxConst<real> c, const real *__restrict__ 
     }
 }
 
-// d1 splitting weights (ref :192-221) into W and both contribution slots
+// d1 splitting weights a (ref :192-221) into both contribution slots (the
+// per-(v, k) sums run through the CSR); on reconditioning also into A1
 template <typename real>
 __global__ void k_sx_d1_weights(long EK, int K, const int *__restrict__ Eu,
                                 const int *__restrict__ Ev,
                                 const real *__restrict__ La_d1, int init,
                                 real condMin, const real *__restrict__ P,
-                                real *__restrict__ Wu, real *__restrict__ Wv,
-                                real *__restrict__ wz) {
+                                real *__restrict__ A1, real *__restrict__ wz) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= EK) return;
     const long e = i / K;
@@ -211,9 +239,8 @@ __global__ void k_sx_d1_weights(long EK, int K, const int *__restrict__ Eu,
         if (a < real(0)) a = -a;
         if (a < condMin) a = condMin;
         w = La_d1[e] / a;
+        A1[i] = w;
     }
-    Wu[i] = w;
-    Wv[i] = w;
     wz[i] = w;
     wz[EK + i] = w;
 }
@@ -287,51 +314,65 @@ __global__ void k_sx_precond_vertex(long VK, SxConst<real> c,
     }
 }
 
-// normalised splitting weights, prox weights/thresholds (ref :230-241,
-// :287-306) and, on reconditioning, subgradients -> auxiliary (:337-358)
+// reconditioning: subgradients -> auxiliary variables with the new weights
+// (ref :337-358)
 template <typename real>
-__global__ void k_sx_precond_edge(long EK, SxConst<real> c,
-                                  const int *__restrict__ Eu,
-                                  const int *__restrict__ Ev,
-                                  const real *__restrict__ La_d1,
-                                  const real *__restrict__ invAux,
-                                  const real *__restrict__ Ga,
-                                  const real *__restrict__ GaQ,
-                                  const real *__restrict__ P,
-                                  const real *__restrict__ Q,
-                                  real *__restrict__ Wu, real *__restrict__ Wv,
-                                  real *__restrict__ Wd1u,
-                                  real *__restrict__ Wd1v,
-                                  real *__restrict__ Th, int recond,
-                                  real *__restrict__ Zu, real *__restrict__ Zv) {
+__global__ void k_sx_recond_edge(long EK, SxConst<real> c, const int *__restrict__ Eu,
+                                 const int *__restrict__ Ev, const real *__restrict__ A1,
+                                 const real *__restrict__ invAux,
+                                 const real *__restrict__ Ga,
+                                 const real *__restrict__ GaQ,
+                                 const real *__restrict__ P,
+                                 const real *__restrict__ Q,
+                                 real *__restrict__ Zu, real *__restrict__ Zv) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= EK) return;
     const int K = c.K;
     const long e = i / K;
     const int k = (int)(i - e * K);
     const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
-    const real wu = Wu[i] * invAux[u];
-    const real wv = Wv[i] * invAux[v];
-    Wu[i] = wu;
-    Wv[i] = wv;
-    if (c.loss != LOSS_LINEAR) {
-        const real a = wu / Ga[u], b = wv / Ga[v], s = a + b;
-        Th[i] = La_d1[e] * s / (a * b);
-        Wd1u[i] = a / s;
-        Wd1v[i] = b / s;
+    const real wu = A1[i] * invAux[u];
+    const real wv = A1[i] * invAux[v];
+    if (c.loss == LOSS_LINEAR) {
+        Zu[i] = P[u] + GaQ[u] - (Ga[u] / wu) * Zu[i];
+        Zv[i] = P[v] + GaQ[v] - (Ga[v] / wv) * Zv[i];
+    } else if (c.loss == LOSS_QUAD) {
+        Zu[i] = P[u] - GaQ[u] * (P[u] - Q[u] + Zu[i] / wu);
+        Zv[i] = P[v] - GaQ[v] * (P[v] - Q[v] + Zv[i] / wv);
+    } else {
+        Zu[i] = P[u] + GaQ[u] / (c.alKal1 + P[u]) - (Ga[u] / wu) * Zu[i];
+        Zv[i] = P[v] + GaQ[v] / (c.alKal1 + P[v]) - (Ga[v] / wv) * Zv[i];
     }
-    if (recond) {
-        if (c.loss == LOSS_LINEAR) {
-            Zu[i] = P[u] + GaQ[u] - (Ga[u] / wu) * Zu[i];
-            Zv[i] = P[v] + GaQ[v] - (Ga[v] / wv) * Zv[i];
-        } else if (c.loss == LOSS_QUAD) {
-            Zu[i] = P[u] - GaQ[u] * (P[u] - Q[u] + Zu[i] / wu);
-            Zv[i] = P[v] - GaQ[v] * (P[v] - Q[v] + Zv[i] / wv);
-        } else {
-            Zu[i] = P[u] + GaQ[u] / (c.alKal1 + P[u]) - (Ga[u] / wu) * Zu[i];
-            Zv[i] = P[v] + GaQ[v] / (c.alKal1 + P[v]) - (Ga[v] / wv) * Zv[i];
-        }
-    }
+}
+
+// stored prox weights and thresholds (ref :287-306) from the factored
+// splitting weights
+template <typename real>
+__global__ void k_sx_prox_store(long EK, int K, const int *__restrict__ Eu,
+                                const int *__restrict__ Ev, const real *__restrict__ A1,
+                                const real *__restrict__ La_d1,
+                                const SxR2<real> *__restrict__ GI, real *__restrict__ Wd1u,
+                                real *__restrict__ Wd1v, real *__restrict__ Th) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= EK) return;
+    const long e = i / K;
+    const int k = (int)(i - e * K);
+    const SxR2<real> gu = GI[(long)Eu[e] * K + k], gv = GI[(long)Ev[e] * K + k];
+    const real la = La_d1[e], a = sx_a(i, e, A1, La_d1);
+    sx_prox_weights<real>(a * gu.y, a * gv.y, gu.x, gv.x, la, Wd1u[i], Wd1v[i], Th[i]);
+}
+
+// (Ga, invAux) pairs of every (v, k), owned and ghost, before the metric
+// is normalised
+template <typename real>
+__global__ void k_sx_gi_pack(long n, const real *__restrict__ Ga, const real *__restrict__ invAux,
+                             SxR2<real> *__restrict__ GI) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SxR2<real> q;
+    q.x = Ga[i];
+    q.y = invAux[i];
+    GI[i] = q;
 }
 
 // normalise the metric of each vertex by its maximum (ref :360-369)
@@ -386,9 +427,9 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     long EK, SxConst<real> c, const int *__restrict__ Eu,
     const int *__restrict__ Ev, const real *__restrict__ FP,
     const real *__restrict__ P, real *__restrict__ Zu, real *__restrict__ Zv,
-    const real *__restrict__ Wd1u, const real *__restrict__ Wd1v,
-    const real *__restrict__ Th, const real *__restrict__ Wu,
-    const real *__restrict__ Wv, real *__restrict__ wz, real rho,
+    const real *__restrict__ A1, const real *__restrict__ La_d1,
+    const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
+    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
     const Ctrl<real> *ctrl, int nb, int xcd) {
     if (ctrl && ctrl->halt) return;
     const int blk = xcd_block(blockIdx.x, nb, xcd);
@@ -411,6 +452,18 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     const real b = FP[v] - Zv[i];
     real zu = Zu[i], zv = Zv[i];
     const real pu = P[u], pv = P[v];
+    // splitting weights from their factors (prox weights: non-linear losses;
+    // contributions: only when this sweep stores W*Z)
+    real wsu = real(0), wsv = real(0), gpu = real(1), gpv = real(1), la = real(0);
+    if ((c.loss != LOSS_LINEAR && !Th) || wz) {
+        la = La_d1[e];
+        const real an = A1 ? A1[i] : la;
+        const SxR2<real> gu = GI[u], gv = GI[v];
+        wsu = an * gu.y;
+        wsv = an * gv.y;
+        gpu = gu.x;
+        gpv = gv.x;
+    }
     if (c.loss == LOSS_LINEAR) {
         const real h = real(0.5) * (a + b);
         a = a - b;
@@ -427,7 +480,9 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
             zv += rho * (h - pv);
         }
     } else {
-        const real wu = Wd1u[i], wv = Wd1v[i], th = Th[i];
+        real wu, wv, th;
+        if (Th) { wu = Wd1u[i]; wv = Wd1v[i]; th = Th[i]; }
+        else sx_prox_weights<real>(wsu, wsv, gpu, gpv, la, wu, wv, th);
         const real h = wu * a + wv * b;
         a = a - b;
         if (a > th) {
@@ -446,8 +501,8 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     Zu[i] = zu;
     Zv[i] = zv;
     if (wz) {
-        wz[i] = Wu[i] * zu;
-        wz[EK + i] = Wv[i] * zv;
+        wz[i] = wsu * zu;
+        wz[EK + i] = wsv * zv;
     }
 }
 
@@ -529,7 +584,9 @@ struct SxVArgs {
     const int *ptr;
     const unsigned *idx;
     const real *wz, *Ga, *GaQ, *Q;
-    const real *Zu, *Zv, *Wu, *Wv;  // !WZ: contributions formed in the sweep
+    const real *Zu, *Zv;  // !WZ: contributions W*Z formed in the sweep from
+    const real *A1, *La_d1;  // the factors of W (sx_a) and the vertex's invAux
+    const SxR2<real> *GI;
     real *P, *FP, *lab;
     int track;
     real *part;
@@ -552,6 +609,7 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     const bool live = vl < vb && v < a.V;
     const long i = v * K + k;
     if (live) {
+        const real inv = WZ ? real(0) : a.GI[i].y;  // 1/Aux of this (v, k)
         const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
         const real *__restrict__ wz = a.wz;
         real s = real(0);
@@ -565,21 +623,23 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
             if (WZ) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) w[q] = wz[(long)sl[q] * K + k];
-            } else {  // W * Z formed here (the reference's product, same rounding)
+            } else {  // W * Z formed here (the reference's products, same rounding)
                 // branch-free: received entries (address 2E + j) sit in the
-                // tails of Zv / Wv (Zv: the sender's W*Z, Wv: 1), so all 16
-                // loads issue together
-                real zq[8], wq[8];
+                // tail of Zv as the sender's W*Z (factor 1), so all 16 loads
+                // issue together
+                real zq[8], aq[8];
+                bool rq[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
                     const long ad = sl[q];
                     const bool sv = ad >= a.E;
-                    const long o = (sv ? ad - a.E : ad) * K + k;
-                    zq[q] = (sv ? a.Zv : a.Zu)[o];
-                    wq[q] = (sv ? a.Wv : a.Wu)[o];
+                    const long ea = sv ? ad - a.E : ad;
+                    rq[q] = ea >= a.E;
+                    zq[q] = (sv ? a.Zv : a.Zu)[ea * K + k];
+                    aq[q] = a.A1 ? a.A1[rq[q] ? 0 : ea * K + k] : a.La_d1[rq[q] ? 0 : ea];
                 }
 #pragma unroll
-                for (int q = 0; q < 8; q++) w[q] = wq[q] * zq[q];
+                for (int q = 0; q < 8; q++) w[q] = rq[q] ? zq[q] : (aq[q] * inv) * zq[q];
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) s += w[q];
@@ -590,8 +650,10 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
                 s += wz[ad * K + k];
             } else {
                 const bool sv = ad >= a.E;
-                const long o = (sv ? ad - a.E : ad) * K + k;
-                s += (sv ? a.Wv : a.Wu)[o] * (sv ? a.Zv : a.Zu)[o];
+                const long ea = sv ? ad - a.E : ad;
+                const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
+                if (ea >= a.E) s += z;
+                else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
             }
         }
         xs[t] = s;
@@ -642,16 +704,20 @@ __global__ void k_fill(long n, real *p, real v) {
 // packed in the plan's push order
 template <typename real>
 __global__ void k_sx_pack_wz(long n, int K, long E, const unsigned *__restrict__ addr,
-                             const real *__restrict__ Wu, const real *__restrict__ Zu,
-                             const real *__restrict__ Wv, const real *__restrict__ Zv,
-                             real *__restrict__ out) {
+                             const int *__restrict__ Eu, const int *__restrict__ Ev,
+                             const real *__restrict__ A1, const real *__restrict__ La_d1,
+                             const SxR2<real> *__restrict__ GI, const real *__restrict__ Zu,
+                             const real *__restrict__ Zv, real *__restrict__ out) {
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n * K) return;
     const long i = t / K;
     const int k = (int)(t - i * K);
     const long ad = addr[i];
-    out[t] = ad >= E ? Wv[(ad - E) * K + k] * Zv[(ad - E) * K + k]
-                     : Wu[ad * K + k] * Zu[ad * K + k];
+    const bool sv = ad >= E;
+    const long e = sv ? ad - E : ad;
+    const long row = sv ? Ev[e] : Eu[e];
+    const real w = sx_a(e * K + k, e, A1, La_d1) * GI[row * K + k].y;
+    out[t] = w * (sv ? Zv : Zu)[e * K + k];
 }
 
 // sum of the evolution partials (distributed: all-reduced before the decision)
@@ -848,7 +914,12 @@ class SimplexSession final : public SessionBase {
     int track_;  // 0, 1 (l1 evolution), 2 (labels)
     DevBuf<int> Eu_, Ev_;
     DevBuf<real> La_d1_, La_f_, Q_, P_, FP_, Pavg_, Ga_, GaQ_, invAux_, lab_;
-    DevBuf<real> Zu_, Zv_, Wu_, Wv_, Wd1u_, Wd1v_, Th_, wz_, part_, opart_, Obj_, Dif_;
+    DevBuf<real> Zu_, Zv_, A1_, wz_, part_, opart_, Obj_, Dif_;
+    DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
+    // stored prox weights/thresholds of the non-linear losses (PFDR_SX_PW=0:
+    // recomputed from the factors in every edge sweep)
+    DevBuf<real> Wd1u_, Wd1v_, Th_;
+    bool sx_pw_ = true;
     DevBuf<Ctrl<real>> ctrl_;
     Ctrl<real> *hctrl_ = nullptr;
     Incidence inc_;
@@ -964,12 +1035,16 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     }
     FP_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
     const size_t EKn = EK_ ? EK_ : 1;
-    // Zv / Wv carry the received contributions after their E*K entries
-    // (Zv: the sender's W*Z, Wv: 1) for the fused vertex sweep
-    Zu_.alloc(EKn); Wu_.alloc(EKn);
-    Zv_.alloc(EKn + (size_t)R_ * K_); Wv_.alloc(EKn + (size_t)R_ * K_);
-    if (R_) k_fill<real><<<grid_for(R_ * K_), kBlock, 0, s>>>(R_ * K_, Wv_.p + EKn, real(1));
-    if (c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
+    // Zv carries the received contributions (the senders' W*Z) after its
+    // E*K entries for the fused vertex sweep
+    Zu_.alloc(EKn);
+    Zv_.alloc(EKn + (size_t)R_ * K_);
+    GI_.alloc(VgK);
+    {
+        const char *pw = getenv("PFDR_SX_PW");
+        sx_pw_ = !(pw && pw[0] == '0');
+    }
+    if (sx_pw_ && c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
     nbe_ = grid_for(E_);
@@ -1001,9 +1076,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     stopped_ = itMax_ <= 0;
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &FP_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
-                            &Zu_, &Zv_, &Wu_, &Wv_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_,
-                            &Obj_, &Dif_})
+                            &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
+                            &Dif_})
         device_bytes += (int64_t)(b->n * sizeof(real));
+    device_bytes += (int64_t)(GI_.n * sizeof(SxR2<real>));
 }
 
 // ref :64-370
@@ -1012,25 +1088,32 @@ void SimplexSession<real>::precondition(bool init) {
     hipStream_t s = stream;
     ProfScope ps(prof, init ? "precondition" : "recondition", s);
     const int gE = grid_for(EK_), gV = grid_for(VK_);
+    const bool first_recond = !init && !A1_.p;
     if (!init) {
         k_sx_recover<real><<<nbv_, kBlock, 0, s>>>(V_, c_, La_f_.p, Q_.p, GaQ_.p, Ga_.p);
         pullK(Ga_);
         if (EK_) k_sx_subgrad<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, P_.p, Q_.p, Ga_.p,
-                                                          GaQ_.p, Wu_.p, Wv_.p, Zu_.p, Zv_.p);
+                                                          GaQ_.p, first_recond ? nullptr : A1_.p,
+                                                          La_d1_.p, invAux_.p, Zu_.p, Zv_.p);
     }
+    if (first_recond) A1_.alloc(EK_ ? EK_ : 1);  // a leaves La_d1 for good
     k_sx_hessian<real><<<gV, kBlock, 0, s>>>(VK_, c_, La_f_.p, P_.p, Q_.p, Ga_.p);
     if (EK_) k_sx_d1_weights<real><<<gE, kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, La_d1_.p, init ? 1 : 0,
-                                                         condMin_, P_.p, Wu_.p, Wv_.p, wz_.p);
+                                                         condMin_, P_.p, A1_.p, wz_.p);
     if (halo_) halo_->push(wz_.p, wz_.p + 2 * EK_, K_ * (int)sizeof(real), s);
     k_sx_precond_vertex<real><<<gV, kBlock, 0, s>>>(VK_, c_, inc_.ptr.p, inc_.idx.p, wz_.p,
                                                     La_f_.p, Q_.p, cap_, Ga_.p, invAux_.p, GaQ_.p);
     pullK(Ga_);
     pullK(invAux_);
     pullK(GaQ_);
-    if (EK_) k_sx_precond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, La_d1_.p, invAux_.p,
-                                                           Ga_.p, GaQ_.p, P_.p, Q_.p, Wu_.p, Wv_.p,
-                                                           Wd1u_.p, Wd1v_.p, Th_.p, init ? 0 : 1,
-                                                           Zu_.p, Zv_.p);
+    if (EK_ && !init)
+        k_sx_recond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, A1_.p, invAux_.p, Ga_.p,
+                                                     GaQ_.p, P_.p, Q_.p, Zu_.p, Zv_.p);
+    k_sx_gi_pack<real><<<grid_for((long)Vg_ * K_), kBlock, 0, s>>>((long)Vg_ * K_, Ga_.p,
+                                                                  invAux_.p, GI_.p);
+    if (EK_ && Th_.p)
+        k_sx_prox_store<real><<<gE, kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, A1_.p, La_d1_.p, GI_.p,
+                                                    Wd1u_.p, Wd1v_.p, Th_.p);
     k_sx_normalise<real><<<nbv_, kBlock, 0, s>>>(V_, K_, Ga_.p);
     PFDR_HIP(hipGetLastError());
 }
@@ -1061,8 +1144,8 @@ void SimplexSession<real>::body() {
         const int nb = grid_for(EK_);
         const int xm = xcd_fit(nb, sx_xcd_e_);
         k_sx_edge_sweep<real><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
-                                                               Zu_.p, Zv_.p, Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               Wu_.p, Wv_.p,
+                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Wd1u_.p, Wd1v_.p, Th_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
                                                                rho_, c, nb, xm);
     }
@@ -1076,7 +1159,7 @@ void SimplexSession<real>::body() {
         a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.FP = FP_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
-        a.Zu = Zu_.p; a.Zv = Zv_.p; a.Wu = Wu_.p; a.Wv = Wv_.p;
+        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.GI = GI_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
         if (sx_nt_ == 256) {
@@ -1132,7 +1215,8 @@ void SimplexSession<real>::push_wz() {
     real *buf = (real *)halo_->push_buffer(eb);
     if (n) {
         k_sx_pack_wz<real><<<grid_for(n * K_), kBlock, 0, stream>>>(n, K_, E_, halo_->push_addr.p,
-                                                                    Wu_.p, Zu_.p, Wv_.p, Zv_.p, buf);
+                                                                    Eu_.p, Ev_.p, A1_.p, La_d1_.p, GI_.p,
+                                                                    Zu_.p, Zv_.p, buf);
         PFDR_HIP(hipGetLastError());
     }
     halo_->push_packed(buf, Zv_.p + EK_, eb, stream);  // the tail of Zv (vertex sweep)
