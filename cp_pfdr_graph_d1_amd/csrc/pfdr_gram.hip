@@ -74,18 +74,37 @@ __device__ __forceinline__ real gram_elem(const real *A, long ld, long i, long k
     return LAYOUT == GRAM_TN ? A[k + i * ld] : A[i + k * ld];
 }
 
+// Block -> (tile bi <= bj of the upper block triangle, contraction chunk z).
+// The dispatcher deals blocks round-robin over the 8 XCDs (block b on XCD
+// b % 8), so XCD x gets the chunks z = x, x + 8, ... with all their tiles
+// together: every XCD has the same share of the work, and the operand
+// panels of a chunk are fetched into that XCD's L2 for all the tiles that
+// share them.  (A 3-D (bi, bj, z) grid put every tile of block row bi on
+// XCD bi: XCD 0 had 8 tiles per chunk, XCD 7 one.)
+__device__ __forceinline__ bool gram_block(int nb, int nchunk, int &bi, int &bj, int &z) {
+    const int ntiles = nb * (nb + 1) / 2;
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    z = (slot / ntiles) * 8 + xcd;
+    int t = slot - (slot / ntiles) * ntiles;
+    if (z >= nchunk) return false;
+    bi = 0;
+    while (t >= nb - bi) { t -= nb - bi; bi++; }
+    bj = bi + t;
+    return true;
+}
+
 // One block = one BT x BT tile (bi <= bj) of the chunk [k0, k1) of the
 // contraction; output partial G (P x P, column-major) of this chunk.
 template <typename real, int LAYOUT>
 __global__ __launch_bounds__(256) void k_gram(int P, long K, const real *__restrict__ A, long ld,
-                                            long kchunk, real *__restrict__ Gpart) {
+                                            long kchunk, int nchunk, real *__restrict__ Gpart) {
     using M = Mfma<real>;
     constexpr int BT = M::BT, BK = M::BK, T = M::T, WT = BT / 2, NT = WT / T;
-    const int bi = blockIdx.x, bj = blockIdx.y;
-    if (bi > bj) return;
-    const long k0 = (long)blockIdx.z * kchunk;
+    int bi, bj, z;
+    if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
+    const long k0 = (long)z * kchunk;
     const long k1 = min(K, k0 + kchunk);
-    real *G = Gpart + (size_t)blockIdx.z * P * P;
+    real *G = Gpart + (size_t)z * P * P;
     __shared__ real Ls[BK][BT + 1], Rs[BK][BT + 1];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wi = w & 1, wj = w >> 1;
@@ -145,16 +164,16 @@ __global__ __launch_bounds__(256) void k_gram(int P, long K, const real *__restr
 // ld % (16 / sizeof(real)) == 0 and a 16-byte aligned A).
 template <typename real, int LAYOUT>
 __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__restrict__ A, long ld,
-                                              long kchunk, real *__restrict__ Gpart) {
+                                              long kchunk, int nchunk, real *__restrict__ Gpart) {
     using M = Mfma<real>;
     constexpr int BT = M::BT, BK = M::BK, T = M::T, WT = BT / 2, NT = WT / T;
     constexpr int VW = 16 / sizeof(real);                 // reals per 16-byte load
     constexpr int NL = BT * BK / (256 * VW);               // vector loads per operand per lane
-    const int bi = blockIdx.x, bj = blockIdx.y;
-    if (bi > bj) return;
-    const long k0 = (long)blockIdx.z * kchunk;
+    int bi, bj, z;
+    if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
+    const long k0 = (long)z * kchunk;
     const long k1 = min(K, k0 + kchunk);
-    real *G = Gpart + (size_t)blockIdx.z * P * P;
+    real *G = Gpart + (size_t)z * P * P;
     __shared__ alignas(16) real Ls[BK][BT + VW], Rs[BK][BT + VW];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wi = w & 1, wj = w >> 1;
@@ -268,6 +287,7 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     const int nb = (P + M::BT - 1) / M::BT;
     const long tiles = (long)nb * (nb + 1) / 2;
     long nchunk = std::max(1L, std::min((2048 + tiles - 1) / tiles, (K + 4 * M::BK - 1) / (4 * M::BK)));
+    if (nchunk > 8) nchunk = (nchunk + 7) / 8 * 8;  // the same number of chunks on every XCD
     long kchunk = (K + nchunk - 1) / nchunk;
     kchunk = ((kchunk + M::BK - 1) / M::BK) * M::BK;
     nchunk = K > 0 ? (K + kchunk - 1) / kchunk : 1;
@@ -277,15 +297,17 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     real *out = G;
     if (nchunk > 1) { part.alloc(PP * nchunk); out = part.p; }
     if (K == 0) { PFDR_HIP(hipMemsetAsync(G, 0, PP * sizeof(real), s)); return; }
-    dim3 grid(nb, nb, (unsigned)nchunk);
+    const long nblk = 8 * ((nchunk + 7) / 8) * tiles;  // see gram_block
+    if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
+    const dim3 grid((unsigned)nblk);
     const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0 &&
                      !(getenv("PFDR_GRAM_SCALAR") && getenv("PFDR_GRAM_SCALAR")[0] == '1');
     if (vec) {
-        if (which == 0) k_gram_v<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
-        else k_gram_v<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+        if (which == 0) k_gram_v<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
+        else k_gram_v<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
     } else {
-        if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
-        else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, out);
+        if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
+        else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
     }
     PFDR_HIP(hipGetLastError());
     if (nchunk > 1) {
