@@ -721,10 +721,13 @@ void QuadSession<real>::body() {
         }
         vertex_sweep(0, nbv_, c, "vertex_sweep");
     }
-    if (gated) {
+    if (gated && !halo_) {
+        k_reduce_decide<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, ctrl_.p,
+                                                   rec_dif_ ? Dif_.p : nullptr, track_ ? 1 : 0);
+    } else if (gated) {  // the partial sums are all-reduced before the decision
         if (track_) {
             k_reduce_pairs<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, 1);
-            if (halo_) halo_->tr->allreduce_sum(red_.p, 2, dtype_of<real>(), s);
+            halo_->tr->allreduce_sum(red_.p, 2, dtype_of<real>(), s);
         }
         k_decide<real><<<1, 64, 0, s>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, track_ ? 1 : 0);
     }

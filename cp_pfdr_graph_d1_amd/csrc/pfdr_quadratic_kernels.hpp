@@ -1036,12 +1036,11 @@ __global__ __launch_bounds__(256) void k_reduce_pairs(int nparts, const real *__
 // iterate evolution and loop control (ref :514-529, :424-429, :447-460);
 // red[0..1] = (sum (X - X_)^2, sum X^2) over all ranks
 template <typename real>
-__global__ void k_decide(Ctrl<real> *ctrl, const real *__restrict__ red,
-                         real *__restrict__ Dif, int track) {
-    if (threadIdx.x != 0 || ctrl->halt) return;
+__device__ __forceinline__ void decide_step(Ctrl<real> *ctrl, real num, real den,
+                                            real *__restrict__ Dif, int track) {
     int it = ctrl->it;
     if (track) {
-        const real num = red[0], den = red[1], eps = ctrl->eps;
+        const real eps = ctrl->eps;
         const real dif = (den > eps) ? num / den : num / eps;
         ctrl->dif = dif;
         if (Dif) Dif[it] = dif;
@@ -1056,6 +1055,37 @@ __global__ void k_decide(Ctrl<real> *ctrl, const real *__restrict__ red,
         ctrl->recond = 1;
         ctrl->halt = 1;
     }
+}
+
+// single GPU: the fixed-order partial sums of k_reduce_pairs and the
+// decision of k_decide in one launch (one kernel boundary less per
+// iteration, which counts for small graphs)
+template <typename real>
+__global__ __launch_bounds__(256) void k_reduce_decide(int nparts, const real *__restrict__ part,
+                                                       real *__restrict__ out, Ctrl<real> *ctrl,
+                                                       real *__restrict__ Dif, int track) {
+    __shared__ real red[2][kBlock / kWave];
+    if (ctrl->halt) return;  // uniform
+    real a = real(0), b = real(0);
+    if (track) {
+        for (int i = threadIdx.x; i < nparts; i += kBlock) {
+            a += part[2 * i];
+            b += part[2 * i + 1];
+        }
+        a = block_sum(a, red[0]);
+        b = block_sum(b, red[1]);
+    }
+    if (threadIdx.x == 0) {
+        if (track) { out[0] = a; out[1] = b; }
+        decide_step(ctrl, a, b, Dif, track);
+    }
+}
+
+template <typename real>
+__global__ void k_decide(Ctrl<real> *ctrl, const real *__restrict__ red,
+                         real *__restrict__ Dif, int track) {
+    if (threadIdx.x != 0 || ctrl->halt) return;
+    decide_step(ctrl, track ? red[0] : real(0), track ? red[1] : real(0), Dif, track);
 }
 
 // ------------------------------------------------------------ objective --

@@ -422,48 +422,13 @@ __global__ void k_sx_labels(int V, int K, const real *__restrict__ P,
 }
 
 // --------------------------------------------------------- iteration ---
+// TV prox + relaxed Z update of one (edge, label) (ref :589-634)
 template <typename real>
-__global__ __launch_bounds__(256) void k_sx_edge_sweep(
-    long EK, SxConst<real> c, const int *__restrict__ Eu,
-    const int *__restrict__ Ev, const real *__restrict__ FP,
-    const real *__restrict__ P, real *__restrict__ Zu, real *__restrict__ Zv,
-    const real *__restrict__ A1, const real *__restrict__ La_d1,
-    const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
-    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
-    const Ctrl<real> *ctrl, int nb, int xcd) {
-    if (ctrl && ctrl->halt) return;
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
-    if (blk >= nb) return;
-    const long i = (long)blk * blockDim.x + threadIdx.x;
-    if (i >= EK) return;
-    const int K = c.K;
-    long e;
-    int k;
-    if (EK <= 0xffffffffl) {  // 32-bit division (uniform branch)
-        const unsigned ue = (unsigned)i / (unsigned)K;
-        e = ue;
-        k = (int)((unsigned)i - ue * (unsigned)K);
-    } else {
-        e = i / K;
-        k = (int)(i - e * K);
-    }
-    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
-    real a = FP[u] - Zu[i];
-    const real b = FP[v] - Zv[i];
-    real zu = Zu[i], zv = Zv[i];
-    const real pu = P[u], pv = P[v];
-    // splitting weights from their factors (prox weights: non-linear losses;
-    // contributions: only when this sweep stores W*Z)
-    real wsu = real(0), wsv = real(0), gpu = real(1), gpv = real(1), la = real(0);
-    if ((c.loss != LOSS_LINEAR && !Th) || wz) {
-        la = La_d1[e];
-        const real an = A1 ? A1[i] : la;
-        const SxR2<real> gu = GI[u], gv = GI[v];
-        wsu = an * gu.y;
-        wsv = an * gv.y;
-        gpu = gu.x;
-        gpv = gv.x;
-    }
+__device__ __forceinline__ void sx_edge_elem(const SxConst<real> &c, real fpu, real fpv, real pu,
+                                             real pv, real &zu, real &zv, real wu, real wv, real th,
+                                             real rho) {
+    real a = fpu - zu;
+    const real b = fpv - zv;
     if (c.loss == LOSS_LINEAR) {
         const real h = real(0.5) * (a + b);
         a = a - b;
@@ -480,9 +445,6 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
             zv += rho * (h - pv);
         }
     } else {
-        real wu, wv, th;
-        if (Th) { wu = Wd1u[i]; wv = Wd1v[i]; th = Th[i]; }
-        else sx_prox_weights<real>(wsu, wsv, gpu, gpv, la, wu, wv, th);
         const real h = wu * a + wv * b;
         a = a - b;
         if (a > th) {
@@ -498,11 +460,87 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
             zv += rho * (h - pv);
         }
     }
-    Zu[i] = zu;
-    Zv[i] = zv;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ Pk<T, N> sx_ld(const T *p) { return *reinterpret_cast<const Pk<T, N> *>(p); }
+template <typename T, int N>
+__device__ __forceinline__ void sx_st(T *p, const Pk<T, N> &x) { *reinterpret_cast<Pk<T, N> *>(p) = x; }
+
+// L consecutive (edge, label) entries per lane (L = 2 when K is even: the
+// pair shares its edge, so every stream and the four K-run gathers move as
+// 8-byte (f32) / 16-byte (f64) accesses, and the endpoint loads and the
+// index division are paid once per pair)
+template <typename real, int L>
+__global__ __launch_bounds__(256) void k_sx_edge_sweep(
+    long EK, SxConst<real> c, const int *__restrict__ Eu,
+    const int *__restrict__ Ev, const real *__restrict__ FP,
+    const real *__restrict__ P, real *__restrict__ Zu, real *__restrict__ Zv,
+    const real *__restrict__ A1, const real *__restrict__ La_d1,
+    const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
+    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
+    const Ctrl<real> *ctrl, int nb, int xcd) {
+    if (ctrl && ctrl->halt) return;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    const long i = ((long)blk * blockDim.x + threadIdx.x) * L;
+    if (i >= EK) return;
+    const int K = c.K;
+    long e;
+    int k;
+    if (EK <= 0xffffffffl) {  // 32-bit division (uniform branch)
+        const unsigned ue = (unsigned)i / (unsigned)K;
+        e = ue;
+        k = (int)((unsigned)i - ue * (unsigned)K);
+    } else {
+        e = i / K;
+        k = (int)(i - e * K);
+    }
+    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    Pk<real, L> zu = sx_ld<real, L>(Zu + i), zv = sx_ld<real, L>(Zv + i);
+    const Pk<real, L> fpu = sx_ld<real, L>(FP + u), fpv = sx_ld<real, L>(FP + v);
+    const Pk<real, L> pu = sx_ld<real, L>(P + u), pv = sx_ld<real, L>(P + v);
+    // splitting weights from their factors (prox weights: non-linear losses
+    // without stored ones; contributions: only when this sweep stores W*Z)
+    real wsu[L], wsv[L], gpu[L], gpv[L], la = real(0);
+#pragma unroll
+    for (int j = 0; j < L; j++) { wsu[j] = wsv[j] = real(0); gpu[j] = gpv[j] = real(1); }
+    if ((c.loss != LOSS_LINEAR && !Th) || wz) {
+        la = La_d1[e];
+#pragma unroll
+        for (int j = 0; j < L; j++) {
+            const real an = A1 ? A1[i + j] : la;
+            const SxR2<real> gu = GI[u + j], gv = GI[v + j];
+            wsu[j] = an * gu.y;
+            wsv[j] = an * gv.y;
+            gpu[j] = gu.x;
+            gpv[j] = gv.x;
+        }
+    }
+    Pk<real, L> du{}, dv{}, th{};
+    if (c.loss != LOSS_LINEAR) {
+        if (Th) {
+            du = sx_ld<real, L>(Wd1u + i);
+            dv = sx_ld<real, L>(Wd1v + i);
+            th = sx_ld<real, L>(Th + i);
+        } else {
+#pragma unroll
+            for (int j = 0; j < L; j++)
+                sx_prox_weights<real>(wsu[j], wsv[j], gpu[j], gpv[j], la, du.v[j], dv.v[j], th.v[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < L; j++)
+        sx_edge_elem<real>(c, fpu.v[j], fpv.v[j], pu.v[j], pv.v[j], zu.v[j], zv.v[j], du.v[j],
+                           dv.v[j], th.v[j], rho);
+    sx_st<real, L>(Zu + i, zu);
+    sx_st<real, L>(Zv + i, zv);
     if (wz) {
-        wz[i] = wsu * zu;
-        wz[EK + i] = wsv * zv;
+#pragma unroll
+        for (int j = 0; j < L; j++) {
+            wz[i + j] = wsu[j] * zu.v[j];
+            wz[EK + i + j] = wsv[j] * zv.v[j];
+        }
     }
 }
 
@@ -916,10 +954,11 @@ class SimplexSession final : public SessionBase {
     DevBuf<real> La_d1_, La_f_, Q_, P_, FP_, Pavg_, Ga_, GaQ_, invAux_, lab_;
     DevBuf<real> Zu_, Zv_, A1_, wz_, part_, opart_, Obj_, Dif_;
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
-    // stored prox weights/thresholds of the non-linear losses (PFDR_SX_PW=0:
-    // recomputed from the factors in every edge sweep)
+    // stored prox weights/thresholds of the non-linear losses (else
+    // recomputed from the factors in every edge sweep; PFDR_SX_PW=0/1)
     DevBuf<real> Wd1u_, Wd1v_, Th_;
     bool sx_pw_ = true;
+    bool sx_pair_ = true;  // PFDR_SX_PAIR=0: one (e, k) per lane in the edge sweep (A/B)
     DevBuf<Ctrl<real>> ctrl_;
     Ctrl<real> *hctrl_ = nullptr;
     Incidence inc_;
@@ -1041,8 +1080,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     Zv_.alloc(EKn + (size_t)R_ * K_);
     GI_.alloc(VgK);
     {
+        const char *pr = getenv("PFDR_SX_PAIR");
+        sx_pair_ = !(pr && pr[0] == '0');
+        // prox weights: recomputed in the pair sweep (C4: 1.076 -> 0.950 ms,
+        // r1zw), stored for the one-per-lane sweep (odd K: 1.24 vs 1.30 ms)
         const char *pw = getenv("PFDR_SX_PW");
-        sx_pw_ = !(pw && pw[0] == '0');
+        sx_pw_ = pw ? pw[0] == '1' : !(sx_pair_ && K_ % 2 == 0);
     }
     if (sx_pw_ && c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
@@ -1141,9 +1184,17 @@ void SimplexSession<real>::body() {
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     if (EK_) {
         ProfScope ps(prof, "sx_edge_sweep", s);
-        const int nb = grid_for(EK_);
+        const int pair = (K_ % 2 == 0 && sx_pair_) ? 2 : 1;  // see k_sx_edge_sweep
+        const int nb = grid_for(EK_ / pair);
         const int xm = xcd_fit(nb, sx_xcd_e_);
-        k_sx_edge_sweep<real><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+        if (pair == 2)
+            k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Wd1u_.p, Wd1v_.p, Th_.p,
+                                                               (vb_ && !sx_wz_) ? nullptr : wz_.p,
+                                                               rho_, c, nb, xm);
+        else
+            k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
