@@ -52,6 +52,21 @@ def cpu_baseline_child(args):
     from workloads import WORKLOADS
     kind = "reference" if oracle.available("ref_omp") else "port"
     lib = oracle.Oracle("ref_omp" if kind == "reference" else "port")
+    if args.workload == "c1":  # the reference's own CPU case: time to tolerance
+        inp = WORKLOADS["c1"].inputs(0, 1)
+        kw = inp["kw"]
+        Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
+        t = time.perf_counter()
+        X, it, _, _ = lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
+                                          kw["La_l1"], 0, int(kw["Ltype"]), None, kw["rho"],
+                                          kw["condMin"], 0.0, kw["difTol"], 10000)
+        el = time.perf_counter() - t
+        print(json.dumps({
+            "value": Eu.size * it / el / 1e6, "unit": "Medge-updates/s",
+            "cores": len(cores) if kind == "reference" else 1, "kind": kind,
+            "converged_iterations": it, "time_to_tolerance_s": el,
+            "sample": "whole C1 solve to difTol 1e-6 (setup included), same inputs"}))
+        return
     inp = WORKLOADS["headline"].inputs(0, 1)
     kw, V = inp["kw"], inp["V"]
     Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
@@ -75,7 +90,7 @@ def cpu_baseline_child(args):
 def run_cpu_baseline(args):
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child",
            "--cpu-k0", str(args.cpu_k0), "--cpu-k1", str(args.cpu_k1),
-           "--cpu-cores", str(args.cpu_cores)]
+           "--cpu-cores", str(args.cpu_cores), "--workload", args.workload]
     try:
         out = subprocess.run(cmd, check=True, capture_output=True, text=True,
                              timeout=900).stdout
@@ -121,7 +136,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first, in its own process, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and wl.name == "headline" and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and wl.name in ("headline", "c1") and not args.no_cpu_baseline:
         cpu = run_cpu_baseline(args)
 
     import torch
