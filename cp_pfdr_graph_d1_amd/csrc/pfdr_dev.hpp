@@ -176,7 +176,17 @@ inline int grid_for(long n, int per_thread = 1) {
 }
 
 // ------------------------------------------------------- device buffers --
-// RAII device allocation (hipMalloc'd, freed on scope exit).
+// Device memory through a per-process cache (pfdr_runtime.cpp): a freed
+// block is kept under its size class and handed out again once the stream
+// that freed it is idle, so repeated calls of similar size (cut pursuit's
+// reduced problems, a caller's solve loop) skip hipMalloc / hipFree, which
+// synchronise the device and cost milliseconds per call.  Bounded by
+// PFDR_DEVICE_CACHE_MB (default 2048; 0 disables); on an out-of-memory
+// hipMalloc the cache is emptied and the allocation retried.
+void *dev_malloc(size_t bytes);
+void dev_free(void *p, size_t bytes) noexcept;
+
+// RAII device allocation (dev_malloc'd, freed on scope exit).
 template <typename T>
 struct DevBuf {
     T *p = nullptr;
@@ -185,11 +195,11 @@ struct DevBuf {
     explicit DevBuf(size_t count) { alloc(count); }
     void alloc(size_t count) {
         release();
+        if (count) p = static_cast<T *>(dev_malloc(count * sizeof(T)));
         n = count;
-        if (count) PFDR_HIP(hipMalloc(&p, count * sizeof(T)));
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p, n * sizeof(T));
         p = nullptr;
         n = 0;
     }
@@ -201,6 +211,29 @@ struct DevBuf {
 
 // Library-owned stream of the calling thread's current device.
 hipStream_t lib_stream();
+
+// Copies between the caller's host arrays and the device.  A host range of
+// at least 1 MiB is pinned (hipHostRegister) for its DMA and unpinned once
+// the stream has drained (release(), or the destructor): the runtime's
+// pageable path stages through its own buffers at 3-10 GB/s, a pinned DMA
+// runs at ~55 GB/s (profiles/r1/r2b_h2d.log).  A range that cannot be
+// pinned (already registered, read-only mapping) is copied as before.
+class HostPins {
+  public:
+    explicit HostPins(hipStream_t s = nullptr) : s_(s) {}
+    ~HostPins();
+    HostPins(const HostPins &) = delete;
+    HostPins &operator=(const HostPins &) = delete;
+    void set_stream(hipStream_t s) { s_ = s; }
+    // asynchronous on the stream; kind: hipMemcpyHostToDevice or DeviceToHost
+    void copy(void *dst, const void *src, size_t bytes, hipMemcpyKind kind);
+    void release();  // synchronise the stream, unpin everything pinned here
+
+  private:
+    hipStream_t s_;
+    void *pinned_[64];
+    int n_ = 0;
+};
 
 // Upload a host array into a fresh device buffer (nullptr stays nullptr).
 template <typename T>

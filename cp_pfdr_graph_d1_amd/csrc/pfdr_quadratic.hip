@@ -15,13 +15,14 @@
 namespace pfdr {
 
 template <typename real>
-static void copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s) {
+static void copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s,
+                    HostPins &pins) {
     if (!src || !n) { d.release(); return; }
     d.alloc(n);
-    PFDR_HIP(hipMemcpyAsync(d.p, src, n * sizeof(real),
-                            mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice
-                                                   : hipMemcpyHostToDevice,
-                            s));
+    if (mem == PFDR_MEM_DEVICE)
+        PFDR_HIP(hipMemcpyAsync(d.p, src, n * sizeof(real), hipMemcpyDeviceToDevice, s));
+    else
+        pins.copy(d.p, src, n * sizeof(real), hipMemcpyHostToDevice);
 }
 
 template <typename real>
@@ -114,6 +115,7 @@ class QuadSession final : public SessionBase {
     DevBuf<int> cnt_part_;
     DevBuf<Ctrl<real>> ctrl_;
     Incidence inc_;
+    HostPins pins_;  // caller arrays pinned for the setup copies
     // split incidence (edges sorted by u): u-run offsets, per-vertex order
     // masks, addresses of the other entries, per-block path flag
     DevBuf<int> uptr_, blkok_;
@@ -161,6 +163,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         throw std::runtime_error("X, Y, Eu, Ev and La_d1 are required");
     PFDR_HIP(hipGetDevice(&device));
     stream = lib_stream();
+    pins_.set_stream(stream);
     hipStream_t s = stream;
     flavour_ = (p->kind == PFDR_KIND_BOUNDS) ? 1 : 0;
     V_ = p->V;
@@ -220,12 +223,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
                                  "length V) and N = -V (V over all ranks)");
     const int mem = p->mem;
     const size_t V = V_, E = E_, Vg = Vg_;
-    copy_in(La_d1_, p->La_d1, E, mem, s);
-    if (flavour_ == 0) copy_in(La_l1_, p->La_l1, V, mem, s);
-    copy_in(Y_, p->Y, mode_ == A_DIRECT ? (size_t)N_ : V, mem, s);
+    copy_in(La_d1_, p->La_d1, E, mem, s, pins_);
+    if (flavour_ == 0) copy_in(La_l1_, p->La_l1, V, mem, s, pins_);
+    copy_in(Y_, p->Y, mode_ == A_DIRECT ? (size_t)N_ : V, mem, s, pins_);
     const size_t asz = mode_ == A_DIRECT ? (size_t)N_ * V : mode_ == A_ATA ? (size_t)Vglob_ * V
                      : mode_ == A_DIAG ? V : 0;
-    copy_in(A_, p->A, asz, mem, s);
+    copy_in(A_, p->A, asz, mem, s, pins_);
     if (reordered_) {  // inputs into the internal labels (identity / diagonal A only)
         permute(La_d1_, emap_.p, E, s);
         permute(La_l1_, order_.p, V, s);
@@ -244,11 +247,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         cap /= L0;
     }
     cap_ = cap;
-    if (Ldiag_) copy_in(L_, p->L, V, mem, s);
+    if (Ldiag_) copy_in(L_, p->L, V, mem, s, pins_);
     if (reordered_ && Ldiag_) permute(L_, order_.p, V, s);
     {   // iterate (X, P) pairs, owned then ghost vertices
         DevBuf<real> X0;
-        copy_in(X0, p->X, V, mem, s);
+        copy_in(X0, p->X, V, mem, s, pins_);
         if (reordered_) permute(X0, order_.p, V, s);
         xp_.alloc(Vg);
         PFDR_HIP(hipMemsetAsync(xp_.p, 0, Vg * sizeof(R2<real>), s));
@@ -325,6 +328,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     PFDR_HIP(hipStreamSynchronize(s));
     // c of the first conditioning: a_e = cw_ La_d1[e] in the edge sweeps
     PFDR_HIP(hipMemcpy(&cw_, &ctrl_.p->c, sizeof(real), hipMemcpyDeviceToHost));
+    pins_.release();
     stopped_ = (itMax_ <= 0);
 
     device_bytes = 0;
@@ -360,7 +364,10 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         Vg_ = V_ + halo_->G;
     } else {
         Vg_ = V_;
-        if (E) {
+        if (E && kind == hipMemcpyHostToDevice) {
+            pins_.copy(Eu_.p, p->Eu, E * 4, kind);
+            pins_.copy(Ev_.p, p->Ev, E * 4, kind);
+        } else if (E) {
             PFDR_HIP(hipMemcpyAsync(Eu_.p, p->Eu, E * 4, kind, s));
             PFDR_HIP(hipMemcpyAsync(Ev_.p, p->Ev, E * 4, kind, s));
         }
@@ -849,15 +856,17 @@ void *QuadSession<real>::device_x() {
 template <typename real>
 void QuadSession<real>::result(void *X_host, int *it, void *Obj_host, void *Dif_host) {
     hipStream_t s = stream;
+    HostPins hp(s);
     if (X_host) {
         void *dx = device_x();
-        PFDR_HIP(hipMemcpyAsync(X_host, dx, sizeof(real) * V_, hipMemcpyDeviceToHost, s));
+        hp.copy(X_host, dx, sizeof(real) * V_, hipMemcpyDeviceToHost);
     }
     if (it) *it = it_;
     if (Obj_host && rec_obj_)
-        PFDR_HIP(hipMemcpyAsync(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost, s));
+        hp.copy(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost);
     if (Dif_host && rec_dif_ && it_ > 0)
-        PFDR_HIP(hipMemcpyAsync(Dif_host, Dif_.p, sizeof(real) * it_, hipMemcpyDeviceToHost, s));
+        hp.copy(Dif_host, Dif_.p, sizeof(real) * it_, hipMemcpyDeviceToHost);
+    hp.release();
     PFDR_HIP(hipStreamSynchronize(s));
 }
 

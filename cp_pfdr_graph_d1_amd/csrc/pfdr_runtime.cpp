@@ -5,6 +5,7 @@
 
 #include <cstdarg>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -68,6 +69,132 @@ hipStream_t lib_stream() {
         PFDR_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
     }
     return streams[dev];
+}
+
+// -------------------------------------------------- device memory cache --
+namespace {
+struct CachedBlock {
+    void *p;
+    int dev;
+    hipStream_t freed_on;  // reusable once this stream is idle
+};
+struct DevCache {
+    std::mutex m;
+    std::multimap<size_t, CachedBlock> free_;  // size class -> blocks
+    size_t cached = 0;
+    size_t cap = 0;
+    DevCache() {
+        const char *e = getenv("PFDR_DEVICE_CACHE_MB");
+        cap = (size_t)(e ? atol(e) : 2048) << 20;
+    }
+};
+DevCache &dev_cache() {
+    static DevCache *c = new DevCache();  // never destroyed: no HIP calls at exit
+    return *c;
+}
+// size classes: powers of two up to 1 MiB, multiples of 2 MiB above
+size_t size_class(size_t b) {
+    if (b <= (size_t(1) << 20)) {
+        size_t r = 256;
+        while (r < b) r <<= 1;
+        return r;
+    }
+    const size_t g = size_t(2) << 20;
+    return (b + g - 1) / g * g;
+}
+void trim_cache(DevCache &c) {  // caller holds c.m
+    for (auto &kv : c.free_) (void)hipFree(kv.second.p);
+    c.free_.clear();
+    c.cached = 0;
+}
+}  // namespace
+
+void *dev_malloc(size_t bytes) {
+    DevCache &c = dev_cache();
+    const size_t sc = size_class(bytes);
+    int dev = 0;
+    PFDR_HIP(hipGetDevice(&dev));
+    if (c.cap) {
+        std::lock_guard<std::mutex> lk(c.m);
+        auto range = c.free_.equal_range(sc);
+        for (auto it = range.first; it != range.second; ++it) {
+            const CachedBlock &b = it->second;
+            if (b.dev != dev) continue;
+            if (b.freed_on && hipStreamQuery(b.freed_on) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;  // kernels queued before the free may still use it
+            }
+            void *p = b.p;
+            c.free_.erase(it);
+            c.cached -= sc;
+            return p;
+        }
+    }
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, sc);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        {
+            std::lock_guard<std::mutex> lk(c.m);
+            (void)hipDeviceSynchronize();
+            trim_cache(c);
+        }
+        e = hipMalloc(&p, sc);
+    }
+    if (e != hipSuccess) throw HipError{e, "hipMalloc", __LINE__};
+    return p;
+}
+
+void dev_free(void *p, size_t bytes) noexcept {
+    if (!p) return;
+    DevCache &c = dev_cache();
+    const size_t sc = size_class(bytes);
+    try {
+        int dev = 0;
+        hipPointerAttribute_t at{};
+        // cached only when freed under the device that owns it (the idle
+        // test needs that device's library stream); otherwise hipFree
+        if (c.cap && hipGetDevice(&dev) == hipSuccess &&
+            hipPointerGetAttributes(&at, p) == hipSuccess && at.device == dev) {
+            const hipStream_t s = lib_stream();
+            std::lock_guard<std::mutex> lk(c.m);
+            if (c.cached + sc <= c.cap) {
+                c.free_.insert({sc, CachedBlock{p, dev, s}});
+                c.cached += sc;
+                return;
+            }
+        }
+    } catch (...) {
+    }
+    (void)hipFree(p);
+}
+
+// ------------------------------------------------------------ HostPins --
+void HostPins::copy(void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+    if (!bytes) return;
+    void *host = kind == hipMemcpyHostToDevice ? const_cast<void *>(src)
+               : kind == hipMemcpyDeviceToHost ? dst : nullptr;
+    if (host && bytes >= (size_t(1) << 20) && n_ < 64) {
+        if (hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess)
+            pinned_[n_++] = host;
+        else
+            (void)hipGetLastError();  // not pinnable: the pageable path copies it
+    }
+    PFDR_HIP(hipMemcpyAsync(dst, src, bytes, kind, s_));
+}
+
+void HostPins::release() {
+    if (!n_) return;
+    const hipError_t e = hipStreamSynchronize(s_);
+    for (int i = 0; i < n_; i++) (void)hipHostUnregister(pinned_[i]);
+    n_ = 0;
+    if (e != hipSuccess) throw HipError{e, "hipStreamSynchronize (HostPins)", __LINE__};
+}
+
+HostPins::~HostPins() {
+    if (!n_) return;
+    (void)hipStreamSynchronize(s_);  // never unpin under a DMA in flight
+    for (int i = 0; i < n_; i++) (void)hipHostUnregister(pinned_[i]);
 }
 
 // ------------------------------------------------------------ Profiler --

@@ -904,11 +904,14 @@ __global__ void k_sx_obj_write(const real *__restrict__ sums, int quad, Ctrl<rea
 
 // ---------------------------------------------------------------- session
 template <typename real>
-static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s) {
+static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s,
+                       HostPins &pins) {
     if (!src || !n) { d.release(); return; }
     d.alloc(n);
-    PFDR_HIP(hipMemcpyAsync(d.p, src, n * sizeof(real),
-                            mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    if (mem == PFDR_MEM_DEVICE)
+        PFDR_HIP(hipMemcpyAsync(d.p, src, n * sizeof(real), hipMemcpyDeviceToDevice, s));
+    else
+        pins.copy(d.p, src, n * sizeof(real), hipMemcpyHostToDevice);
 }
 
 static int mask_words(int D) { return (D + 63) / 64; }
@@ -962,6 +965,7 @@ class SimplexSession final : public SessionBase {
     DevBuf<Ctrl<real>> ctrl_;
     Ctrl<real> *hctrl_ = nullptr;
     Incidence inc_;
+    HostPins pins_;  // caller arrays pinned for the setup copies
     int nbv_, nbe_;
     int vb_ = 0, nbs_ = 0, sx_nt_ = 256;  // fused vertex sweep: vertices, blocks, threads
     // false (default): the vertex sweep forms W*Z from the gathered Z and W
@@ -1004,6 +1008,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         throw std::runtime_error("P, Q, Eu, Ev and La_d1 are required");
     PFDR_HIP(hipGetDevice(&device));
     stream = lib_stream();
+    pins_.set_stream(stream);
     hipStream_t s = stream;
     V_ = p->V; K_ = p->K; E_ = p->E;
     EK_ = E_ * K_; VK_ = (long)V_ * K_;
@@ -1041,7 +1046,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         Vg_ = V_;
         Vglob_ = V_;
         Eu_.alloc(E_ ? E_ : 1); Ev_.alloc(E_ ? E_ : 1);
-        if (E_) {
+        if (E_ && kind == hipMemcpyHostToDevice) {
+            pins_.copy(Eu_.p, p->Eu, E_ * sizeof(int), kind);
+            pins_.copy(Ev_.p, p->Ev, E_ * sizeof(int), kind);
+        } else if (E_) {
             PFDR_HIP(hipMemcpyAsync(Eu_.p, p->Eu, E_ * sizeof(int), kind, s));
             PFDR_HIP(hipMemcpyAsync(Ev_.p, p->Ev, E_ * sizeof(int), kind, s));
         }
@@ -1049,11 +1057,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     check_endpoints(Eu_.p, Ev_.p, E_, Vg_, s);
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg.p, e_offset, halo_.get(), inc_, s);
     const size_t VgK = (size_t)Vg_ * K_;
-    sx_copy_in(La_d1_, p->La_d1, E_, mem, s);
-    if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s);
+    sx_copy_in(La_d1_, p->La_d1, E_, mem, s, pins_);
+    if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s, pins_);
     for (auto q : {std::make_pair(&Q_, p->Y), std::make_pair(&P_, (const void *)p->X)}) {
         q.first->alloc(VgK);  // owned rows, then the ghosts' from their owners
-        PFDR_HIP(hipMemcpyAsync(q.first->p, q.second, VK_ * sizeof(real), kind, s));
+        if (kind == hipMemcpyHostToDevice) pins_.copy(q.first->p, q.second, VK_ * sizeof(real), kind);
+        else PFDR_HIP(hipMemcpyAsync(q.first->p, q.second, VK_ * sizeof(real), kind, s));
         pullK(*q.first);
     }
     if (K_ <= 64 && !env_flag_off("PFDR_SX_FUSED")) {
@@ -1116,6 +1125,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     pullK(FP_);
     if (rec_obj_) objective();
     PFDR_HIP(hipStreamSynchronize(s));
+    pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &FP_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
@@ -1323,12 +1333,14 @@ int SimplexSession<real>::run(int iters) {
 template <typename real>
 void SimplexSession<real>::result(void *X_host, int *it, void *Obj_host, void *Dif_host) {
     hipStream_t s = stream;
-    if (X_host) PFDR_HIP(hipMemcpyAsync(X_host, P_.p, sizeof(real) * VK_, hipMemcpyDeviceToHost, s));
+    HostPins hp(s);
+    if (X_host) hp.copy(X_host, P_.p, sizeof(real) * VK_, hipMemcpyDeviceToHost);
     if (it) *it = it_;
     if (Obj_host && rec_obj_)
-        PFDR_HIP(hipMemcpyAsync(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost, s));
+        hp.copy(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost);
     if (Dif_host && rec_dif_ && it_ > 0)
-        PFDR_HIP(hipMemcpyAsync(Dif_host, Dif_.p, sizeof(real) * it_, hipMemcpyDeviceToHost, s));
+        hp.copy(Dif_host, Dif_.p, sizeof(real) * it_, hipMemcpyDeviceToHost);
+    hp.release();
     PFDR_HIP(hipStreamSynchronize(s));
 }
 
