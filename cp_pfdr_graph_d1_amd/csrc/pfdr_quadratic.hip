@@ -192,8 +192,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (xc && atoi(xc) >= 2) xcd_e_ = atoi(xc);
         const char *xv = getenv("PFDR_XCD_CHUNK_V");  // vertex sweep: idem
         if (xv && atoi(xv) >= 2) xcd_v_ = atoi(xv);
-        const char *g = getenv("PFDR_GB");  // 8 (default) or 16
-        if (g && atoi(g) == 16) gb_ = 16;
+        const char *g = getenv("PFDR_GB");  // 8 (default), 4 or 16
+        if (g && (atoi(g) == 16 || atoi(g) == 4)) gb_ = atoi(g);
         // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us)
         const char *u = getenv("PFDR_USTAGE");
         us_ = !(u && u[0] == '0');
@@ -683,6 +683,7 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
     ProfScope ps(prof, name, s);
     if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
+    else if (gb_ == 4) k_vertex_sweep<real, 4><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
     else k_vertex_sweep<real, 16><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }
 
