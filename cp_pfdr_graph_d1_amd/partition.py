@@ -110,7 +110,7 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
     parts = split_edges(Eu, off)
     hub = C.c_void_p()
     pfdr._check(lib.pfdr_loopback_create(C.byref(hub), C.c_int(k)), "pfdr_loopback_create")
-    results, errors = [None] * k, [None] * k
+    results, errors, queries = [None] * k, [None] * k, [None] * k
 
     def rank_main(r):
         try:
@@ -138,6 +138,8 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              difTol=difTol, itMax=itMax, record_obj=record_obj,
                              record_dif=record_dif, K=K, al=al, nranks=k, rank=r, comm=hub.value,
                              comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e)
+            if kind != pfdr.PFDR_KIND_SIMPLEX:
+                queries[r] = {q: s.query(q) for q in ("split_blocks", "ustaged")}
             s.run(itMax)
             results[r] = s.result()
             s.close()
@@ -158,7 +160,8 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
     if len(its) != 1:
         raise pfdr.PFDRError("ranks disagree on the iteration count: %s" % its)
     it = its.pop()
-    return X, it, results[0][2], results[0][3], {"off": off, "edges": [p.size for p in parts]}
+    return X, it, results[0][2], results[0][3], {"off": off, "edges": [p.size for p in parts],
+                                                 "queries": queries}
 
 
 def comm_init(nranks, rank, device_tensor_broadcast):

@@ -37,13 +37,14 @@ def _single(wl_name, **extra):
     return inp, X, rel
 
 
-def _partitioned(wl, inp, k):
+def _partitioned(wl, inp, k, info=False):
     from cp_pfdr_graph_d1_amd import partition as P
     kw = inp["kw"]
-    return P.solve_loopback(k, wl.kind, wl.dtype, kw["Eu"], kw["Ev"], kw["La_d1"], kw["X0"],
-                            kw["Y"], La_l1=kw.get("La_l1"), rho=kw["rho"],
-                            condMin=kw["condMin"], itMax=ITS, K=kw.get("K", 0),
-                            al=kw.get("al", 0.0))[0]
+    r = P.solve_loopback(k, wl.kind, wl.dtype, kw["Eu"], kw["Ev"], kw["La_d1"], kw["X0"],
+                         kw["Y"], La_l1=kw.get("La_l1"), rho=kw["rho"],
+                         condMin=kw["condMin"], itMax=ITS, K=kw.get("K", 0),
+                         al=kw.get("al", 0.0))
+    return (r[0], r[4]) if info else r[0]
 
 
 def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
@@ -52,8 +53,12 @@ def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
     inp, X1, _ = _single("headline")
     assert np.all(np.isfinite(X1))
     for k in (2, 4):
-        Xk = _partitioned(WORKLOADS["headline"], inp, k)
+        Xk, info = _partitioned(WORKLOADS["headline"], inp, k, info=True)
         assert np.array_equal(Xk, X1), "partitioned (%d ranks) differs" % k
+        # every rank's slab keeps the fast paths of u-sorted edges (the
+        # weak-scaling bench runs exactly these sessions over RCCL)
+        for q in info["queries"]:
+            assert q["ustaged"] == 1 and q["split_blocks"] > 0, q
     _, Xr, rel = _single("headline", reorder=pfdr.REORDER_ON)
     assert rel == 1
     assert np.array_equal(Xr, X1)
