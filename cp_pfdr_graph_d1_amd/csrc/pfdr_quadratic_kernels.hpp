@@ -120,12 +120,31 @@ template <typename real> struct GatherCap;
 template <> struct GatherCap<float> { static constexpr int v = 4096; };
 template <> struct GatherCap<double> { static constexpr int v = 4096; };
 
+// exclusive prefix sum over the block's lanes (lane order), all lanes call
+__device__ __forceinline__ int block_excl_scan(int x, int *lds /* kBlock / kWave */) {
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    int inc = x;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += y;
+    }
+    if (lane == kWave - 1) lds[w] = inc;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < w; i++) base += lds[i];
+    return base + inc - x;
+}
+
 // Split incidence of a graph whose edges are sorted by their u end (see
 // k_split_build): the u-end contributions of vertex v are the contiguous
 // run wz[uptr[v] .. uptr[v+1]) (side-major wz, u ends first), so only the
 // OTHER entries (v ends and received contributions) need an address,
-// oidx[ptr[v] - uptr[v] ...], and a 32-bit mask per vertex says, entry by
-// entry in the reference's order, which list the next term comes from.
+// oidx[ptr[v] - uptr[v] ...], and one 32-bit code per vertex says, entry by
+// entry in the reference's order, which list the next term comes from
+// (bit i set: the vertex's next own u-run entry), with a terminator bit at
+// position deg.  The lanes' offsets into the two lists are a block scan of
+// the codes' counts, so a lane reads 4 bytes of metadata, not 12.
 // The block's u-runs are staged with coalesced loads (no index, no
 // pointer chase), the others gathered; both lists meet in LDS and each
 // lane adds its vertex's terms in the reference's (e, side) order.
@@ -133,16 +152,14 @@ template <> struct GatherCap<double> { static constexpr int v = 4096; };
 template <typename real, int GB>
 __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__restrict__ ptr,
                                           const int *__restrict__ uptr,
-                                          const unsigned *__restrict__ mask,
+                                          const unsigned *__restrict__ code,
                                           const unsigned *__restrict__ oidx,
-                                          const real *__restrict__ wz, real *lds) {
+                                          const real *__restrict__ wz, real *lds, int *scan) {
     constexpr int CU = GatherCap<real>::v / 2;
     const int tid = threadIdx.x;
     const int vend = min(v0 + kBlock, V);
-    // per-lane bookkeeping first: its latency hides under the staging
-    int p0 = 0, p1 = 0, u0 = 0;
-    unsigned m = 0u;
-    if (v < V) { p0 = ptr[v]; p1 = ptr[v + 1]; u0 = uptr[v]; m = mask[v]; }
+    // per-lane code first: its latency hides under the staging
+    unsigned m = (v < V) ? code[v] : 0u;
     const int ua = uptr[v0], ub = uptr[vend];
     const int oa = ptr[v0] - ua, ob = ptr[vend] - ub;
     const int nu = ub - ua, no = ob - oa;
@@ -168,11 +185,14 @@ __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__res
             if (j < no) lds[CU + j] = wo[u];
         }
     }
-    __syncthreads();
+    // lane offsets into the staged lists: counts (u | others << 16) scanned
+    const int deg = m ? 31 - __clz(m) : 0;
+    const int cu = m ? __popc(m) - 1 : 0;
+    const int off = block_excl_scan(cu | ((deg - cu) << 16), scan);  // syncs the block
     real s = real(0);
     if (v < V) {
-        int pu = u0 - ua, po = CU + (p0 - u0) - oa;
-        for (int i = p0; i < p1; i++) {
+        int pu = off & 0xffff, po = CU + (off >> 16);
+        for (int i = 0; i < deg; i++) {
             const bool own = m & 1u;
             s += lds[own ? pu : po];
             pu += own;
@@ -202,10 +222,11 @@ static __global__ void k_uptr(long E, int V, const int *__restrict__ Eu, int *__
     for (int v = lo; v <= hi; v++) uptr[v] = (int)e;
 }
 
-// One lane per vertex: mask (bit i: the i-th CSR entry is the vertex's next
-// own u-run contribution) and the other entries' addresses in CSR order.
-// blkok[b] = 1 when every vertex of block b has <= 32 entries with its
-// u-run in edge order, and the block's runs fit the LDS halves (cap).
+// One lane per vertex: code (bit i: the i-th CSR entry is the vertex's next
+// own u-run contribution; terminator bit at the degree) and the other
+// entries' addresses in CSR order.  blkok[b] = 1 when every vertex of block
+// b has <= 31 entries with its u-run in edge order, and the block's runs
+// fit the LDS halves (cap).
 static __global__ __launch_bounds__(256) void k_split_build(int V, long E, const int *__restrict__ ptr,
                                                      const unsigned *__restrict__ idx,
                                                      const int *__restrict__ uptr, long ototal,
@@ -220,7 +241,7 @@ static __global__ __launch_bounds__(256) void k_split_build(int V, long E, const
         const long o0 = (long)p0 - u0;
         unsigned m = 0u;
         int cu = 0, co = 0;
-        if (p1 - p0 > 32) ok = 0;
+        if (p1 - p0 > 31) ok = 0;
         for (int j = p0; j < p1; j++) {
             const unsigned id = idx[j];
             if ((long)id < E) {
@@ -233,7 +254,7 @@ static __global__ __launch_bounds__(256) void k_split_build(int V, long E, const
             }
         }
         if (cu != u1 - u0) ok = 0;
-        mask[v] = m;
+        mask[v] = (p1 - p0 <= 31) ? (m | (1u << (p1 - p0))) : 0u;
     }
     const int all = __syncthreads_and(ok);
     if (threadIdx.x == 0) {
@@ -952,6 +973,7 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
+    __shared__ int scan[kBlock / kWave];
     const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
     const int blk = a.bbeg + lb;
@@ -968,7 +990,7 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     }
     real x;
     if (a.blkok && a.blkok[blk])  // block-uniform
-        x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds);
+        x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
         x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
     real num = real(0), den = real(0);
