@@ -67,23 +67,31 @@ def cpu_baseline_child(args):
             "converged_iterations": it, "time_to_tolerance_s": el,
             "sample": "whole C1 solve to difTol 1e-6 (setup included), same inputs"}))
         return
-    inp = WORKLOADS["headline"].inputs(0, 1)
+    name = args.workload if args.workload in ("c2", "c4") else "headline"
+    inp = WORKLOADS[name].inputs(0, 1)
     kw, V = inp["kw"], inp["V"]
     Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
+    if name != "headline":  # bounded sample: about 10 s of host work
+        args.cpu_k0, args.cpu_k1 = 1, 3
     times = {}
     for k in (args.cpu_k0, args.cpu_k1):
         t = time.perf_counter()
-        lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"], kw["La_l1"],
-                            0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
+        if name == "c4":
+            lib.loss_d1_simplex(kw["X0"].copy(), kw["Y"], kw["K"], Eu, Ev, kw["La_d1"],
+                                al=kw["al"], La_f=None, rho=kw["rho"], condMin=kw["condMin"],
+                                difRcd=0.0, difTol=0.0, itMax=k)
+        else:
+            lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
+                                kw["La_l1"], 0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
         times[k] = time.perf_counter() - t
     per_it = (times[args.cpu_k1] - times[args.cpu_k0]) / (args.cpu_k1 - args.cpu_k0)
     print(json.dumps({
         "value": Eu.size / per_it / 1e6, "unit": "Medge-updates/s",
         "cores": len(cores) if kind == "reference" else 1, "kind": kind,
         "iter_per_s": 1.0 / per_it,
-        "sample": "full headline graph (V=%d, E=%d) fp32, per-iteration time = "
+        "sample": "full %s graph (V=%d, E=%d) fp32, per-iteration time = "
                   "(T(%d it) - T(%d it)) / %d, setup excluded" % (
-                      V, Eu.size, args.cpu_k1, args.cpu_k0, args.cpu_k1 - args.cpu_k0),
+                      name, V, Eu.size, args.cpu_k1, args.cpu_k0, args.cpu_k1 - args.cpu_k0),
         "setup_s": times[args.cpu_k0] - args.cpu_k0 * per_it}))
 
 
@@ -136,7 +144,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first, in its own process, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and wl.name in ("headline", "c1") and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and wl.name in ("headline", "c1", "c2", "c4") and \
+            not args.no_cpu_baseline:
         cpu = run_cpu_baseline(args)
 
     import torch
