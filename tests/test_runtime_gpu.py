@@ -1,0 +1,79 @@
+"""GPU: the runtime around the solvers (pfdr_runtime.cpp).  Drop-in calls of
+alternating sizes and types reuse cached device blocks and pin the caller's
+host arrays; every call must still equal the restatement of the reference
+bit for bit (f64) — a stale or aliased cached block would show up here —
+and the host arrays must be usable (unpinned) afterwards."""
+import numpy as np
+import pytest
+
+from cp_pfdr_graph_d1_amd import pfdr
+from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(n, dt, seed):
+    shape = (n, n)
+    Eu, Ev = grid_graph(shape, 4)
+    V = n * n
+    Y = piecewise_observation(shape, seed, dt)
+    return V, Eu, Ev, Y
+
+
+def test_alternating_calls_reuse_cached_memory(gpu_lib, oracle_port):
+    k = 12
+    seq = [(40, np.float64), (300, np.float32), (40, np.float64), (520, np.float64),
+           (300, np.float32), (17, np.float64), (520, np.float64), (40, np.float64)]
+    for i, (n, dt) in enumerate(seq):
+        V, Eu, Ev, Y = _case(n, dt, i)
+        args = (np.zeros(V, dt), Y, None, 0, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                np.full(V, 0.01, dt), 0, pfdr.DIAG, None, 1.5, 1e-3, 0.0, 0.0, k)
+        X, it, _, Dif = gpu_lib.quadratic_d1_l1(*args, dif=True)
+        Xo, ito, _, _ = oracle_port.quadratic_d1_l1(*args)
+        assert it == ito == k
+        if dt == np.float64:
+            assert np.array_equal(X, Xo), (n, i)
+        else:
+            assert np.linalg.norm(X - Xo) <= 1e-6 * np.linalg.norm(Xo), (n, i)
+        # the caller's arrays were pinned only for the copies: still ordinary memory
+        Y[:] = 0
+        X[:] = 1
+
+
+def _host_pinned(lib_hip, n, dt):
+    import ctypes as C
+    p = C.c_void_p()
+    assert lib_hip.hipHostMalloc(C.byref(p), C.c_size_t(n * np.dtype(dt).itemsize), 0) == 0
+    buf = (C.c_char * (n * np.dtype(dt).itemsize)).from_address(p.value)
+    return p, np.frombuffer(buf, dt)
+
+
+def test_already_pinned_caller_arrays(gpu_lib):
+    """caller arrays that are already page-locked (hipHostMalloc) cannot be
+    registered again; their copies take the runtime's path and the result is
+    unchanged"""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")  # the runtime the library already loaded
+    V, Eu, Ev, Y = _case(600, np.float32, 3)  # 1.4 MB arrays: above the pinning threshold
+    La, L1 = np.full(Eu.size, 0.1, np.float32), np.full(V, 0.01, np.float32)
+    Xs, _, _, _ = gpu_lib.quadratic_d1_l1(np.zeros(V, np.float32), Y, None, 0, Eu, Ev, La, L1, 0,
+                                          pfdr.DIAG, None, 1.5, 1e-3, 0.0, 0.0, 5)
+    px, Xp = _host_pinned(hip, V, np.float32)
+    py, Yp = _host_pinned(hip, V, np.float32)
+    Xp[:] = 0
+    Yp[:] = Y
+    f = C.POINTER(C.c_float)
+    it = C.c_int(0)
+    Eu32, Ev32 = np.ascontiguousarray(Eu, np.int32), np.ascontiguousarray(Ev, np.int32)
+    rc = gpu_lib.lib.pfdr_quadratic_d1_l1_f32(
+        C.c_int(V), C.c_int(Eu.size), C.c_int(0), Xp.ctypes.data_as(f), Yp.ctypes.data_as(f),
+        None, Eu32.ctypes.data_as(C.POINTER(C.c_int)), Ev32.ctypes.data_as(C.POINTER(C.c_int)),
+        La.ctypes.data_as(f), L1.ctypes.data_as(f), C.c_int(0), C.c_int(pfdr.DIAG), None,
+        C.c_float(1.5), C.c_float(1e-3), C.c_float(0.0), C.c_float(0.0), C.c_int(5), C.byref(it),
+        None, None, C.c_int(0))
+    try:
+        assert rc == 0 and it.value == 5
+        assert np.array_equal(Xp, Xs)
+    finally:
+        hip.hipHostFree(px)
+        hip.hipHostFree(py)
