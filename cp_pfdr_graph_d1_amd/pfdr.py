@@ -92,6 +92,13 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise PFDRError("%s is missing: build it with "
                             "`make -C cp_pfdr_graph_d1_amd/csrc`" % LIB_PATH)
+        # torch (when installed) first: its bundled HIP runtime is then the one
+        # the library binds to, and torch.cuda keeps working in this process
+        # (loaded the other way round, torch finds no GPU: INTEGRATION.md)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         # PFDR_LIB_PATH: A/B of compile-time variants of the same library
         lib = C.CDLL(os.environ.get("PFDR_LIB_PATH") or LIB_PATH)
         lib.pfdr_last_error.restype = C.c_char_p

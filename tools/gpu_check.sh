@@ -19,7 +19,7 @@ step() {  # name limit cmd...
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }   # 1 = test failures only
 step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf -s; rc=$?
 fatal $rc && exit $rc
-[ "${SKIP_SMOKE:-0}" = 1 ] || { step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?; }
+[ "${SKIP_SMOKE:-0}" = 1 ] || { step smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" || exit $?; }
 [ "${SKIP_BENCH:-0}" = 1 ] || { step bench 900 python bench.py ${BENCH_ARGS:-} || exit $?; }
 if [ "${PROFILE:-1}" = 1 ]; then
     step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
