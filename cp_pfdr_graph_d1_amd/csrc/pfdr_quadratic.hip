@@ -90,6 +90,8 @@ class QuadSession final : public SessionBase {
     int xcd_e_ = 64, xcd_v_ = 16;
     int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
     bool us_ = true;             // edge sweep stages the u ends of u-sorted edges
+    bool seq_lane_ = false;      // amplitude sum by one lane (k_seq_sum) instead of mono_sum
+    DevBuf<char> mono_ws_;       // mono_sum scratch (tile summaries)
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
     // emap_[edge position] = original edge id (setup only)
@@ -197,6 +199,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us)
         const char *u = getenv("PFDR_USTAGE");
         us_ = !(u && u[0] == '0');
+        // amplitude sum: workgroup binade scan (default) or the one-lane loop
+        const char *q = getenv("PFDR_SEQSUM");
+        seq_lane_ = q && strcmp(q, "lane") == 0;
     }
     // prox selection (ref l1 :499-512, bounds :472-490)
     positivity_ = 0;
@@ -566,8 +571,14 @@ void QuadSession<real>::amplitude(bool init) {
         k_gather<real><<<nbv_, kBlock, 0, s>>>(V_, absval_.p, where_.p, amp_orig_.p);
         amp = amp_orig_.p;
     }
-    k_seq_sum<real><<<1, kBlock, 0, s>>>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_,
-                                         cnt_part_.p, csum_.p, ccnt_.p);
+    if (seq_lane_)
+        k_seq_sum<real><<<1, kBlock, 0, s>>>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_,
+                                             cnt_part_.p, csum_.p, ccnt_.p);
+    else {
+        if (mono_ws_.n < mono_ws_bytes<real>(V_)) mono_ws_.alloc(mono_ws_bytes<real>(V_));
+        mono_sum<real>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_, cnt_part_.p, csum_.p,
+                       ccnt_.p, mono_ws_.p, s);
+    }
     PFDR_HIP(hipGetLastError());
     if (halo_) {
         Transport &tr = *halo_->tr;

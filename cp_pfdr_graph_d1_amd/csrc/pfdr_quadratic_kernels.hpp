@@ -35,6 +35,7 @@
 #include <memory>
 
 #include "pfdr_graph.hpp"
+#include "pfdr_monosum.hpp"
 #include "pfdr_session.hpp"
 
 namespace pfdr {
@@ -505,54 +506,6 @@ __global__ __launch_bounds__(256) void k_amp(int V, int src,
     int nz = (v < V) && (a > real(0) || a < real(0));
     nz = block_sum(nz, red);
     if (threadIdx.x == 0) cnt_part[blockIdx.x] = nz;
-}
-
-// Sum of |a| accumulated strictly sequentially in increasing v, seeded with
-// the running sum of the lower ranks — the reference's single-thread order
-// over the global vertex range — so the metric rounds exactly as the
-// reference's.  One workgroup: all lanes stage chunks in LDS (double
-// buffered), lane 0 adds them in order.  Also reduces the nonzero counts.
-template <typename real>
-__global__ __launch_bounds__(256) void k_seq_sum(int V, const real *__restrict__ absval,
-                                                 const real *__restrict__ seed,
-                                                 int nparts, const int *__restrict__ cnt_part,
-                                                 real *__restrict__ sum_out,
-                                                 long long *__restrict__ cnt_out) {
-    constexpr int CH = 4096;
-    __shared__ alignas(16) real buf[2][CH];
-    __shared__ long long red[kBlock / kWave];
-    long long cnt = 0;
-    for (int i = threadIdx.x; i < nparts; i += kBlock) cnt += cnt_part[i];
-    cnt = block_sum(cnt, red);
-    real s = seed ? *seed : real(0);
-    int cur = 0;
-    for (long j = threadIdx.x; j < min((long)CH, (long)V); j += kBlock) buf[0][j] = absval[j];
-    __syncthreads();
-    for (long c0 = 0; c0 < V; c0 += CH) {
-        const long n = min((long)CH, (long)V - c0);
-        const long nxt = c0 + CH;
-        if (threadIdx.x == 0) {
-            s = ordered_add(s, buf[cur], (int)n);
-        } else if (threadIdx.x >= kWave && nxt < V) {
-            // waves 1-3 stage the next chunk, 16 loads in flight per lane
-            constexpr int B = 16, NL = kBlock - kWave;
-            const int m = (int)min((long)CH, (long)V - nxt);
-            for (int j0 = threadIdx.x - kWave; j0 < m; j0 += B * NL) {
-                real x[B];
-#pragma unroll
-                for (int u = 0; u < B; u++) x[u] = absval[nxt + min(j0 + u * NL, m - 1)];
-#pragma unroll
-                for (int u = 0; u < B; u++)
-                    if (j0 + u * NL < m) buf[cur ^ 1][j0 + u * NL] = x[u];
-            }
-        }
-        __syncthreads();
-        cur ^= 1;
-    }
-    if (threadIdx.x == 0) {
-        *sum_out = s;
-        *cnt_out = cnt;
-    }
 }
 
 // c = n / sum|a| (first call) or sum|a| / n (reconditioning) (ref :154)

@@ -37,6 +37,7 @@ EXPORTED = (
     "pfdr_loss_d1_simplex_f32", "pfdr_loss_d1_simplex_f64",
     "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
     "pfdr_gram_f32", "pfdr_gram_f64", "pfdr_operator_norm_f32", "pfdr_operator_norm_f64",
+    "pfdr_sequential_sum_f32", "pfdr_sequential_sum_f64",
     "pfdr_cp_reduce_f32", "pfdr_cp_reduce_f64",
     "pfdr_cpgraph_create", "pfdr_cpgraph_destroy", "pfdr_cpgraph_set_active",
     "pfdr_cpgraph_get_active", "pfdr_cpgraph_set_components", "pfdr_cpgraph_get_components",
@@ -611,6 +612,21 @@ def gram(A, which=0, device=False):
                                              PFDR_MEM_HOST, C.c_void_p(G.ctypes.data),
                                              C.byref(ms)), "pfdr_gram")
     return np.ascontiguousarray(G), ms.value
+
+
+def sequential_sum(a, seed=0.0, method=0):
+    """seed + a[0] + ... + a[n-1] rounded as the one-thread loop, for
+    nonnegative terms (the preconditioner's amplitude sum).  method 0: the
+    workgroup binade scan the solvers use, 1: one lane.  Returns (sum, ms)."""
+    lib = load()
+    a = np.ascontiguousarray(a)
+    ct, sfx, _ = _real(a.dtype)
+    fn = getattr(lib, "pfdr_sequential_sum_" + sfx)
+    fn.argtypes = [C.c_int64, C.c_void_p, C.c_int, ct, C.c_int, C.c_void_p, C.c_void_p]
+    out, ms = ct(0), C.c_double(0.0)
+    _check(fn(a.size, C.c_void_p(a.ctypes.data) if a.size else None, PFDR_MEM_HOST, ct(seed),
+              method, C.byref(out), C.byref(ms)), "pfdr_sequential_sum")
+    return a.dtype.type(out.value), ms.value
 
 
 def operator_norm(A, nTol=1e-3, itMax=100, nbInit=10, symmetric=False, device=False,

@@ -188,6 +188,16 @@ void pfdr_session_destroy(pfdr_session *s);
  * src/CP_PFDR_graph_quadratic_d1_l1.cpp:688-702). */
 int pfdr_gram_f32(int which, int M, int N, const float *A, int mem, float *G, double *ms);
 int pfdr_gram_f64(int which, int M, int N, const double *A, int mem, double *G, double *ms);
+/* Strictly sequential sum seed + a[0] + ... + a[n-1] of NONNEGATIVE terms,
+ * rounded exactly as the one-thread loop: the preconditioner's amplitude sum
+ * (src/PFDR_graph_quadratic_d1_l1.cpp:146-152, _bounds.cpp:143-149).  method 0:
+ * workgroup binade scan (what the solvers use), 1: one-lane loop.  mem =
+ * PFDR_MEM_HOST / _DEVICE for a; *ms (may be NULL) receives the kernel time.
+ * Negative terms give an unspecified result. */
+int pfdr_sequential_sum_f32(int64_t n, const float *a, int mem, float seed, int method,
+                            float *out, double *ms);
+int pfdr_sequential_sum_f64(int64_t n, const double *a, int mem, double seed, int method,
+                            double *out, double *ms);
 /* Squared operator norm ||A||^2 by the power method (reference
  * operator_norm_matrix<real>, include/operator_norm_matrix.hpp:12-14, same
  * argument meaning; deterministic starts).  *gram_ms (may be NULL): time of
