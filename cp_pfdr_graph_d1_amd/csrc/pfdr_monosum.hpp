@@ -90,8 +90,11 @@ struct MonoTile {
     static constexpr long TILE = (long)kMonoThreads * J;     // terms per tile
 };
 
+constexpr int kMonoSerial = 256;  // terms added by one lane after each exit
+
 // Shared state of a workgroup walking terms one tile at a time.
 struct MonoShared {
+    alignas(16) char ser[kMonoSerial * sizeof(double)];
     long long w0[kMonoThreads / kWave], w1[kMonoThreads / kWave];
     int exit_at;
     int k;
@@ -176,8 +179,9 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
                 for (int j = 0; j < J; j++)
                     if (base + (long)t * J + j < start) x[j] = real(0);
             }
-            long long i0, i1;
-            mono_run(x, ue, i0, i1);
+            long long r0, r1;
+            mono_run(x, ue, r0, r1);
+            long long i0 = r0, i1 = r1;
             mono_wave_scan<real>(i0, i1, lane);
             if (lane == kWave - 1) {
                 sh.w0[w] = i0;
@@ -195,23 +199,28 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
                 q1 = b1;
             }
             compose<real>(q0, q1, e0, e1);
-            // walk the lane's terms from its exact starting count
+            // this lane's exact starting count; only a lane whose run ends
+            // outside the binade walks its terms to find the exit
             long long cur = sat_add<real>(S, (S & 1) ? e1 : e0), cex = 0;
+            const long long end = sat_add<real>(cur, (cur & 1) ? r1 : r0);
             int mine = INT_MAX;
             real xex = real(0);
+            if (end >= TOP) {
 #pragma unroll
-            for (int j = 0; j < J; j++) {
-                long long fl;
-                int cls;
-                grid_term(x[j], ue, fl, cls);  // recomputed: fewer live registers
-                const long long inc = grid_inc<real>(fl, cls, cur);
-                if (mine == INT_MAX && (cls == 3 || cur + inc >= TOP)) {
-                    mine = t * J + j;
-                    cex = cur;
-                    xex = x[j];
+                for (int j = 0; j < J; j++) {
+                    long long fl;
+                    int cls;
+                    grid_term(x[j], ue, fl, cls);  // recomputed: fewer live registers
+                    const long long inc = grid_inc<real>(fl, cls, cur);
+                    if (mine == INT_MAX && (cls == 3 || cur + inc >= TOP)) {
+                        mine = t * J + j;
+                        cex = cur;
+                        xex = x[j];
+                    }
+                    cur = sat_add<real>(cur, inc);
                 }
-                cur = sat_add<real>(cur, inc);
             }
+            cur = end;
             if (mine != INT_MAX) atomicMin(&sh.exit_at, mine);
             __syncthreads();
             const int ex = sh.exit_at;
@@ -227,7 +236,17 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
             __syncthreads();
             s = (real)sh.sd;
             if (t == 0) sh.exit_at = INT_MAX;
+            // exits cluster where the sum is young (it doubles every few
+            // terms): the next kMonoSerial terms are added by one lane, from LDS
             start = base + ex + 1;
+            const int m = (int)min((long)kMonoSerial, hi - start);
+            real *buf = reinterpret_cast<real *>(sh.ser);
+            for (int i = t; i < m; i += NT) buf[i] = a[start + i];
+            __syncthreads();
+            if (t == 0) sh.sd = (double)ordered_add(s, buf, m);
+            __syncthreads();
+            s = (real)sh.sd;
+            start += m;
             have = false;
             left = true;
             __syncthreads();
