@@ -123,6 +123,27 @@ void build_incidence(const int *dEu, const int *dEv, int V, long E,
     PFDR_HIP(hipStreamSynchronize(s));
 }
 
+// CSR from rows listed in the wanted order within each row: stable radix
+// sort over the row bits (rows >= V were set to V and sort last)
+void build_incidence_rows(const unsigned *rows, unsigned *srows, const unsigned *vals, long n,
+                          int V, Incidence &inc, hipStream_t s) {
+    inc.V = V;
+    inc.n = n;
+    inc.ptr.alloc((size_t)V + 1);
+    inc.idx.alloc((size_t)(n > 0 ? n : 1));
+    unsigned bits = 1;
+    while (bits < 32 && ((1ull << bits) <= (unsigned long long)V)) bits++;
+    size_t tmp_bytes = 0;
+    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, rows, srows, vals, inc.idx.p,
+                                       (size_t)n, 0, bits, s));
+    DevBuf<char> tmp(tmp_bytes > 0 ? tmp_bytes : 1);
+    PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, rows, srows, vals, inc.idx.p,
+                                       (size_t)n, 0, bits, s));
+    k_incidence_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(srows, n, V, inc.ptr.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
 // Keyed CSR: entry i has key = (row << 32) | order and value = address of
 // its contribution.  Rows >= V (non-owned slots, key ~0) sort last and are
 // ignored.  ptr[v] = first sorted position of row v.

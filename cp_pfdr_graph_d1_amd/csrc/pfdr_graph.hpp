@@ -25,6 +25,11 @@ void build_incidence(const int *dEu, const int *dEv, int V, long E,
 void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int V,
                            Incidence &inc, hipStream_t s);
 
+// Same CSR when the n entries are already listed in summation order:
+// rows[i] (rows >= V set to V, dropped) stably sorted into srows.
+void build_incidence_rows(const unsigned *rows, unsigned *srows, const unsigned *vals, long n,
+                          int V, Incidence &inc, hipStream_t s);
+
 // Row offsets ptr[0..V] of n keys sorted by row (row = key >> 32).
 void keyed_rows(const unsigned long long *skey, long n, int V, int *ptr, hipStream_t s);
 

@@ -580,10 +580,30 @@ __global__ void k_slot_keys(long E, const int *__restrict__ Eu, const int *__res
     vals[E + e] = (unsigned)(E + e);
 }
 
+// rows of the 2E local slots in slot order 2e + side (rows >= V -> V)
+__global__ void k_slot_rows(long E, const int *__restrict__ Eu, const int *__restrict__ Ev, int V,
+                            unsigned *__restrict__ rows, unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int u = Eu[e], v = Ev[e];
+    reinterpret_cast<uint2 *>(rows)[e] = make_uint2(u < V ? u : V, v < V ? v : V);
+    reinterpret_cast<uint2 *>(vals)[e] = make_uint2((unsigned)e, (unsigned)(E + e));
+}
+
 void contribution_incidence(const int *Eu, const int *Ev, long E, int V, const unsigned *eg,
                             long e_offset, const Halo *halo, Incidence &inc, hipStream_t s) {
     const long R = halo ? halo->R : 0;
     const long n = 2 * E + R;
+    if (!R && !eg && E) {
+        // edge ids ascend with e and nothing is received: listed in slot
+        // order, the slots only need a STABLE sort by row (radix passes over
+        // the row bits alone, 32-bit keys)
+        DevBuf<unsigned> rows(n), vals(n), srows(n);
+        k_slot_rows<<<grid_for(E), kBlock, 0, s>>>(E, Eu, Ev, V, rows.p, vals.p);
+        PFDR_HIP(hipGetLastError());
+        build_incidence_rows(rows.p, srows.p, vals.p, n, V, inc, s);
+        return;
+    }
     DevBuf<unsigned long long> keys(n ? n : 1);
     DevBuf<unsigned> vals(n ? n : 1);
     if (E) {
