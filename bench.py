@@ -229,10 +229,13 @@ def main():
     reordered = bool(sess.query("reordered"))
     quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
     split_blocks = sess.query("split_blocks") if quad else 0
+    symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     # the edge sweep's kernel: u ends staged in LDS for u-sorted edges
     kname = "k_" + wl.dominant
     if wl.dominant == "edge_sweep" and quad and sess.query("ustaged"):
         kname = "k_edge_sweep_us"
+    if wl.dominant == "symv" and symv:
+        kname = "k_symv_tiles+k_symv_finish"
     sess.close()
     if world > 1:
         dist.destroy_process_group()
@@ -266,6 +269,7 @@ def main():
             "device_bytes": dev_bytes,
             "relabelled": reordered,
             "split_incidence_blocks": split_blocks,
+            **({"symv_upper_triangle": bool(symv)} if wl.dominant == "symv" else {}),
             "finite": finite,
         },
         "roofline": {

@@ -80,12 +80,27 @@ __device__ __forceinline__ real gram_elem(const real *A, long ld, long i, long k
 // together: every XCD has the same share of the work, and the operand
 // panels of a chunk are fetched into that XCD's L2 for all the tiles that
 // share them.  (A 3-D (bi, bj, z) grid put every tile of block row bi on
-// XCD bi: XCD 0 had 8 tiles per chunk, XCD 7 one.)
+// XCD bi: XCD 0 had 8 tiles per chunk, XCD 7 one.)  With fewer than 8
+// chunks (large P: A^tA of a wide A), XCD x gets the x-th eighth of the
+// tiles of every chunk instead (consecutive tiles share their row panel);
+// dealing chunks to XCDs there left 7 of the 8 XCDs idle.
+__host__ __device__ __forceinline__ long gram_slots(int nb, long nchunk) {
+    const long ntiles = (long)nb * (nb + 1) / 2;
+    return nchunk % 8 == 0 ? nchunk * ntiles : 8 * ((ntiles + 7) / 8) * nchunk;
+}
 __device__ __forceinline__ bool gram_block(int nb, int nchunk, int &bi, int &bj, int &z) {
     const int ntiles = nb * (nb + 1) / 2;
     const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    z = (slot / ntiles) * 8 + xcd;
-    int t = slot - (slot / ntiles) * ntiles;
+    int t;
+    if (nchunk % 8 == 0) {
+        z = (slot / ntiles) * 8 + xcd;
+        t = slot - (slot / ntiles) * ntiles;
+    } else {
+        const int per = (ntiles + 7) / 8;
+        z = slot / per;
+        t = xcd * per + (slot - z * per);
+        if (t >= ntiles) return false;
+    }
     if (z >= nchunk) return false;
     bi = 0;
     while (t >= nb - bi) { t -= nb - bi; bi++; }
@@ -252,19 +267,30 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
         }
         __syncthreads();
     }
+    // epilogue through LDS: each wave writes its T x T MFMA tiles as whole
+    // column segments of G (T contiguous reals per column) and, off the
+    // diagonal, the mirror tile the same way (the accumulator map puts
+    // consecutive lanes on consecutive COLUMNS: storing it directly made one
+    // of the two writes a stride-P scatter, which dominated for large P)
+    __shared__ real Os[4][T][T + 1];
+    real(*O)[T + 1] = Os[w];
+    constexpr int JS = 64 / T;
+    const int li = lane % T, lj = lane / T;
 #pragma unroll
     for (int x = 0; x < NT; x++)
 #pragma unroll
-        for (int y = 0; y < NT; y++)
+        for (int y = 0; y < NT; y++) {
+            const long ib = i0 + wi * WT + x * T, jb = j0 + wj * WT + y * T;
 #pragma unroll
-            for (int r = 0; r < M::NR; r++) {
-                const long i = i0 + wi * WT + x * T + M::row(lane, r);
-                const long j = j0 + wj * WT + y * T + M::col(lane, r);
-                if (i < P && j < P) {
-                    G[i + j * P] = acc[x][y][r];
-                    if (bi != bj) G[j + i * P] = acc[x][y][r];
-                }
-            }
+            for (int r = 0; r < M::NR; r++) O[M::row(lane, r)][M::col(lane, r)] = acc[x][y][r];
+            __syncthreads();
+            for (int j = lj; j < T; j += JS)
+                if (ib + li < P && jb + j < P) G[(ib + li) + (jb + j) * P] = O[li][j];
+            if (bi != bj)
+                for (int i = lj; i < T; i += JS)
+                    if (jb + li < P && ib + i < P) G[(jb + li) + (ib + i) * P] = O[i][li];
+            __syncthreads();
+        }
 }
 
 // G = sum of the chunk partials, in chunk order
@@ -297,7 +323,7 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     real *out = G;
     if (nchunk > 1) { part.alloc(PP * nchunk); out = part.p; }
     if (K == 0) { PFDR_HIP(hipMemsetAsync(G, 0, PP * sizeof(real), s)); return; }
-    const long nblk = 8 * ((nchunk + 7) / 8) * tiles;  // see gram_block
+    const long nblk = gram_slots(nb, nchunk);  // see gram_block
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
     const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0 &&

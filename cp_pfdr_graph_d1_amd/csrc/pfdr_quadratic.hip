@@ -155,6 +155,13 @@ class QuadSession final : public SessionBase {
     void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name);
     void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name);
     const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
+    // A^tA mode on one GPU with an exactly symmetric matrix: products from the
+    // block upper triangle (k_symv_tiles / k_symv_finish, half the bytes)
+    bool symv_ = false;
+    int snb_ = 0;
+    DevBuf<real> spart_;
+    void plan_symv();
+    template <int EPI> void ata_product(ColArgs<real> ca);
 };
 
 // ----------------------------------------------------------------- setup --
@@ -292,7 +299,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         rows_nb_ = (V_ + rows_cpb_ - 1) / rows_cpb_;
         Rpart_.alloc((size_t)rows_nb_ * N_);
     }
-    if (mode_ == A_ATA) { pre_.alloc(V); xout_.alloc(V); xfull_.alloc(Vglob_); }
+    if (mode_ == A_ATA) { pre_.alloc(V); xout_.alloc(V); xfull_.alloc(Vglob_); plan_symv(); }
     if (mode_ == A_DIRECT && halo_) Rsum_.alloc(N_);
 
     // control block
@@ -341,7 +348,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
                             &pre_, &Z2_, &A1_, &wz_, &R_, &Rpart_,
-                            &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_})
+                            &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_, &spart_})
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
@@ -499,10 +506,9 @@ void QuadSession<real>::forward_dense(int gate) {
         ProfScope ps(prof, "gemv_cols", s);
         k_col_dot<real, EPI_FWD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
     } else {
-        ca.len = (int)Vglob_;
         ca.w = full_x();
         ProfScope ps(prof, "symv", s);
-        k_col_dot<real, EPI_FWD_ATA><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+        ata_product<EPI_FWD_ATA>(ca);
     }
     PFDR_HIP(hipGetLastError());
 }
@@ -528,6 +534,50 @@ const real *QuadSession<real>::full_x() {
     return xfull_.p;
 }
 
+// (A^tA) w of the owned columns with epilogue EPI: block upper triangle when
+// symv_ (one GPU, exactly symmetric matrix), else one wave per column
+template <typename real>
+template <int EPI>
+void QuadSession<real>::ata_product(ColArgs<real> ca) {
+    hipStream_t s = stream;
+    ca.A = A_.p; ca.ncols = V_; ca.len = (int)Vglob_;
+    if (symv_) {
+        const long nt = (long)snb_ * (snb_ + 1) / 2;
+        k_symv_tiles<real><<<nt, kBlock, 0, s>>>(V_, A_.p, ca.w, spart_.p, ca.ctrl, ca.gate);
+        k_symv_finish<real, EPI><<<(V_ + 63) / 64, kBlock, 0, s>>>(snb_, spart_.p, ca);
+    } else {
+        k_col_dot<real, EPI><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+    }
+    PFDR_HIP(hipGetLastError());
+}
+
+// symmetric products (PFDR_SYMV: 0 off, 1 whenever valid, default for
+// V >= 4 T): one GPU, V a multiple of the 16-byte vector, A 16-byte aligned,
+// and the caller's matrix exactly symmetric (k_sym_check, one pass at setup;
+// a matrix that is not keeps the column dots, which read it as given)
+template <typename real>
+void QuadSession<real>::plan_symv() {
+    using S = SymT<real>;
+    const char *e = getenv("PFDR_SYMV");
+    const int want = e ? atoi(e) : 2;
+    if (halo_ || !want || (want == 2 && V_ < 4 * S::T)) return;
+    if (V_ % S::VW || ((uintptr_t)A_.p % 16)) return;
+    hipStream_t s = stream;
+    DevBuf<int> flag(1);
+    PFDR_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    const long n64 = (V_ + 63) / 64;
+    k_sym_check<real><<<n64 * (n64 + 1) / 2, kBlock, 0, s>>>(V_, A_.p, flag.p);
+    PFDR_HIP(hipGetLastError());
+    int f = 1;
+    PFDR_HIP(hipMemcpyAsync(&f, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    if (f) return;
+    symv_ = true;
+    snb_ = (V_ + S::T - 1) / S::T;
+    spart_.alloc((size_t)snb_ * V_);
+    symv = 1;
+}
+
 // gradient of the smooth part at the current X into grad_ (reconditioning)
 template <typename real>
 void QuadSession<real>::gradient() {
@@ -543,9 +593,8 @@ void QuadSession<real>::gradient() {
             ca.len = N_; ca.w = R_.p;
             k_col_dot<real, EPI_GRAD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
         } else {
-            ca.len = (int)Vglob_;
             ca.w = full_x();
-            k_col_dot<real, EPI_GRAD_ATA><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+            ata_product<EPI_GRAD_ATA>(ca);
         }
     }
     PFDR_HIP(hipGetLastError());
@@ -643,10 +692,10 @@ void QuadSession<real>::objective() {
     pull(xp_.p, sizeof(R2<real>));  // TV of boundary edges needs the ghosts' X
     if (mode_ == A_ATA) {
         ColArgs<real> ca{};
-        ca.A = A_.p; ca.ncols = V_; ca.len = (int)Vglob_; ca.out = pre_.p;
+        ca.out = pre_.p;
         ca.ctrl = c; ca.gate = GATE_OBJ;
         ca.w = full_x();
-        k_col_dot<real, EPI_STORE><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+        ata_product<EPI_STORE>(ca);
         papp = pre_.p;
     }
     k_obj_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, mode_, xp_.p, A_.p, papp, Y_.p,

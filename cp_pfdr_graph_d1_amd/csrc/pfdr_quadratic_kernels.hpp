@@ -347,6 +347,32 @@ struct ColArgs {
     int gate;
 };
 
+template <typename real, int EPI>
+__device__ __forceinline__ void col_epilogue(const ColArgs<real> &a, long col, real acc) {
+    if (EPI == EPI_STORE || EPI == EPI_SELF) {
+        a.out[col] = acc;
+    } else if (EPI == EPI_DIV) {
+        a.out[col] = acc / a.div[col];
+    } else if (EPI == EPI_GRAD_DIRECT) {
+        a.out[col] = -acc;
+    } else if (EPI == EPI_GRAD_ATA) {
+        real p = acc;
+        p -= a.Y[col];
+        a.out[col] = p;
+    } else {
+        real p;
+        if (EPI == EPI_FWD_DIRECT) {
+            p = -acc;
+        } else {
+            p = acc;
+            p -= a.Y[col];
+        }
+        R2<real> q = a.xp[col];
+        q.y = real(2) * q.x - a.Ga[col] * p;
+        a.xp[col] = q;
+    }
+}
+
 // One wave64 per column: 16-byte loads of the column (and of w, which
 // every wave re-reads from L2), wave-shuffle reduction, fused epilogue.
 // ref: diag of A^tA :102-110, pseudo-inverse :126-134, apply A^tA
@@ -374,28 +400,156 @@ __global__ __launch_bounds__(256) void k_col_dot(ColArgs<real> a) {
     }
     acc = wave_sum(acc);
     if (lane != 0) return;
-    if (EPI == EPI_STORE || EPI == EPI_SELF) {
-        a.out[col] = acc;
-    } else if (EPI == EPI_DIV) {
-        a.out[col] = acc / a.div[col];
-    } else if (EPI == EPI_GRAD_DIRECT) {
-        a.out[col] = -acc;
-    } else if (EPI == EPI_GRAD_ATA) {
-        real p = acc;
-        p -= a.Y[col];
-        a.out[col] = p;
-    } else {
-        real p;
-        if (EPI == EPI_FWD_DIRECT) {
-            p = -acc;
+    col_epilogue<real, EPI>(a, col, acc);
+}
+
+// ------------------------------------------- symmetric A^tA products --
+// A^tA is symmetric, so y = (A^tA) w needs only its block upper triangle:
+// half the HBM bytes of one wave per column (k_col_dot).  Tile (bi, bj),
+// bi <= bj, is T x T entries (32 row groups of one 16-byte vector: T = 128
+// f32 / 64 f64, 64 KB / 32 KB); its row part A_IJ w_J goes to part[bj][I],
+// its column part A_IJ^t w_I (bi < bj) to part[bi][J]; every (block, row)
+// slot has exactly one writer and k_symv_finish sums part[0..nb)[r] in that
+// fixed order (deterministic; a regrouping of the reference's column dot
+// products :368-376, :432-440, :462-464 like k_col_dot's).  Taken only when
+// the caller's matrix is exactly symmetric (k_sym_check), V % VW == 0 and
+// A is 16-byte aligned.
+template <typename real>
+struct SymT {
+    static constexpr int VW = Vec<real>::kPer16B, T = 32 * VW, CPT = T / 8;
+};
+
+// t = bj (bj + 1) / 2 + bi with 0 <= bi <= bj (column-major upper triangle)
+__device__ __forceinline__ void tri_index(long t, int &bi, int &bj) {
+    long j = (long)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (j * (j + 1) / 2 > t) j--;
+    while ((j + 1) * (j + 2) / 2 <= t) j++;
+    bj = (int)j;
+    bi = (int)(t - j * (j + 1) / 2);
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_symv_tiles(int V, const real *__restrict__ A,
+                                                    const real *__restrict__ w,
+                                                    real *__restrict__ part,
+                                                    const Ctrl<real> *ctrl, int gate) {
+    if (gated(ctrl, gate)) return;
+    using S = SymT<real>;
+    constexpr int VW = S::VW, T = S::T, CPT = S::CPT;
+    __shared__ real wI[T], wJ[T], csum[T];
+    __shared__ real rsum[8][T];
+    int bi, bj;
+    tri_index(blockIdx.x, bi, bj);
+    const int I0 = bi * T, J0 = bj * T;
+    const int tid = threadIdx.x;
+    const int rg = tid & 31, cg = tid >> 5;  // row group (16 B of a column), column group
+    const int r0 = I0 + rg * VW;
+    const bool rok = r0 < V;  // V % VW == 0: the lane's whole vector is in range
+    Pk<real, VW> a[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; k++) {
+        const int c = J0 + cg * CPT + k;
+        if (rok && c < V) {
+            a[k] = ldv<real, VW>(A + (size_t)V * c + r0);
         } else {
-            p = acc;
-            p -= a.Y[col];
+#pragma unroll
+            for (int j = 0; j < VW; j++) a[k].v[j] = real(0);
         }
-        R2<real> q = a.xp[col];
-        q.y = real(2) * q.x - a.Ga[col] * p;
-        a.xp[col] = q;
     }
+    if (tid < T) {
+        wI[tid] = (I0 + tid < V) ? w[I0 + tid] : real(0);
+        wJ[tid] = (J0 + tid < V) ? w[J0 + tid] : real(0);
+    }
+    __syncthreads();
+    // row part: this lane's VW rows over its CPT columns
+    real racc[VW];
+#pragma unroll
+    for (int j = 0; j < VW; j++) racc[j] = real(0);
+#pragma unroll
+    for (int k = 0; k < CPT; k++) {
+        const real wc = wJ[cg * CPT + k];
+#pragma unroll
+        for (int j = 0; j < VW; j++) racc[j] += a[k].v[j] * wc;
+    }
+#pragma unroll
+    for (int j = 0; j < VW; j++) rsum[cg][rg * VW + j] = racc[j];
+    // column part: column dots over the tile's rows, summed across the 32
+    // row groups of the half-wave (xor butterfly: every lane holds the same sum)
+    const bool offdiag = bi != bj;
+    if (offdiag) {
+        real wr[VW];
+#pragma unroll
+        for (int j = 0; j < VW; j++) wr[j] = wI[rg * VW + j];
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            real s = real(0);
+#pragma unroll
+            for (int j = 0; j < VW; j++) s += a[k].v[j] * wr[j];
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
+            if (rg == k) csum[cg * CPT + k] = s;
+        }
+    }
+    __syncthreads();
+    if (tid < T) {
+        const int r = I0 + tid;
+        if (r < V) {
+            real s = rsum[0][tid];
+#pragma unroll
+            for (int g = 1; g < 8; g++) s += rsum[g][tid];
+            part[(size_t)bj * V + r] = s;
+        }
+        const int c = J0 + tid;
+        if (offdiag && c < V) part[(size_t)bi * V + c] = csum[tid];
+    }
+}
+
+// 64 rows per block, the nb slots of a row split over 4 waves (8 loads in
+// flight per lane; one lane walking all nb slots was latency bound), the
+// four quarter sums added in a fixed order
+template <typename real, int EPI>
+__global__ __launch_bounds__(256) void k_symv_finish(int nb, const real *__restrict__ part,
+                                                     ColArgs<real> a) {
+    if (gated(a.ctrl, a.gate)) return;
+    __shared__ real q4[4][64];
+    const int rl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + rl;
+    const int per = (nb + 3) / 4, b0 = g * per, b1 = min(nb, b0 + per);
+    real acc = real(0);
+    if (r < a.ncols) {
+#pragma unroll 8
+        for (int b = b0; b < b1; b++) acc += part[(size_t)b * a.ncols + r];
+    }
+    q4[g][rl] = acc;
+    __syncthreads();
+    if (g == 0 && r < a.ncols)
+        col_epilogue<real, EPI>(a, r, ((q4[0][rl] + q4[1][rl]) + q4[2][rl]) + q4[3][rl]);
+}
+
+// flag[0] = 1 unless A (V x V, column major) is exactly symmetric: tile
+// (bi, bj), bi <= bj, of 64 x 64 entries against the mirror tile staged in LDS
+template <typename real>
+__global__ __launch_bounds__(256) void k_sym_check(int V, const real *__restrict__ A,
+                                                   int *__restrict__ flag) {
+    constexpr int T = 64;
+    __shared__ real m[T][T + 1];
+    int bi, bj;
+    tri_index(blockIdx.x, bi, bj);
+    const int I0 = bi * T, J0 = bj * T;
+    for (int i = threadIdx.x; i < T * T; i += blockDim.x) {
+        const int r = i & (T - 1), c = i >> 6;  // mirror tile: rows J, columns I
+        if (J0 + r < V && I0 + c < V) m[c][r] = A[(size_t)V * (I0 + c) + J0 + r];
+    }
+    __syncthreads();
+    bool bad = false;
+    for (int i = threadIdx.x; i < T * T; i += blockDim.x) {
+        const int r = i & (T - 1), c = i >> 6;  // tile: rows I, columns J
+        if (I0 + r < V && J0 + c < V) {
+            const real x = A[(size_t)V * (J0 + c) + I0 + r];
+            bad |= !(x == m[r][c]);
+        }
+    }
+    if (bad) flag[0] = 1;
 }
 
 // R partials: part[b][n] = sum_{v in block b} A[n + N v] X[v]

@@ -357,6 +357,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     if (!strcmp(what, "reordered")) *value = s->impl->reordered;
     else if (!strcmp(what, "split_blocks")) *value = s->impl->split_blocks;
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
+    else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
     return PFDR_OK;

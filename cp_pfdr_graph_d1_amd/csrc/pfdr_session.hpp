@@ -55,6 +55,7 @@ class SessionBase {
     int64_t reordered = 0;  // internal locality relabelling applied
     int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
+    int64_t symv = 0;          // A^tA products from the block upper triangle
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

@@ -262,4 +262,68 @@ class C5(Workload):
                          "%d GPU slab(s)" % world, graph="640x640x640")
 
 
-WORKLOADS = {w.name: w for w in (Headline(), HeadlineShuffled(), C1(), C2(), C3(), C4(), C5())}
+class C3AtA(Workload):
+    """config 3, A^tA variant ("The A^tA (N<0) variant
+    runs at V=32,768"): A (N = 1024 x V = 32,768, f32) random on the device,
+    A^tA = 32,768^2 f32 (4.3 GB) formed on the matrix cores (k_gram_v, the
+    only MFMA-shaped step), then PFDR with N = -V; the per-iteration product
+    reads the block upper triangle of the exactly symmetric matrix
+    (k_symv_tiles + k_symv_finish, priced at SURVEY's V(V+1)/2 unique entries)."""
+    name = "c3_ata"
+    metric = "PFDR_graph_quadratic_d1_l1<float> A^tA N=-32768 (from A 1024x32768): iterations/s"
+    partitionable = False
+    dominant = "symv"
+    steps = 50
+
+    def inputs(self, rank, world):
+        import time
+        import torch
+        N, nx, ny = 1024, 256, 128
+        V = nx * ny
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3 + rank)
+        # column-major N x V matrix A = (V, N) contiguous tensor
+        At = ((torch.rand((V, N), generator=g, device="cuda") - 0.5) * (12.0 / N) ** 0.5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        AtA, gram_ms = pfdr.gram(At, which=0, device=True)  # V x V, exactly symmetric
+        torch.cuda.synchronize()
+        gram_s = time.perf_counter() - t0
+        x0 = torch.zeros(V, device="cuda")
+        x0[: V // 3] = 1.0
+        x0[V // 3: 2 * V // 3] = -0.5
+        AtY = torch.mv(At, torch.mv(At.t(), x0))
+        n2, _ = pfdr.operator_norm(At, nTol=1e-3, itMax=100, nbInit=10, device=True)
+        L = torch.tensor([n2], dtype=torch.float32, device="cuda")
+        Eu, Ev = pfdr.gen_grid_edges((nx, ny), 4)
+        E = Eu.size
+        dev = lambda a, t=torch.float32: torch.as_tensor(a, dtype=t, device="cuda")
+        kw = dict(Eu=dev(Eu, torch.int32), Ev=dev(Ev, torch.int32),
+                  La_d1=torch.full((E,), 0.05, device="cuda"), X0=torch.zeros(V, device="cuda"),
+                  Y=AtY.contiguous(), A=AtA, N=-V,
+                  La_l1=torch.full((V,), 0.005, device="cuda"), L=L, Ltype=pfdr.SCAL,
+                  rho=1.5, condMin=1e-3, device=True)
+        self._keep = (At, AtA, AtY, L, kw)
+        nbt = (V + 127) // 128  # 128 x 128 MFMA block tiles, upper triangle computed
+        gram_exec = 2.0 * N * 128 * 128 * nbt * (nbt + 1) // 2
+        return dict(V=V, E=E, kw=kw, vtx_begin=0, e_offset=0,
+                    desc="C3 A^tA: A 1024x32768 fp32 -> A^tA 32768^2 fp32 (4.3 GB) on the matrix "
+                         "cores, 256x128 4-NN, N=-V path",
+                    graph="256x128",
+                    extra={"gram": {"kernel_ms": round(gram_ms, 3), "wall_s": round(gram_s, 4),
+                                    "TFLOPs_executed": round(gram_exec / (gram_ms * 1e-3) / 1e12, 1)
+                                    if gram_ms > 0 else None,
+                                    "mfma_frac": round(gram_exec / (gram_ms * 1e-3) / 157.3e12, 3)
+                                    if gram_ms > 0 else None,
+                                    "full_product_TFLOP": round(2.0 * N * V * V / 1e12, 3),
+                                    "peak_TFLOPs_f32_mfma": 157.3}})
+
+    def dominant_bytes(self, V, E):
+        # SURVEY.md §8(d): A^tA adds V(V+1)/2 unique entries per iteration
+        return 4 * V * (V + 1) // 2 + 12 * V
+
+    def iteration_bytes(self, V, E):
+        return 4 * V * (V + 1) // 2 + self.edge_bytes * E + self.vertex_bytes * V
+
+
+WORKLOADS = {w.name: w for w in (Headline(), HeadlineShuffled(), C1(), C2(), C3(), C3AtA(), C4(), C5())}
