@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="time the steps without per-kernel HIP events (A/B runs)")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-k0", type=int, default=2)
     ap.add_argument("--cpu-k1", type=int, default=12)
@@ -190,7 +192,7 @@ def main():
     # launch: for a small solve timed to tolerance they would be part of the
     # time, so that run is timed bare and a second, profiled solve gives the
     # kernel means)
-    sess.profile(not converge)
+    sess.profile(not converge and not args.no_kernel_events)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()

@@ -186,6 +186,14 @@ inline int grid_for(long n, int per_thread = 1) {
 void *dev_malloc(size_t bytes);
 void dev_free(void *p, size_t bytes) noexcept;
 
+// Small pinned host blocks (kPinnedSmall bytes: loop-control mirrors, flags)
+// pooled for the process: hipHostMalloc / hipHostFree cost ~30 / ~250 us
+// (the free synchronises the device), a large share of a small drop-in call.
+// Return a block only once no copy into or out of it is in flight.
+constexpr size_t kPinnedSmall = 256;
+void *pinned_small_get();
+void pinned_small_put(void *p) noexcept;
+
 // RAII device allocation (dev_malloc'd, freed on scope exit).
 template <typename T>
 struct DevBuf {

@@ -151,9 +151,12 @@ bool bfs_order(const int *Eu, const int *Ev, long E, int V, DevBuf<int> &order,
     DevBuf<char> tmp(tb ? tb : 1);
     k_bfs_init<<<grid_for(V), kBlock, 0, s>>>(V, lvl.p, pmin.p);
     PFDR_HIP(hipGetLastError());
-    int *h = nullptr;  // pinned: [count, root]
-    PFDR_HIP(hipHostMalloc(&h, 2 * sizeof(int), hipHostMallocDefault));
-    struct Free { int *h; ~Free() { (void)hipHostFree(h); } } fr{h};
+    int *h = static_cast<int *>(pinned_small_get());  // pinned: [count, root]
+    struct Free {
+        int *h;
+        hipStream_t s;
+        ~Free() { (void)hipStreamSynchronize(s); pinned_small_put(h); }
+    } fr{h, s};
     int placed = 0, L = 0, roots = 0, levels = 0;
     auto sort_place = [&](int n, int base) {
         size_t b = tb;

@@ -66,7 +66,10 @@ class QuadSession final : public SessionBase {
   public:
     explicit QuadSession(const pfdr_problem *p);
     ~QuadSession() override {
-        if (hctrl_) (void)hipHostFree(hctrl_);
+        if (hctrl_) {
+            (void)hipStreamSynchronize(stream);  // no control-block copy in flight
+            pinned_small_put(hctrl_);
+        }
         for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
         if (comm_) (void)hipStreamDestroy(comm_);
     }
@@ -154,6 +157,11 @@ class QuadSession final : public SessionBase {
     void plan_overlap();
     void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name);
     void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name);
+    VArgs<real> vargs(int bbeg, int bend, const Ctrl<real> *c);
+    // small single-GPU graphs: a chunk of iterations in one workgroup launch
+    // (k_tiny_iterate; PFDR_TINY = max edges, 0 = off)
+    bool tiny_ = false;
+    void tiny_chunk(int n);
     const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
     // A^tA mode on one GPU with an exactly symmetric matrix: products from the
     // block upper triangle (k_symv_tiles / k_symv_finish, half the bytes)
@@ -304,7 +312,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
 
     // control block
     ctrl_.alloc(1);
-    PFDR_HIP(hipHostMalloc(&hctrl_, sizeof(Ctrl<real>), hipHostMallocDefault));
+    static_assert(sizeof(Ctrl<real>) <= kPinnedSmall, "control block");
+    hctrl_ = static_cast<Ctrl<real> *>(pinned_small_get());
     std::memset(hctrl_, 0, sizeof(Ctrl<real>));
     const real difTol2 = difTol_ * difTol_;
     hctrl_->obj_it = -1;
@@ -356,6 +365,14 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (halo_) {
         const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
         if (!(o && o[0] == '0')) plan_overlap();
+    } else if (!rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) && E_ > 0) {
+        const char *t = getenv("PFDR_TINY");
+        // one workgroup walks the vertex blocks one after another (~3 us of
+        // dependent loads each): it beats two launches per iteration only up
+        // to two blocks (r3g: 256 vertices 8.1 -> 4.0 us/it; 1024: 9.8 -> 14.5)
+        const long maxE = t ? atol(t) : 4096;
+        tiny_ = E_ <= maxE && nbv_ <= (t ? 32 : 2);
+        tiny = tiny_ ? 1 : 0;
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
@@ -730,9 +747,21 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
 }
 
 template <typename real>
-void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name) {
-    if (bend <= bbeg) return;
-    hipStream_t s = stream;
+void QuadSession<real>::tiny_chunk(int n) {
+    const bool gated = track_ || rec_obj_;
+    TinyArgs<real> t{};
+    t.E = E_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Z2 = Z2_.p; t.A1 = A1_.p; t.La_d1 = La_d1_.p;
+    t.cw = cw_; t.rho = rho_; t.gi = gi_.p; t.wz = wz_.p;
+    t.va = vargs(0, nbv_, nullptr);
+    t.red = red_.p; t.ctrl = gated ? ctrl_.p : nullptr; t.Dif = rec_dif_ ? Dif_.p : nullptr;
+    t.track = track_ ? 1 : 0; t.iters = n;
+    ProfScope ps(prof, "tiny_iterate", stream);
+    k_tiny_iterate<real><<<1, kBlock, 0, stream>>>(t);
+    PFDR_HIP(hipGetLastError());
+}
+
+template <typename real>
+VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     VArgs<real> a{};
     a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p; a.wz = wz_.p;
     a.uptr = uptr_.p; a.mask = mask_.p; a.oidx = oidx_.p; a.blkok = blkok_.p;
@@ -741,6 +770,14 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
     a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
+    return a;
+}
+
+template <typename real>
+void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name) {
+    if (bend <= bbeg) return;
+    hipStream_t s = stream;
+    VArgs<real> a = vargs(bbeg, bend, c);
     ProfScope ps(prof, name, s);
     if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
     else if (gb_ == 4) k_vertex_sweep<real, 4><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
@@ -871,7 +908,8 @@ int QuadSession<real>::run(int iters) {
     // all-reduced values, so the control blocks agree
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
-        for (int i = 0; i < n; i++) body();
+        if (tiny_) tiny_chunk(n);
+        else for (int i = 0; i < n; i++) body();
         if (gated) {
             pull_ctrl();
             it_ = hctrl_->it;

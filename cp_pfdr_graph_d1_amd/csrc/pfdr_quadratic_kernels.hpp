@@ -1075,15 +1075,10 @@ template <typename real> struct VSweep;
 template <> struct VSweep<float> { static constexpr int waves = 8; };
 template <> struct VSweep<double> { static constexpr int waves = 4; };
 
+// one vertex block `blk` (all 256 lanes of the calling block take part)
 template <typename real, int GB>
-__global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs<real> a) {
-    if (a.ctrl && a.ctrl->halt) return;
-    __shared__ real lds[GatherCap<real>::v];
-    __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[kBlock / kWave];
-    const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
-    if (lb >= a.nb) return;
-    const int blk = a.bbeg + lb;
+__device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
+                                             real (*red)[kBlock / kWave], int *scan) {
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     // per-vertex operands first: their latency hides under the gather
@@ -1147,6 +1142,17 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     }
 }
 
+template <typename real, int GB>
+__global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real lds[GatherCap<real>::v];
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int scan[kBlock / kWave];
+    const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (lb >= a.nb) return;
+    vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan);
+}
+
 // fixed-order sum of per-block partial pairs into out[0..1]
 template <typename real>
 __global__ __launch_bounds__(256) void k_reduce_pairs(int nparts, const real *__restrict__ part,
@@ -1190,11 +1196,10 @@ __device__ __forceinline__ void decide_step(Ctrl<real> *ctrl, real num, real den
 // decision of k_decide in one launch (one kernel boundary less per
 // iteration, which counts for small graphs)
 template <typename real>
-__global__ __launch_bounds__(256) void k_reduce_decide(int nparts, const real *__restrict__ part,
-                                                       real *__restrict__ out, Ctrl<real> *ctrl,
-                                                       real *__restrict__ Dif, int track) {
-    __shared__ real red[2][kBlock / kWave];
-    if (ctrl->halt) return;  // uniform
+__device__ __forceinline__ void reduce_decide_block(int nparts, const real *__restrict__ part,
+                                                    real *__restrict__ out, Ctrl<real> *ctrl,
+                                                    real *__restrict__ Dif, int track,
+                                                    real (*red)[kBlock / kWave]) {
     real a = real(0), b = real(0);
     if (track) {
         for (int i = threadIdx.x; i < nparts; i += kBlock) {
@@ -1207,6 +1212,73 @@ __global__ __launch_bounds__(256) void k_reduce_decide(int nparts, const real *_
     if (threadIdx.x == 0) {
         if (track) { out[0] = a; out[1] = b; }
         decide_step(ctrl, a, b, Dif, track);
+    }
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_reduce_decide(int nparts, const real *__restrict__ part,
+                                                       real *__restrict__ out, Ctrl<real> *ctrl,
+                                                       real *__restrict__ Dif, int track) {
+    __shared__ real red[2][kBlock / kWave];
+    if (ctrl->halt) return;  // uniform
+    reduce_decide_block(nparts, part, out, ctrl, Dif, track, red);
+}
+
+// ------------------------------------------------ small graphs, one launch --
+// Up to `iters` whole iterations of a small single-GPU graph in ONE
+// workgroup: edge pass (per-edge edge_full, as the sweeps' lanes do), the
+// vertex blocks in order (vertex_block, the same ordered sums and
+// per-block evolution partials), the fixed-order reduction and decision
+// (reduce_decide_block), with workgroup barriers between the phases.  Every
+// value is computed by the same device code as the multi-launch path, so
+// the iterates are identical bit for bit; what goes is the 2-3 launches per
+// iteration that bound CP's reduced problems (~10 us of dispatch each).
+template <typename real>
+struct TinyArgs {
+    long E;
+    const int *Eu, *Ev;
+    real *Z2;
+    const real *A1, *La_d1;
+    real cw, rho;
+    const R2<real> *gi;
+    real *wz;
+    VArgs<real> va;     // nb = every vertex block, bbeg 0
+    real *red;          // (num, den) of the last evolution
+    Ctrl<real> *ctrl;   // null: no tracking, run exactly `iters`
+    real *Dif;
+    int track, iters;
+};
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_tiny_iterate(TinyArgs<real> t) {
+    __shared__ real lds[GatherCap<real>::v];
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int scan[kBlock / kWave];
+    __shared__ int halt;
+    R2<real> *xp = t.va.xp;
+    for (int i = 0; i < t.iters; i++) {
+        if (t.ctrl) {
+            if (threadIdx.x == 0) halt = t.ctrl->halt;
+            __syncthreads();
+            if (halt) break;  // uniform
+        }
+        for (long e = threadIdx.x; e < t.E; e += kBlock) {
+            const int u = t.Eu[e], v = t.Ev[e];
+            real zu = t.Z2[2 * e], zv = t.Z2[2 * e + 1], ou, ov;
+            edge_full<real>(xp[u], xp[v], t.gi[u], t.gi[v], edge_a(e, t.A1, t.La_d1, t.cw),
+                            t.La_d1[e], zu, zv, ou, ov, t.rho);
+            t.Z2[2 * e] = zu;
+            t.Z2[2 * e + 1] = zv;
+            t.wz[e] = ou;
+            t.wz[t.E + e] = ov;
+        }
+        __syncthreads();
+        for (int b = 0; b < t.va.nb; b++) {  // LDS reused block after block
+            vertex_block<real, 8>(t.va, b, lds, red, scan);
+            __syncthreads();
+        }
+        if (t.ctrl) reduce_decide_block(t.va.nb, t.va.part, t.red, t.ctrl, t.Dif, t.track, red);
+        __syncthreads();
     }
 }
 

@@ -169,6 +169,43 @@ void dev_free(void *p, size_t bytes) noexcept {
     (void)hipFree(p);
 }
 
+// ------------------------------------------------------ pinned blocks --
+namespace {
+struct PinnedPool {
+    std::mutex m;
+    std::vector<void *> free_;
+};
+PinnedPool &pinned_pool() {
+    static PinnedPool *p = new PinnedPool;  // outlives the HIP runtime's teardown
+    return *p;
+}
+}  // namespace
+
+void *pinned_small_get() {
+    PinnedPool &pp = pinned_pool();
+    {
+        std::lock_guard<std::mutex> lk(pp.m);
+        if (!pp.free_.empty()) {
+            void *p = pp.free_.back();
+            pp.free_.pop_back();
+            return p;
+        }
+    }
+    void *p = nullptr;
+    PFDR_HIP(hipHostMalloc(&p, kPinnedSmall, hipHostMallocDefault));
+    return p;
+}
+
+void pinned_small_put(void *p) noexcept {
+    if (!p) return;
+    PinnedPool &pp = pinned_pool();
+    try {
+        std::lock_guard<std::mutex> lk(pp.m);
+        pp.free_.push_back(p);
+    } catch (...) {
+    }
+}
+
 // ------------------------------------------------------------ HostPins --
 void HostPins::copy(void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
     if (!bytes) return;
@@ -213,6 +250,14 @@ hipEvent_t Profiler::take() {
     hipEvent_t e;
     PFDR_HIP(hipEventCreate(&e));
     return e;
+}
+
+void Profiler::reserve(int n) {
+    for (int i = (int)pool_.size(); i < n; i++) {
+        hipEvent_t e;
+        PFDR_HIP(hipEventCreate(&e));
+        pool_.push_back(e);
+    }
 }
 
 void Profiler::begin(const char *name, hipStream_t s) {
@@ -324,7 +369,10 @@ extern "C" void *pfdr_session_device_x(pfdr_session *s) {
 
 extern "C" int pfdr_session_set_profiling(pfdr_session *s, int on) {
     if (!s) return report_error("pfdr_session_set_profiling", "null session");
-    s->impl->prof.on = (on != 0);
+    PFDR_GUARD("pfdr_session_set_profiling", {
+        s->impl->prof.on = (on != 0);
+        if (on) s->impl->prof.reserve(1024);  // no event creation between timed launches
+    });
     return PFDR_OK;
 }
 
@@ -358,6 +406,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "split_blocks")) *value = s->impl->split_blocks;
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
+    else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
     return PFDR_OK;

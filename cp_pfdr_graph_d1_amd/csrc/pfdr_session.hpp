@@ -20,6 +20,7 @@ class Profiler {
     void begin(const char *name, hipStream_t s);
     void end(hipStream_t s);
     void resolve();  // call after the stream has been synchronised
+    void reserve(int n);  // pre-create n events (no hipEventCreate between launches)
     bool stats(const char *name, int *launches, double *mean_ms) const;
 
   private:
@@ -56,6 +57,7 @@ class SessionBase {
     int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
     int64_t symv = 0;          // A^tA products from the block upper triangle
+    int64_t tiny = 0;          // small graph: iterations in one workgroup launch
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

@@ -937,7 +937,12 @@ template <typename real>
 class SimplexSession final : public SessionBase {
   public:
     explicit SimplexSession(const pfdr_problem *p);
-    ~SimplexSession() override { if (hctrl_) (void)hipHostFree(hctrl_); }
+    ~SimplexSession() override {
+        if (hctrl_) {
+            (void)hipStreamSynchronize(stream);  // no control-block copy in flight
+            pinned_small_put(hctrl_);
+        }
+    }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
     void *device_x() override { return P_.p; }
@@ -1109,7 +1114,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     }
 
     ctrl_.alloc(1);
-    PFDR_HIP(hipHostMalloc(&hctrl_, sizeof(Ctrl<real>), hipHostMallocDefault));
+    static_assert(sizeof(Ctrl<real>) <= kPinnedSmall, "control block");
+    hctrl_ = static_cast<Ctrl<real> *>(pinned_small_get());
     std::memset(hctrl_, 0, sizeof(Ctrl<real>));
     hctrl_->obj_it = -1;
     hctrl_->itMax = itMax_;
