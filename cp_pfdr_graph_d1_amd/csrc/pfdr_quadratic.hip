@@ -232,6 +232,18 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         prox_ = (haslo && hashi) ? PROX_BOX : haslo ? PROX_LO : hashi ? PROX_HI : PROX_NONE;
     }
 
+    // small single-GPU graphs iterate in one workgroup (k_tiny_iterate): one
+    // workgroup walks the vertex blocks one after another (~3 us of dependent
+    // loads each), which beats two launches per iteration only up to two
+    // blocks (r3g: 256 vertices 8.1 -> 4.0 us/it; 1024: 9.8 -> 14.5).  The
+    // split incidence is not built for them (one setup round trip less).
+    if (!(p->nranks > 1 || p->comm) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
+        E_ > 0) {
+        const char *t = getenv("PFDR_TINY");
+        const long maxE = t ? atol(t) : 4096;
+        tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= (t ? 32 : 2);
+        tiny = tiny_ ? 1 : 0;
+    }
     // graph, partition plan, incidence CSR
     setup_graph(p);
     // dense A on a partition: this rank's columns (its vertices); A^tA columns
@@ -365,14 +377,6 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (halo_) {
         const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
         if (!(o && o[0] == '0')) plan_overlap();
-    } else if (!rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) && E_ > 0) {
-        const char *t = getenv("PFDR_TINY");
-        // one workgroup walks the vertex blocks one after another (~3 us of
-        // dependent loads each): it beats two launches per iteration only up
-        // to two blocks (r3g: 256 vertices 8.1 -> 4.0 us/it; 1024: 9.8 -> 14.5)
-        const long maxE = t ? atol(t) : 4096;
-        tiny_ = E_ <= maxE && nbv_ <= (t ? 32 : 2);
-        tiny = tiny_ ? 1 : 0;
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
@@ -434,7 +438,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
-    build_split();
+    if (!tiny_) build_split();
 }
 
 // Split incidence for the vertex sweep (split_sum): when the edges are
