@@ -21,7 +21,11 @@ def _mat(M, N, seed, dt):
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
-@pytest.mark.parametrize("shape", [(100, 37), (333, 129), (64, 300), (1000, 257), (20000, 96)])
+# (64, 3000) / (96, 4096) with which = 0: hundreds of output tiles and one
+# contraction chunk -- every XCD takes an eighth of the tiles (gram_block),
+# ragged (300 tiles over 8 x 38 slots) and even (528 over 8 x 66)
+@pytest.mark.parametrize("shape", [(100, 37), (333, 129), (64, 300), (1000, 257), (20000, 96),
+                                   (64, 3000), (96, 4096)])
 @pytest.mark.parametrize("which", [0, 1])
 def test_gram_matches_numpy(gpu_lib, dt, shape, which):
     A = _mat(*shape, seed=sum(shape) + which, dt=dt)
