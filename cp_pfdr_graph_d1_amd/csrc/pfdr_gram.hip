@@ -189,7 +189,13 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
     const long k0 = (long)z * kchunk;
     const long k1 = min(K, k0 + kchunk);
     real *G = Gpart + (size_t)z * P * P;
-    __shared__ alignas(16) real Ls[BK][BT + VW], Rs[BK][BT + VW];
+    // row pad: NT stores 16-byte vectors (pad VW keeps them aligned); TN
+    // stores the K-contiguous loads transposed, one real at a time, and a
+    // pad of VW put a wave's (i, k) slots on 16 of the 32 banks (4-way
+    // conflicts, 12 % of the cycles in SQ_LDS_BANK_CONFLICT on A^tA, r3q):
+    // a pad of 1 spreads them (f32)
+    constexpr int PADC = (LAYOUT == GRAM_TN && sizeof(real) == 4) ? 1 : VW;
+    __shared__ alignas(16) real Ls[BK][BT + PADC], Rs[BK][BT + PADC];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wi = w & 1, wj = w >> 1;
     const long i0 = (long)bi * BT, j0 = (long)bj * BT;
