@@ -232,16 +232,17 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         prox_ = (haslo && hashi) ? PROX_BOX : haslo ? PROX_LO : hashi ? PROX_HI : PROX_NONE;
     }
 
-    // small single-GPU graphs iterate in one workgroup (k_tiny_iterate): one
-    // workgroup walks the vertex blocks one after another (~3 us of dependent
-    // loads each), which beats two launches per iteration only up to two
-    // blocks (r3g: 256 vertices 8.1 -> 4.0 us/it; 1024: 9.8 -> 14.5).  The
-    // split incidence is not built for them (one setup round trip less).
+    // small single-GPU graphs iterate in one 1024-lane workgroup
+    // (k_tiny_iterate, four vertex blocks at a time): faster than two
+    // launches per iteration up to ~10 vertex blocks (r3u, us/iteration:
+    // 256 vertices 8.2 -> 2.2, 1024: 9.8 -> 4.6, 2025: 9.8 -> 8.4, 4096:
+    // 10.2 -> 16), so up to 8 blocks and 8192 edges.  The split incidence is
+    // not built for them (one setup round trip less).
     if (!(p->nranks > 1 || p->comm) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
         E_ > 0) {
         const char *t = getenv("PFDR_TINY");
-        const long maxE = t ? atol(t) : 4096;
-        tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= (t ? 32 : 2);
+        const long maxE = t ? atol(t) : 8192;
+        tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= (t ? 32 : 8);
         tiny = tiny_ ? 1 : 0;
     }
     // graph, partition plan, incidence CSR
@@ -760,7 +761,7 @@ void QuadSession<real>::tiny_chunk(int n) {
     t.red = red_.p; t.ctrl = gated ? ctrl_.p : nullptr; t.Dif = rec_dif_ ? Dif_.p : nullptr;
     t.track = track_ ? 1 : 0; t.iters = n;
     ProfScope ps(prof, "tiny_iterate", stream);
-    k_tiny_iterate<real><<<1, kBlock, 0, stream>>>(t);
+    k_tiny_iterate<real><<<1, kTiny, 0, stream>>>(t);
     PFDR_HIP(hipGetLastError());
 }
 

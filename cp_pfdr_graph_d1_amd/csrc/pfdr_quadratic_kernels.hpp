@@ -1075,27 +1075,34 @@ template <typename real> struct VSweep;
 template <> struct VSweep<float> { static constexpr int waves = 8; };
 template <> struct VSweep<double> { static constexpr int waves = 4; };
 
-// one vertex block `blk` (all 256 lanes of the calling block take part)
-template <typename real, int GB>
-__device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
-                                             real (*red)[kBlock / kWave], int *scan) {
-    const int v0 = blk * kBlock;
-    const int v = v0 + threadIdx.x;
-    // per-vertex operands first: their latency hides under the gather
+// per-vertex operands of the vertex sweep (loaded before the sum: their
+// latency hides under the gather)
+template <typename real>
+struct VOps {
     R2<real> q{};
     real th = real(0), yv = real(0), gv = real(0), av = real(0);
+};
+template <typename real>
+__device__ __forceinline__ VOps<real> vertex_ops(const VArgs<real> &a, int v) {
+    VOps<real> o;
     if (v < a.V) {
-        q = a.xp[v];
-        if (a.prox == PROX_L1) th = a.Th_l1[v];
-        if (a.fwd) { yv = a.Y[v]; gv = a.Ga[v]; }
-        if (a.fwd == 2) av = a.A[v];
+        o.q = a.xp[v];
+        if (a.prox == PROX_L1) o.th = a.Th_l1[v];
+        if (a.fwd) { o.yv = a.Y[v]; o.gv = a.Ga[v]; }
+        if (a.fwd == 2) o.av = a.A[v];
     }
-    real x;
-    if (a.blkok && a.blkok[blk])  // block-uniform
-        x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
-    else
-        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
-    real num = real(0), den = real(0);
+    return o;
+}
+
+// after the ordered sum x of vertex v: prox, evolution terms, next forward
+// step (ref :499-529 then :355-464 of the next iteration)
+template <typename real>
+__device__ __forceinline__ void vertex_finish(const VArgs<real> &a, int v, real x,
+                                              const VOps<real> &o, real &num, real &den) {
+    num = real(0);
+    den = real(0);
+    R2<real> q = o.q;
+    const real th = o.th, yv = o.yv, gv = o.gv, av = o.av;
     if (v < a.V) {
         switch (a.prox) {
             case PROX_L1: {
@@ -1132,6 +1139,22 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
         }
         a.xp[v] = q;
     }
+}
+
+// one vertex block `blk` (all 256 lanes of the calling block take part)
+template <typename real, int GB>
+__device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
+                                             real (*red)[kBlock / kWave], int *scan) {
+    const int v0 = blk * kBlock;
+    const int v = v0 + threadIdx.x;
+    const VOps<real> o = vertex_ops(a, v);
+    real x;
+    if (a.blkok && a.blkok[blk])  // block-uniform
+        x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
+    else
+        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+    real num, den;
+    vertex_finish(a, v, x, o, num, den);
     if (a.track) {
         num = block_sum(num, red[0]);
         den = block_sum(den, red[1]);
@@ -1227,12 +1250,12 @@ __global__ __launch_bounds__(256) void k_reduce_decide(int nparts, const real *_
 // ------------------------------------------------ small graphs, one launch --
 // Up to `iters` whole iterations of a small single-GPU graph in ONE
 // workgroup: edge pass (per-edge edge_full, as the sweeps' lanes do), the
-// vertex blocks in order (vertex_block, the same ordered sums and
-// per-block evolution partials), the fixed-order reduction and decision
-// (reduce_decide_block), with workgroup barriers between the phases.  Every
-// value is computed by the same device code as the multi-launch path, so
-// the iterates are identical bit for bit; what goes is the 2-3 launches per
-// iteration that bound CP's reduced problems (~10 us of dispatch each).
+// vertex pass (the ordered sums, vertex_finish and the per-block evolution
+// partials), the fixed-order reduction and decision (decide_step), with
+// workgroup barriers between the phases.  Every value is computed by the
+// same device code or the same sequence of operations as the multi-launch
+// path, so the iterates are identical bit for bit; what goes is the 2-3
+// launches per iteration that bound CP's reduced problems (~10 us each).
 template <typename real>
 struct TinyArgs {
     long E;
@@ -1249,20 +1272,27 @@ struct TinyArgs {
     int track, iters;
 };
 
+// 1024 lanes: four vertex blocks at a time; each lane adds its vertex's
+// CSR entries in order directly (the sequence gather_sum / split_sum add),
+// then vertex_finish; the evolution partials of each 256-vertex block and
+// the reduction before the decision repeat block_sum's tree exactly
+// (wave_sum, then the block's 4 wave sums in order).
+constexpr int kTiny = 1024;
+
 template <typename real>
-__global__ __launch_bounds__(256) void k_tiny_iterate(TinyArgs<real> t) {
-    __shared__ real lds[GatherCap<real>::v];
-    __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[kBlock / kWave];
+__global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
+    __shared__ real wred[2][kTiny / kWave];
     __shared__ int halt;
-    R2<real> *xp = t.va.xp;
-    for (int i = 0; i < t.iters; i++) {
+    const int tid = threadIdx.x;
+    const VArgs<real> &a = t.va;
+    R2<real> *xp = a.xp;
+    for (int it = 0; it < t.iters; it++) {
         if (t.ctrl) {
-            if (threadIdx.x == 0) halt = t.ctrl->halt;
+            if (tid == 0) halt = t.ctrl->halt;
             __syncthreads();
             if (halt) break;  // uniform
         }
-        for (long e = threadIdx.x; e < t.E; e += kBlock) {
+        for (long e = tid; e < t.E; e += kTiny) {
             const int u = t.Eu[e], v = t.Ev[e];
             real zu = t.Z2[2 * e], zv = t.Z2[2 * e + 1], ou, ov;
             edge_full<real>(xp[u], xp[v], t.gi[u], t.gi[v], edge_a(e, t.A1, t.La_d1, t.cw),
@@ -1273,11 +1303,49 @@ __global__ __launch_bounds__(256) void k_tiny_iterate(TinyArgs<real> t) {
             t.wz[t.E + e] = ov;
         }
         __syncthreads();
-        for (int b = 0; b < t.va.nb; b++) {  // LDS reused block after block
-            vertex_block<real, 8>(t.va, b, lds, red, scan);
-            __syncthreads();
+        for (int b0 = 0; b0 < a.nb; b0 += kTiny / kBlock) {
+            const int blk = b0 + tid / kBlock;
+            const int v = blk * kBlock + (tid & (kBlock - 1));
+            real num = real(0), den = real(0);
+            if (blk < a.nb) {
+                const VOps<real> o = vertex_ops(a, v);
+                real x = real(0);
+                if (v < a.V)
+                    for (int j = a.ptr[v]; j < a.ptr[v + 1]; j++) x += a.wz[a.idx[j]];
+                vertex_finish(a, v, x, o, num, den);
+            }
+            if (a.track) {
+                num = wave_sum(num);
+                den = wave_sum(den);
+                if ((tid & (kWave - 1)) == 0) { wred[0][tid / kWave] = num; wred[1][tid / kWave] = den; }
+                __syncthreads();
+                if ((tid & (kBlock - 1)) == 0 && blk < a.nb) {
+                    real sn = real(0), sd = real(0);
+                    const int w0 = tid / kWave;
+                    for (int i = 0; i < kBlock / kWave; i++) { sn += wred[0][w0 + i]; sd += wred[1][w0 + i]; }
+                    a.part[2 * blk] = sn;
+                    a.part[2 * blk + 1] = sd;
+                }
+                __syncthreads();
+            }
         }
-        if (t.ctrl) reduce_decide_block(t.va.nb, t.va.part, t.red, t.ctrl, t.Dif, t.track, red);
+        __syncthreads();
+        if (t.ctrl) {  // k_reduce_decide on the first 256 lanes, its tree exactly
+            real sa = real(0), sb = real(0);
+            if (t.track && tid < kBlock)
+                for (int i = tid; i < a.nb; i += kBlock) { sa += a.part[2 * i]; sb += a.part[2 * i + 1]; }
+            sa = wave_sum(sa);
+            sb = wave_sum(sb);
+            if ((tid & (kWave - 1)) == 0 && tid < kBlock) { wred[0][tid / kWave] = sa; wred[1][tid / kWave] = sb; }
+            __syncthreads();
+            if (tid == 0) {
+                real na = real(0), nb = real(0);
+                if (t.track)
+                    for (int i = 0; i < kBlock / kWave; i++) { na += wred[0][i]; nb += wred[1][i]; }
+                if (t.track) { t.red[0] = na; t.red[1] = nb; }
+                decide_step(t.ctrl, na, nb, t.Dif, t.track);
+            }
+        }
         __syncthreads();
     }
 }
