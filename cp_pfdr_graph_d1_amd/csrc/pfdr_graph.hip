@@ -119,8 +119,8 @@ void build_incidence(const int *dEu, const int *dEv, int V, long E,
     k_incidence_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey.p, n, V,
                                                        inc.ptr.p);
     PFDR_HIP(hipGetLastError());
-    // the temporaries are freed at scope exit: make sure the stream is done
-    PFDR_HIP(hipStreamSynchronize(s));
+    // temporaries freed at scope exit: dev_free reuses them only once the
+    // stream is idle (or synchronises before a real hipFree)
 }
 
 // CSR from rows listed in the wanted order within each row: stable radix
@@ -140,8 +140,7 @@ void build_incidence_rows(const unsigned *rows, unsigned *srows, const unsigned 
     PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, rows, srows, vals, inc.idx.p,
                                        (size_t)n, 0, bits, s));
     k_incidence_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(srows, n, V, inc.ptr.p);
-    PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipStreamSynchronize(s));
+    PFDR_HIP(hipGetLastError());  // temporaries: see build_incidence
 }
 
 // Keyed CSR: entry i has key = (row << 32) | order and value = address of
@@ -181,8 +180,7 @@ void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int
     PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, keys, skey.p, vals, inc.idx.p,
                                        (size_t)n, 0, 32 + vbits + 1, s));
     k_keyed_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey.p, n, V, inc.ptr.p);
-    PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipStreamSynchronize(s));
+    PFDR_HIP(hipGetLastError());  // temporaries: see build_incidence
 }
 
 }  // namespace pfdr

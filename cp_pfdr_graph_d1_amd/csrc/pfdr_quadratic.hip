@@ -291,8 +291,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         k_xp_init<real><<<grid_for(V), kBlock, 0, s>>>(V_, X0.p, xp_.p);
         PFDR_HIP(hipGetLastError());
         pull(xp_.p, sizeof(R2<real>));
-        PFDR_HIP(hipStreamSynchronize(s));
-    }
+    }  // X0 goes back to the device cache (reused once the stream is idle)
     // edge state and per-vertex metric
     const size_t En = E ? E : 1;
     Z2_.alloc(2 * En);

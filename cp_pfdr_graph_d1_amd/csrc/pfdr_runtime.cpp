@@ -166,6 +166,9 @@ void dev_free(void *p, size_t bytes) noexcept {
         }
     } catch (...) {
     }
+    // not cached: no kernel may still use it (callers free scratch right
+    // after enqueuing its last use, relying on the cache's idle rule)
+    (void)hipDeviceSynchronize();
     (void)hipFree(p);
 }
 
