@@ -342,3 +342,75 @@ extern "C" int pfdr_gen_piecewise_f64(int nx, uint64_t seed, double noise,
                                       int64_t v0, int64_t v1, double *Y) {
     return gen_piecewise(nx, seed, noise, v0, v1, Y);
 }
+
+// out[i] = lo + (hi - lo) * U(seed, i0 + i), rounded once from double:
+// the dense matrices of C3 (A ~ U(-h, h)) reproducible on any host
+template <typename T>
+static int gen_uniform(uint64_t seed, int64_t i0, int64_t n, double lo, double hi, T *out) {
+    if (n < 0 || !out) return -1;
+    host_parallel_for(0, n, [&](int64_t i) {
+        out[i] = (T)(lo + (hi - lo) * uniform(seed, (uint64_t)(i0 + i)));
+    });
+    return 0;
+}
+extern "C" int pfdr_gen_uniform_f32(uint64_t seed, int64_t i0, int64_t n, double lo,
+                                    double hi, float *out) {
+    return gen_uniform(seed, i0, n, lo, hi, out);
+}
+extern "C" int pfdr_gen_uniform_f64(uint64_t seed, int64_t i0, int64_t n, double lo,
+                                    double hi, double *out) {
+    return gen_uniform(seed, i0, n, lo, hi, out);
+}
+
+// y[n] = sum_v A[n + N v] x[v] for the column-major N-by-V matrix A, each
+// row accumulated in double in increasing v (so the result does not depend
+// on the thread count or the host), rounded once: the observations Y = A x0
+// of C3.  Threads own row ranges and walk v outermost (contiguous columns).
+template <typename T>
+static int gen_matvec(int64_t N, int64_t V, const T *A, const T *x, T *y) {
+    if (N <= 0 || V < 0 || !A || !x || !y) return -1;
+    const int64_t rows = 64;
+    const int64_t nb = (N + rows - 1) / rows;
+    host_parallel_for(0, nb, [&](int64_t b) {
+        const int64_t n0 = b * rows, n1 = std::min(N, n0 + rows);
+        double acc[rows];
+        for (int64_t n = n0; n < n1; n++) acc[n - n0] = 0.0;
+        for (int64_t v = 0; v < V; v++) {
+            const T *a = A + N * v;
+            const double xv = (double)x[v];
+            for (int64_t n = n0; n < n1; n++) acc[n - n0] += (double)a[n] * xv;
+        }
+        for (int64_t n = n0; n < n1; n++) y[n] = (T)acc[n - n0];
+    });
+    return 0;
+}
+extern "C" int pfdr_gen_matvec_f32(int64_t N, int64_t V, const float *A, const float *x,
+                                   float *y) {
+    return gen_matvec(N, V, A, x, y);
+}
+extern "C" int pfdr_gen_matvec_f64(int64_t N, int64_t V, const double *A, const double *x,
+                                   double *y) {
+    return gen_matvec(N, V, A, x, y);
+}
+
+// symmetric, diagonally dominant V-by-V matrix (an A^tA stand-in that any
+// host reproduces bit for bit): off-diagonal (u, v) = s (2 U(seed, min V +
+// max) - 1), diagonal d.  Column-major = row-major (symmetric).
+template <typename T>
+static int gen_symmetric(int64_t V, uint64_t seed, double s, double d, T *G) {
+    if (V < 0 || !G) return -1;
+    host_parallel_for(0, V, [&](int64_t v) {
+        for (int64_t u = 0; u < V; u++) {
+            const int64_t a = std::min(u, v), b = std::max(u, v);
+            G[u + V * v] = u == v ? (T)d
+                                  : (T)(s * (2.0 * uniform(seed, (uint64_t)(a * V + b)) - 1.0));
+        }
+    });
+    return 0;
+}
+extern "C" int pfdr_gen_symmetric_f32(int64_t V, uint64_t seed, double s, double d, float *G) {
+    return gen_symmetric(V, seed, s, d, G);
+}
+extern "C" int pfdr_gen_symmetric_f64(int64_t V, uint64_t seed, double s, double d, double *G) {
+    return gen_symmetric(V, seed, s, d, G);
+}

@@ -167,6 +167,13 @@ class QuadSession final : public SessionBase {
     // block upper triangle (k_symv_tiles / k_symv_finish, half the bytes)
     bool symv_ = false;
     int snb_ = 0;
+    // small dense problems on one GPU (CP's reduced problems): every dot
+    // product in the reference's sequential order (k_col_seq, k_rows_seq),
+    // bit-exact; PFDR_DENSE_EXACT = 0 off, 1 always (one GPU), default when
+    // the longest chain (max(N, V) direct, V for A^tA) is <= kExactChain
+    bool exact_ = false;
+    static constexpr long kExactChain = 8192;
+    template <int EPI> void col_product(ColArgs<real> ca);
     DevBuf<real> spart_;
     void plan_symv();
     template <int EPI> void ata_product(ColArgs<real> ca);
@@ -254,6 +261,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (mode_ == A_ATA && -(long)N_ != Vglob_)
         throw std::runtime_error("N < 0 requires A = A^tA (columns of the owned vertices, "
                                  "length V) and N = -V (V over all ranks)");
+    if ((mode_ == A_DIRECT || mode_ == A_ATA) && !halo_) {
+        const char *x = getenv("PFDR_DENSE_EXACT");
+        const long chain = mode_ == A_DIRECT ? std::max<long>(N_, V_) : (long)V_;
+        exact_ = x ? (x[0] == '1') : chain <= kExactChain;
+        dense_exact = exact_ ? 1 : 0;
+    }
     const int mem = p->mem;
     const size_t V = V_, E = E_, Vg = Vg_;
     copy_in(La_d1_, p->La_d1, E, mem, s, pins_);
@@ -340,7 +353,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (mode_ == A_DIRECT) {
         ColArgs<real> ca{};
         ca.A = A_.p; ca.ncols = V_; ca.len = N_; ca.out = diag_.p;
-        k_col_dot<real, EPI_SELF><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+        col_product<EPI_SELF>(ca);
     } else {
         k_diag<real><<<grid_for(V), kBlock, 0, s>>>(V_, mode_, A_.p, Vglob_, v0_, diag_.p);
     }
@@ -497,6 +510,12 @@ template <typename real>
 void QuadSession<real>::gemv_rows(int gate) {
     hipStream_t s = stream;
     ProfScope ps(prof, "gemv_rows", s);
+    if (exact_) {
+        k_rows_seq<real><<<grid_for(N_), kBlock, 0, s>>>(N_, V_, A_.p, xp_.p, Y_.p, R_.p,
+                                                        gate ? ctrl_.p : nullptr, gate);
+        PFDR_HIP(hipGetLastError());
+        return;
+    }
     k_rows_partial<real><<<rows_nb_, kBlock, 0, s>>>(N_, V_, A_.p, xp_.p, rows_cpb_, Rpart_.p,
                                                     gate ? ctrl_.p : nullptr, gate);
     const Ctrl<real> *c = gate ? ctrl_.p : nullptr;
@@ -525,7 +544,7 @@ void QuadSession<real>::forward_dense(int gate) {
         gemv_rows(gate == GATE_NONE ? GATE_NONE : (rec_obj_ ? GATE_ACTIVE_OR_OBJ : GATE_ACTIVE));
         ca.len = N_; ca.w = R_.p;
         ProfScope ps(prof, "gemv_cols", s);
-        k_col_dot<real, EPI_FWD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+        col_product<EPI_FWD_DIRECT>(ca);
     } else {
         ca.w = full_x();
         ProfScope ps(prof, "symv", s);
@@ -562,13 +581,27 @@ template <int EPI>
 void QuadSession<real>::ata_product(ColArgs<real> ca) {
     hipStream_t s = stream;
     ca.A = A_.p; ca.ncols = V_; ca.len = (int)Vglob_;
-    if (symv_) {
+    if (exact_) {
+        col_product<EPI>(ca);
+    } else if (symv_) {
         const long nt = (long)snb_ * (snb_ + 1) / 2;
         k_symv_tiles<real><<<nt, kBlock, 0, s>>>(V_, A_.p, ca.w, spart_.p, ca.ctrl, ca.gate);
         k_symv_finish<real, EPI><<<(V_ + 63) / 64, kBlock, 0, s>>>(snb_, spart_.p, ca);
     } else {
         k_col_dot<real, EPI><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
     }
+    PFDR_HIP(hipGetLastError());
+}
+
+// column dots with epilogue EPI: sequential order (exact_) or one wave per column
+template <typename real>
+template <int EPI>
+void QuadSession<real>::col_product(ColArgs<real> ca) {
+    hipStream_t s = stream;
+    if (exact_)
+        k_col_seq<real, EPI><<<grid_for(ca.ncols), kBlock, 0, s>>>(ca);
+    else
+        k_col_dot<real, EPI><<<grid_for((long)ca.ncols * 64), kBlock, 0, s>>>(ca);
     PFDR_HIP(hipGetLastError());
 }
 
@@ -581,7 +614,7 @@ void QuadSession<real>::plan_symv() {
     using S = SymT<real>;
     const char *e = getenv("PFDR_SYMV");
     const int want = e ? atoi(e) : 2;
-    if (halo_ || !want || (want == 2 && V_ < 4 * S::T)) return;
+    if (halo_ || exact_ || !want || (want == 2 && V_ < 4 * S::T)) return;
     if (V_ % S::VW || ((uintptr_t)A_.p % 16)) return;
     hipStream_t s = stream;
     DevBuf<int> flag(1);
@@ -612,7 +645,7 @@ void QuadSession<real>::gradient() {
         if (mode_ == A_DIRECT) {
             gemv_rows(GATE_NONE);
             ca.len = N_; ca.w = R_.p;
-            k_col_dot<real, EPI_GRAD_DIRECT><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+            col_product<EPI_GRAD_DIRECT>(ca);
         } else {
             ca.w = full_x();
             ata_product<EPI_GRAD_ATA>(ca);
@@ -629,7 +662,7 @@ void QuadSession<real>::amplitude(bool init) {
     if (init && mode_ == A_DIRECT) {
         ColArgs<real> ca{};
         ca.A = A_.p; ca.ncols = V_; ca.len = N_; ca.w = Y_.p; ca.out = pre_.p; ca.div = diag_.p;
-        k_col_dot<real, EPI_DIV><<<grid_for((long)V_ * 64), kBlock, 0, s>>>(ca);
+        col_product<EPI_DIV>(ca);
     }
     k_amp<real><<<nbv_, kBlock, 0, s>>>(V_, init ? (mode_ == A_DIRECT ? 1 : 0) : 2, Y_.p, diag_.p,
                                         pre_.p, xp_.p, absval_.p, cnt_part_.p);

@@ -403,6 +403,68 @@ __global__ __launch_bounds__(256) void k_col_dot(ColArgs<real> a) {
     col_epilogue<real, EPI>(a, col, acc);
 }
 
+// Sequential-order column dots for small dense problems (the reduced
+// problems cut pursuit hands over): one lane per column adds c[i] w[i] for
+// i = 0, 1, ... exactly as the reference's loops do (:102-110, :126-134,
+// :368-376, :432-440), so the dense modes round like the reference, bit for
+// bit.  The chain is `len` dependent adds per lane, hence only below the
+// session's exact-dense limit; 4 x 16-byte loads in flight ahead of the adds.
+template <typename real, int EPI>
+__global__ __launch_bounds__(256) void k_col_seq(ColArgs<real> a) {
+    if (gated(a.ctrl, a.gate)) return;
+    const long col = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= a.ncols) return;
+    const real *c = a.A + (size_t)a.len * col;
+    const real *w = (EPI == EPI_SELF) ? c : a.w;
+    constexpr int VW = Vec<real>::kPer16B, U = 4;
+    real acc = real(0);
+    int i = 0;
+    if ((a.len % VW) == 0 && ((uintptr_t)a.A % 16) == 0 && ((uintptr_t)w % 16) == 0) {
+        for (; i + U * VW <= a.len; i += U * VW) {
+            Pk<real, VW> x[U], y[U];
+#pragma unroll
+            for (int q = 0; q < U; q++) {
+                x[q] = ldv<real, VW>(c + i + q * VW);
+                y[q] = ldv<real, VW>(w + i + q * VW);
+            }
+#pragma unroll
+            for (int q = 0; q < U; q++)
+#pragma unroll
+                for (int j = 0; j < VW; j++) acc += x[q].v[j] * y[q].v[j];
+        }
+    }
+    for (; i < a.len; i++) acc += c[i] * w[i];
+    col_epilogue<real, EPI>(a, col, acc);
+}
+
+// R[n] = Y[n] - sum_v A[n + N v] X[v], v ascending in one lane per row
+// (ref :356-367 order; loads coalesced across the lanes), single GPU
+template <typename real>
+__global__ __launch_bounds__(256) void k_rows_seq(int N, int V, const real *__restrict__ A,
+                                                  const R2<real> *__restrict__ xp,
+                                                  const real *__restrict__ Y,
+                                                  real *__restrict__ R, const Ctrl<real> *ctrl,
+                                                  int gate) {
+    if (gated(ctrl, gate)) return;
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    constexpr int U = 8;
+    real acc = real(0);
+    int v = 0;
+    for (; v + U <= V; v += U) {
+        real c[U], x[U];
+#pragma unroll
+        for (int q = 0; q < U; q++) {
+            c[q] = A[(size_t)N * (v + q) + n];
+            x[q] = xp[v + q].x;
+        }
+#pragma unroll
+        for (int q = 0; q < U; q++) acc += c[q] * x[q];
+    }
+    for (; v < V; v++) acc += A[(size_t)N * v + n] * xp[v].x;
+    R[n] = Y[n] - acc;
+}
+
 // ------------------------------------------- symmetric A^tA products --
 // A^tA is symmetric, so y = (A^tA) w needs only its block upper triangle:
 // half the HBM bytes of one wave per column (k_col_dot).  Tile (bi, bj),

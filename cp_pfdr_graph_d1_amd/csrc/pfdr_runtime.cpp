@@ -410,6 +410,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
+    else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
     return PFDR_OK;

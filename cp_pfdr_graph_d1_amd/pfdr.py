@@ -54,6 +54,8 @@ EXPORTED = (
     "pfdr_plan_set_incoming", "pfdr_plan_finish", "pfdr_plan_destroy",
     "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
     "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
+    "pfdr_gen_uniform_f32", "pfdr_gen_uniform_f64", "pfdr_gen_matvec_f32",
+    "pfdr_gen_matvec_f64", "pfdr_gen_symmetric_f32", "pfdr_gen_symmetric_f64",
 )
 
 
@@ -830,3 +832,37 @@ def gen_piecewise(nx, V, seed, dtype=np.float32, noise=0.2, v_range=None):
           else load().pfdr_gen_piecewise_f64)
     fn(nx, seed, noise, v0, v1, Y.ctypes.data)
     return Y
+
+
+def _gen_fn(name, dtype):
+    _, sfx, _ = _real(dtype)
+    return getattr(load(), "pfdr_gen_%s_%s" % (name, sfx))
+
+
+def gen_uniform(seed, n, lo, hi, dtype=np.float32, i0=0, out=None):
+    """out[i] = lo + (hi - lo) U(seed, i0 + i) (native, multi-threaded)."""
+    out = np.empty(n, dtype) if out is None else out
+    fn = _gen_fn("uniform", out.dtype)
+    fn.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_double, C.c_double, C.c_void_p]
+    _check(fn(seed, i0, n, lo, hi, out.ctypes.data), "pfdr_gen_uniform")
+    return out
+
+
+def gen_matvec(A_cm, N, V, x):
+    """y = A x for the column-major N-by-V matrix held in A_cm (length N V),
+    each row summed in double in increasing column order (deterministic)."""
+    y = np.empty(N, A_cm.dtype)
+    x = np.ascontiguousarray(x, A_cm.dtype)
+    fn = _gen_fn("matvec", A_cm.dtype)
+    fn.argtypes = [C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    _check(fn(N, V, A_cm.ctypes.data, x.ctypes.data, y.ctypes.data), "pfdr_gen_matvec")
+    return y
+
+
+def gen_symmetric(V, seed, s, d, dtype=np.float32):
+    """Symmetric diagonally dominant V-by-V matrix (flat, column-major)."""
+    G = np.empty(V * V, dtype)
+    fn = _gen_fn("symmetric", dtype)
+    fn.argtypes = [C.c_int64, C.c_uint64, C.c_double, C.c_double, C.c_void_p]
+    _check(fn(V, seed, s, d, G.ctypes.data), "pfdr_gen_symmetric")
+    return G

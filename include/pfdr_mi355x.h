@@ -175,7 +175,9 @@ int pfdr_session_sync(pfdr_session *s);
 /* Bytes of device memory held by the session. */
 int64_t pfdr_session_device_bytes(pfdr_session *s);
 /* Session facts by name: "reordered" (1 when the internal locality
- * relabelling is active), "device_bytes". */
+ * relabelling is active), "device_bytes", "split_blocks", "ustaged",
+ * "symv", "tiny", "dense_exact" (1: the dense products run in the
+ * reference's sequential order, bit-exact; small single-GPU problems). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 
@@ -338,6 +340,18 @@ int pfdr_gen_piecewise_f32(int nx, uint64_t seed, double noise,
     int64_t v_begin, int64_t v_end, float *Y);
 int pfdr_gen_piecewise_f64(int nx, uint64_t seed, double noise,
     int64_t v_begin, int64_t v_end, double *Y);
+/* Dense inputs (C3): out[i] = lo + (hi-lo) U(seed, i0+i); y = A x with each
+ * row accumulated in double in increasing column order (host- and
+ * thread-count independent); a symmetric diagonally dominant V-by-V matrix
+ * (off-diagonal s (2U - 1), diagonal d). */
+int pfdr_gen_uniform_f32(uint64_t seed, int64_t i0, int64_t n, double lo, double hi,
+    float *out);
+int pfdr_gen_uniform_f64(uint64_t seed, int64_t i0, int64_t n, double lo, double hi,
+    double *out);
+int pfdr_gen_matvec_f32(int64_t N, int64_t V, const float *A, const float *x, float *y);
+int pfdr_gen_matvec_f64(int64_t N, int64_t V, const double *A, const double *x, double *y);
+int pfdr_gen_symmetric_f32(int64_t V, uint64_t seed, double s, double d, float *G);
+int pfdr_gen_symmetric_f64(int64_t V, uint64_t seed, double s, double d, double *G);
 
 #ifdef __cplusplus
 }

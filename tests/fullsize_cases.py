@@ -1,0 +1,173 @@
+"""TEST INFRASTRUCTURE — the BASELINE.json configurations at their FULL size
+(SURVEY.md §8(d)), as deterministic inputs any host regenerates bit for bit
+with the library's native generators (splitmix64 laws, no device needed):
+
+  c1_fixk25 / c1_conv  C1: 256x256 4-NN, l22 semantics (N = 0, DIAG), f64;
+                       25 fixed iterations, and converged to difTol 1e-6
+  headline_k3          10M-vertex jittered 6-NN (E = 60M), f32, 3 iterations
+  c2_k2                256^3 6-NN (V 16.8M, E 50.1M), f32, 2 iterations
+  c3_direct_k2         dense A, N = 1024 x V = 2M (8.2 GB) f32, direct (N > 0)
+                       path, SCAL L, 2 iterations
+  c3_ata_k3            A^tA mode (N = -V) at SURVEY's V = 32,768 (4.3 GB):
+                       a symmetric diagonally dominant stand-in matrix, 3 its
+  c4_k2                simplex K = 10, KL al = 0.1, 2236^2 8-nbr (V 5.0M,
+                       E 20.0M), f32, 2 iterations
+  c5_k1                bounds [0, 1], 640^3 6-NN (V 262M, E 785M), f32, 1 it
+
+tests/golden/make_fullsize.py runs the REFERENCE (oracle/_ref/
+libpfdr_ref_seq.so) on each and commits digests (tests/golden/fullsize/);
+tests/test_fullsize_pin_gpu.py runs the MI355X library through its C ABI
+on the same inputs and compares.
+"""
+import numpy as np
+
+from cp_pfdr_graph_d1_amd import pfdr
+
+# C3 scalar Lipschitz constant L = ||A||^2: computed once by
+# make_fullsize.py (power method in float64) and stored with the digest
+CASES = ("c1_fixk25", "c1_conv", "headline_k3", "c2_k2", "c3_direct_k2", "c3_ata_k3",
+         "c4_k2", "c5_k1")
+SAMPLE_SEED = 0x5EED
+
+
+def sample_index(n, m, seed=SAMPLE_SEED):
+    """m distinct-ish deterministic sample positions in [0, n) (sorted)."""
+    u = pfdr.gen_uniform(seed, min(m, n), 0.0, 1.0, np.float64)
+    idx = np.unique(np.minimum((u * n).astype(np.int64), n - 1))
+    return idx
+
+
+def _piecewise_l1(shape, seed, conn, dtype, La_d1=0.1, La_l1=0.01, knn=False):
+    if knn:
+        Eu, Ev = pfdr.gen_knn_jitter_grid(shape, 6, 6, 0.25)
+    else:
+        Eu, Ev = pfdr.gen_grid_edges(shape, conn)
+    V = int(np.prod(shape))
+    Y = pfdr.gen_piecewise(shape[0], V, seed, dtype, 0.2)
+    E = Eu.size
+    return dict(V=V, E=E, X0=np.zeros(V, dtype), Y=Y, Eu=Eu, Ev=Ev,
+                La_d1=np.full(E, La_d1, dtype), La_l1=np.full(V, La_l1, dtype))
+
+
+def build(name, L_c3=None):
+    """-> dict(solver, dtype, args (reference argument names), sample_m)"""
+    if name.startswith("c1"):
+        from cp_pfdr_graph_d1_amd.graphs import grid_graph, uniform
+        Eu, Ev = grid_graph((256, 256), 4)
+        V, E = 65536, Eu.size
+        x = np.arange(V) % 256
+        Y = np.where(x < 128, 1.0, -0.5) + (2 * uniform(1, np.arange(V)) - 1) * 0.2
+        conv = name == "c1_conv"
+        # l22: La_l2 = NULL -> identity weights, DIAG with A = L = NULL
+        a = dict(X0=np.zeros(V), Y=Y, A=None, N=0, Eu=Eu.astype(np.int32),
+                 Ev=Ev.astype(np.int32), La_d1=np.full(E, 0.1), La_l1=np.full(V, 0.01),
+                 positivity=0, Ltype=pfdr.DIAG, L=None, rho=1.5, condMin=1e-3, difRcd=0.0,
+                 difTol=1e-6 if conv else 0.0, itMax=10000 if conv else 25)
+        return dict(solver="l1", dtype=np.float64, args=a, sample_m=V)
+    if name == "headline_k3":
+        d = _piecewise_l1((250, 200, 200), 2, 6, np.float32, knn=True)
+        # headline Y: gen_piecewise(nx=250, seed 2) as tools/workloads.py
+        a = dict(d, A=None, N=0, positivity=0, Ltype=pfdr.SCAL, L=None, rho=1.5,
+                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=3)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=4096)
+    if name == "c2_k2":
+        d = _piecewise_l1((256, 256, 256), 2, 6, np.float32)
+        a = dict(d, A=None, N=0, positivity=0, Ltype=pfdr.SCAL, L=None, rho=1.5,
+                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=2)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=4096)
+    if name == "c3_direct_k2":
+        N, nx, ny = 1024, 2000, 1000
+        V = nx * ny
+        h = (3.0 / N) ** 0.5  # U(-h, h): variance 1/N
+        A = pfdr.gen_uniform(3, N * V, -h, h, np.float32)  # column-major N x V
+        x0 = np.zeros(V, np.float32)
+        x0[: V // 3] = 1.0
+        x0[V // 3: 2 * V // 3] = -0.5
+        Y = pfdr.gen_matvec(A, N, V, x0)
+        Eu, Ev = pfdr.gen_grid_edges((nx, ny), 4)
+        E = Eu.size
+        L = None if L_c3 is None else np.array([L_c3], np.float32)
+        a = dict(X0=np.zeros(V, np.float32), Y=Y, A=A, N=N, Eu=Eu, Ev=Ev,
+                 La_d1=np.full(E, 0.05, np.float32), La_l1=np.full(V, 0.005, np.float32),
+                 positivity=0, Ltype=pfdr.SCAL, L=L, rho=1.5, condMin=1e-3, difRcd=0.0,
+                 difTol=0.0, itMax=2)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=65536)
+    if name == "c3_ata_k3":
+        nx, ny = 256, 128
+        V = nx * ny
+        G = pfdr.gen_symmetric(V, 33, 1.0 / V, 1.0, np.float32)
+        AtY = pfdr.gen_piecewise(nx, V, 34, np.float32, 0.2)
+        Eu, Ev = pfdr.gen_grid_edges((nx, ny), 4)
+        E = Eu.size
+        # Gershgorin: ||G|| <= 1 + (V - 1)/V < 2
+        a = dict(X0=np.zeros(V, np.float32), Y=AtY, A=G, N=-V, Eu=Eu, Ev=Ev,
+                 La_d1=np.full(E, 0.05, np.float32), La_l1=np.full(V, 0.005, np.float32),
+                 positivity=0, Ltype=pfdr.SCAL, L=np.array([2.0], np.float32), rho=1.5,
+                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=3)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=V)
+    if name == "c4_k2":
+        from cp_pfdr_graph_d1_amd.graphs import simplex_observation
+        n, K = 2236, 10
+        V = n * n
+        Eu, Ev = pfdr.gen_grid_edges((n, n), 8)
+        v = np.arange(V)
+        lab = ((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)
+        Q = simplex_observation(V, K, 4, lab, np.float32)
+        E = Eu.size
+        a = dict(P0=Q.copy(), Q=Q, K=K, Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32),
+                 al=0.1, La_f=None, rho=1.0, condMin=0.1, difRcd=0.0, difTol=0.0, itMax=2)
+        return dict(solver="simplex", dtype=np.float32, args=a, sample_m=16384)
+    if name == "c5_k1":
+        shape = (640, 640, 640)
+        Eu, Ev = pfdr.gen_grid_edges(shape, 6)
+        V = 640 ** 3
+        Y = pfdr.gen_piecewise(640, V, 5, np.float32, 0.2)
+        E = Eu.size
+        a = dict(X0=np.zeros(V, np.float32), Y=Y, A=None, N=0, Eu=Eu, Ev=Ev,
+                 La_d1=np.full(E, 0.1, np.float32), lo=0.0, hi=1.0, Ltype=pfdr.SCAL, L=None,
+                 rho=1.5, condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=1)
+        return dict(solver="bounds", dtype=np.float32, args=a, sample_m=4096)
+    raise KeyError(name)
+
+
+def run(lib, case):
+    """Run `case` on `lib` (pfdr.Lib() or oracle.Oracle(...): same argument
+    lists) -> (X, it, Dif)."""
+    a, s = case["args"], case["solver"]
+    if s == "l1":
+        X, it, _, Dif = lib.quadratic_d1_l1(
+            a["X0"], a["Y"], a["A"], a["N"], a["Eu"], a["Ev"], a["La_d1"], a["La_l1"],
+            a["positivity"], a["Ltype"], a["L"], a["rho"], a["condMin"], a["difRcd"],
+            a["difTol"], a["itMax"], dif=True)
+    elif s == "bounds":
+        X, it, _, Dif = lib.quadratic_d1_bounds(
+            a["X0"], a["Y"], a["A"], a["N"], a["Eu"], a["Ev"], a["La_d1"], a["lo"], a["hi"],
+            a["Ltype"], a["L"], a["rho"], a["condMin"], a["difRcd"], a["difTol"], a["itMax"],
+            dif=True)
+    else:
+        X, it, _, Dif = lib.loss_d1_simplex(
+            a["P0"], a["Q"], a["K"], a["Eu"], a["Ev"], a["La_d1"], a["al"], a["La_f"],
+            a["rho"], a["condMin"], a["difRcd"], a["difTol"], a["itMax"], dif=True)
+    return X, it, Dif[:it]
+
+
+def input_digest(case):
+    """sha256 over every input array of the case (sorted by name): proves the
+    GPU box regenerated the very inputs the reference was run on."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(case["args"]):
+        v = case["args"][k]
+        if isinstance(v, np.ndarray):
+            h.update(k.encode())
+            h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()
+
+
+def digest(X, it, Dif, sample_m):
+    import hashlib
+    idx = sample_index(X.size, sample_m)
+    return dict(sha256=np.str_(hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest()),
+                norm2=np.float64(np.linalg.norm(X.astype(np.float64))), it=np.int32(it),
+                Dif=np.asarray(Dif), idx=idx.astype(np.int64), sample=X[idx].copy(),
+                size=np.int64(X.size), finite=np.bool_(np.all(np.isfinite(X))))

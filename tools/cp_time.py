@@ -1,12 +1,12 @@
-"""End-to-end cut-pursuit timing: the reference's CP driver
-(src/CP_PFDR_graph_quadratic_d1_l1.cpp, compiled unchanged by oracle/Makefile)
+"""End-to-end cut-pursuit timing: one of the reference's CP drivers
+(src/CP_PFDR_graph_*.cpp, compiled unchanged by oracle/Makefile)
 linked with the reference PFDR (CPU, sequential PFDR objects as in the parity
 test) and with libpfdr_mi355x.so (the drop-in).  Prints one JSON line per
 problem: CP wall times of both builds, whether the CP outputs are
 identical, and (PFDR_TRACE=1) the drop-in's per-call setup / iterate /
 copy-back split.
 
-    python tools/cp_time.py [--shapes 256x256,512x512] [--dtype f32]
+    python tools/cp_time.py [--shapes 256x256,512x512] [--dtype f32] [--kind l1 --mode diag]
 """
 import argparse
 import json
@@ -23,25 +23,13 @@ sys.path.insert(0, ROOT)
 REF = os.path.join(ROOT, "oracle", "_ref")
 
 
-def write_problem(path, shape, dt, seed, la_d1=0.3, la_l1=0.02, cp_itmax=8, pfdr_itmax=2000):
-    """in.bin of oracle/harness/cp_driver.cpp: l22-style CP problem on a
-    4-neighbour grid (A = diag, Y = A * observation)."""
-    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, uniform
-    Eu, Ev = grid_graph(shape, 4)
-    V = int(np.prod(shape))
-    Y = piecewise_observation(shape, seed, dt, noise=0.4)
-    A = (0.5 + uniform(seed + 1, np.arange(V))).astype(dt)
-    with open(path, "wb") as f:
-        np.array([V, Eu.size, 1 if dt == np.float64 else 0, cp_itmax, pfdr_itmax, 0],
-                 np.int32).tofile(f)
-        np.array([1e-4, 1e-5, 1.5, 1e-3], np.float64).tofile(f)
-        (A * Y).astype(dt).tofile(f)
-        A.tofile(f)
-        Eu.astype(np.int32).tofile(f)
-        Ev.astype(np.int32).tofile(f)
-        np.full(Eu.size, la_d1, dt).tofile(f)
-        np.full(V, la_l1, dt).tofile(f)
-    return V, Eu.size
+def write_problem(path, shape, dt, kind="l1", mode="diag"):
+    """in.bin of oracle/harness/cp_drivers.cpp (tests/cp_problems.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cp_problems as P
+    p = P.problem(kind, mode, dt, nx=shape[0], ny=shape[1])
+    P.write(path, p)
+    return p["V"], p["E"]
 
 
 def run(drv, inp, out, env=None):
@@ -59,20 +47,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="256x256,512x512,1024x1024")
     ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--kind", default="l1", help="l1, duplex, bounds or simplex")
+    ap.add_argument("--mode", default="diag", help="diag, identity, direct, AtA")
     args = ap.parse_args()
     dt = np.float64 if args.dtype == "f64" else np.float32
     tmp = tempfile.mkdtemp()
     for sh in args.shapes.split(","):
         shape = tuple(int(x) for x in sh.split("x"))
         inp = os.path.join(tmp, "in.bin")
-        V, E = write_problem(inp, shape, dt, 7)
-        t_ref, rv, it, _, o_ref = run(os.path.join(REF, "cp_driver_ref"), inp,
+        V, E = write_problem(inp, shape, dt, args.kind, args.mode)
+        t_ref, rv, it, _, o_ref = run(os.path.join(REF, "cp_%s_ref" % args.kind), inp,
                                       os.path.join(tmp, "o1"))
-        t_gpu, rv2, it2, calls, o_gpu = run(os.path.join(REF, "cp_driver_mi355x"), inp,
+        t_gpu, rv2, it2, calls, o_gpu = run(os.path.join(REF, "cp_%s_mi355x" % args.kind), inp,
                                             os.path.join(tmp, "o2"), {"PFDR_TRACE": "1"})
         s = lambda k: round(sum(float(c[k]) for c in calls), 3)
         print(json.dumps({
-            "shape": sh, "dtype": args.dtype, "V": V, "E": E, "rV": rv, "CP_it": it,
+            "shape": sh, "kind": args.kind, "mode": args.mode, "dtype": args.dtype, "V": V, "E": E, "rV": rv, "CP_it": it,
             "identical": o_ref == o_gpu and (rv, it) == (rv2, it2),
             "cp_ref_cpu_s": t_ref, "cp_mi355x_s": t_gpu,
             "pfdr_calls": len(calls),
