@@ -13,8 +13,12 @@ reported separately).
 
 N > 1 (launched by torch.distributed.run, one process per GPU): every rank
 owns a z-slab of the graph (1-D vertex-range partition, RCCL halo exchange,
-DESIGN.md §6); the headline is weak-scaled (a 10M-vertex slab per GPU);
-``value`` = all ranks' edge updates / max-over-ranks time.
+DESIGN.md §6).  Default ``--scaling strong``: the metric's fixed 10M-vertex
+graph is split across the N GPUs; ``--scaling weak`` gives every GPU a
+10M-vertex slab of an N-times taller grid.  ``value`` = all ranks' edge
+updates / max-over-ranks time.  The ranks bootstrap over a gloo (host)
+process group; the one RCCL communicator of the process is the library's
+(halo exchanges, scalar all-reduces, the max-over-ranks timing reduction).
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
 (HIP events on the session stream over the timed region; PMC traffic from
@@ -126,6 +130,8 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="headline")
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
+                    help="N > 1: split the configuration's graph (strong) or one slab per GPU (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-kernel HIP events (A/B runs)")
@@ -155,27 +161,30 @@ def main():
     from cp_pfdr_graph_d1_amd import pfdr
 
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1:  # host bootstrap only: the data path uses the library's RCCL communicator
+        dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    strong = args.scaling == "strong" or wl.scaling == "strong"
     t = time.perf_counter()
-    inp = wl.inputs(rank, world)
+    inp = wl.inputs(rank, world, strong)
     gen_s = time.perf_counter() - t
     V, E = inp["V"], inp["E"]
     converge = bool(inp.get("converge", False))
     kw = inp["kw"]
-    dist_kw, parallelism = {}, "single"
+    dist_kw, parallelism, comm = {}, "single", None
     if world > 1 and wl.partitionable:  # 1-D vertex-range partition, RCCL halo over xGMI
         from cp_pfdr_graph_d1_amd import partition
         comm = partition.comm_init(world, rank, lambda x: dist.broadcast(x, 0))
         dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
                        vtx_begin=inp["vtx_begin"], e_offset=inp["e_offset"])
-        parallelism = "vertex-partition x%d (RCCL halo)" % world
+        parallelism = "vertex-partition x%d (RCCL halo), %s scaling" % (
+            world, "strong" if strong else "weak")
     elif world > 1:
+        strong = False
         parallelism = "independent replicas x%d" % world
     warm = 0 if converge else args.warmup
     itMax = steps if converge else warm + steps
@@ -203,11 +212,12 @@ def main():
     done = it - warm
     assert converge or done == steps, (it, warm, steps)
     el_max, E_all = el, E * world
-    if world > 1:
-        tt = torch.tensor([el, float(E)], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        el_max, E_all = float(tt[0].item()), int(tt[1].item())
+    if world > 1:  # host reductions (gloo): max time, total edges
+        tmax = torch.tensor([el], dtype=torch.float64)
+        tsum = torch.tensor([E], dtype=torch.int64)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        el_max, E_all = float(tmax[0]), int(tsum[0])
     if converge:
         res_timed = sess.result()
         sess.close()
@@ -231,6 +241,7 @@ def main():
     reordered = bool(sess.query("reordered"))
     quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
     split_blocks = sess.query("split_blocks") if quad else 0
+    chunks = sess.query("pipeline_chunks") if quad else 0
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     # the edge sweep's kernel: u ends staged in LDS for u-sorted edges
     kname = "k_" + wl.dominant
@@ -239,6 +250,9 @@ def main():
     if wl.dominant == "symv" and symv:
         kname = "k_symv_tiles+k_symv_finish"
     sess.close()
+    if comm:
+        from cp_pfdr_graph_d1_amd import partition
+        partition.comm_destroy(comm)
     if world > 1:
         dist.destroy_process_group()
     if rank != 0:
@@ -257,7 +271,7 @@ def main():
         "ms_per_step": round(ms_step, 4),
         "iter_per_s": round(1e3 / ms_step, 2),
         "higher_is_better": True,
-        "scaling": wl.scaling,
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64" if wl.dtype == np.float64 else "f32",
         "data": "synthetic",
@@ -271,6 +285,7 @@ def main():
             "device_bytes": dev_bytes,
             "relabelled": reordered,
             "split_incidence_blocks": split_blocks,
+            "pipeline_chunks": chunks,
             **({"symv_upper_triangle": bool(symv)} if wl.dominant == "symv" else {}),
             "finite": finite,
         },

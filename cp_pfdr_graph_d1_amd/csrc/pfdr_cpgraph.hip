@@ -622,6 +622,7 @@ struct CpGraphBase {
     long E = 0;
     int dtype = PFDR_F32;
     hipStream_t s = nullptr;
+    int dev = 0;  // device of s (calls from any thread run on it)
     DevBuf<int> Eu, Ev;
     Incidence inc;
     DevBuf<uint8_t> active;
@@ -907,6 +908,7 @@ using pfdr::report_error;
 
 #define CPG_TRY(fn, body)                                  \
     try {                                                  \
+        pfdr::StreamScope sc_(h->g->s, h->g->dev);         \
         body;                                              \
     } catch (const pfdr::HipError &h) {                    \
         return report_error(fn, h);                        \
@@ -925,6 +927,7 @@ static pfdr::CpGraphBase *cpg_new(int V, int E, const int *Eu, const int *Ev, co
     g->E = E;
     g->dtype = sizeof(real) == 4 ? PFDR_F32 : PFDR_F64;
     g->s = lib_stream();
+    PFDR_HIP(hipGetDevice(&g->dev));
     const auto k = kind_in(mem);
     g->Eu.alloc(E > 0 ? E : 1);
     g->Ev.alloc(E > 0 ? E : 1);
@@ -968,17 +971,27 @@ extern "C" int pfdr_cpgraph_create(pfdr_cpgraph **out, int dtype, int V, int E, 
         return report_error(fn, "invalid arguments");
     if ((long)E * 2 >= (1L << 31)) return report_error(fn, "E must be < 2^30");
     *out = nullptr;
-    CPG_TRY(fn, {
+    try {
         pfdr::CpGraphBase *g = dtype == PFDR_F32
                                    ? cpg_new<float>(V, E, Eu, Ev, La_d1, La_l1, mem)
                                    : cpg_new<double>(V, E, Eu, Ev, La_d1, La_l1, mem);
         *out = new pfdr_cpgraph{g};
-    })
+    } catch (const pfdr::HipError &h) {
+        return report_error(fn, h);
+    } catch (const std::exception &ex) {
+        return report_error(fn, ex.what());
+    }
+    return PFDR_OK;
 }
 
 extern "C" void pfdr_cpgraph_destroy(pfdr_cpgraph *g) {
     if (!g) return;
-    delete g->g;
+    try {
+        pfdr::StreamScope sc(g->g->s, g->g->dev);
+        (void)hipStreamSynchronize(g->g->s);
+        delete g->g;
+    } catch (...) {
+    }
     delete g;
 }
 

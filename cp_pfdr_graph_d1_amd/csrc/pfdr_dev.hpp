@@ -217,8 +217,39 @@ struct DevBuf {
     T *get() const { return p; }
 };
 
-// Library-owned stream of the calling thread's current device.
+// Library-owned stream of the calling thread's current device, or, inside
+// a StreamScope, the stream of the session being driven: every allocation,
+// free and copy of a session call is then ordered on the session's stream
+// whichever thread makes the call (the device cache's idle test included).
 hipStream_t lib_stream();
+
+// Binds the calling thread to a session's device and stream for the
+// duration of one C-ABI call (run, result, destroy from any thread).
+class StreamScope {
+  public:
+    StreamScope(hipStream_t s, int device);
+    ~StreamScope();
+    StreamScope(const StreamScope &) = delete;
+    StreamScope &operator=(const StreamScope &) = delete;
+
+  private:
+    hipStream_t prev_s_;
+    int prev_dev_ = -1, dev_ = -1;
+};
+
+// Returns a pinned_small_get() block on scope exit, after synchronising the
+// stream that may still copy into it (error paths included).
+struct PinnedSmall {
+    void *p;
+    hipStream_t s;
+    explicit PinnedSmall(hipStream_t st) : p(pinned_small_get()), s(st) {}
+    ~PinnedSmall() {
+        (void)hipStreamSynchronize(s);
+        pinned_small_put(p);
+    }
+    PinnedSmall(const PinnedSmall &) = delete;
+    PinnedSmall &operator=(const PinnedSmall &) = delete;
+};
 
 // Copies between the caller's host arrays and the device.  A host range of
 // at least 1 MiB is pinned (hipHostRegister) for its DMA and unpinned once

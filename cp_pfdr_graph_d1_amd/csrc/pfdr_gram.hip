@@ -569,7 +569,8 @@ real operator_norm_device(int M, int N, const real *A, real nTol, int itMax, int
         apply(X.p, Y.p);
         k_col_norms<real><<<B, 256, 0, s>>>(n, Y.p, b.p);
         std::swap(X.p, Y.p);
-        int *hrun = static_cast<int *>(pinned_small_get());
+        PinnedSmall pin(s);  // returned on every exit path
+        int *hrun = static_cast<int *>(pin.p);
         for (int it = 0; it < itMax; it++) {
             k_col_scale<real><<<grid_for((long)n * B), kBlock, 0, s>>>(n, B, X.p, b.p);
             apply(X.p, Y.p);
@@ -582,7 +583,6 @@ real operator_norm_device(int M, int N, const real *A, real nTol, int itMax, int
             PFDR_HIP(hipStreamSynchronize(s));
             if (*hrun == 0) break;
         }
-        pinned_small_put(hrun);  // the loop ended on a synchronised stream
         std::vector<real> hb(B);
         PFDR_HIP(hipMemcpyAsync(hb.data(), b.p, B * sizeof(real), hipMemcpyDeviceToHost, s));
         PFDR_HIP(hipStreamSynchronize(s));

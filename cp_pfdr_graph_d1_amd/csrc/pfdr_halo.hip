@@ -2,10 +2,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "pfdr_halo.hpp"
 
@@ -61,6 +63,53 @@ static void pack_u(int n, const unsigned *idx, const void *src, void *dst, int e
 }
 
 // ------------------------------------------------------------ Transport --
+double Transport::comm_timeout_s() {
+    const char *t = getenv("PFDR_COMM_TIMEOUT");
+    const double v = t ? atof(t) : 120.0;
+    return v > 0 ? v : 120.0;
+}
+
+std::string Transport::describe() const {
+    char m[160];
+    snprintf(m, sizeof m, "rank %d of %d, %s, iteration %ld, last collective: ", rank, nranks,
+             phase, iteration);
+    return std::string(m) + last_op;
+}
+
+// poll the stream; past the timeout, report what this rank was waiting for
+void Transport::wait(hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int spins = 0;
+    while (true) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) PFDR_HIP(e);
+        const double el =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > timeout_s) {
+            char m[96];
+            snprintf(m, sizeof m, "halo exchange stalled for %.0f s (PFDR_COMM_TIMEOUT): ", el);
+            const std::string msg = m + describe();
+            fprintf(stderr, "[pfdr watchdog] %s\n", msg.c_str());
+            fflush(stderr);
+            on_timeout();
+            throw std::runtime_error(msg);
+        }
+        if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+static std::string peers_bytes(const std::vector<size_t> &b, int self) {
+    std::string out = "{";
+    char m[48];
+    for (size_t q = 0; q < b.size(); q++) {
+        if ((int)q == self || !b[q]) continue;
+        snprintf(m, sizeof m, "%s%zu: %zu B", out.size() > 1 ? ", " : "", q, b[q]);
+        out += m;
+    }
+    return out + "}";
+}
+
 void Transport::allgather_i64(int64_t mine, std::vector<int64_t> &all, hipStream_t s) {
     all.assign(nranks, 0);
     all[rank] = mine;
@@ -70,7 +119,7 @@ void Transport::allgather_i64(int64_t mine, std::vector<int64_t> &all, hipStream
     PFDR_HIP(hipMemcpyAsync(d.p + rank, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
     allreduce_sum(d.p, nranks, 2, s);
     PFDR_HIP(hipMemcpyAsync(all.data(), d.p, sizeof(int64_t) * nranks, hipMemcpyDeviceToHost, s));
-    PFDR_HIP(hipStreamSynchronize(s));
+    wait(s);
 }
 
 void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
@@ -84,7 +133,7 @@ void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
     PFDR_HIP(hipMemcpyAsync(cnt.p, hc.data(), sizeof(int64_t) * n * n, hipMemcpyHostToDevice, s));
     allreduce_sum(cnt.p, n * n, 2, s);
     PFDR_HIP(hipMemcpyAsync(hc.data(), cnt.p, sizeof(int64_t) * n * n, hipMemcpyDeviceToHost, s));
-    PFDR_HIP(hipStreamSynchronize(s));
+    wait(s);
     std::vector<DevBuf<int64_t>> ds(n), dr(n);
     std::vector<const void *> sp(n, nullptr);
     std::vector<void *> rp(n, nullptr);
@@ -112,7 +161,7 @@ void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
         if (rb[q])
             PFDR_HIP(hipMemcpyAsync(recv[q].data(), dr[q].p, rb[q], hipMemcpyDeviceToHost, s));
     }
-    PFDR_HIP(hipStreamSynchronize(s));
+    wait(s);
 }
 
 // ----------------------------------------------------------------- RCCL --
@@ -128,9 +177,14 @@ class RcclTransport final : public Transport {
 
   public:
     RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) { nranks = n; rank = r; }
+    // a stalled communicator cannot be used again: abort it so the peers'
+    // operations fail too instead of waiting on this rank
+    void on_timeout() override { (void)ncclCommAbort(comm_); }
     void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
                   hipStream_t s) override {
+        last_op = "grouped send/recv, send " + peers_bytes(sbytes, rank) + " recv " +
+                  peers_bytes(rbytes, rank);
         ck(ncclGroupStart(), "group start");
         for (int q = 0; q < nranks; q++) {
             if (q == rank) continue;
@@ -141,15 +195,23 @@ class RcclTransport final : public Transport {
     }
     void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
         ncclDataType_t t = dtype == PFDR_F32 ? ncclFloat32 : dtype == PFDR_F64 ? ncclFloat64 : ncclInt64;
+        last_op = "all-reduce of " + std::to_string(n) + " values, all peers";
         ck(ncclAllReduce(dev, dev, n, t, ncclSum, comm_, s), "allreduce");
     }
     void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
-        if (rank > 0) ck(ncclRecv(dev, bytes, ncclChar, rank - 1, comm_, s), "chain recv");
+        if (rank > 0) {
+            last_op = "chain recv of " + std::to_string(bytes) + " B from " + std::to_string(rank - 1);
+            ck(ncclRecv(dev, bytes, ncclChar, rank - 1, comm_, s), "chain recv");
+        }
     }
     void chain_send(const void *dev, size_t bytes, hipStream_t s) override {
-        if (rank + 1 < nranks) ck(ncclSend(dev, bytes, ncclChar, rank + 1, comm_, s), "chain send");
+        if (rank + 1 < nranks) {
+            last_op = "chain send of " + std::to_string(bytes) + " B to " + std::to_string(rank + 1);
+            ck(ncclSend(dev, bytes, ncclChar, rank + 1, comm_, s), "chain send");
+        }
     }
     void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
+        last_op = "broadcast of " + std::to_string(bytes) + " B from " + std::to_string(root);
         ck(ncclBroadcast(dev, dev, bytes, ncclChar, root, comm_, s), "broadcast");
     }
 };
@@ -165,6 +227,8 @@ struct LoopHub {
     std::condition_variable cv;
     int count = 0;
     long gen = 0;
+    bool aborted = false;        // a rank failed or stalled: every waiter throws
+    std::string why;
     struct Post {
         std::vector<const void *> send;
         std::vector<size_t> sbytes;
@@ -181,15 +245,40 @@ struct LoopHub {
             if (p.chain) (void)hipEventDestroy(p.chain);
         }
     }
-    void barrier() {
+    void abort(const std::string &reason) {
         std::unique_lock<std::mutex> l(m);
+        if (!aborted) { aborted = true; why = reason; }
+        cv.notify_all();
+    }
+    [[noreturn]] void fail_locked(const Transport &t, const char *what) {
+        throw std::runtime_error(std::string("loopback ") + what + " (" + t.describe() + "): " + why);
+    }
+    // wait until `ready()` (hub mutex held) under the watchdog
+    template <typename F>
+    void wait_until(std::unique_lock<std::mutex> &l, const Transport &t, F ready) {
+        const auto dl = std::chrono::steady_clock::now() +
+                        std::chrono::duration<double>(t.timeout_s);
+        if (!cv.wait_until(l, dl, [&] { return aborted || ready(); })) {
+            aborted = true;
+            char b[96];
+            snprintf(b, sizeof b, "rank %d stalled for %.0f s (PFDR_COMM_TIMEOUT)", t.rank,
+                     t.timeout_s);
+            why = b;
+            fprintf(stderr, "[pfdr watchdog] loopback %s: %s\n", t.describe().c_str(), b);
+            cv.notify_all();
+        }
+        if (aborted) fail_locked(t, "aborted");
+    }
+    void barrier(const Transport &t) {
+        std::unique_lock<std::mutex> l(m);
+        if (aborted) fail_locked(t, "aborted");
         const long g = gen;
         if (++count == k) {
             count = 0;
             gen++;
             cv.notify_all();
         } else {
-            cv.wait(l, [&] { return gen != g; });
+            wait_until(l, t, [&] { return gen != g; });
         }
     }
 };
@@ -224,11 +313,12 @@ class LoopbackTransport final : public Transport {
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
                   hipStream_t s) override {
         ensure_events();
+        last_op = "exchange, send " + peers_bytes(sbytes, rank) + " recv " + peers_bytes(rbytes, rank);
         auto &me = hub_->post[rank];
         me.send = send;
         me.sbytes = sbytes;
         PFDR_HIP(hipEventRecord(me.ready, s));
-        hub_->barrier();
+        hub_->barrier(*this);
         for (int q = 0; q < nranks; q++) {
             if (q == rank || !rbytes[q]) continue;
             auto &pq = hub_->post[q];
@@ -237,17 +327,18 @@ class LoopbackTransport final : public Transport {
             PFDR_HIP(hipMemcpyAsync(recv[q], pq.send[rank], rbytes[q], hipMemcpyDeviceToDevice, s));
         }
         PFDR_HIP(hipEventRecord(me.done, s));
-        hub_->barrier();
+        hub_->barrier(*this);
         for (int q = 0; q < nranks; q++)
             if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].done, 0));
-        hub_->barrier();  // nobody re-records `done` before every wait is enqueued
+        hub_->barrier(*this);  // nobody re-records `done` before every wait is enqueued
     }
     void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
         ensure_events();
+        last_op = "all-reduce of " + std::to_string(n) + " values";
         auto &me = hub_->post[rank];
         me.ptr = dev;
         PFDR_HIP(hipEventRecord(me.ready, s));
-        hub_->barrier();
+        hub_->barrier(*this);
         for (int q = 0; q < nranks; q++)
             if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].ready, 0));
         const size_t eb = dtype == PFDR_F32 ? 4 : 8;
@@ -266,12 +357,12 @@ class LoopbackTransport final : public Transport {
                                                          (long long *)tmp.p);
         PFDR_HIP(hipGetLastError());
         PFDR_HIP(hipEventRecord(me.done, s));
-        hub_->barrier();
+        hub_->barrier(*this);
         for (int q = 0; q < nranks; q++)
             if (q != rank) PFDR_HIP(hipStreamWaitEvent(s, hub_->post[q].done, 0));
         PFDR_HIP(hipMemcpyAsync(dev, tmp.p, (size_t)n * eb, hipMemcpyDeviceToDevice, s));
         PFDR_HIP(hipStreamSynchronize(s));  // tmp / ptrs die here
-        hub_->barrier();
+        hub_->barrier(*this);
     }
     void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
         ensure_events();
@@ -280,7 +371,7 @@ class LoopbackTransport final : public Transport {
         auto &me = hub_->post[rank];
         {
             std::unique_lock<std::mutex> l(hub_->m);
-            hub_->cv.wait(l, [&] { return prev.chain_seq > me.chain_seq; });
+            hub_->wait_until(l, *this, [&] { return prev.chain_seq > me.chain_seq; });
         }
         PFDR_HIP(hipStreamWaitEvent(s, prev.chain, 0));
         PFDR_HIP(hipMemcpyAsync(dev, prev.ptr, bytes, hipMemcpyDeviceToDevice, s));
@@ -301,7 +392,7 @@ class LoopbackTransport final : public Transport {
             std::unique_lock<std::mutex> l(hub_->m);
             me.chain_seq++;
         }
-        hub_->barrier();  // keep dev alive until the successor copied it
+        hub_->barrier(*this);  // keep dev alive until the successor copied it
     }
     void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
         ensure_events();
@@ -310,15 +401,19 @@ class LoopbackTransport final : public Transport {
             me.ptr = dev;
             PFDR_HIP(hipEventRecord(me.ready, s));
         }
-        hub_->barrier();
+        hub_->barrier(*this);
         if (rank != root) {
             PFDR_HIP(hipStreamWaitEvent(s, hub_->post[root].ready, 0));
             PFDR_HIP(hipMemcpyAsync(dev, hub_->post[root].ptr, bytes, hipMemcpyDeviceToDevice, s));
         }
         PFDR_HIP(hipStreamSynchronize(s));
-        hub_->barrier();
+        hub_->barrier(*this);
     }
 };
+
+void loopback_abort(void *hub, const char *reason) {
+    static_cast<LoopHub *>(hub)->abort(reason ? reason : "a peer rank failed");
+}
 
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int n, int r) {
     return std::unique_ptr<Transport>(new LoopbackTransport(hub, n, r));
@@ -627,6 +722,12 @@ extern "C" int pfdr_loopback_create(void **hub_out, int nranks) {
     if (!hub_out || nranks < 1 || nranks > 64)
         return pfdr::report_error("pfdr_loopback_create", "invalid arguments");
     *hub_out = new pfdr::LoopHub(nranks);
+    return PFDR_OK;
+}
+
+extern "C" int pfdr_loopback_abort(void *hub, const char *reason) {
+    if (!hub) return pfdr::report_error("pfdr_loopback_abort", "null hub");
+    pfdr::loopback_abort(hub, reason);
     return PFDR_OK;
 }
 

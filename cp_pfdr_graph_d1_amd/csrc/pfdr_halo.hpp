@@ -19,6 +19,7 @@
 // tested on one GPU against the unpartitioned solver.
 #pragma once
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "pfdr_graph.hpp"
@@ -28,7 +29,20 @@ namespace pfdr {
 class Transport {
   public:
     int nranks = 1, rank = 0;
+    // watchdog context: what the session is doing (set by the sessions) and
+    // the last collective enqueued (set by the transports); a stall longer
+    // than timeout_s (PFDR_COMM_TIMEOUT, default 120 s) is reported with
+    // them and fails the call instead of hanging
+    const char *phase = "setup";
+    long iteration = 0;
+    std::string last_op = "none";
+    double timeout_s = comm_timeout_s();
+    static double comm_timeout_s();
+    std::string describe() const;
     virtual ~Transport() = default;
+    // wait for stream s (instead of hipStreamSynchronize) under the watchdog
+    virtual void wait(hipStream_t s);
+    virtual void on_timeout() {}
     // point-to-point exchange with every peer (entries for this rank and
     // zero sizes are skipped); enqueued on s
     virtual void exchange(const std::vector<const void *> &send,
@@ -52,6 +66,8 @@ class Transport {
 
 std::unique_ptr<Transport> make_rccl_transport(void *comm, int nranks, int rank);
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
+// wake every rank waiting on the hub with an error (a rank failed)
+void loopback_abort(void *hub, const char *reason);
 
 // Partition plan of one rank plus its device-side exchange buffers.
 struct Halo {

@@ -143,6 +143,7 @@ class QuadSession final : public SessionBase {
     void body();
     void push_ctrl();
     void pull_ctrl();
+    void wait_stream();
     void print_progress();
     void pull(void *base, int eb) { if (halo_) halo_->pull(base, eb, stream); }
     // halo / compute overlap (partitioned sessions): the halo exchanges run
@@ -162,6 +163,14 @@ class QuadSession final : public SessionBase {
     // (k_tiny_iterate; PFDR_TINY = max edges, 0 = off)
     bool tiny_ = false;
     void tiny_chunk(int n);
+    // pipelined iteration (single GPU, u-sorted edges, label bandwidth below
+    // the chunk size): vertex chunks k = 0..C-1 run as edge sweep of chunk
+    // k+1, then vertex sweep of chunk k, so each chunk's DR contributions are
+    // read back while they are still in the 256 MB Infinity Cache
+    // (PFDR_CHUNKS = C; 0 off)
+    std::vector<int> pblk_;    // vertex-block boundaries of the chunks (C + 1)
+    std::vector<long> pedge_;  // edge boundaries (C + 1), multiples of the lane width
+    void plan_pipeline();
     const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
     // A^tA mode on one GPU with an exactly symmetric matrix: products from the
     // block upper triangle (k_symv_tiles / k_symv_finish, half the bytes)
@@ -390,6 +399,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (halo_) {
         const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
         if (!(o && o[0] == '0')) plan_overlap();
+    } else if (!tiny_) {
+        plan_pipeline();
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
@@ -502,7 +513,18 @@ void QuadSession<real>::push_ctrl() {
 template <typename real>
 void QuadSession<real>::pull_ctrl() {
     PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
-    PFDR_HIP(hipStreamSynchronize(stream));
+    wait_stream();
+}
+
+// host wait for the session stream; partitioned sessions wait under the
+// transport's watchdog (a stalled halo exchange fails the call with the
+// rank, peers, bytes and iteration instead of hanging)
+template <typename real>
+void QuadSession<real>::wait_stream() {
+    if (!halo_) { PFDR_HIP(hipStreamSynchronize(stream)); return; }
+    halo_->tr->phase = "iterations";
+    halo_->tr->iteration = it_;
+    halo_->tr->wait(stream);
 }
 
 // R = Y - A X (direct mode), gated
@@ -851,6 +873,14 @@ void QuadSession<real>::body() {
         PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
         vertex_sweep(0, blo_, c, "vertex_sweep_b");
         vertex_sweep(bhi_, nbv_, c, "vertex_sweep_b");
+    } else if (pblk_.size() > 1) {
+        // chunked: E(0), then E(k+1), V(k) for every chunk k
+        const int C = (int)pblk_.size() - 1;
+        edge_sweep(pedge_[0], pedge_[1], c, "edge_sweep");
+        for (int k = 0; k < C; k++) {
+            if (k + 1 < C) edge_sweep(pedge_[k + 1], pedge_[k + 2], c, "edge_sweep");
+            vertex_sweep(pblk_[k], pblk_[k + 1], c, "vertex_sweep");
+        }
     } else {
         if (halo_) {
             ProfScope ps(prof, "halo_pull", s);
@@ -876,6 +906,45 @@ void QuadSession<real>::body() {
     PFDR_HIP(hipGetLastError());
     if (mode_ == A_DIRECT || mode_ == A_ATA) forward_dense(gated ? GATE_ACTIVE : GATE_NONE);
     if (rec_obj_) objective();
+}
+
+// chunk plan of the pipelined iteration: C chunks of whole vertex blocks,
+// each at least the label bandwidth + 1 vertices, so that the edges of chunk
+// k + 1 (u ends in it) only touch chunks k..k+2 and every edge touching
+// chunk k is swept before its vertex sweep; edge boundaries rounded UP to
+// the lane width (the few edges moved into the previous range have their u
+// end at its last vertex's successor and touch no chunk before it)
+template <typename real>
+void QuadSession<real>::plan_pipeline() {
+    const char *e = getenv("PFDR_CHUNKS");
+    const int want = e ? atoi(e) : 0;
+    if (want < 2 || !uptr_.p || !E_ || rec_obj_) return;
+    hipStream_t s = stream;
+    constexpr int EPT = Vec<real>::kPer16B;
+    DevBuf<int> d(1);
+    PFDR_HIP(hipMemsetAsync(d.p, 0, sizeof(int), s));
+    k_bandwidth<<<std::min(grid_for(E_), 4096), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, d.p);
+    PFDR_HIP(hipGetLastError());
+    int bw = 0;
+    PFDR_HIP(hipMemcpyAsync(&bw, d.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    const int minb = (bw + 1 + kBlock - 1) / kBlock;  // blocks per chunk at least
+    const int C = std::min(want, nbv_ / std::max(minb, 1));
+    if (C < 2) return;
+    std::vector<int> up((size_t)V_ + 1);
+    PFDR_HIP(hipMemcpy(up.data(), uptr_.p, sizeof(int) * ((size_t)V_ + 1), hipMemcpyDeviceToHost));
+    pblk_.assign(C + 1, 0);
+    pedge_.assign(C + 1, 0);
+    for (int k = 0; k <= C; k++) {
+        pblk_[k] = (int)((long)nbv_ * k / C);
+        const long ev = up[std::min((long)V_, (long)pblk_[k] * kBlock)];
+        pedge_[k] = std::min((long)E_, (ev + EPT - 1) / EPT * EPT);
+    }
+    pedge_[0] = 0;
+    pedge_[C] = E_;
+    for (int k = 0; k < C; k++)
+        if (pblk_[k + 1] - pblk_[k] < minb) { pblk_.clear(); pedge_.clear(); return; }
+    pipeline_chunks = C;
 }
 
 // interior edge range and vertex-block range of a partitioned session (the
@@ -972,7 +1041,7 @@ int QuadSession<real>::run(int iters) {
             next_print_ = it_ + verbose_;
         }
     }
-    PFDR_HIP(hipStreamSynchronize(stream));
+    wait_stream();
     if (prof.on) prof.resolve();
     return it_;
 }

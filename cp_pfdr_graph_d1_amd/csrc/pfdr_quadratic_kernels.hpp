@@ -223,6 +223,23 @@ static __global__ void k_uptr(long E, int V, const int *__restrict__ Eu, int *__
     for (int v = lo; v <= hi; v++) uptr[v] = (int)e;
 }
 
+// max |Eu[e] - Ev[e]| (the graph's label bandwidth; atomicMax of block maxima)
+static __global__ void k_bandwidth(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                   int *__restrict__ bw) {
+    __shared__ int red[kBlock / kWave];
+    int m = 0;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x)
+        m = max(m, abs(Eu[e] - Ev[e]));
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; w++) m = max(m, red[w]);
+        atomicMax(bw, m);
+    }
+}
+
 // One lane per vertex: code (bit i: the i-th CSR entry is the vertex's next
 // own u-run contribution; terminator bit at the degree) and the other
 // entries' addresses in CSR order.  blkok[b] = 1 when every vertex of block

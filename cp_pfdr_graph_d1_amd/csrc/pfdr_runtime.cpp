@@ -59,7 +59,25 @@ int report_error(const char *fn, const char *msg) {
     return PFDR_ERR_ARG;
 }
 
+static thread_local hipStream_t g_scope_stream = nullptr;
+
+StreamScope::StreamScope(hipStream_t s, int device) : prev_s_(g_scope_stream) {
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess && cur != device) {
+        PFDR_HIP(hipSetDevice(device));
+        prev_dev_ = cur;
+    }
+    dev_ = device;
+    g_scope_stream = s;
+}
+
+StreamScope::~StreamScope() {
+    g_scope_stream = prev_s_;
+    if (prev_dev_ >= 0) (void)hipSetDevice(prev_dev_);
+}
+
 hipStream_t lib_stream() {
+    if (g_scope_stream) return g_scope_stream;
     // one non-blocking stream per (thread, device)
     static thread_local hipStream_t streams[64] = {};
     int dev = 0;
@@ -167,8 +185,26 @@ void dev_free(void *p, size_t bytes) noexcept {
     } catch (...) {
     }
     // not cached: no kernel may still use it (callers free scratch right
-    // after enqueuing its last use, relying on the cache's idle rule)
-    (void)hipDeviceSynchronize();
+    // after enqueuing its last use on the library / session stream, relying
+    // on the cache's idle rule): drain that stream -- on the pointer's own
+    // device -- before hipFree, not the whole device
+    int cur = -1, owner = -1;
+    hipPointerAttribute_t at{};
+    if (hipGetDevice(&cur) == hipSuccess && hipPointerGetAttributes(&at, p) == hipSuccess)
+        owner = at.device;
+    (void)hipGetLastError();
+    if (owner >= 0 && owner != cur) {
+        (void)hipSetDevice(owner);
+        (void)hipDeviceSynchronize();  // another device's block: its streams are not ours
+        (void)hipFree(p);
+        (void)hipSetDevice(cur);
+        return;
+    }
+    try {
+        (void)hipStreamSynchronize(lib_stream());
+    } catch (...) {
+        (void)hipDeviceSynchronize();
+    }
     (void)hipFree(p);
 }
 
@@ -353,6 +389,7 @@ extern "C" int pfdr_session_create(pfdr_session **out, const pfdr_problem *p) {
 extern "C" int pfdr_session_run(pfdr_session *s, int iters, int *it_total) {
     if (!s) return report_error("pfdr_session_run", "null session");
     PFDR_GUARD("pfdr_session_run", {
+        StreamScope sc(s->impl->stream, s->impl->device);
         int it = s->impl->run(iters);
         if (it_total) *it_total = it;
     });
@@ -362,12 +399,24 @@ extern "C" int pfdr_session_run(pfdr_session *s, int iters, int *it_total) {
 extern "C" int pfdr_session_result(pfdr_session *s, void *X, int *it,
                                    void *Obj, void *Dif) {
     if (!s) return report_error("pfdr_session_result", "null session");
-    PFDR_GUARD("pfdr_session_result", { s->impl->result(X, it, Obj, Dif); });
+    PFDR_GUARD("pfdr_session_result", {
+        StreamScope sc(s->impl->stream, s->impl->device);
+        s->impl->result(X, it, Obj, Dif);
+    });
     return PFDR_OK;
 }
 
 extern "C" void *pfdr_session_device_x(pfdr_session *s) {
-    return s ? s->impl->device_x() : nullptr;
+    if (!s) return nullptr;
+    try {
+        StreamScope sc(s->impl->stream, s->impl->device);
+        return s->impl->device_x();
+    } catch (const HipError &h) {
+        report_error("pfdr_session_device_x", h);
+    } catch (const std::exception &ex) {
+        report_error("pfdr_session_device_x", ex.what());
+    }
+    return nullptr;
 }
 
 extern "C" int pfdr_session_set_profiling(pfdr_session *s, int on) {
@@ -384,6 +433,7 @@ extern "C" int pfdr_session_kernel_stats(pfdr_session *s, const char *kernel,
     if (!s || !kernel || !launches || !mean_ms)
         return report_error("pfdr_session_kernel_stats", "null argument");
     PFDR_GUARD("pfdr_session_kernel_stats", {
+        StreamScope sc(s->impl->stream, s->impl->device);
         PFDR_HIP(hipStreamSynchronize(s->impl->stream));
         s->impl->prof.resolve();
         s->impl->prof.stats(kernel, launches, mean_ms);
@@ -411,6 +461,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
+    else if (!strcmp(what, "pipeline_chunks")) *value = s->impl->pipeline_chunks;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
     return PFDR_OK;
@@ -419,6 +470,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
 extern "C" void pfdr_session_destroy(pfdr_session *s) {
     if (!s) return;
     try {
+        StreamScope sc(s->impl->stream, s->impl->device);
         (void)hipStreamSynchronize(s->impl->stream);
         delete s->impl;
     } catch (...) {

@@ -59,6 +59,7 @@ class SessionBase {
     int64_t symv = 0;          // A^tA products from the block upper triangle
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
+    int64_t pipeline_chunks = 0;  // pipelined iteration: vertex chunks per iteration
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

@@ -954,6 +954,7 @@ class SimplexSession final : public SessionBase {
     long Vglob_;    // vertices over all ranks
     long E_, EK_, VK_, R_ = 0;
     std::unique_ptr<Halo> halo_;  // vertex partition (null on one GPU)
+    void wait_stream();
     DevBuf<real> red_;            // all-reduced scalars
     real rho_, condMin_, difTol_, difRcd_, cap_;
     bool rec_obj_, rec_dif_;
@@ -1298,7 +1299,7 @@ int SimplexSession<real>::run(int iters) {
         for (int i = 0; i < n; i++) body();
         if (gated) {
             PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
-            PFDR_HIP(hipStreamSynchronize(stream));
+            wait_stream();
             it_ = hctrl_->it;
             if (hctrl_->stop) {
                 stopped_ = true;
@@ -1331,9 +1332,18 @@ int SimplexSession<real>::run(int iters) {
             next_print_ = it_ + verbose_;
         }
     }
-    PFDR_HIP(hipStreamSynchronize(stream));
+    wait_stream();
     if (prof.on) prof.resolve();
     return it_;
+}
+
+// host wait for the session stream (partitioned: under the transport's watchdog)
+template <typename real>
+void SimplexSession<real>::wait_stream() {
+    if (!halo_) { PFDR_HIP(hipStreamSynchronize(stream)); return; }
+    halo_->tr->phase = "iterations";
+    halo_->tr->iteration = it_;
+    halo_->tr->wait(stream);
 }
 
 template <typename real>

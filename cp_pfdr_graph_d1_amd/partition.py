@@ -8,8 +8,8 @@
   over any transport (the CPU tests use torch.distributed/gloo).
 * ``solve_loopback``: k ranks as k threads on one GPU (loopback transport);
   returns the concatenated result, which equals the unpartitioned solve.
-* ``comm_init``: RCCL communicator for one process per GPU, the id broadcast
-  over an existing torch.distributed process group.
+* ``comm_init``: the RCCL communicator for one process per GPU, its unique id
+  broadcast over a host (gloo) process group.
 """
 import ctypes as C
 import threading
@@ -143,8 +143,9 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
             s.run(itMax)
             results[r] = s.result()
             s.close()
-        except Exception as ex:  # reported by the caller
+        except Exception as ex:  # reported by the caller; wake the other ranks
             errors[r] = ex
+            lib.pfdr_loopback_abort(hub, ("rank %d failed: %s" % (r, ex))[:200].encode())
 
     th = [threading.Thread(target=rank_main, args=(r,)) for r in range(k)]
     for t in th:
@@ -152,9 +153,10 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
     for t in th:
         t.join()
     lib.pfdr_loopback_destroy(hub)
-    for ex in errors:
-        if ex is not None:
-            raise ex
+    # the first failure is the cause; the others are its consequence
+    first = [ex for ex in errors if ex is not None and "aborted" not in str(ex)]
+    for ex in first or [ex for ex in errors if ex is not None]:
+        raise ex
     X = np.concatenate([res[0] for res in results])
     its = {res[1] for res in results}
     if len(its) != 1:
@@ -164,19 +166,34 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                                                  "queries": queries}
 
 
-def comm_init(nranks, rank, device_tensor_broadcast):
-    """RCCL communicator (one process per GPU).  ``device_tensor_broadcast``
-    broadcasts a uint8 torch tensor from rank 0 in place (e.g.
-    torch.distributed.broadcast)."""
+def comm_init(nranks, rank, host_broadcast):
+    """RCCL communicator of this rank (one process per GPU): rank 0 creates
+    the unique id, ``host_broadcast`` broadcasts a CPU uint8 torch tensor from
+    rank 0 in place (e.g. ``lambda t: torch.distributed.broadcast(t, 0)`` on a
+    gloo group), every rank joins.  This is the only RCCL communicator of the
+    process: the halo exchanges, the scalar all-reduces and the timing
+    reduction all use it (torch's own NCCL group is never opened)."""
     import torch
     lib = pfdr.load()
     buf = (C.c_char * 128)()
     if rank == 0:
         pfdr._check(lib.pfdr_comm_unique_id(buf), "pfdr_comm_unique_id")
-    t = torch.tensor(list(bytes(buf)), dtype=torch.uint8, device="cuda")
-    device_tensor_broadcast(t)
-    raw = bytes(t.cpu().tolist())
-    idb = (C.c_char * 128).from_buffer_copy(raw)
+    t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+    host_broadcast(t)
+    idb = (C.c_char * 128).from_buffer_copy(bytes(t.tolist()))
     comm = C.c_void_p()
     pfdr._check(lib.pfdr_comm_init(C.byref(comm), nranks, rank, idb), "pfdr_comm_init")
     return comm.value
+
+
+def comm_max(comm, value):
+    """max over the ranks of a host double, through the RCCL communicator"""
+    v = C.c_double(float(value))
+    pfdr._check(pfdr.load().pfdr_comm_allreduce_max_f64(comm, C.byref(v)),
+                "pfdr_comm_allreduce_max_f64")
+    return v.value
+
+
+def comm_destroy(comm):
+    if comm:
+        pfdr._check(pfdr.load().pfdr_comm_destroy(comm), "pfdr_comm_destroy")

@@ -49,7 +49,7 @@ EXPORTED = (
     "pfdr_session_kernel_stats", "pfdr_session_sync",
     "pfdr_session_device_bytes", "pfdr_session_query", "pfdr_session_destroy",
     "pfdr_comm_unique_id", "pfdr_comm_init", "pfdr_comm_destroy",
-    "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create",
+    "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create", "pfdr_loopback_abort",
     "pfdr_loopback_destroy", "pfdr_plan_create", "pfdr_plan_get",
     "pfdr_plan_set_incoming", "pfdr_plan_finish", "pfdr_plan_destroy",
     "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
@@ -445,6 +445,15 @@ def proj_simplex_metric(X, M, A):
     return out.reshape(X.shape, order="F")
 
 
+def _producers_done():
+    """Device inputs are read on the library's own stream, which does not
+    wait for torch's: finish the kernels torch has queued (the producers of
+    the tensors handed over) before the library reads them
+    (include/pfdr_mi355x.h, PFDR_MEM_DEVICE)."""
+    import torch
+    torch.cuda.current_stream().synchronize()
+
+
 # ------------------------------------------------------------- sessions ---
 class Session:
     """Device-resident solve: setup once, iterate in steps (benchmarks,
@@ -461,6 +470,8 @@ class Session:
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
+        if device:
+            _producers_done()
 
         def addr(a, is_int=False):
             if a is None:
@@ -597,6 +608,7 @@ def gram(A, which=0, device=False):
     ms = C.c_double(0.0)
     if device:
         import torch
+        _producers_done()
         N, M = A.shape
         P = N if which == 0 else M
         G = torch.empty((P, P), dtype=A.dtype, device=A.device)
@@ -641,6 +653,7 @@ def operator_norm(A, nTol=1e-3, itMax=100, nbInit=10, symmetric=False, device=Fa
     gms = C.c_double(0.0)
     if device:
         import torch
+        _producers_done()
         Nn, Mm = A.shape
         if symmetric:
             Mm, Nn = 0, Nn

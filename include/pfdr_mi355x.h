@@ -110,6 +110,12 @@ int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
 
 #define PFDR_MEM_HOST 0    /* pointers are host memory (copied in) */
 #define PFDR_MEM_DEVICE 1  /* pointers are device memory of the current device */
+/* Ordering of device inputs: the library reads (and, for the session's
+ * lifetime, keeps reading nothing but its own copies of) the caller's
+ * device arrays on its own non-blocking stream, which does not wait for the
+ * caller's streams.  Every write into those arrays must be complete before
+ * the call (e.g. synchronise the producing stream; the Python front-end
+ * synchronises torch's current stream).  Outputs are complete on return. */
 
 /* Internal vertex relabelling for cache locality (breadth-first order,
  * pfdr_order.hip): AUTO applies it when the labels look random (V >= 2^20 and
@@ -296,7 +302,14 @@ int pfdr_comm_init(void **comm_out, int nranks, int rank, const void *id);
 int pfdr_comm_destroy(void *comm);
 int pfdr_comm_allreduce_max_f64(void *comm, double *value);
 int pfdr_loopback_create(void **hub_out, int nranks);
+/* a failing rank wakes the others: their pending and later exchanges fail */
+int pfdr_loopback_abort(void *hub, const char *reason);
 int pfdr_loopback_destroy(void *hub);
+/* Watchdog: a rank whose collective does not complete within
+ * PFDR_COMM_TIMEOUT seconds (default 120) prints
+ * "[pfdr watchdog] ... rank r of n, <phase>, iteration i, last collective:
+ * <op, peers, bytes>" to stderr, aborts the communicator (RCCL) or the hub
+ * (loopback) and fails the call with that message (no retry). */
 
 /* Host-only partition planner (what the partitioned session runs at setup;
  * exposed so the partition logic can be driven by any transport, e.g. the

@@ -28,6 +28,7 @@ from cp_pfdr_graph_d1_amd import pfdr
 CASES = ("c1_fixk25", "c1_conv", "headline_k3", "c2_k2", "c3_direct_k2", "c3_ata_k3",
          "c4_k2", "c5_k1")
 SAMPLE_SEED = 0x5EED
+DENSE = ("c3_direct_k2", "c3_ata_k3")
 
 
 def sample_index(n, m, seed=SAMPLE_SEED):

@@ -65,12 +65,31 @@ def main():
             extra["L"] = np.float32(L)
         else:
             case = F.build(name)
+        in_sha = F.input_digest(case)
         t1 = time.perf_counter()
         X, it, Dif = F.run(ref, case)
         t2 = time.perf_counter()
         d = F.digest(X, it, Dif, case["sample_m"])
+        if name in F.DENSE:
+            # the same problem through the reference's double instantiation
+            # (inputs widened exactly): the accuracy yardstick of the f32 runs
+            # (the reference's sequential f32 dot products over V terms carry
+            # rounding error of their own)
+            a = case["args"]
+            for k in ("X0", "Y", "A", "La_d1", "La_l1", "L"):
+                if a.get(k) is not None:
+                    a[k] = a[k].astype(np.float64)
+            del X
+            t3 = time.perf_counter()
+            X64, it64, _ = F.run(ref, case)
+            d64 = F.digest(X64, it64, np.zeros(0), case["sample_m"])
+            extra["ref64_sample"] = d64["sample"]
+            extra["ref64_norm2"] = d64["norm2"]
+            extra["ref64_it"] = d64["it"]
+            print("  f64 reference %.1fs" % (time.perf_counter() - t3), flush=True)
+            X = X64
         d.update(extra)
-        d["in_sha256"] = np.str_(F.input_digest(case))
+        d["in_sha256"] = np.str_(in_sha)
         d["meta_build"] = np.str_("reference src/PFDR_*.cpp, g++ -O3 -ffp-contract=off, no OpenMP")
         d["meta_seconds"] = np.float64(t2 - t1)
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)

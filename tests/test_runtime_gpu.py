@@ -77,3 +77,55 @@ def test_already_pinned_caller_arrays(gpu_lib):
     finally:
         hip.hipHostFree(px)
         hip.hipHostFree(py)
+
+
+def test_session_driven_from_other_threads(gpu_lib, oracle_port):
+    """A session created on one thread and run, read back and destroyed on
+    others (reconditioning frees scratch mid-run), while a second thread
+    solves other problems through the device cache: every allocation and
+    free of a session call is ordered on the session's stream, so no block
+    is handed to another stream while the session still uses it.  Results
+    equal the restatement bit for bit (f64)."""
+    import threading
+    k = 40
+    V, Eu, Ev, Y = _case(160, np.float64, 5)
+    args = (np.zeros(V), Y, None, 0, Eu, Ev, np.full(Eu.size, 0.1), np.full(V, 0.01), 0,
+            pfdr.DIAG, None, 1.5, 1e-3, 1e-2, 0.0, k)
+    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(*args)
+    box, errs = {}, []
+
+    def create():
+        box["s"] = pfdr.Session(pfdr.PFDR_KIND_L1, np.float64, V, Eu.size, Eu, Ev,
+                                np.full(Eu.size, 0.1), np.zeros(V), Y, La_l1=np.full(V, 0.01),
+                                Ltype=pfdr.DIAG, difRcd=1e-2, itMax=k)
+
+    def churn():  # other work through the same device cache meanwhile
+        try:
+            for i in range(6):
+                Vb, Eb, Fb, Yb = _case(90 + 7 * i, np.float64, 20 + i)
+                gpu_lib.quadratic_d1_l1(np.zeros(Vb), Yb, None, 0, Eb, Fb, np.full(Eb.size, 0.1),
+                                        np.full(Vb, 0.01), 0, pfdr.DIAG, None, 1.5, 1e-3, 1e-2,
+                                        0.0, 30)
+        except Exception as ex:
+            errs.append(ex)
+
+    def run_and_read():
+        try:
+            box["s"].run(k)
+            box["r"] = box["s"].result()
+            box["s"].close()
+        except Exception as ex:
+            errs.append(ex)
+
+    t = threading.Thread(target=create)
+    t.start()
+    t.join()
+    a, b = threading.Thread(target=run_and_read), threading.Thread(target=churn)
+    a.start()
+    b.start()
+    a.join()
+    b.join()
+    assert not errs, errs
+    X, it = box["r"][0], box["r"][1]
+    assert it == ito == k
+    assert np.array_equal(X, Xo)

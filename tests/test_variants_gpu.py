@@ -3,7 +3,8 @@ iterates bit for bit, so none of them can drift from the reference.
 
 Quadratic solvers: split incidence / CSR gather in the vertex sweep, u ends
 staged in LDS / Eu streamed in the edge sweep (PFDR_SPLIT, PFDR_USTAGE),
-amplitude sum by the workgroup binade scan / one lane (PFDR_SEQSUM).
+amplitude sum by the workgroup binade scan / one lane (PFDR_SEQSUM), the
+pipelined (chunked) iteration schedule (PFDR_CHUNKS).
 Simplex: two (edge, label) entries per lane / one (PFDR_SX_PAIR), prox
 weights recomputed from the factored splitting weights / stored
 (PFDR_SX_PW).  Every golden case of the reference, with reconditioning where
@@ -50,7 +51,8 @@ def test_quadratic_variants_identical(gpu_lib, name, fixed):
     c, g = G.load(name)
     base = _replay(gpu_lib, c, fixed, {"PFDR_SPLIT": "1", "PFDR_USTAGE": "1"})
     for env in ({"PFDR_SPLIT": "0", "PFDR_USTAGE": "1"}, {"PFDR_SPLIT": "1", "PFDR_USTAGE": "0"},
-                {"PFDR_SPLIT": "0", "PFDR_USTAGE": "0"}, {"PFDR_SEQSUM": "lane"}):
+                {"PFDR_SPLIT": "0", "PFDR_USTAGE": "0"}, {"PFDR_SEQSUM": "lane"},
+                {"PFDR_TINY": "0", "PFDR_CHUNKS": "3"}, {"PFDR_TINY": "0", "PFDR_CHUNKS": "2"}):
         _same(base, _replay(gpu_lib, c, fixed, env))
     if fixed and base[0].dtype == np.float64:
         assert np.array_equal(base[0], g["fixk_X"])

@@ -12,5 +12,5 @@ for cfg in $(echo ${CFGS:-base} | tr ',' ' '); do
   envs=$(echo $cfg | tr ';' ' ')
   [ "$cfg" = base ] && envs=""
   env $envs timeout -k 10 300 python bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline ${BENCH_EXTRA:-} > $OUT/bench_$i.log 2>&1 || exit $?
-  python -c "import json;d=json.loads(open('$OUT/bench_$i.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$cfg', d['ms_per_step'], d['value'], 'edge', r['mean_ms'], 'vertex', r.get('kernels_mean_ms', {}).get('vertex_sweep'), r['frac'])"
+  python -c "import json;d=json.loads(open('$OUT/bench_$i.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$cfg', d['ms_per_step'], d['value'], 'edge', r['mean_ms'], 'vertex', r.get('kernels_mean_ms', {}).get('vertex_sweep'), r['frac'], 'chunks', d['config'].get('pipeline_chunks'))"
 done

@@ -28,10 +28,8 @@ def main():
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
 
-    def bcast(t):  # uint8 CUDA tensor, broadcast through gloo on the host
-        h = t.cpu()
-        dist.broadcast(h, 0)
-        t.copy_(h.to(t.device))
+    def bcast(t):  # uint8 CPU tensor, broadcast through gloo
+        dist.broadcast(t, 0)
 
     shape = (40, 30, 32)
     V = int(np.prod(shape))

@@ -25,9 +25,11 @@ class Workload:
     steps = 50
     itMax_extra = 0
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         """-> dict(V, E, kw (pfdr.Session kwargs), vtx_begin, e_offset, desc,
-        graph[, converge])"""
+        graph[, converge]) of this rank.  strong: the configuration's graph
+        is split across the ranks (z- or row-slabs); weak: every rank owns a
+        copy-sized slab of a graph stacked `world` times."""
         raise NotImplementedError
 
     def dominant_bytes(self, V, E):
@@ -57,23 +59,33 @@ def _grid_slab(shape3, rank, world, conn, strong):
 
 
 class Headline(Workload):
+    """The 10M-vertex / 60M-edge 6-NN graph.  Strong scaling (default): the
+    fixed graph split into z-slabs of 200/N planes (1.25M vertices per GPU
+    at N = 8); weak: a 10M-vertex slab per GPU of a 250x200x(200 N) grid."""
     name = "headline"
     metric = "PFDR iter/s and Medge-updates/s, 10M-vertex 6-NN graph, 1/2/4/8 MI355X"
     SHAPE = (250, 200, 200)
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         nx, ny, nz = self.SHAPE
-        g = (nx, ny, nz * world)
-        V = nx * ny * nz
-        v0 = rank * V
-        Eu, Ev = pfdr.gen_knn_jitter_grid(g, 6, 6, 0.25, (v0, v0 + V))
-        Y = pfdr.gen_piecewise(nx, V * world, 2, np.float32, 0.2, (v0, v0 + V))
+        if strong:
+            g = (nx, ny, nz)
+            z0, z1 = (nz * rank) // world, (nz * (rank + 1)) // world
+        else:
+            g = (nx, ny, nz * world)
+            z0, z1 = nz * rank, nz * (rank + 1)
+        v0, v1 = nx * ny * z0, nx * ny * z1
+        V, V_all = v1 - v0, nx * ny * g[2]
+        Eu, Ev = pfdr.gen_knn_jitter_grid(g, 6, 6, 0.25, (v0, v1))
+        Y = pfdr.gen_piecewise(nx, V_all, 2, np.float32, 0.2, (v0, v1))
         E = Eu.size
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
                   Y=Y, La_l1=np.full(V, 0.01, np.float32), rho=1.5, condMin=1e-3)
-        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=rank * E,
+        return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=6 * v0,
                     desc="PFDR_graph_quadratic_d1_l1<float>, identity A, l1 + TV, jittered "
-                         "%dx%dx%d grid, 6-NN (V=%d, E=%d per GPU)" % (nx, ny, nz, V, E),
+                         "%dx%dx%d grid, 6-NN (V=%d, E=%d%s)" % (
+                             g[0], g[1], g[2], V_all, 6 * V_all,
+                             "" if world == 1 else ", z-slab of %d vertices on this GPU" % V),
                     graph="%dx%dx%d" % g)
 
 
@@ -84,7 +96,7 @@ class HeadlineShuffled(Headline):
     name = "headline_shuffled"
     partitionable = False
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import uniform
         d = Headline.inputs(self, 0, 1)
         kw, V, E = d["kw"], d["V"], d["E"]
@@ -109,7 +121,7 @@ class C1(Workload):
     steps = 10000
     partitionable = False
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import grid_graph, uniform
         Eu, Ev = grid_graph((256, 256), 4)
         V = 65536
@@ -124,12 +136,13 @@ class C1(Workload):
 
 
 class C2(Workload):
-    """config 2: 256^3 6-NN grid, identity A, fp32 (weak: one 256^3 per GPU)"""
+    """config 2: 256^3 6-NN grid, identity A, fp32 (strong: z-slabs of the
+    grid; weak: one 256^3 per GPU)"""
     name = "c2"
     metric = "PFDR_graph_quadratic_d1_l1<float> 256^3 6-NN: Medge-updates/s"
 
-    def inputs(self, rank, world):
-        g, V_all, v0, v1, Eu, Ev = _grid_slab((256, 256, 256), rank, world, 6, strong=False)
+    def inputs(self, rank, world, strong=True):
+        g, V_all, v0, v1, Eu, Ev = _grid_slab((256, 256, 256), rank, world, 6, strong=strong)
         V = v1 - v0
         Y = pfdr.gen_piecewise(256, V_all, 2, np.float32, 0.2, (v0, v1))
         E = Eu.size
@@ -150,7 +163,7 @@ class C3(Workload):
     dominant = "gemv_cols"
     steps = 20
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         import torch
         N, nx, ny = 1024, 2000, 1000
         V = nx * ny
@@ -210,7 +223,8 @@ class C3(Workload):
 
 class C4(Workload):
     """config 4: simplex K = 10, KL al = 0.1, 2236^2 8-neighbour grid, fp32;
-    N > 1: weak scaling, each GPU a 2236^2 row slab (K-wide halos)"""
+    N > 1: row slabs of the grid (strong) or a 2236^2 slab per GPU (weak),
+    K-wide halos"""
     name = "c4"
     metric = "PFDR_graph_loss_d1_simplex<float> K=10 KL 5M-vertex 8-NN: Medge-updates/s"
     kind = pfdr.PFDR_KIND_SIMPLEX
@@ -220,21 +234,26 @@ class C4(Workload):
     vertex_bytes = 10 * 4 * 4
     steps = 20
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
         n = 2236
-        V = n * n
-        g = (n, n * world)
-        v0 = rank * V
+        if strong:
+            g = (n, n)
+            r0, r1 = (n * rank) // world, (n * (rank + 1)) // world
+        else:
+            g = (n, n * world)
+            r0, r1 = n * rank, n * (rank + 1)
+        v0 = n * r0
+        V = n * (r1 - r0)
         Eu, Ev = pfdr.gen_grid_edges(g, 8, (v0, v0 + V))
-        v = np.arange(V)
-        lab = ((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)
+        v = np.arange(V) + (v0 if strong else 0)
+        lab = ((v % n) * 4 // n) + 4 * (((v // n) % n) * 3 // n)
         Q = simplex_observation(V, self.K, 4, lab, np.float32, v0=v0)
         E = Eu.size
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32), X0=Q.copy(), Y=Q,
                   K=self.K, al=0.1, rho=1.0, condMin=0.1)
         return dict(V=V, E=E, kw=kw, vtx_begin=v0, e_offset=pfdr.grid_edge_count(g, 8, v0),
-                    desc="C4: 2236^2 8-neighbour grid (V=%d, E=%d per GPU), K=10, KL al=0.1, "
+                    desc="C4: 2236^2 8-neighbour grid (V=%d, E=%d on this GPU), K=10, KL al=0.1, "
                          "fp32" % (V, E),
                     graph="%dx%d" % g)
 
@@ -249,7 +268,7 @@ class C5(Workload):
     vertex_bytes = 16
     steps = 10
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         g, V_all, v0, v1, Eu, Ev = _grid_slab((640, 640, 640), rank, world, 6, strong=True)
         V = v1 - v0
         Y = pfdr.gen_piecewise(640, V_all, 5, np.float32, 0.2, (v0, v1))
@@ -275,7 +294,7 @@ class C3AtA(Workload):
     dominant = "symv"
     steps = 50
 
-    def inputs(self, rank, world):
+    def inputs(self, rank, world, strong=True):
         import time
         import torch
         N, nx, ny = 1024, 256, 128
