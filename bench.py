@@ -45,12 +45,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
 # ------------------------------------------------------------ CPU baseline --
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline_child(args):
     """Runs in its own process: time the reference CPU path (oracle/_ref
     OpenMP build if present, else the restatement) on this host."""
     avail = sorted(os.sched_getaffinity(0))
     cores = avail[: min(len(avail), args.cpu_cores)]
     os.sched_setaffinity(0, cores)  # omp_get_num_procs honours the mask
+    host = {"cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": len(avail)}
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from workloads import WORKLOADS
@@ -69,14 +80,38 @@ def cpu_baseline_child(args):
             "value": Eu.size * it / el / 1e6, "unit": "Medge-updates/s",
             "cores": len(cores) if kind == "reference" else 1, "kind": kind,
             "converged_iterations": it, "time_to_tolerance_s": el,
-            "sample": "whole C1 solve to difTol 1e-6 (setup included), same inputs"}))
+            "sample": "whole C1 solve to difTol 1e-6 (setup included), same inputs", **host}))
         return
-    name = args.workload if args.workload in ("c2", "c4") else "headline"
-    inp = WORKLOADS[name].inputs(0, 1)
-    kw, V = inp["kw"], inp["V"]
-    Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
+    name = args.workload if args.workload in ("c2", "c3", "c4", "c5") else "headline"
+    sample = "full %s graph" % name
+    if name == "c3":  # host-generated A (the pinned law of tests/fullsize_cases.py)
+        from cp_pfdr_graph_d1_amd import pfdr
+        N, nx, ny = 1024, 2000, 1000
+        V = nx * ny
+        h = (3.0 / N) ** 0.5
+        A = pfdr.gen_uniform(3, N * V, -h, h, np.float32)
+        x0 = np.zeros(V, np.float32)
+        x0[: V // 3], x0[V // 3: 2 * V // 3] = 1.0, -0.5
+        Eu, Ev = pfdr.gen_grid_edges((nx, ny), 4)
+        L = np.array([(1.0 + (V / N) ** 0.5) ** 2], np.float32)  # ||A||^2 of U(-h, h), N x V
+        kw = dict(Y=pfdr.gen_matvec(A, N, V, x0), A=A, N=N, La_d1=np.full(Eu.size, 0.05, np.float32),
+                  La_l1=np.full(V, 0.005, np.float32), X0=np.zeros(V, np.float32), rho=1.5,
+                  condMin=1e-3, L=L)
+        sample = "C3 direct N=1024 x V=2M (A 8.2 GB host-generated)"
+    elif name == "c5":  # a 640x640x80 6-NN grid: the size of one GPU's slab at N = 8
+        from cp_pfdr_graph_d1_amd import pfdr
+        Eu, Ev = pfdr.gen_grid_edges((640, 640, 80), 6)
+        V = 640 * 640 * 80
+        kw = dict(X0=np.zeros(V, np.float32), Y=pfdr.gen_piecewise(640, V, 5, np.float32, 0.2),
+                  La_d1=np.full(Eu.size, 0.1, np.float32), lo=0.0, hi=1.0, rho=1.5, condMin=1e-3)
+        sample = "C5 law on a 640x640x80 6-NN grid (1/8 of 640^3: one GPU's share at N=8)"
+    else:
+        inp = WORKLOADS[name].inputs(0, 1)
+        kw, V = inp["kw"], inp["V"]
+        Eu, Ev = kw["Eu"], kw["Ev"]
+    Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
     if name != "headline":  # bounded sample: about 10 s of host work
-        args.cpu_k0, args.cpu_k1 = 1, 3
+        args.cpu_k0, args.cpu_k1 = 1, (2 if name == "c3" else 3)
     times = {}
     for k in (args.cpu_k0, args.cpu_k1):
         t = time.perf_counter()
@@ -84,6 +119,13 @@ def cpu_baseline_child(args):
             lib.loss_d1_simplex(kw["X0"].copy(), kw["Y"], kw["K"], Eu, Ev, kw["La_d1"],
                                 al=kw["al"], La_f=None, rho=kw["rho"], condMin=kw["condMin"],
                                 difRcd=0.0, difTol=0.0, itMax=k)
+        elif name == "c5":
+            lib.quadratic_d1_bounds(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
+                                    kw["lo"], kw["hi"], 0, None, kw["rho"], kw["condMin"], 0.0,
+                                    0.0, k)
+        elif name == "c3":
+            lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], kw["A"], kw["N"], Eu, Ev, kw["La_d1"],
+                                kw["La_l1"], 0, 0, kw["L"], kw["rho"], kw["condMin"], 0.0, 0.0, k)
         else:
             lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
                                 kw["La_l1"], 0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
@@ -93,10 +135,10 @@ def cpu_baseline_child(args):
         "value": Eu.size / per_it / 1e6, "unit": "Medge-updates/s",
         "cores": len(cores) if kind == "reference" else 1, "kind": kind,
         "iter_per_s": 1.0 / per_it,
-        "sample": "full %s graph (V=%d, E=%d) fp32, per-iteration time = "
+        "sample": "%s (V=%d, E=%d) fp32, per-iteration time = "
                   "(T(%d it) - T(%d it)) / %d, setup excluded" % (
-                      name, V, Eu.size, args.cpu_k1, args.cpu_k0, args.cpu_k1 - args.cpu_k0),
-        "setup_s": times[args.cpu_k0] - args.cpu_k0 * per_it}))
+                      sample, V, Eu.size, args.cpu_k1, args.cpu_k0, args.cpu_k1 - args.cpu_k0),
+        "setup_s": times[args.cpu_k0] - args.cpu_k0 * per_it, **host}))
 
 
 def run_cpu_baseline(args):
@@ -114,14 +156,18 @@ def run_cpu_baseline(args):
 def pmc_traffic(kernel, E):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
     summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
-    when it was taken on this workload size; else None."""
+    when it was taken on this workload size AND on the kernel sources built
+    into this library (sha256 of csrc/*.hip, *.hpp); else (None, reason)."""
     try:
+        from kernel_hash import kernel_source_sha256
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-        if d.get("workload_E") == E:
-            return d["kernels"][kernel]["hbm_bytes_per_launch"]
-    except Exception:
-        pass
-    return None
+        if d.get("workload_E") != E:
+            return None, "PMC summary taken on another workload"
+        if d.get("kernel_source_sha256") != kernel_source_sha256():
+            return None, "stale: PMC summary taken on other kernel sources"
+        return d["kernels"][kernel]["hbm_bytes_per_launch"], None
+    except Exception as ex:
+        return None, "no PMC summary (%s)" % type(ex).__name__
 
 
 def main():
@@ -135,6 +181,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-kernel HIP events (A/B runs)")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="one rank through the whole distributed path (gloo bootstrap, RCCL "
+                         "communicator, partitioned session): a one-GPU rehearsal of N > 1")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-k0", type=int, default=2)
     ap.add_argument("--cpu-k1", type=int, default=12)
@@ -150,9 +199,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_on = world > 1 or args.dist_selftest
     # CPU baseline first, in its own process, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and wl.name in ("headline", "c1", "c2", "c4") and \
+    if rank == 0 and world == 1 and wl.name in ("headline", "c1", "c2", "c3", "c4", "c5") and \
             not args.no_cpu_baseline:
         cpu = run_cpu_baseline(args)
 
@@ -161,11 +211,16 @@ def main():
     from cp_pfdr_graph_d1_amd import pfdr
 
     torch.cuda.set_device(local)
-    if world > 1:  # host bootstrap only: the data path uses the library's RCCL communicator
+    if dist_on:  # host bootstrap only: the data path uses the library's RCCL communicator
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("gloo")
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier()
 
     strong = args.scaling == "strong" or wl.scaling == "strong"
@@ -176,7 +231,7 @@ def main():
     converge = bool(inp.get("converge", False))
     kw = inp["kw"]
     dist_kw, parallelism, comm = {}, "single", None
-    if world > 1 and wl.partitionable:  # 1-D vertex-range partition, RCCL halo over xGMI
+    if dist_on and wl.partitionable:  # 1-D vertex-range partition, RCCL halo over xGMI
         from cp_pfdr_graph_d1_amd import partition
         comm = partition.comm_init(world, rank, lambda x: dist.broadcast(x, 0))
         dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
@@ -197,11 +252,14 @@ def main():
         del kw
     if warm:
         sess.run(warm)
-    # per-kernel HIP events in the timed region (a few µs of host work per
-    # launch: for a small solve timed to tolerance they would be part of the
-    # time, so that run is timed bare and a second, profiled solve gives the
-    # kernel means)
-    sess.profile(not converge and not args.no_kernel_events)
+    # per-kernel HIP events in the timed region, on the dominant kernels only
+    # and on every PERIOD-th launch (an event pair costs ~6-9 us of GPU time,
+    # profiles/r2/r2d_launch_gap.log); a small solve timed to tolerance is
+    # timed bare and a second, profiled solve gives the kernel means
+    timed = sorted({wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep",
+                    "sx_vertex_sweep", "gemv_cols", "gemv_rows"})
+    period = 4 if world == 1 else 8
+    sess.profile(not converge and not args.no_kernel_events, period=period, only=timed)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -212,7 +270,7 @@ def main():
     done = it - warm
     assert converge or done == steps, (it, warm, steps)
     el_max, E_all = el, E * world
-    if world > 1:  # host reductions (gloo): max time, total edges
+    if dist_on:  # host reductions (gloo): max time, total edges
         tmax = torch.tensor([el], dtype=torch.float64)
         tsum = torch.tensor([E], dtype=torch.int64)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -222,7 +280,7 @@ def main():
         res_timed = sess.result()
         sess.close()
         sess = pfdr.Session(wl.kind, wl.dtype, V, E, itMax=itMax, **kw, **dist_kw)
-        sess.profile(True)
+        sess.profile(True, only=timed)
         sess.run(steps)
         torch.cuda.synchronize()
         del kw
@@ -230,11 +288,6 @@ def main():
              "sx_edge_sweep", "sx_vertex_sweep", "sx_average", "sx_project", "gemv_rows",
              "gemv_cols", "halo_pull", "halo_push")
     stats = {k: sess.kernel_stats(k) for k in names}
-    if stats["edge_sweep_b"][0] and wl.dominant == "edge_sweep":
-        # partitioned with halo overlap: interior + boundary launches per step
-        n_i, m_i = stats["edge_sweep"]
-        n_b, m_b = stats["edge_sweep_b"]
-        stats[wl.dominant] = (n_i, m_i + m_b * n_b / max(n_i, 1))
     res = res_timed if converge else sess.result()
     finite = bool(np.all(np.isfinite(res[0])))
     dev_bytes = sess.device_bytes()
@@ -243,6 +296,9 @@ def main():
     split_blocks = sess.query("split_blocks") if quad else 0
     chunks = sess.query("pipeline_chunks") if quad else 0
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
+    # partitioned with halo overlap: the timed "edge_sweep" launch covers the
+    # interior edges only (the boundary edges run after the halo pull)
+    E_dom = sess.query("interior_edges") if quad else E
     # the edge sweep's kernel: u ends staged in LDS for u-sorted edges
     kname = "k_" + wl.dominant
     if wl.dominant == "edge_sweep" and quad and sess.query("ustaged"):
@@ -253,13 +309,14 @@ def main():
     if comm:
         from cp_pfdr_graph_d1_amd import partition
         partition.comm_destroy(comm)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     if rank != 0:
         return
     ms_step = el_max / max(done, 1) * 1e3
+    traffic, traffic_note = pmc_traffic(kname, E)
     n_dom, ms_dom = stats[wl.dominant]
-    alg = wl.dominant_bytes(V, E)
+    alg = wl.dominant_bytes(V, E_dom)
     achieved = alg / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
     out = {
         "metric": wl.metric,
@@ -296,8 +353,11 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(kname, E),
+            "traffic": traffic,
+            **({"traffic_note": traffic_note} if traffic_note else {}),
             "algorithmic_bytes_per_launch": int(alg),
+            "timed_launches": "every %d-th launch of %s" % (period, ", ".join(
+                k for k in timed if stats.get(k, (0,))[0])),
             "launches": n_dom,
             "mean_ms": round(ms_dom, 5),
             "kernels_mean_ms": {k: round(v[1], 5) for k, v in stats.items() if v[0]},

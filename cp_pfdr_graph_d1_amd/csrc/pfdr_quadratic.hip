@@ -4,6 +4,7 @@
 // of a 1-D vertex-range partition (pfdr_halo.hpp).  Kernels: see
 // pfdr_quadratic_kernels.hpp.
 #include <cstring>
+#include <map>
 #include <stdexcept>
 
 #include <rocprim/rocprim.hpp>
@@ -72,6 +73,7 @@ class QuadSession final : public SessionBase {
         }
         for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
         if (comm_) (void)hipStreamDestroy(comm_);
+        drop_graphs();
     }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
@@ -132,6 +134,18 @@ class QuadSession final : public SessionBase {
     bool stopped_ = false;
     int chunk_ = 32;
     int next_print_ = 0;
+    // hipGraph of a chunk of iterations (single GPU, unprofiled): a replayed
+    // kernel boundary costs ~1.6 us of GPU time, a launched one ~2.8 us
+    // (profiles/r2/r2d_launch_gap.log) -- the difference is a large share of
+    // an iteration of a small graph.  Re-captured after a reconditioning
+    // (new kernel arguments).  PFDR_GRAPH=0 launches directly.
+    bool graphs_ok_ = false;
+    std::map<int, hipGraphExec_t> graphs_;
+    void run_bodies(int n);
+    void drop_graphs() {
+        for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+        graphs_.clear();
+    }
 
     void setup_graph(const pfdr_problem *p);
     void amplitude(bool init);
@@ -156,8 +170,12 @@ class QuadSession final : public SessionBase {
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
-    void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name);
-    void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name);
+    // one launch over [ebeg, eend) and, if not empty, [ebeg2, eend2)
+    void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name,
+                    long ebeg2 = 0, long eend2 = 0);
+    // one launch over the blocks [bbeg, bend) and, if not empty, [bbeg2, bend2)
+    void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name,
+                      int bbeg2 = 0, int bend2 = 0);
     VArgs<real> vargs(int bbeg, int bend, const Ctrl<real> *c);
     // small single-GPU graphs: a chunk of iterations in one workgroup launch
     // (k_tiny_iterate; PFDR_TINY = max edges, 0 = off)
@@ -385,6 +403,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     PFDR_HIP(hipMemcpy(&cw_, &ctrl_.p->c, sizeof(real), hipMemcpyDeviceToHost));
     pins_.release();
     stopped_ = (itMax_ <= 0);
+    interior_edges = E_;
 
     device_bytes = 0;
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
@@ -401,6 +420,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (!(o && o[0] == '0')) plan_overlap();
     } else if (!tiny_) {
         plan_pipeline();
+        const char *g = getenv("PFDR_GRAPH");
+        graphs_ok_ = !(g && g[0] == '0') && itMax_ >= 2 * chunk_;
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
@@ -790,19 +811,23 @@ void QuadSession<real>::objective() {
 }
 
 template <typename real>
-void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name) {
+void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name,
+                                   long ebeg2, long eend2) {
+    constexpr int EPT = Vec<real>::kPer16B;
+    if (eend <= ebeg) { ebeg = ebeg2; eend = eend2; ebeg2 = eend2 = 0; }
     if (eend <= ebeg) return;
     hipStream_t s = stream;
-    constexpr int EPT = Vec<real>::kPer16B;
     ProfScope ps(prof, name, s);
-    const int nb = grid_for(eend - ebeg, EPT), xm = xcd_fit(nb, xcd_e_), g = xcd_grid(nb, xm);
+    ERange rg{ebeg, eend, ebeg2, eend2, grid_for(eend - ebeg, EPT)};
+    const int nb = rg.nb0 + (eend2 > ebeg2 ? grid_for(eend2 - ebeg2, EPT) : 0);
+    const int xm = xcd_fit(nb, xcd_e_), g = xcd_grid(nb, xm);
     if (us_ && uptr_.p)
         k_edge_sweep_us<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p,
                                                    cw_, gi_.p, La_d1_.p, wz_.p, rho_, c, nb,
-                                                   xm, ebeg, eend);
+                                                   xm, rg);
     else
         k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
-                                                La_d1_.p, wz_.p, rho_, c, nb, xm, ebeg, eend);
+                                                La_d1_.p, wz_.p, rho_, c, nb, xm, rg);
 }
 
 template <typename real>
@@ -829,14 +854,23 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
     a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
+    a.bsplit = a.nb; a.bjump = 0;
     return a;
 }
 
 template <typename real>
-void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name) {
+void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name,
+                                     int bbeg2, int bend2) {
+    if (bend <= bbeg) { bbeg = bbeg2; bend = bend2; bbeg2 = bend2 = 0; }
     if (bend <= bbeg) return;
     hipStream_t s = stream;
     VArgs<real> a = vargs(bbeg, bend, c);
+    if (bend2 > bbeg2) {  // second range: logical blocks past the first jump to it
+        a.bsplit = bend - bbeg;
+        a.bjump = bbeg2 - bend;
+        a.nb += bend2 - bbeg2;
+        a.xcd = xcd_fit(a.nb, xcd_v_);
+    }
     ProfScope ps(prof, name, s);
     if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
     else if (gb_ == 4) k_vertex_sweep<real, 4><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
@@ -860,8 +894,7 @@ void QuadSession<real>::body() {
         PFDR_HIP(hipEventRecord(ev_[1], comm_));
         edge_sweep(elo_, ehi_, c, "edge_sweep");
         PFDR_HIP(hipStreamWaitEvent(s, ev_[1], 0));
-        edge_sweep(0, elo_, c, "edge_sweep_b");
-        edge_sweep(ehi_, E_, c, "edge_sweep_b");
+        edge_sweep(0, elo_, c, "edge_sweep_b", ehi_, E_);  // both boundary ranges, one launch
         PFDR_HIP(hipEventRecord(ev_[2], s));
         PFDR_HIP(hipStreamWaitEvent(comm_, ev_[2], 0));
         {
@@ -871,8 +904,7 @@ void QuadSession<real>::body() {
         PFDR_HIP(hipEventRecord(ev_[3], comm_));
         vertex_sweep(blo_, bhi_, c, "vertex_sweep");
         PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
-        vertex_sweep(0, blo_, c, "vertex_sweep_b");
-        vertex_sweep(bhi_, nbv_, c, "vertex_sweep_b");
+        vertex_sweep(0, blo_, c, "vertex_sweep_b", bhi_, nbv_);
     } else if (pblk_.size() > 1) {
         // chunked: E(0), then E(k+1), V(k) for every chunk k
         const int C = (int)pblk_.size() - 1;
@@ -992,7 +1024,35 @@ void QuadSession<real>::plan_overlap() {
     PFDR_HIP(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
     for (hipEvent_t &e : ev_) PFDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     overlap_ = true;
+    interior_edges = ehi_ - elo_;
     (void)s;
+}
+
+template <typename real>
+void QuadSession<real>::run_bodies(int n) {
+    if (!graphs_ok_ || prof.on) {
+        for (int i = 0; i < n; i++) body();
+        return;
+    }
+    auto it = graphs_.find(n);
+    if (it == graphs_.end()) {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        try {
+            for (int i = 0; i < n; i++) body();
+        } catch (...) {
+            (void)hipStreamEndCapture(stream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        PFDR_HIP(hipStreamEndCapture(stream, &g));
+        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        PFDR_HIP(e);
+        it = graphs_.emplace(n, ge).first;
+    }
+    PFDR_HIP(hipGraphLaunch(it->second, stream));
 }
 
 template <typename real>
@@ -1015,7 +1075,7 @@ int QuadSession<real>::run(int iters) {
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
         if (tiny_) tiny_chunk(n);
-        else for (int i = 0; i < n; i++) body();
+        else run_bodies(n);
         if (gated) {
             pull_ctrl();
             it_ = hctrl_->it;
@@ -1024,6 +1084,7 @@ int QuadSession<real>::run(int iters) {
             } else if (hctrl_->recond) {
                 if (verbose_) { print_progress(); printf("Reconditioning... "); fflush(stdout); }
                 precondition(false);
+                drop_graphs();  // A1_ now holds the splitting weights' factors
                 difRcd2_ *= real(0.01);  // ref :458
                 hctrl_->difRcd = difRcd2_;
                 hctrl_->recond = 0;

@@ -961,6 +961,18 @@ __device__ __forceinline__ void edge_full(const R2<real> &pu, const R2<real> &pv
     ov = wv * zv;
 }
 
+// One or two edge ranges of one launch: logical blocks [0, nb0) sweep
+// [b0, e0), the others [b1, e1) (a partitioned session's two boundary
+// ranges, before and after the interior run, in a single launch)
+struct ERange {
+    long b0, e0, b1, e1;
+    int nb0;
+    __device__ __forceinline__ void pick(int &blk, long &ebeg, long &eend) const {
+        if (blk < nb0) { ebeg = b0; eend = e0; }
+        else { blk -= nb0; ebeg = b1; eend = e1; }
+    }
+};
+
 // Edge sweep over the edges [ebeg, eend) (ebeg a multiple of the lane
 // width); writes the DR contributions W*Z side-major: wz[e] (u end),
 // wz[E + e] (v end), so the u-side run of a vertex is contiguous.  Streams
@@ -971,11 +983,13 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
-    real rho, const Ctrl<real> *ctrl, int nb, int xcd, long ebeg, long eend) {
+    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;
+    long ebeg, eend;
+    rg.pick(blk, ebeg, eend);
     const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
     if (e0 >= eend) return;
     if (e0 + EPT <= eend) {
@@ -1035,15 +1049,17 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
     const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
     const real *__restrict__ La_d1, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
-    int nb, int xcd, long ebeg, long eend) {
+    int nb, int xcd, ERange rg) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int CAP = USpan<real>::v;
     __shared__ int s_ptr[CAP + 1];
     __shared__ R2<real> s_xp[CAP];
     __shared__ R2<real> s_gi[CAP];
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
+    long ebeg, eend;
+    rg.pick(blk, ebeg, eend);
     const int tid = threadIdx.x;
     const long eb = ebeg + (long)blk * kBlock * EPT;
     const long el = min(eb + (long)kBlock * EPT, eend) - 1;  // block's last edge
@@ -1130,6 +1146,7 @@ struct VArgs {
     int V;
     int nb, xcd;            // logical blocks of this launch, XCD-aware order
     int bbeg;               // first block of this launch (vertex block bbeg*256)
+    int bsplit, bjump;      // logical blocks >= bsplit skip bjump blocks (two ranges)
     const int *ptr;
     const unsigned *idx;
     const int *uptr;        // split incidence (null: CSR gather everywhere)
@@ -1250,8 +1267,9 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
     __shared__ int scan[kBlock / kWave];
-    const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
+    int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
+    if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan);
 }
 

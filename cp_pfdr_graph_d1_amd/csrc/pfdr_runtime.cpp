@@ -274,6 +274,12 @@ HostPins::~HostPins() {
 }
 
 // ------------------------------------------------------------ Profiler --
+// Timing events without the system-scope fence: a default event pair costs
+// ~9 us of GPU time per bracketed launch on MI355X, ~6 us without the fence
+// (tools/exp_launch_gap.hip, profiles/r2/r2d_launch_gap.log).  The events
+// are only read after the stream is synchronised.
+static constexpr unsigned kProfEventFlags = hipEventDisableSystemFence;
+
 Profiler::~Profiler() {
     for (auto &p : pend_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : pool_) (void)hipEventDestroy(e);
@@ -287,19 +293,24 @@ hipEvent_t Profiler::take() {
         return e;
     }
     hipEvent_t e;
-    PFDR_HIP(hipEventCreate(&e));
+    PFDR_HIP(hipEventCreateWithFlags(&e, kProfEventFlags));
     return e;
 }
 
 void Profiler::reserve(int n) {
     for (int i = (int)pool_.size(); i < n; i++) {
         hipEvent_t e;
-        PFDR_HIP(hipEventCreate(&e));
+        PFDR_HIP(hipEventCreateWithFlags(&e, kProfEventFlags));
         pool_.push_back(e);
     }
 }
 
-void Profiler::begin(const char *name, hipStream_t s) {
+bool Profiler::begin(const char *name, hipStream_t s) {
+    if (!only.empty()) {
+        bool hit = false;
+        for (const auto &o : only) hit |= (o == name);
+        if (!hit) return false;
+    }
     auto it = ids_.find(name);
     int id;
     if (it == ids_.end()) {
@@ -307,12 +318,15 @@ void Profiler::begin(const char *name, hipStream_t s) {
         ids_[name] = id;
         total_ms_.push_back(0.0);
         count_.push_back(0);
+        seen_.push_back(0);
     } else {
         id = it->second;
     }
+    if (seen_[id]++ % (period > 0 ? period : 1)) return false;
     open_id_ = id;
     open_ev_ = take();
     PFDR_HIP(hipEventRecord(open_ev_, s));
+    return true;
 }
 
 void Profiler::end(hipStream_t s) {
@@ -419,10 +433,28 @@ extern "C" void *pfdr_session_device_x(pfdr_session *s) {
     return nullptr;
 }
 
+extern "C" int pfdr_session_profile_filter(pfdr_session *s, const char *names) {
+    if (!s) return report_error("pfdr_session_profile_filter", "null session");
+    auto &o = s->impl->prof.only;
+    o.clear();
+    if (names) {
+        std::string n(names);
+        size_t a = 0;
+        while (a <= n.size()) {
+            size_t b = n.find(',', a);
+            if (b == std::string::npos) b = n.size();
+            if (b > a) o.push_back(n.substr(a, b - a));
+            a = b + 1;
+        }
+    }
+    return PFDR_OK;
+}
+
 extern "C" int pfdr_session_set_profiling(pfdr_session *s, int on) {
     if (!s) return report_error("pfdr_session_set_profiling", "null session");
     PFDR_GUARD("pfdr_session_set_profiling", {
         s->impl->prof.on = (on != 0);
+        s->impl->prof.period = on > 1 ? on : 1;
         if (on) s->impl->prof.reserve(1024);  // no event creation between timed launches
     });
     return PFDR_OK;
@@ -462,6 +494,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "pipeline_chunks")) *value = s->impl->pipeline_chunks;
+    else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());
     return PFDR_OK;

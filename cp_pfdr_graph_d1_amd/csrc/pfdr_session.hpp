@@ -11,13 +11,18 @@
 namespace pfdr {
 
 // HIP-event timing of named kernels on the session stream.  When enabled,
-// every launch of a profiled kernel is bracketed by two events; durations
-// are resolved after the stream has been synchronised.
+// every `period`-th launch of a profiled kernel (all kernels, or those named
+// in `only`) is bracketed by two events; durations are resolved after the
+// stream has been synchronised.  An event pair costs ~9 us of GPU time on
+// MI355X (profiles/r2/r2d_launch_gap.log): sampling keeps that out of the
+// timed iterations of small or partitioned graphs.
 class Profiler {
   public:
     bool on = false;
+    int period = 1;
+    std::vector<std::string> only;
     ~Profiler();
-    void begin(const char *name, hipStream_t s);
+    bool begin(const char *name, hipStream_t s);  // false: this launch not timed
     void end(hipStream_t s);
     void resolve();  // call after the stream has been synchronised
     void reserve(int n);  // pre-create n events (no hipEventCreate between launches)
@@ -29,7 +34,7 @@ class Profiler {
     std::vector<hipEvent_t> pool_;
     std::map<std::string, int> ids_;
     std::vector<double> total_ms_;
-    std::vector<int> count_;
+    std::vector<int> count_, seen_;
     int open_id_ = -1;
     hipEvent_t open_ev_ = nullptr;
     hipEvent_t take();
@@ -40,7 +45,7 @@ struct ProfScope {
     hipStream_t s;
     bool on;
     ProfScope(Profiler &pr, const char *name, hipStream_t st)
-        : p(pr), s(st), on(pr.on) { if (on) p.begin(name, s); }
+        : p(pr), s(st), on(pr.on && pr.begin(name, st)) {}
     ~ProfScope() { if (on) p.end(s); }
 };
 
@@ -60,6 +65,7 @@ class SessionBase {
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
     int64_t pipeline_chunks = 0;  // pipelined iteration: vertex chunks per iteration
+    int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;

@@ -45,7 +45,7 @@ EXPORTED = (
     "pfdr_cpgraph_get_reduced", "pfdr_cpgraph_merge", "pfdr_cpgraph_gradient",
     "pfdr_cpgraph_capacities", "pfdr_cpgraph_activate",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
-    "pfdr_session_device_x", "pfdr_session_set_profiling",
+    "pfdr_session_device_x", "pfdr_session_set_profiling", "pfdr_session_profile_filter",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
     "pfdr_session_device_bytes", "pfdr_session_query", "pfdr_session_destroy",
     "pfdr_comm_unique_id", "pfdr_comm_init", "pfdr_comm_destroy",
@@ -523,9 +523,13 @@ class Session:
     def sync(self):
         _check(self.lib.pfdr_session_sync(self.h), "pfdr_session_sync")
 
-    def profile(self, on=True):
-        _check(self.lib.pfdr_session_set_profiling(self.h, C.c_int(int(on))),
-               "pfdr_session_set_profiling")
+    def profile(self, on=True, period=1, only=None):
+        """time kernels with HIP events: every `period`-th launch, of the
+        kernels named in `only` (all when None)"""
+        _check(self.lib.pfdr_session_profile_filter(
+            self.h, None if not only else ",".join(only).encode()), "pfdr_session_profile_filter")
+        _check(self.lib.pfdr_session_set_profiling(
+            self.h, C.c_int(0 if not on else max(int(period), 1))), "pfdr_session_set_profiling")
 
     def kernel_stats(self, name):
         n, ms = C.c_int(0), C.c_double(0.0)

@@ -171,9 +171,14 @@ int pfdr_session_result(pfdr_session *s, void *X_host, int *it, void *Obj_host,
                         void *Dif_host);
 /* Device pointer of the current iterate (valid until destroy). */
 void *pfdr_session_device_x(pfdr_session *s);
-/* Kernel timing: when enabled, HIP events bracket each launch of the named
- * kernels on the session stream; stats give launches and mean duration. */
+/* Kernel timing: when enabled, HIP events bracket the launches of the named
+ * kernels on the session stream; stats give timed launches and mean
+ * duration.  on = 0 off, 1 every launch, P >= 2 every P-th launch of each
+ * kernel (an event pair costs ~6-9 us of GPU time: sampling keeps it out of
+ * short iterations).  The filter restricts timing to a comma-separated list
+ * of kernel names (NULL or "" = all). */
 int pfdr_session_set_profiling(pfdr_session *s, int on);
+int pfdr_session_profile_filter(pfdr_session *s, const char *names);
 int pfdr_session_kernel_stats(pfdr_session *s, const char *kernel,
                               int *launches, double *mean_ms);
 /* Synchronise the session stream. */

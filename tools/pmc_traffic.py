@@ -35,9 +35,12 @@ def counter(dirname, name):
 def main(root, workload="headline", E=60000000, V=10000000):
     fetch = counter(os.path.join(root, "fetch"), "FETCH_SIZE")
     write = counter(os.path.join(root, "write"), "WRITE_SIZE")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from kernel_hash import kernel_source_sha256
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel "
                      "trace only), bench.py --workload %s" % workload,
-           "workload": workload, "workload_E": E, "workload_V": V, "kernels": {}}
+           "workload": workload, "workload_E": E, "workload_V": V,
+           "kernel_source_sha256": kernel_source_sha256(), "kernels": {}}
     for k in sorted(set(fetch) & set(write)):
         if not k.startswith("k_"):
             continue

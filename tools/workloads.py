@@ -89,6 +89,16 @@ class Headline(Workload):
                     graph="%dx%dx%d" % g)
 
 
+class HeadlineSlab8(Headline):
+    """Rehearsal of one rank of the 8-GPU strong split on one GPU: the
+    250x200x25 graph (1.25M vertices, 7.5M edges) every rank owns at N = 8,
+    as a standalone single-GPU problem (no halo): the compute floor of an
+    8-GPU iteration."""
+    name = "headline_slab8"
+    partitionable = False
+    SHAPE = (250, 200, 25)
+
+
 class HeadlineShuffled(Headline):
     """SURVEY.md §8(d) headline ordering (ii): the same graph and data with a
     random vertex relabelling and an edge shuffle (seed 7).  Single GPU: a
@@ -345,4 +355,5 @@ class C3AtA(Workload):
         return 4 * V * (V + 1) // 2 + self.edge_bytes * E + self.vertex_bytes * V
 
 
-WORKLOADS = {w.name: w for w in (Headline(), HeadlineShuffled(), C1(), C2(), C3(), C3AtA(), C4(), C5())}
+WORKLOADS = {w.name: w for w in (Headline(), HeadlineSlab8(), HeadlineShuffled(), C1(), C2(), C3(),
+                                  C3AtA(), C4(), C5())}
