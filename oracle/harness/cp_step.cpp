@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <cstdint>
+#include <ctime>
 
 #include "graph.hpp"
 #include "PFDR_graph_quadratic_d1_l1.hpp"
@@ -44,8 +45,22 @@ struct Rec {
     int called, rV, rE;
     int *rEu, *rEv;
     void *rLa_d1, *rLa_l1, *rY, *rAA;
+    /* dense modes (N != 0): the N handed to PFDR (-rV premultiplied, N
+     * direct), its data vector (rY or Y), matrix (rAA rV x rV or rA N x rV)
+     * and DIAG Lipschitz metric L[rV] */
+    int n, dense;
+    void *dY, *dA, *dL;
 };
 static Rec *g_rec = nullptr;
+
+/* The operator norm of the reduced problem is seeded with time(NULL)
+ * (src/operator_norm_matrix.cpp:182): a constant here (this library is
+ * linked -Bsymbolic so its own calls bind to it) makes the recorded L
+ * reproducible. */
+extern "C" time_t time(time_t *t) {
+    if (t) *t = (time_t)1;
+    return (time_t)1;
+}
 
 template <typename real>
 void PFDR_graph_quadratic_d1_l1(const int V, const int E, const int N, real *X, const real *Y,
@@ -62,8 +77,15 @@ void PFDR_graph_quadratic_d1_l1(const int V, const int E, const int N, real *X, 
         memcpy(g_rec->rEv, Ev, sizeof(int) * E);
         memcpy(g_rec->rLa_d1, La_d1, sizeof(real) * E);
         if (La_l1) memcpy(g_rec->rLa_l1, La_l1, sizeof(real) * V);
-        memcpy(g_rec->rY, Y, sizeof(real) * V);
-        if (A) memcpy(g_rec->rAA, A, sizeof(real) * V);
+        g_rec->n = N;
+        if (!g_rec->dense) {
+            memcpy(g_rec->rY, Y, sizeof(real) * V);
+            if (A) memcpy(g_rec->rAA, A, sizeof(real) * V);
+        } else {
+            memcpy(g_rec->dY, Y, sizeof(real) * (N > 0 ? N : V));
+            memcpy(g_rec->dA, A, sizeof(real) * (N > 0 ? (size_t)N * V : (size_t)V * V));
+            memcpy(g_rec->dL, L, sizeof(real) * V);
+        }
     }
     ref_rec_pfdr_l1<real>(V, E, N, X, Y, A, Eu, Ev, La_d1, La_l1, positivity, Ltype, L, rho,
                           condMin, difRcd, difTol, itMax, it, Obj, Dif, verbose);
@@ -88,12 +110,12 @@ static Graph<real, real, real> *make_graph(int V, int E, const int *Eu, const in
 }
 
 template <typename real>
-static int init(int V, int E, const real *Y, const real *A, const int *Eu, const int *Ev,
+static int init(int V, int E, int N, const real *Y, const real *A, const int *Eu, const int *Ev,
                 const real *La_d1, const real *La_l1, int positivity, real *rX0) {
     int rV = 0, CP_it = 0;
     int *Cv = (int *)malloc(sizeof(int) * V);
     real *rX = nullptr;
-    CP_PFDR_graph_quadratic_d1_l1<real>(V, E, 0, &rV, Cv, &rX, Y, A, Eu, Ev, La_d1, La_l1,
+    CP_PFDR_graph_quadratic_d1_l1<real>(V, E, N, &rV, Cv, &rX, Y, A, Eu, Ev, La_d1, La_l1,
                                         positivity, (real)0, 0, &CP_it, (real)1.5, (real)1e-3,
                                         (real)0, (real)1e-4, 10, nullptr, nullptr, nullptr, 0,
                                         nullptr);
@@ -104,15 +126,15 @@ static int init(int V, int E, const real *Y, const real *A, const int *Eu, const
 }
 
 template <typename real>
-static int step(int V, int E, const real *Y, const real *A, const int *Eu, const int *Ev,
+static int step(int V, int E, int N, const real *Y, const real *A, const int *Eu, const int *Ev,
                 const real *La_d1, const real *La_l1, int positivity, real CP_difTol,
                 real rho, real condMin, real difRcd, real difTol, int itMax,
                 /* state in / out */
                 uint8_t *active, int *Cv, int *Vc, int *rVc, int *rV, real *rX,
-                uint8_t *segment,
+                const real *R_in, uint8_t *segment,
                 /* recorded reduced problem */
                 int *called, int *rE, int *rEu, int *rEv, real *rLa_d1, real *rLa_l1, real *rY,
-                real *rAA) {
+                real *rAA, int *n_out, real *dY, real *dA, real *dL) {
     CPql1_Restart<real> rs;
     rs.G = make_graph<real>(V, E, Eu, Ev);
     for (int e = 0; e < E; e++) {
@@ -124,17 +146,22 @@ static int step(int V, int E, const real *Y, const real *A, const int *Eu, const
     rs.rVc = (int *)malloc(sizeof(int) * (*rV + 1));
     memcpy(rs.rVc, rVc, sizeof(int) * (*rV + 1));
     rs.R = nullptr;
+    if (N > 0) {  /* the residual Y - A X of the state (the caller's) */
+        rs.R = (real *)malloc(sizeof(real) * N);
+        memcpy(rs.R, R_in, sizeof(real) * N);
+    }
     real *x = (real *)malloc(sizeof(real) * (*rV));
     memcpy(x, rX, sizeof(real) * (*rV));
-    Rec rec{0, 0, 0, rEu, rEv, rLa_d1, rLa_l1, rY, rAA};
+    Rec rec{0, 0, 0, rEu, rEv, rLa_d1, rLa_l1, rY, rAA, 0, N != 0, dY, dA, dL};
     g_rec = &rec;
     int CP_it = 0;
-    CP_PFDR_graph_quadratic_d1_l1<real>(V, E, 0, rV, Cv, &x, Y, A, Eu, Ev, La_d1, La_l1,
+    CP_PFDR_graph_quadratic_d1_l1<real>(V, E, N, rV, Cv, &x, Y, A, Eu, Ev, La_d1, La_l1,
                                         positivity, CP_difTol, 1, &CP_it, rho, condMin, difRcd,
                                         difTol, itMax, nullptr, nullptr, nullptr, 0, &rs);
     g_rec = nullptr;
     *called = rec.called;
     *rE = rec.rE;
+    if (n_out) *n_out = rec.n;
     for (int e = 0; e < E; e++) active[e] = rs.G->arcs[2 * e].is_active;
     for (int v = 0; v < V; v++) segment[v] = (uint8_t)rs.G->what_segment(v);
     memcpy(Vc, rs.Vc, sizeof(int) * V);
@@ -144,6 +171,7 @@ static int step(int V, int E, const real *Y, const real *A, const int *Eu, const
     delete rs.G;
     free(rs.Vc);
     free(rs.rVc);
+    free(rs.R);
     return CP_it;
 }
 
@@ -166,16 +194,32 @@ static real maxflow(int V, int E, const int *Eu, const int *Ev, const real *tr_c
     extern "C" int cp_ref_init_##SFX(int V, int E, const T *Y, const T *A, const int *Eu,     \
                                      const int *Ev, const T *La_d1, const T *La_l1, int pos,   \
                                      T *rX0) {                                                 \
-        return init<T>(V, E, Y, A, Eu, Ev, La_d1, La_l1, pos, rX0);                            \
+        return init<T>(V, E, 0, Y, A, Eu, Ev, La_d1, La_l1, pos, rX0);                         \
+    }                                                                                          \
+    extern "C" int cp_ref_init_dense_##SFX(int V, int E, int N, const T *Y, const T *A,       \
+                                           const int *Eu, const int *Ev, const T *La_d1,       \
+                                           const T *La_l1, int pos, T *rX0) {                  \
+        return init<T>(V, E, N, Y, A, Eu, Ev, La_d1, La_l1, pos, rX0);                         \
+    }                                                                                          \
+    extern "C" int cp_ref_step_dense_##SFX(                                                    \
+        int V, int E, int N, const T *Y, const T *A, const int *Eu, const int *Ev,             \
+        const T *La_d1, const T *La_l1, int pos, T CP_difTol, T rho, T condMin, T difRcd,      \
+        T difTol, int itMax, uint8_t *active, int *Cv, int *Vc, int *rVc, int *rV, T *rX,      \
+        const T *R, uint8_t *segment, int *called, int *rE, int *rEu, int *rEv, T *rLa_d1,     \
+        T *rLa_l1, int *n_out, T *dY, T *dA, T *dL) {                                          \
+        return step<T>(V, E, N, Y, A, Eu, Ev, La_d1, La_l1, pos, CP_difTol, rho, condMin,      \
+                       difRcd, difTol, itMax, active, Cv, Vc, rVc, rV, rX, R, segment, called,  \
+                       rE, rEu, rEv, rLa_d1, rLa_l1, nullptr, nullptr, n_out, dY, dA, dL);     \
     }                                                                                          \
     extern "C" int cp_ref_step_##SFX(                                                          \
         int V, int E, const T *Y, const T *A, const int *Eu, const int *Ev, const T *La_d1,    \
         const T *La_l1, int pos, T CP_difTol, T rho, T condMin, T difRcd, T difTol, int itMax, \
         uint8_t *active, int *Cv, int *Vc, int *rVc, int *rV, T *rX, uint8_t *segment,         \
         int *called, int *rE, int *rEu, int *rEv, T *rLa_d1, T *rLa_l1, T *rY, T *rAA) {       \
-        return step<T>(V, E, Y, A, Eu, Ev, La_d1, La_l1, pos, CP_difTol, rho, condMin, difRcd, \
-                       difTol, itMax, active, Cv, Vc, rVc, rV, rX, segment, called, rE, rEu,   \
-                       rEv, rLa_d1, rLa_l1, rY, rAA);                                          \
+        return step<T>(V, E, 0, Y, A, Eu, Ev, La_d1, La_l1, pos, CP_difTol, rho, condMin,      \
+                       difRcd, difTol, itMax, active, Cv, Vc, rVc, rV, rX, nullptr, segment,    \
+                       called, rE, rEu, rEv, rLa_d1, rLa_l1, rY, rAA, nullptr, nullptr,         \
+                       nullptr, nullptr);                                                       \
     }                                                                                          \
     extern "C" T cp_ref_maxflow_##SFX(int V, int E, const int *Eu, const int *Ev,              \
                                       const T *tr_cap, const T *r_cap, uint8_t *segment) {     \

@@ -388,6 +388,71 @@ class CPStepRef:
                    "rY": rY[:n].copy(), "rAA": rAA[:n].copy()}
         return new, seg, red
 
+    def init_dense(self, Y, A, N, Eu, Ev, La_d1, La_l1, positivity):
+        """rX0 of the reference's initialize() for any N (one component)."""
+        Y = np.ascontiguousarray(Y)
+        ct, sfx = _real(Y.dtype)
+        A = None if A is None else np.ascontiguousarray(A, Y.dtype)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, Y.dtype)
+        V = int(np.asarray(La_l1).size) if La_l1 is not None else int(Eu.max()) + 1
+        rX0 = np.zeros(1, Y.dtype)
+        getattr(self.lib, "cp_ref_init_dense_" + sfx)(
+            C.c_int(V), C.c_int(Eu.size), C.c_int(N), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, Y.dtype), ct), _ptr(La_l1, ct),
+            C.c_int(int(positivity)), _ptr(rX0, ct))
+        return rX0
+
+    def step_dense(self, V, N, Y, A, Eu, Ev, La_d1, La_l1, positivity, CP_difTol, state, R,
+                   rho=1.5, condMin=1e-3, difRcd=0.0, difTol=1e-5, itMax=2000):
+        """One reference CP iteration with a dense A (N > 0: N-by-V column
+        major, with the state's residual R = Y - A X; N < 0: A^tA), from
+        ``state``; returns (new state, recorded dense reduced problem or
+        None): n handed to PFDR, its data vector, matrix and L[rV]."""
+        Y = np.ascontiguousarray(Y)
+        dt = Y.dtype
+        ct, sfx = _real(dt)
+        E = Eu.size
+        A = np.ascontiguousarray(A, dt)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+        act = np.array(state["active"], np.uint8, copy=True)
+        Cv = np.array(state["Cv"], np.int32, copy=True)
+        Vc = np.array(state["Vc"], np.int32, copy=True)
+        rV = C.c_int(int(state["rVc"].size - 1))
+        rVc = np.zeros(V + 1, np.int32)
+        rVc[:rV.value + 1] = state["rVc"]
+        rX = np.zeros(V, dt)
+        rX[:rV.value] = state["rX"]
+        R = None if R is None else np.ascontiguousarray(R, dt)
+        seg = np.zeros(V, np.uint8)
+        called, rE, n = C.c_int(0), C.c_int(0), C.c_int(0)
+        rEu = np.zeros(E + V, np.int32)
+        rEv = np.zeros(E + V, np.int32)
+        rLa = np.zeros(E + V, dt)
+        rL1 = np.zeros(V, dt)
+        dY = np.zeros(max(abs(N), V), dt)
+        dA = np.zeros(max(abs(N), V) * V, dt)
+        dL = np.zeros(V, dt)
+        getattr(self.lib, "cp_ref_step_dense_" + sfx)(
+            C.c_int(V), C.c_int(E), C.c_int(N), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, dt), ct), _ptr(La_l1, ct), C.c_int(int(positivity)),
+            ct(CP_difTol), ct(rho), ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax),
+            _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int),
+            C.byref(rV), _ptr(rX, ct), _ptr(R, ct), _ptr(seg, C.c_uint8), C.byref(called),
+            C.byref(rE), _ptr(rEu, C.c_int), _ptr(rEv, C.c_int), _ptr(rLa, ct), _ptr(rL1, ct),
+            C.byref(n), _ptr(dY, ct), _ptr(dA, ct), _ptr(dL, ct))
+        k = rV.value
+        new = {"active": act, "Cv": Cv, "Vc": Vc, "rVc": rVc[:k + 1].copy(), "rX": rX[:k].copy()}
+        red = None
+        if called.value:
+            nn = n.value
+            red = {"n": nn, "Y": dY[:(nn if nn > 0 else k)].copy(),
+                   "A": dA[:(nn * k if nn > 0 else k * k)].copy(), "L": dL[:k].copy()}
+        return new, red
+
     def maxflow(self, Eu, Ev, tr_cap, r_cap):
         """Segments (0 source, 1 sink) of the reference's BK maxflow."""
         tr_cap = np.ascontiguousarray(tr_cap)

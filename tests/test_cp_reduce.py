@@ -92,3 +92,71 @@ def test_gpu_builder_bitexact(gpu_lib, oracle_port, dt, kind, preAt, size):
     # the power method stops on a relative evolution below nTol: without a
     # spectral gap it can stop short of the top eigenvalue
     assert np.allclose(g["L"], l * l * c, rtol=2e-2)
+
+
+# ---- pinned to the REFERENCE: the dense reduced problems its cut pursuit
+# handed to PFDR (tests/golden/make_cp_dense_golden.py, N > 0 direct and
+# premultiplied branches, N < 0), iteration by iteration
+import os  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DENSE_PINS = sorted(f[:-4] for f in os.listdir(GOLD) if f.startswith("cp_dense_"))
+
+
+def _pinned_iterations(name):
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    N, V = int(g["in_N"]), int(g["in_Y"].size if int(g["in_N"]) <= 0 else g["in_La_l1"].size)
+    A = g["in_A"]
+    Am = A.reshape(V, N).T if N > 0 else A.reshape(V, V)
+    ks = sorted({int(k.split("_")[0][1:]) for k in g.files if k.startswith("k") and "_red_" in k})
+    return g, N, V, Am, ks
+
+
+def _check_pin(out, g, k, N):
+    n = int(g["k%d_red_n" % k])
+    A, Y = g["k%d_red_A" % k], g["k%d_red_Y" % k]
+    if n > 0:   # direct reduced matrix rA (N x rV, column major), original Y
+        assert np.array_equal(out["rA"].T.ravel(), A), "rA"
+        assert np.array_equal(Y, g["in_Y"])
+    else:       # premultiplied: rAA (rV x rV) and rY
+        assert np.array_equal(np.asarray(out["rAA"]).ravel(), A), "rAA"
+        assert np.array_equal(out["rY"], Y), "rY"
+    return n
+
+
+@pytest.mark.parametrize("name", DENSE_PINS)
+def test_restatement_pinned_to_reference_dense(oracle_port, name):
+    """the restatement rebuilds, from the components the reference used,
+    the exact arrays the reference handed to PFDR, and the reference's L is
+    Leq^2 times one operator-norm estimate c"""
+    g, N, V, Am, ks = _pinned_iterations(name)
+    assert ks, "no recorded PFDR call"
+    branches = set()
+    for k in ks:
+        n = int(g["k%d_red_n" % k])
+        o = oracle_port.cp_reduce(N, Am, g["in_Y"], g["k%d_rVc" % k], g["k%d_Vc" % k],
+                                  preAt=n < 0)
+        branches.add(_check_pin(o, g, k, N) > 0)
+        L = g["k%d_red_L" % k].astype(np.float64)
+        c = L / o["Leq"].astype(np.float64) ** 2
+        assert np.allclose(c, c.mean(), rtol=1e-5), "L = Leq^2 c with one c"
+    if "direct_few" in name:
+        assert branches == {True}
+    else:
+        assert branches == {False}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", DENSE_PINS)
+def test_gpu_builder_pinned_to_reference_dense(gpu_lib, name):
+    """pfdr_cp_reduce on the reference's recorded components: rA / rAA / rY
+    bit for bit as the reference built them; L within the power method's
+    tolerance of the reference's (its starts are time-seeded, ours fixed)"""
+    from cp_pfdr_graph_d1_amd import pfdr
+    g, N, V, Am, ks = _pinned_iterations(name)
+    for k in ks:
+        n = int(g["k%d_red_n" % k])
+        out = pfdr.cp_reduce(N, Am, g["in_Y"], g["k%d_rVc" % k], g["k%d_Vc" % k], preAt=n < 0)
+        _check_pin(out, g, k, N)
+        L_ref = g["k%d_red_L" % k].astype(np.float64)
+        assert np.allclose(out["L"], L_ref, rtol=2e-2), (k, np.max(np.abs(out["L"] / L_ref - 1)))
