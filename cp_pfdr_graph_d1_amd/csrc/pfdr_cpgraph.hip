@@ -596,6 +596,22 @@ __global__ void k_cp_trcap(int V, int cut, int positivity, const real *__restric
     tr[v] = t;
 }
 
+// the bounds driver's cuts (src/CP_PFDR_graph_quadratic_d1_bounds.cpp:386-534):
+// cut 1 +inf on components at max (max < inf), else DfS; cut 2 +inf on
+// components at min (-inf < min), else -DfS; cut 0 DfS
+template <typename real>
+__global__ void k_cp_trcap_bounds(int V, int cut, real mn, real mx, const int *__restrict__ Cv,
+                                  const real *__restrict__ rX, const real *__restrict__ DfS,
+                                  real *__restrict__ tr) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const real inf = Lim<real>::huge, x = rX[Cv[v]];
+    real t = DfS[v];
+    if (cut == 1) t = (mx < inf && x == mx) ? inf : DfS[v];
+    else if (cut == 2) t = (-inf < mn && x == mn) ? inf : -DfS[v];
+    tr[v] = t;
+}
+
 template <typename real>
 __global__ void k_cp_rcap(long E, const uint8_t *__restrict__ active, const real *__restrict__ La,
                           real *__restrict__ rc) {
@@ -642,6 +658,9 @@ struct CpGraphBase {
     virtual int merge(double eps, double difTol) = 0;
     virtual void gradient(int N, const void *A, const void *Y, const void *R, int mem) = 0;
     virtual void capacities(int cut, int positivity, void *tr, void *rc, int mem) = 0;
+    // bounds driver: box [mn, mx] (+-HUGE_VAL for none) instead of l1 / positivity
+    virtual void capacities_bounds(int cut, double mn, double mx, void *tr, void *rc,
+                                   int mem) = 0;
     virtual void set_values(const void *rX, int mem) = 0;
     virtual void get_reduced(int *rEu_o, int *rEv_o, void *rLa_o, void *rL1_o, int mem) = 0;
     virtual void get_dfs(void *out, int mem) = 0;
@@ -871,10 +890,17 @@ struct CpGraph : CpGraphBase {
         PFDR_HIP(hipStreamSynchronize(s));
     }
 
+    void capacities_bounds(int cut, double mn, double mx, void *tr, void *rc, int mem) override {
+        capacities_impl(cut, 0, true, (real)mn, (real)mx, tr, rc, mem);
+    }
     void capacities(int cut, int positivity, void *tr, void *rc, int mem) override {
-        if (!DfS.p) throw std::runtime_error("capacities: compute the gradient first");
         if (cut == 2 && !positivity && !has_l1)
             throw std::runtime_error("capacities: cut 2 without positivity needs La_l1");
+        capacities_impl(cut, positivity, false, real(0), real(0), tr, rc, mem);
+    }
+    void capacities_impl(int cut, int positivity, bool bounds, real mn, real mx, void *tr,
+                         void *rc, int mem) {
+        if (!DfS.p) throw std::runtime_error("capacities: compute the gradient first");
         DevBuf<real> btr, brc;
         real *dtr = (real *)tr, *drc = (real *)rc;
         if (mem != PFDR_MEM_DEVICE) {
@@ -883,7 +909,10 @@ struct CpGraph : CpGraphBase {
             dtr = btr.p;
             drc = brc.p;
         }
-        if (tr)
+        if (tr && bounds)
+            k_cp_trcap_bounds<real><<<grid_for(V), kBlock, 0, s>>>(V, cut, mn, mx, Cv.p, rX.p,
+                                                                   DfS.p, dtr);
+        else if (tr)
             k_cp_trcap<real><<<grid_for(V), kBlock, 0, s>>>(V, cut, positivity,
                                                             has_l1 ? L1.p : nullptr, Cv.p, rX.p,
                                                             DfS.p, dtr);
@@ -1093,6 +1122,14 @@ extern "C" int pfdr_cpgraph_capacities(pfdr_cpgraph *h, int cut, int positivity,
                                        void *r_cap, int mem) {
     if (!h || cut < 0 || cut > 2) return report_error("pfdr_cpgraph_capacities", "invalid arguments");
     CPG_TRY("pfdr_cpgraph_capacities", h->g->capacities(cut, positivity, tr_cap, r_cap, mem))
+}
+
+extern "C" int pfdr_cpgraph_capacities_bounds(pfdr_cpgraph *h, int cut, double min, double max,
+                                              void *tr_cap, void *r_cap, int mem) {
+    if (!h || cut < 0 || cut > 2)
+        return report_error("pfdr_cpgraph_capacities_bounds", "invalid arguments");
+    CPG_TRY("pfdr_cpgraph_capacities_bounds",
+            h->g->capacities_bounds(cut, min, max, tr_cap, r_cap, mem))
 }
 
 extern "C" int pfdr_cpgraph_activate(pfdr_cpgraph *h, const uint8_t *segment, int mem,

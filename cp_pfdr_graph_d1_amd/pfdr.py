@@ -43,7 +43,7 @@ EXPORTED = (
     "pfdr_cpgraph_get_active", "pfdr_cpgraph_set_components", "pfdr_cpgraph_get_components",
     "pfdr_cpgraph_set_values", "pfdr_cpgraph_components", "pfdr_cpgraph_reduced_graph",
     "pfdr_cpgraph_get_reduced", "pfdr_cpgraph_merge", "pfdr_cpgraph_gradient",
-    "pfdr_cpgraph_capacities", "pfdr_cpgraph_activate",
+    "pfdr_cpgraph_capacities", "pfdr_cpgraph_capacities_bounds", "pfdr_cpgraph_activate",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling", "pfdr_session_profile_filter",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -810,6 +810,15 @@ class CPGraph:
         rc = np.empty(self.E, self.dtype)
         self._call("pfdr_cpgraph_capacities", C.c_int(cut), C.c_int(int(positivity)),
                    self._p(tr), self._p(rc), PFDR_MEM_HOST)
+        return tr, rc
+
+    def capacities_bounds(self, cut, lo=-np.inf, hi=np.inf):
+        """bounds driver (src/CP_PFDR_graph_quadratic_d1_bounds.cpp:386-534)
+        -> (tr_cap[V], r_cap[E]) of cut 0 (no bound), 1 or 2"""
+        tr = np.empty(self.V, self.dtype)
+        rc = np.empty(self.E, self.dtype)
+        self._call("pfdr_cpgraph_capacities_bounds", C.c_int(cut), C.c_double(lo),
+                   C.c_double(hi), self._p(tr), self._p(rc), PFDR_MEM_HOST)
         return tr, rc
 
     def activate(self, segment):

@@ -288,6 +288,12 @@ int pfdr_cpgraph_gradient(pfdr_cpgraph *g, int N, const void *A, const void *Y,
  * activity BEFORE this cut's activations; either may be NULL */
 int pfdr_cpgraph_capacities(pfdr_cpgraph *g, int cut, int positivity,
     void *tr_cap, void *r_cap, int mem);
+/* the same for CP_PFDR_graph_quadratic_d1_bounds (graph created without
+ * La_l1): cut 0 when min = -inf and max = inf; cut 1 (+1_U): +inf on the
+ * components at max, else DfS; cut 2 (-1_U): +inf on the components at min,
+ * else -DfS (src/CP_PFDR_graph_quadratic_d1_bounds.cpp:386-534) */
+int pfdr_cpgraph_capacities_bounds(pfdr_cpgraph *g, int cut, double min, double max,
+    void *tr_cap, void *r_cap, int mem);
 /* activate the inactive edges whose ends lie in different segments[V] */
 int pfdr_cpgraph_activate(pfdr_cpgraph *g, const uint8_t *segment, int mem,
     int *activated);

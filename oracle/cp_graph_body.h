@@ -241,6 +241,25 @@ void FN(oracle_cp_gradient)(int N, int V, int E, const REAL *A, const REAL *Y, c
  * and no positivity, :415-430); cut 1: directions +1_U (:442-476); cut 2:
  * directions -1_U (:478-518).  Edge capacities from the activity BEFORE
  * the cut's own activations (:420-429, :464-474, :519-535). */
+/* the bounds driver's cuts (src/CP_PFDR_graph_quadratic_d1_bounds.cpp:386-534):
+ * cut 0 (min = -inf, max = inf) tr = DfS; cut 1 (directions +1_U): +inf on
+ * components at max (when max < inf), else DfS; cut 2 (-1_U): +inf on
+ * components at min (when -inf < min), else -DfS; edges as above */
+void FN(oracle_cp_capacities_bounds)(int cut, int V, int E, const REAL *La_d1, REAL mn, REAL mx,
+                                     const uint8_t *active, const int *Cv, const REAL *rX,
+                                     const REAL *DfS, REAL *tr_cap, REAL *r_cap)
+{
+    int v, e;
+    const REAL inf = ORACLE_HUGE;
+    for (v = 0; v < V; v++) {
+        const REAL x = rX[Cv[v]];
+        if (cut == 1) tr_cap[v] = (mx < inf && x == mx) ? inf : DfS[v];
+        else if (cut == 2) tr_cap[v] = (-inf < mn && x == mn) ? inf : -DfS[v];
+        else tr_cap[v] = DfS[v];
+    }
+    for (e = 0; e < E; e++) r_cap[e] = active[e] ? (REAL)0 : La_d1[e];
+}
+
 void FN(oracle_cp_capacities)(int cut, int V, int E, const REAL *La_d1, const REAL *La_l1,
                               int positivity, const uint8_t *active, const int *Cv,
                               const REAL *rX, const REAL *DfS, REAL *tr_cap, REAL *r_cap)

@@ -306,6 +306,29 @@ class Oracle:
         return tr, rc
 
 
+def _cap_bounds(self, cut, La_d1, lo, hi, active, Cv, rX, DfS):
+    """bounds driver :386-534 -> (tr_cap[V], r_cap[E])"""
+    self._port_only("cp_capacities_bounds")
+    DfS = np.ascontiguousarray(DfS)
+    dt = DfS.dtype
+    ct, sfx = _real(dt)
+    La_d1 = np.ascontiguousarray(La_d1, dt)
+    act = np.ascontiguousarray(active, np.uint8)
+    Cv = np.ascontiguousarray(Cv, np.int32)
+    rX = np.ascontiguousarray(rX, dt)
+    V, E = DfS.size, La_d1.size
+    tr = np.empty(V, dt)
+    rc = np.empty(E, dt)
+    self._fn("cp_capacities_bounds", sfx)(
+        C.c_int(cut), C.c_int(V), C.c_int(E), _ptr(La_d1, ct), ct(lo), ct(hi),
+        _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(rX, ct), _ptr(DfS, ct), _ptr(tr, ct),
+        _ptr(rc, ct))
+    return tr, rc
+
+
+Oracle.cp_capacities_bounds = _cap_bounds
+
+
 class CPStepRef:
     """The REFERENCE's cut-pursuit iteration (oracle/_ref/libcp_step_ref.so,
     built from /root/reference/src by ``make -C oracle ref``; only where the
@@ -466,3 +489,74 @@ class CPStepRef:
         fn(C.c_int(tr_cap.size), C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
            _ptr(tr_cap, ct), _ptr(r_cap, ct), _ptr(seg, C.c_uint8))
         return seg
+
+
+class CPStepRefBounds:
+    """The REFERENCE's bounds cut pursuit, one iteration at a time
+    (oracle/_ref/libcp_step_bounds_ref.so, harness/cp_step_bounds.cpp; only
+    where the reference exists).  N = 0 (identity / diagonal A)."""
+
+    PATH = os.path.join(HERE, "_ref", "libcp_step_bounds_ref.so")
+
+    @staticmethod
+    def available():
+        return os.path.exists(CPStepRefBounds.PATH)
+
+    def __init__(self):
+        if CPStepRefBounds.PATH not in _CACHE:
+            _CACHE[CPStepRefBounds.PATH] = C.CDLL(CPStepRefBounds.PATH)
+        self.lib = _CACHE[CPStepRefBounds.PATH]
+
+    def init(self, Y, A, Eu, Ev, La_d1, lo, hi):
+        Y = np.ascontiguousarray(Y)
+        ct, sfx = _real(Y.dtype)
+        A = None if A is None else np.ascontiguousarray(A, Y.dtype)
+        rX0 = np.zeros(1, Y.dtype)
+        getattr(self.lib, "cp_refb_init_" + sfx)(
+            C.c_int(Y.size), C.c_int(Eu.size), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, Y.dtype), ct), ct(lo), ct(hi), _ptr(rX0, ct))
+        return rX0
+
+    def step(self, Y, A, Eu, Ev, La_d1, lo, hi, CP_difTol, state, rho=1.5, condMin=1e-3,
+             difRcd=0.0, difTol=1e-4, itMax=1000):
+        """-> (new state, last cut's segments, reduced problem or None)"""
+        Y = np.ascontiguousarray(Y)
+        dt = Y.dtype
+        ct, sfx = _real(dt)
+        V, E = Y.size, Eu.size
+        A = None if A is None else np.ascontiguousarray(A, dt)
+        act = np.array(state["active"], np.uint8, copy=True)
+        Cv = np.array(state["Cv"], np.int32, copy=True)
+        Vc = np.array(state["Vc"], np.int32, copy=True)
+        rV = C.c_int(int(state["rVc"].size - 1))
+        rVc = np.zeros(V + 1, np.int32)
+        rVc[:rV.value + 1] = state["rVc"]
+        rX = np.zeros(V, dt)
+        rX[:rV.value] = state["rX"]
+        seg = np.zeros(V, np.uint8)
+        called, rE = C.c_int(0), C.c_int(0)
+        rEu = np.zeros(E + V, np.int32)
+        rEv = np.zeros(E + V, np.int32)
+        rLa = np.zeros(E + V, dt)
+        rY = np.zeros(V, dt)
+        rAA = np.zeros(V, dt)
+        getattr(self.lib, "cp_refb_step_" + sfx)(
+            C.c_int(V), C.c_int(E), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, dt), ct), ct(lo), ct(hi), ct(CP_difTol), ct(rho),
+            ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax), _ptr(act, C.c_uint8),
+            _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int), C.byref(rV), _ptr(rX, ct),
+            _ptr(seg, C.c_uint8), C.byref(called), C.byref(rE), _ptr(rEu, C.c_int),
+            _ptr(rEv, C.c_int), _ptr(rLa, ct), _ptr(rY, ct), _ptr(rAA, ct))
+        n = rV.value
+        new = {"active": act, "Cv": Cv, "Vc": Vc, "rVc": rVc[:n + 1].copy(),
+               "rX": rX[:n].copy()}
+        red = None
+        if called.value:
+            m = rE.value
+            red = {"rEu": rEu[:m].copy(), "rEv": rEv[:m].copy(), "rLa_d1": rLa[:m].copy(),
+                   "rLa_l1": None, "rY": rY[:n].copy(), "rAA": rAA[:n].copy()}
+        return new, seg, red

@@ -82,6 +82,77 @@ def make_cases():
     return cases
 
 
+def make_bounds_cases():
+    """cases of the bounds driver (src/CP_PFDR_graph_quadratic_d1_bounds.cpp):
+    a box both of whose ends bind, one-sided boxes, no bound (one cut), a
+    k-NN multigraph with a diagonal A"""
+    inf = float("inf")
+    cases = {}
+    for dt, nm in ((np.float32, "f32"), (np.float64, "f64")):
+        eps = float(np.finfo(dt).eps)
+        Eu, Ev = grid_graph((24, 20), 4)
+        V = 24 * 20
+        for tag, lo, hi in (("box", 0.0, 1.0), ("lower", 0.0, inf), ("upper", -inf, 0.8),
+                            ("free", -inf, inf)):
+            cases["cp_bounds_%s_%s" % (tag, nm)] = dict(
+                Y=_y(V, 24, 21, dt, noise=0.3), A=None, Eu=Eu, Ev=Ev,
+                La_d1=np.full(Eu.size, 0.05, dt), lo=lo, hi=hi, CP_difTol=1e-3)
+        Ku, Kv = knn_jitter_grid((10, 8, 6), k=6, seed=22)
+        Vk = 10 * 8 * 6
+        cases["cp_bounds_knn_diag_" + nm] = dict(
+            Y=_y(Vk, 10, 23, dt), A=(0.5 + uniform(24, np.arange(Vk))).astype(dt), Eu=Ku,
+            Ev=Kv, La_d1=np.full(Ku.size, 0.02, dt), lo=-0.2, hi=1.1, CP_difTol=1e-4)
+        for c in cases.values():
+            c.setdefault("eps", eps)
+    return cases
+
+
+def cp_graph_iteration_bounds(o, maxflow, case, state, rX_new=None):
+    """cp_graph_iteration for the bounds driver: gradient (no l1 term) ->
+    one cut (no bound) or two (+1_U then -1_U, :386-534) -> components ->
+    reduced graph (no rLa_l1) -> merge"""
+    c = case
+    V = c["Y"].size
+    dt = c["Y"].dtype
+    act0 = np.asarray(state["active"], np.uint8)
+    DfS = o.cp_gradient(0, V, c["A"], c["Y"], None, c["Eu"], c["Ev"], c["La_d1"], None,
+                        act0, state["Cv"], state["Vc"], state["rVc"], state["rX"])
+    out = {"DfS": DfS}
+    lo, hi = c["lo"], c["hi"]
+    if lo == -np.inf and hi == np.inf:
+        tr, rc = o.cp_capacities_bounds(0, c["La_d1"], lo, hi, act0, state["Cv"], state["rX"],
+                                        DfS)
+        seg = maxflow(tr, rc)
+        act, w = o.cp_activate(c["Eu"], c["Ev"], seg, act0)
+        out["caps"] = [(tr, rc)]
+        out["segments"] = [seg]
+    else:
+        tr1, rc1 = o.cp_capacities_bounds(1, c["La_d1"], lo, hi, act0, state["Cv"],
+                                          state["rX"], DfS)
+        seg1 = maxflow(tr1, rc1)
+        tr2, rc2 = o.cp_capacities_bounds(2, c["La_d1"], lo, hi, act0, state["Cv"],
+                                          state["rX"], DfS)
+        act, w1 = o.cp_activate(c["Eu"], c["Ev"], seg1, act0)
+        seg2 = maxflow(tr2, rc2)
+        act, w2 = o.cp_activate(c["Eu"], c["Ev"], seg2, act)
+        w = w1 + w2
+        out["caps"] = [(tr1, rc1), (tr2, rc2)]
+        out["segments"] = [seg1, seg2]
+    out["activated"] = w
+    out["active_pre"] = act
+    if w == 0:
+        return out
+    Cv, Vc, rVc = o.cp_components(V, c["Eu"], c["Ev"], act)
+    out.update(Cv=Cv, Vc=Vc, rVc=rVc)
+    out["reduced"] = o.cp_reduced_graph(V, c["Eu"], c["Ev"], c["La_d1"], None, act, Cv, Vc,
+                                        rVc, cp_eps(dt, c["CP_difTol"]))
+    if rX_new is not None:
+        out["active_post"], out["merged"] = o.cp_merge(
+            c["Eu"], c["Ev"], Cv, np.asarray(rX_new, dt), cp_eps(dt, c["CP_difTol"]),
+            c["CP_difTol"], act)
+    return out
+
+
 def cp_eps(dt, CP_difTol):
     """:236-251: eps = CP_difTol if 0 < CP_difTol < machine eps, else it"""
     m = float(np.finfo(dt).eps)

@@ -22,7 +22,9 @@ Before saving, the script checks the oracle restatement
 (oracle/cp_graph_body.h) against every iteration: its capacities fed to the
 reference maxflow give the reference's last segments, and its activation,
 components, reduced graph and merge give the reference's state and reduced
-problem exactly.  Usage:  python tests/golden/make_cp_golden.py
+problem exactly.  Usage:  python tests/golden/make_cp_golden.py [--bounds]
+(--bounds: the cases of the bounds driver, CP_PFDR_graph_quadratic_d1_bounds,
+ through oracle/_ref/libcp_step_bounds_ref.so; files cp_bounds_*.npz)
 """
 import os
 import sys
@@ -32,15 +34,15 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 sys.path.insert(0, HERE)
-from oracle import CPStepRef, Oracle  # noqa: E402
+from oracle import CPStepRef, CPStepRefBounds, Oracle  # noqa: E402
 import cp_cases as CC  # noqa: E402
 
 
-def check_iteration(o, ref, c, state, new, seg_last, red):
+def check_iteration(o, ref, c, state, new, seg_last, red, iteration=CC.cp_graph_iteration):
     """The oracle chain against one reference iteration; returns derived
     first-cut segments (or None)."""
-    d = CC.cp_graph_iteration(o, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc), c,
-                              state, rX_new=new["rX"])
+    d = iteration(o, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc), c, state,
+                  rX_new=new["rX"])
     assert np.array_equal(d["segments"][-1], seg_last), "last cut segments"
     if d["activated"] == 0:
         assert red is None
@@ -61,7 +63,52 @@ def check_iteration(o, ref, c, state, new, seg_last, red):
     return d["segments"][0] if len(d["segments"]) == 2 else None
 
 
+def main_bounds():
+    """the bounds driver (src/CP_PFDR_graph_quadratic_d1_bounds.cpp), same
+    records; maxflow of the derived first cut through the l1 library's BK
+    (same vendored graph code)"""
+    o = Oracle("port")
+    refb = CPStepRefBounds()
+    mf = CPStepRef()
+    for name, c in CC.make_bounds_cases().items():
+        out = {}
+        for k, v in c.items():
+            if v is not None:
+                out["in_" + k] = np.asarray(v)
+        V, E = c["Y"].size, c["Eu"].size
+        rX0 = refb.init(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["lo"], c["hi"])
+        state = {"active": np.zeros(E, np.uint8), "Cv": np.zeros(V, np.int32),
+                 "Vc": np.arange(V, dtype=np.int32), "rVc": np.array([0, V], np.int32),
+                 "rX": rX0}
+        hist = []
+        for k in range(CC.STEPS):
+            new, seg, red = refb.step(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["lo"],
+                                      c["hi"], c["CP_difTol"], state)
+            seg_first = check_iteration(o, mf, c, state, new, seg, red,
+                                        CC.cp_graph_iteration_bounds)
+            for key, val in state.items():
+                out["k%d_in_%s" % (k, key)] = val
+            for key, val in new.items():
+                out["k%d_out_%s" % (k, key)] = val
+            out["k%d_seg_last" % k] = seg
+            if seg_first is not None:
+                out["k%d_seg_first" % k] = seg_first
+            if red is not None:
+                for key, val in red.items():
+                    if val is not None:
+                        out["k%d_red_%s" % (k, key)] = val
+            hist.append("%d:%d/%s" % (new["rVc"].size - 1, int(new["active"].sum()),
+                                       "-" if red is None else red["rEu"].size))
+            state = new
+        out["meta_steps"] = np.int32(CC.STEPS)
+        out["meta_build"] = np.str_("g++ -O3 -ffp-contract=off, no OpenMP")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+        print("%-26s V=%d E=%d  rV:active/rE per iteration %s" % (name, V, E, " ".join(hist)))
+
+
 def main():
+    if "--bounds" in sys.argv:
+        return main_bounds()
     o = Oracle("port")
     ref = CPStepRef()
     for name, c in CC.make_cases().items():

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import cp_cases as CC
-from test_cp_graph_oracle import NAMES, iteration_state, load_case
+from test_cp_graph_oracle import BNAMES, NAMES, iteration_state, load_case
 
 pytestmark = pytest.mark.gpu
 
@@ -35,14 +35,18 @@ def _eq(a, b, what):
         assert np.array_equal(a, b), (what, np.flatnonzero(a != b)[:5])
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", NAMES + BNAMES)
 def test_gpu_replays_reference_cp(cpgraph_cls, oracle_port, name):
     c, d = load_case(name)
     o = oracle_port
     dt = c["Y"].dtype
     eps = CC.cp_eps(dt, c["CP_difTol"])
     g = cpgraph_cls(c["Y"].size, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"])
-    two_cuts = c["La_l1"] is not None or c["positivity"]
+    bounds = name in BNAMES
+    if bounds:  # the bounds driver (src/CP_PFDR_graph_quadratic_d1_bounds.cpp)
+        two_cuts = not (c["lo"] == -np.inf and c["hi"] == np.inf)
+    else:
+        two_cuts = c["La_l1"] is not None or c["positivity"]
     for k in range(int(d["meta_steps"])):
         st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
         g.set_active(st["active"])
@@ -55,9 +59,14 @@ def test_gpu_replays_reference_cp(cpgraph_cls, oracle_port, name):
         cuts = (1, 2) if two_cuts else (0,)
         caps = {}
         for cut in cuts:
-            tr, rc = g.capacities(cut, c["positivity"])
-            otr, orc = o.cp_capacities(cut, c["La_d1"], c["La_l1"], c["positivity"],
-                                       st["active"], st["Cv"], st["rX"], oD)
+            if bounds:
+                tr, rc = g.capacities_bounds(cut, c["lo"], c["hi"])
+                otr, orc = o.cp_capacities_bounds(cut, c["La_d1"], c["lo"], c["hi"],
+                                                  st["active"], st["Cv"], st["rX"], oD)
+            else:
+                tr, rc = g.capacities(cut, c["positivity"])
+                otr, orc = o.cp_capacities(cut, c["La_d1"], c["La_l1"], c["positivity"],
+                                           st["active"], st["Cv"], st["rX"], oD)
             _eq(tr, otr, "tr_cap cut %d" % cut)
             _eq(rc, orc, "r_cap cut %d" % cut)
             caps[cut] = (tr, rc)

@@ -1,6 +1,8 @@
 """The oracle's CP graph steps (oracle/cp_graph_body.h, SURVEY.md §8(f)
 ranks 2-3) against the reference's own cut-pursuit iterations
-(tests/golden/cp_*.npz, made by tests/golden/make_cp_golden.py).
+(tests/golden/cp_*.npz, made by tests/golden/make_cp_golden.py): the l1
+driver's and (cp_bounds_*) the bounds driver's, whose cuts use the box
+instead of the l1 term (src/CP_PFDR_graph_quadratic_d1_bounds.cpp:386-534).
 
 Per recorded iteration: gradient -> capacities -> (the iteration's
 segments, from the fixture) -> activation -> components -> reduced graph
@@ -22,7 +24,11 @@ from oracle import CPStepRef
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 FILES = sorted(glob.glob(os.path.join(GOLDEN, "cp_*.npz")))
-NAMES = [os.path.basename(f)[:-4] for f in FILES if not f.endswith("cp_cases.npz")]
+_ALL = [os.path.basename(f)[:-4] for f in FILES]
+# the l1 driver's iterations; the bounds driver's (cp_bounds_*); the dense
+# reduced problems are test_cp_reduce.py's (cp_dense_*)
+NAMES = [n for n in _ALL if not n.startswith(("cp_bounds_", "cp_dense_"))]
+BNAMES = [n for n in _ALL if n.startswith("cp_bounds_")]
 
 
 def load_case(name):
@@ -30,8 +36,11 @@ def load_case(name):
     c = {k[3:]: d[k] for k in d.files if k.startswith("in_")}
     for k in ("A", "La_l1"):
         c.setdefault(k, None)
-    c["positivity"] = int(c["positivity"])
+    c["positivity"] = int(c.get("positivity", 0))
     c["CP_difTol"] = float(c["CP_difTol"])
+    for k in ("lo", "hi"):
+        if k in c:
+            c[k] = float(c[k])
     return c, d
 
 
@@ -41,18 +50,20 @@ def iteration_state(d, k, io):
 
 def test_fixtures_present():
     assert len(NAMES) >= 10, NAMES
+    assert len(BNAMES) >= 10, BNAMES
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", NAMES + BNAMES)
 def test_oracle_replays_reference_cp(oracle_port, name):
     c, d = load_case(name)
     o = oracle_port
+    step = CC.cp_graph_iteration_bounds if name in BNAMES else CC.cp_graph_iteration
     for k in range(int(d["meta_steps"])):
         st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
         segs = [d["k%d_seg_first" % k]] if ("k%d_seg_first" % k) in d.files else []
         segs.append(d["k%d_seg_last" % k])
         it = iter(segs)
-        r = CC.cp_graph_iteration(o, lambda tr, rc: next(it), c, st, rX_new=new["rX"])
+        r = step(o, lambda tr, rc: next(it), c, st, rX_new=new["rX"])
         if r["activated"] == 0:
             assert ("k%d_red_rEu" % k) not in d.files
             continue
@@ -73,14 +84,14 @@ def test_oracle_replays_reference_cp(oracle_port, name):
 
 
 @pytest.mark.skipif(not CPStepRef.available(), reason="reference harness not built here")
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", NAMES + BNAMES)
 def test_oracle_capacities_through_reference_maxflow(oracle_port, name):
     c, d = load_case(name)
     ref = CPStepRef()
+    step = CC.cp_graph_iteration_bounds if name in BNAMES else CC.cp_graph_iteration
     for k in range(int(d["meta_steps"])):
         st = iteration_state(d, k, "in")
-        r = CC.cp_graph_iteration(oracle_port, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc),
-                                  c, st)
+        r = step(oracle_port, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc), c, st)
         assert np.array_equal(r["segments"][-1], d["k%d_seg_last" % k])
         if ("k%d_seg_first" % k) in d.files:
             assert np.array_equal(r["segments"][0], d["k%d_seg_first" % k])
