@@ -181,6 +181,16 @@ class QuadSession final : public SessionBase {
     // (k_tiny_iterate; PFDR_TINY = max edges, 0 = off)
     bool tiny_ = false;
     void tiny_chunk(int n);
+    // mid-size single-GPU graphs: a chunk of iterations in one persistent
+    // launch of coopG_ resident workgroups with grid barriers
+    // (k_coop_iterate; PFDR_COOP = most vertex blocks, 0 = off, the
+    // default: slower than graph-replayed launches, see kCoopBlocks;
+    // PFDR_COOP_G = most workgroups)
+    bool coop_ok_ = false, coop_ = false;
+    int coopG_ = 0;
+    DevBuf<unsigned> bar_;
+    void plan_coop();
+    void coop_chunk(int n);
     // pipelined iteration (single GPU, u-sorted edges, label bandwidth below
     // the chunk size): vertex chunks k = 0..C-1 run as edge sweep of chunk
     // k+1, then vertex sweep of chunk k, so each chunk's DR contributions are
@@ -200,6 +210,12 @@ class QuadSession final : public SessionBase {
     // the longest chain (max(N, V) direct, V for A^tA) is <= kExactChain
     bool exact_ = false;
     static constexpr long kExactChain = 8192;
+    // default PFDR_COOP: off.  Measured on C1 (r2m/r2n): 37 us per iteration
+    // with 256 workgroups against 14.6 for the graph-replayed launches -- a
+    // grid barrier must write back and invalidate the L2 of every XCD (their
+    // L2s are not coherent), once per workgroup, which costs more than the
+    // kernel boundary it replaces
+    static constexpr long kCoopBlocks = 0;
     template <int EPI> void col_product(ColArgs<real> ca);
     DevBuf<real> spart_;
     void plan_symv();
@@ -278,6 +294,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         const long maxE = t ? atol(t) : 8192;
         tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= (t ? 32 : 8);
         tiny = tiny_ ? 1 : 0;
+        coop_ok_ = !tiny_;
     }
     // graph, partition plan, incidence CSR
     setup_graph(p);
@@ -419,7 +436,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
         if (!(o && o[0] == '0')) plan_overlap();
     } else if (!tiny_) {
-        plan_pipeline();
+        if (coop_ok_) plan_coop();
+        if (!coop_) plan_pipeline();
         const char *g = getenv("PFDR_GRAPH");
         graphs_ok_ = !(g && g[0] == '0') && itMax_ >= 2 * chunk_;
     }
@@ -844,6 +862,46 @@ void QuadSession<real>::tiny_chunk(int n) {
     PFDR_HIP(hipGetLastError());
 }
 
+// persistent launch for mid-size graphs: every workgroup must be resident
+// (grid barriers), so the grid is capped by the occupancy of the kernel and
+// by the CUs; the runtime's cooperative launch checks it again
+template <typename real>
+void QuadSession<real>::plan_coop() {
+    const char *e = getenv("PFDR_COOP");
+    const long maxb = e ? atol(e) : kCoopBlocks;
+    if (maxb <= 0 || nbv_ > maxb) return;
+    int cus = 0, occ = 0;
+    PFDR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    PFDR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void *>(k_coop_iterate<real, 8>), kBlock, 0));
+    const char *g = getenv("PFDR_COOP_G");
+    constexpr long EB = (long)kBlock * Vec<real>::kPer16B;  // edges per workgroup chunk
+    long G = std::max<long>(nbv_, (E_ + EB - 1) / EB);
+    G = std::min<long>(G, (long)cus * std::max(occ, 1));
+    G = std::min<long>(G, g && atol(g) > 0 ? atol(g) : cus);
+    if (G < 1) return;
+    coopG_ = (int)G;
+    bar_.alloc(2);
+    PFDR_HIP(hipMemsetAsync(bar_.p, 0, 2 * sizeof(unsigned), stream));
+    coop_ = true;
+    coop = coopG_;
+}
+
+template <typename real>
+void QuadSession<real>::coop_chunk(int n) {
+    const bool gated = track_ || rec_obj_;
+    CoopArgs<real> t{};
+    t.E = E_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Z2 = Z2_.p; t.A1 = A1_.p; t.La_d1 = La_d1_.p;
+    t.cw = cw_; t.rho = rho_; t.gi = gi_.p; t.wz = wz_.p;
+    t.va = vargs(0, nbv_, nullptr);
+    t.red = red_.p; t.ctrl = gated ? ctrl_.p : nullptr; t.Dif = rec_dif_ ? Dif_.p : nullptr;
+    t.track = track_ ? 1 : 0; t.iters = n; t.bar = bar_.p;
+    void *args[] = {&t};
+    ProfScope ps(prof, "coop_iterate", stream);
+    PFDR_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_coop_iterate<real, 8>),
+                                        dim3(coopG_), dim3(kBlock), args, 0, stream));
+}
+
 template <typename real>
 VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     VArgs<real> a{};
@@ -1075,6 +1133,7 @@ int QuadSession<real>::run(int iters) {
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
         if (tiny_) tiny_chunk(n);
+        else if (coop_) coop_chunk(n);
         else run_bodies(n);
         if (gated) {
             pull_ctrl();

@@ -978,19 +978,15 @@ struct ERange {
 // wz[E + e] (v end), so the u-side run of a vertex is contiguous.  Streams
 // per edge: Eu, Ev, Z (r/w), La_d1, the two contributions (+ A1 after a
 // reconditioning); gathers (X, P) and (Ga, invAux) of both ends.
+// one lane's EPT edges [e0, e0 + EPT) of the edges [.., eend): the lane
+// body of k_edge_sweep, shared with the persistent k_coop_iterate (whose
+// xp is rewritten between its edge passes: no __restrict__ on it)
 template <typename real>
-__global__ __launch_bounds__(256) void k_edge_sweep(
-    long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
-    const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
-    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
-    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg) {
-    if (ctrl && ctrl->halt) return;
+__device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int *__restrict__ Eu,
+                                          const int *__restrict__ Ev, const R2<real> *xp,
+                                          real *Z2, const real *A1, real cw, const R2<real> *gi,
+                                          const real *__restrict__ La_d1, real *wz, real rho) {
     constexpr int EPT = Vec<real>::kPer16B;
-    int blk = xcd_block(blockIdx.x, nb, xcd);
-    if (blk >= nb) return;
-    long ebeg, eend;
-    rg.pick(blk, ebeg, eend);
-    const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
     if (e0 >= eend) return;
     if (e0 + EPT <= eend) {
         const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
@@ -1029,6 +1025,22 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
             wz[E + e] = ov;
         }
     }
+}
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_edge_sweep(
+    long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
+    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
+    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg) {
+    if (ctrl && ctrl->halt) return;
+    constexpr int EPT = Vec<real>::kPer16B;
+    int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    long ebeg, eend;
+    rg.pick(blk, ebeg, eend);
+    const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
+    edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, wz, rho);
 }
 
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
@@ -1444,6 +1456,90 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
             }
         }
         __syncthreads();
+    }
+}
+
+// ------------------------------------- mid-size graphs, one launch --
+// A chunk of whole iterations of a single-GPU graph in ONE launch of G
+// workgroups that are all resident (cooperative launch, G <= the CUs):
+// per iteration the edge pass (chunks of kBlock * EPT edges dealt over the
+// workgroups, each lane running k_edge_sweep's lane body), a grid barrier,
+// the vertex pass (vertex blocks dealt over the workgroups, vertex_block as
+// in k_vertex_sweep, per-block evolution partials), a grid barrier; then
+// EVERY workgroup sums the partials with k_reduce_decide's tree and takes
+// the same decision on its own copy of the control block (workgroup 0
+// alone writes it and Dif), so the loop needs no third barrier and every
+// workgroup leaves it at the same iteration.  Same device code, same
+// operation order as the multi-launch path: iterates, iteration counts and
+// Dif are identical bit for bit; what goes is 2-3 launches per iteration
+// (the latency floor of C1-sized graphs and CP's reduced problems).
+template <typename real>
+struct CoopArgs {
+    long E;
+    const int *Eu, *Ev;
+    real *Z2;
+    const real *A1, *La_d1;
+    real cw, rho;
+    const R2<real> *gi;
+    real *wz;
+    VArgs<real> va;     // nb = every vertex block, bbeg 0, no XCD order
+    real *red;          // (num, den) of the last evolution
+    Ctrl<real> *ctrl;   // null: no tracking, run exactly `iters`
+    real *Dif;
+    int track, iters;
+    unsigned *bar;      // grid barrier state (2 words, zero at first use)
+};
+
+template <typename real, int GB>
+__global__ __launch_bounds__(256) void k_coop_iterate(CoopArgs<real> t) {
+    constexpr int EPT = Vec<real>::kPer16B;
+    __shared__ real lds[GatherCap<real>::v];
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int scan[kBlock / kWave];
+    __shared__ Ctrl<real> c;
+    const unsigned G = gridDim.x;
+    const int tid = threadIdx.x;
+    const VArgs<real> &a = t.va;
+    if (t.ctrl) {
+        if (tid == 0) c = *t.ctrl;
+        __syncthreads();
+        if (c.halt) return;  // every workgroup reads the same control block
+    }
+    const long nbe = (t.E + (long)kBlock * EPT - 1) / ((long)kBlock * EPT);
+    for (int it = 0; it < t.iters; it++) {
+        for (long b = blockIdx.x; b < nbe; b += G)
+            edge_lane<real>((b * kBlock + tid) * EPT, t.E, t.E, t.Eu, t.Ev, a.xp, t.Z2, t.A1,
+                            t.cw, t.gi, t.La_d1, t.wz, t.rho);
+        grid_sync(t.bar, G);
+        for (int blk = blockIdx.x; blk < a.nb; blk += G) {
+            vertex_block<real, GB>(a, blk, lds, red, scan);
+            __syncthreads();  // lds / scan reused by the next block
+        }
+        if (!t.ctrl) {
+            if (it + 1 < t.iters) grid_sync(t.bar, G);
+            continue;
+        }
+        grid_sync(t.bar, G);
+        // k_reduce_decide, in every workgroup
+        real sa = real(0), sb = real(0);
+        if (t.track) {
+            for (int i = tid; i < a.nb; i += kBlock) {
+                sa += a.part[2 * i];
+                sb += a.part[2 * i + 1];
+            }
+            sa = block_sum(sa, red[0]);
+            sb = block_sum(sb, red[1]);
+        }
+        if (tid == 0) {
+            decide_step(&c, sa, sb, blockIdx.x == 0 ? t.Dif : nullptr, t.track);
+            if (blockIdx.x == 0) {
+                if (t.track) { t.red[0] = sa; t.red[1] = sb; }
+                t.ctrl->it = c.it; t.ctrl->dif = c.dif;
+                t.ctrl->stop = c.stop; t.ctrl->recond = c.recond; t.ctrl->halt = c.halt;
+            }
+        }
+        __syncthreads();
+        if (c.halt) break;  // the same decision in every workgroup
     }
 }
 
