@@ -273,3 +273,194 @@ void FN(oracle_cp_capacities)(int cut, int V, int E, const REAL *La_d1, const RE
     }
     for (e = 0; e < E; e++) r_cap[e] = active[e] ? (REAL)0 : La_d1[e];
 }
+
+/* ------------------------------------------------------------------------
+ * The simplex driver's steps (reference src/CP_PFDR_graph_loss_d1_simplex.cpp),
+ * K labels, P[v*K + k] layouts, single-threaded.  al: 0 linear loss, 1
+ * quadratic, 0 < al < 1 smoothed KL (al_K = al/K, al_1 = 1 - al,
+ * al_K_al_1 = al_K/al_1, :208-212); eps is the driver's finite-difference
+ * precision (:214-231), passed by the caller.
+ * ------------------------------------------------------------------------ */
+
+/* :733-766 (and initialize() :96-108 for the single first component):
+ * per component the sums of Q over its vertices in Vc order; linear loss:
+ * rQ = the sums, rP = the corner of the largest (first on ties); otherwise
+ * rQ = rP = sums / size, rLa_f = size */
+void FN(oracle_cp_simplex_reduced)(int K, REAL al, const REAL *Q, const int *Vc, const int *rVc,
+                                   int rV, REAL *rP, REAL *rQ, REAL *rLa_f)
+{
+    int rv, s, k, i;
+    for (rv = 0; rv < rV; rv++) {
+        REAL *rPv = rP + (size_t)rv * K, *rQv = rQ + (size_t)rv * K;
+        for (k = 0; k < K; k++) rPv[k] = (REAL)0;
+        for (s = rVc[rv]; s < rVc[rv + 1]; s++) {
+            const REAL *Qv = Q + (size_t)Vc[s] * K;
+            for (k = 0; k < K; k++) rPv[k] += Qv[k];
+        }
+        if (al == (REAL)0) {
+            REAL a = rPv[i = 0];
+            for (k = 1; k < K; k++)
+                if (rPv[k] > a) a = rPv[i = k];
+            for (k = 0; k < K; k++) {
+                rQv[k] = rPv[k];
+                rPv[k] = (k == i) ? (REAL)1 : (REAL)0;
+            }
+        } else {
+            i = rVc[rv + 1] - rVc[rv];
+            for (k = 0; k < K; k++) {
+                rQv[k] = rPv[k] / i;
+                rPv[k] = rQv[k];
+            }
+            if (rLa_f) rLa_f[rv] = (REAL)i;
+        }
+    }
+}
+
+/* :327-376 gradient DfS[V*K] of the loss at the piecewise-constant rP plus
+ * the d1 term over the active arcs in the maxflow graph's order; then
+ * :525-536 rDi[rV], the most confident label of each component (first on
+ * ties) */
+void FN(oracle_cp_simplex_gradient)(int K, int V, int E, REAL al, const REAL *Q, const int *Eu,
+                                    const int *Ev, const REAL *La_d1, const uint8_t *active,
+                                    const int *Cv, int rV, const REAL *rP, REAL eps, REAL *DfS,
+                                    int *rDi)
+{
+    int *first = (int *)malloc(sizeof(int) * (V > 0 ? V : 1));
+    int *next = (int *)malloc(sizeof(int) * (2 * (size_t)E + 1));
+    int v, k, a, rv, i;
+    REAL al_K = (REAL)0, al_1 = (REAL)0, al_K_al_1 = (REAL)0;
+    if ((REAL)0 < al && al < (REAL)1) {
+        al_K = al / K;
+        al_1 = (REAL)1 - al;
+        al_K_al_1 = al_K / al_1;
+    }
+    cpg_lists(V, E, Eu, Ev, first, next);
+    for (v = 0; v < V; v++) {
+        REAL *D = DfS + (size_t)v * K;
+        const REAL *Qv = Q + (size_t)v * K, *rPv = rP + (size_t)Cv[v] * K;
+        for (k = 0; k < K; k++) {
+            if (al == (REAL)0) D[k] = -Qv[k];
+            else if (al == (REAL)1) D[k] = rPv[k] - Qv[k];
+            else D[k] = -(al_K + al_1 * Qv[k]) / (al_K_al_1 + rPv[k]);
+        }
+    }
+    for (v = 0; v < V; v++) {
+        REAL *D = DfS + (size_t)v * K;
+        const REAL *rPv = rP + (size_t)Cv[v] * K;
+        for (a = first[v]; a != -1; a = next[a]) {
+            if (active[a >> 1]) {
+                const REAL *rPu = rP + (size_t)Cv[cpg_head(a, Eu, Ev)] * K;
+                const REAL w = La_d1[a >> 1];
+                for (k = 0; k < K; k++) {
+                    const REAL d = rPv[k] - rPu[k];
+                    if (d > eps) D[k] += w;
+                    else if (d < -eps) D[k] -= w;
+                }
+            }
+        }
+    }
+    for (rv = 0; rv < rV; rv++) {
+        const REAL *rPv = rP + (size_t)rv * K;
+        REAL m = rPv[0];
+        i = 0;
+        for (k = 1; k < K; k++)
+            if (rPv[k] > m) m = rPv[i = k];
+        rDi[rv] = i;
+    }
+    free(first);
+    free(next);
+}
+
+/* :542-595 capacities of alpha-expansion n (1 <= n < K): source/sink per
+ * vertex from its component's label i = rDi and its current alternative
+ * Djv, then the d1 terms of the inactive edges in edge order (tr_cap[u] +=
+ * c - a, tr_cap[v] -= c); r_cap[e] is the capacity of arc 2e (u -> v), arc
+ * 2e + 1 has none */
+void FN(oracle_cp_simplex_capacities)(int K, int V, int E, int n, const int *Eu, const int *Ev,
+                                      const REAL *La_d1, const uint8_t *active, const int *Vc,
+                                      const int *rVc, int rV, const int *rDi, const int *Djv,
+                                      const REAL *DfS, REAL *tr_cap, REAL *r_cap)
+{
+    int rv, s, v, i, j, k, e;
+    for (rv = 0; rv < rV; rv++) {
+        i = rDi[rv];
+        j = n > i ? n : (n - 1);
+        for (s = rVc[rv]; s < rVc[rv + 1]; s++) {
+            const REAL *D;
+            v = Vc[s];
+            D = DfS + (size_t)v * K;
+            k = Djv[v];
+            if (k == 0) tr_cap[v] = D[j] - D[i];
+            else if (k == n) tr_cap[v] = (REAL)0;
+            else if (k > i) tr_cap[v] = D[j] - D[k];
+            else tr_cap[v] = D[j] - D[k - 1];
+        }
+    }
+    for (e = 0; e < E; e++) {
+        if (active[e]) {
+            r_cap[e] = (REAL)0;
+        } else {
+            const int u = Eu[e];
+            v = Ev[e];
+            j = Djv[u];
+            k = Djv[v];
+            {
+                const REAL a = (j == k) ? (REAL)0 : (REAL)2 * La_d1[e];
+                const REAL b = (REAL)2 * La_d1[e], c = (REAL)2 * La_d1[e];
+                tr_cap[u] += c - a;
+                tr_cap[v] -= c;
+                r_cap[e] = b + c - a;
+            }
+        }
+    }
+}
+
+/* :782-803 deactivate the active edges whose components' label vectors
+ * differ by at most eps in every label; returns how many */
+int FN(oracle_cp_simplex_merge)(int K, int E, const int *Eu, const int *Ev, const int *Cv,
+                                const REAL *rP, REAL eps, uint8_t *active)
+{
+    int e, k, n = 0;
+    for (e = 0; e < E; e++) {
+        if (active[e]) {
+            const REAL *rPu = rP + (size_t)Cv[Eu[e]] * K, *rPv = rP + (size_t)Cv[Ev[e]] * K;
+            REAL a = (REAL)0;
+            for (k = 0; k < K; k++) {
+                REAL d = rPu[k] - rPv[k];
+                if (d < (REAL)0) d = -d;
+                if (d > a) a = d;
+            }
+            if (a <= eps) {
+                active[e] = 0;
+                n++;
+            }
+        }
+    }
+    return n;
+}
+
+#ifndef ORACLE_CPG_SIMPLEX_INT_DEFINED
+#define ORACLE_CPG_SIMPLEX_INT_DEFINED
+/* :600-604 the sink side of expansion n takes alternative n */
+void oracle_cp_simplex_expand(int V, int n, const uint8_t *segment, int *Djv)
+{
+    int v;
+    for (v = 0; v < V; v++)
+        if (segment[v]) Djv[v] = n;
+}
+
+/* :608-618 activate the inactive edges whose ends took different
+ * alternatives; returns how many */
+int oracle_cp_simplex_activate(int E, const int *Eu, const int *Ev, const int *Djv,
+                               uint8_t *active)
+{
+    int e, s = 0;
+    for (e = 0; e < E; e++) {
+        if (!active[e] && Djv[Eu[e]] != Djv[Ev[e]]) {
+            active[e] = 1;
+            s++;
+        }
+    }
+    return s;
+}
+#endif

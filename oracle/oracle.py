@@ -560,3 +560,198 @@ class CPStepRefBounds:
             red = {"rEu": rEu[:m].copy(), "rEv": rEv[:m].copy(), "rLa_d1": rLa[:m].copy(),
                    "rLa_l1": None, "rY": rY[:n].copy(), "rAA": rAA[:n].copy()}
         return new, seg, red
+
+
+# ---- the simplex driver's steps (oracle/cp_graph_body.h, port only),
+# src/CP_PFDR_graph_loss_d1_simplex.cpp; P layouts are vertex-major [v*K + k]
+def _sx_reduced(self, K, al, Q, Vc, rVc):
+    """:733-766 -> (rP[rV*K], rQ[rV*K], rLa_f[rV] or None when al == 0)"""
+    self._port_only("cp_simplex_reduced")
+    Q = np.ascontiguousarray(Q)
+    ct, sfx = _real(Q.dtype)
+    Vc = np.ascontiguousarray(Vc, np.int32)
+    rVc = np.ascontiguousarray(rVc, np.int32)
+    rV = rVc.size - 1
+    rP = np.empty(rV * K, Q.dtype)
+    rQ = np.empty(rV * K, Q.dtype)
+    rLa_f = np.empty(rV, Q.dtype) if al != 0 else None
+    self._fn("cp_simplex_reduced", sfx)(
+        C.c_int(K), ct(al), _ptr(Q, ct), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int), C.c_int(rV),
+        _ptr(rP, ct), _ptr(rQ, ct), _ptr(rLa_f, ct))
+    return rP, rQ, rLa_f
+
+
+def _sx_gradient(self, K, al, Q, Eu, Ev, La_d1, active, Cv, rP, eps):
+    """:327-376 and :525-536 -> (DfS[V*K], rDi[rV])"""
+    self._port_only("cp_simplex_gradient")
+    Q = np.ascontiguousarray(Q)
+    dt = Q.dtype
+    ct, sfx = _real(dt)
+    V = Q.size // K
+    rP = np.ascontiguousarray(rP, dt)
+    rV = rP.size // K
+    Eu = np.ascontiguousarray(Eu, np.int32)
+    Ev = np.ascontiguousarray(Ev, np.int32)
+    DfS = np.empty(V * K, dt)
+    rDi = np.empty(rV, np.int32)
+    self._fn("cp_simplex_gradient", sfx)(
+        C.c_int(K), C.c_int(V), C.c_int(Eu.size), ct(al), _ptr(Q, ct), _ptr(Eu, C.c_int),
+        _ptr(Ev, C.c_int), _ptr(np.ascontiguousarray(La_d1, dt), ct),
+        _ptr(np.ascontiguousarray(active, np.uint8), C.c_uint8),
+        _ptr(np.ascontiguousarray(Cv, np.int32), C.c_int), C.c_int(rV), _ptr(rP, ct), ct(eps),
+        _ptr(DfS, ct), _ptr(rDi, C.c_int))
+    return DfS, rDi
+
+
+def _sx_capacities(self, K, n, Eu, Ev, La_d1, active, Vc, rVc, rDi, Djv, DfS):
+    """:542-595 -> (tr_cap[V], r_cap[E]: arc 2e; arc 2e + 1 has none)"""
+    self._port_only("cp_simplex_capacities")
+    DfS = np.ascontiguousarray(DfS)
+    dt = DfS.dtype
+    ct, sfx = _real(dt)
+    V = DfS.size // K
+    Eu = np.ascontiguousarray(Eu, np.int32)
+    Ev = np.ascontiguousarray(Ev, np.int32)
+    rVc = np.ascontiguousarray(rVc, np.int32)
+    tr = np.empty(V, dt)
+    rc = np.empty(Eu.size, dt)
+    self._fn("cp_simplex_capacities", sfx)(
+        C.c_int(K), C.c_int(V), C.c_int(Eu.size), C.c_int(n), _ptr(Eu, C.c_int),
+        _ptr(Ev, C.c_int), _ptr(np.ascontiguousarray(La_d1, dt), ct),
+        _ptr(np.ascontiguousarray(active, np.uint8), C.c_uint8),
+        _ptr(np.ascontiguousarray(Vc, np.int32), C.c_int), _ptr(rVc, C.c_int),
+        C.c_int(rVc.size - 1), _ptr(np.ascontiguousarray(rDi, np.int32), C.c_int),
+        _ptr(np.ascontiguousarray(Djv, np.int32), C.c_int), _ptr(DfS, ct), _ptr(tr, ct),
+        _ptr(rc, ct))
+    return tr, rc
+
+
+def _sx_expand(self, n, segment, Djv):
+    """:600-604 -> new Djv"""
+    self._port_only("cp_simplex_expand")
+    D = np.array(Djv, np.int32, copy=True)
+    seg = np.ascontiguousarray(segment, np.uint8)
+    self.lib.oracle_cp_simplex_expand(C.c_int(D.size), C.c_int(n), _ptr(seg, C.c_uint8),
+                                      _ptr(D, C.c_int))
+    return D
+
+
+def _sx_activate(self, Eu, Ev, Djv, active):
+    """:608-618 -> (new active, count)"""
+    self._port_only("cp_simplex_activate")
+    Eu = np.ascontiguousarray(Eu, np.int32)
+    Ev = np.ascontiguousarray(Ev, np.int32)
+    act = np.array(active, np.uint8, copy=True)
+    fn = self.lib.oracle_cp_simplex_activate
+    fn.restype = C.c_int
+    n = fn(C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(np.ascontiguousarray(Djv, np.int32), C.c_int), _ptr(act, C.c_uint8))
+    return act, int(n)
+
+
+def _sx_merge(self, K, Eu, Ev, Cv, rP, eps, active):
+    """:782-803 -> (new active, deactivated count)"""
+    self._port_only("cp_simplex_merge")
+    rP = np.ascontiguousarray(rP)
+    ct, sfx = _real(rP.dtype)
+    Eu = np.ascontiguousarray(Eu, np.int32)
+    Ev = np.ascontiguousarray(Ev, np.int32)
+    act = np.array(active, np.uint8, copy=True)
+    fn = self._fn("cp_simplex_merge", sfx)
+    fn.restype = C.c_int
+    n = fn(C.c_int(K), C.c_int(Eu.size), _ptr(Eu, C.c_int), _ptr(Ev, C.c_int),
+           _ptr(np.ascontiguousarray(Cv, np.int32), C.c_int), _ptr(rP, ct), ct(eps),
+           _ptr(act, C.c_uint8))
+    return act, int(n)
+
+
+Oracle.cp_simplex_reduced = _sx_reduced
+Oracle.cp_simplex_gradient = _sx_gradient
+Oracle.cp_simplex_capacities = _sx_capacities
+Oracle.cp_simplex_expand = _sx_expand
+Oracle.cp_simplex_activate = _sx_activate
+Oracle.cp_simplex_merge = _sx_merge
+
+
+class CPStepRefSimplex:
+    """The REFERENCE's simplex cut pursuit, one iteration at a time
+    (oracle/_ref/libcp_step_simplex_ref.so, harness/cp_step_simplex.cpp;
+    only where the reference exists), and its BK maxflow with the simplex
+    driver's arc capacities."""
+
+    PATH = os.path.join(HERE, "_ref", "libcp_step_simplex_ref.so")
+
+    @staticmethod
+    def available():
+        return os.path.exists(CPStepRefSimplex.PATH)
+
+    def __init__(self):
+        if CPStepRefSimplex.PATH not in _CACHE:
+            _CACHE[CPStepRefSimplex.PATH] = C.CDLL(CPStepRefSimplex.PATH)
+        self.lib = _CACHE[CPStepRefSimplex.PATH]
+
+    def init(self, K, al, Q, Eu, Ev, La_d1):
+        Q = np.ascontiguousarray(Q)
+        ct, sfx = _real(Q.dtype)
+        rP0 = np.zeros(K, Q.dtype)
+        getattr(self.lib, "cp_refs_init_" + sfx)(
+            C.c_int(K), C.c_int(Q.size // K), C.c_int(Eu.size), ct(al), _ptr(Q, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, Q.dtype), ct), _ptr(rP0, ct))
+        return rP0
+
+    def step(self, K, al, Q, Eu, Ev, La_d1, CP_difTol, state, rho=1.5, condMin=1e-3,
+             difRcd=0.0, difTol=1e-3, itMax=1000):
+        """-> (new state, last expansion's segments, reduced problem or None)"""
+        Q = np.ascontiguousarray(Q)
+        dt = Q.dtype
+        ct, sfx = _real(dt)
+        V, E = Q.size // K, Eu.size
+        act = np.array(state["active"], np.uint8, copy=True)
+        Cv = np.array(state["Cv"], np.int32, copy=True)
+        Vc = np.array(state["Vc"], np.int32, copy=True)
+        rV = C.c_int(int(state["rVc"].size - 1))
+        rVc = np.zeros(V + 1, np.int32)
+        rVc[:rV.value + 1] = state["rVc"]
+        rP = np.zeros(V * K, dt)
+        rP[:rV.value * K] = state["rP"]
+        seg = np.zeros(V, np.uint8)
+        called, rE = C.c_int(0), C.c_int(0)
+        rEu = np.zeros(E + V, np.int32)
+        rEv = np.zeros(E + V, np.int32)
+        rLa = np.zeros(E + V, dt)
+        rQ = np.zeros(V * K, dt)
+        rLa_f = np.zeros(V, dt)
+        rP0 = np.zeros(V * K, dt)
+        getattr(self.lib, "cp_refs_step_" + sfx)(
+            C.c_int(K), C.c_int(V), C.c_int(E), ct(al), _ptr(Q, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, dt), ct), ct(CP_difTol), ct(rho), ct(condMin),
+            ct(difRcd), ct(difTol), C.c_int(itMax), _ptr(act, C.c_uint8), _ptr(Cv, C.c_int),
+            _ptr(Vc, C.c_int), _ptr(rVc, C.c_int), C.byref(rV), _ptr(rP, ct),
+            _ptr(seg, C.c_uint8), C.byref(called), C.byref(rE), _ptr(rEu, C.c_int),
+            _ptr(rEv, C.c_int), _ptr(rLa, ct), _ptr(rQ, ct), _ptr(rLa_f, ct), _ptr(rP0, ct))
+        n = rV.value
+        new = {"active": act, "Cv": Cv, "Vc": Vc, "rVc": rVc[:n + 1].copy(),
+               "rP": rP[:n * K].copy()}
+        red = None
+        if called.value:
+            m = rE.value
+            red = {"rEu": rEu[:m].copy(), "rEv": rEv[:m].copy(), "rLa_d1": rLa[:m].copy(),
+                   "rQ": rQ[:n * K].copy(), "rLa_f": rLa_f[:n].copy() if al != 0 else None,
+                   "rP0": rP0[:n * K].copy()}
+        return new, seg, red
+
+    def maxflow(self, Eu, Ev, tr_cap, r_cap):
+        """Segments (0 source, 1 sink) with arc 2e from r_cap[e], arc 2e+1 none."""
+        tr_cap = np.ascontiguousarray(tr_cap)
+        ct, sfx = _real(tr_cap.dtype)
+        seg = np.zeros(tr_cap.size, np.uint8)
+        getattr(self.lib, "cp_refs_maxflow_" + sfx)(
+            C.c_int(tr_cap.size), C.c_int(Eu.size),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int), _ptr(tr_cap, ct),
+            _ptr(np.ascontiguousarray(r_cap, tr_cap.dtype), ct), _ptr(seg, C.c_uint8))
+        return seg

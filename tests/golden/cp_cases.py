@@ -202,3 +202,106 @@ def cp_graph_iteration(o, maxflow, case, state, rX_new=None):
             c["Eu"], c["Ev"], Cv, np.asarray(rX_new, dt), cp_eps(dt, c["CP_difTol"]),
             c["CP_difTol"], act)
     return out
+
+
+# ------------------------------------------------ the simplex driver --
+def _q(V, K, nx, seed, dt, noise=0.35):
+    """label likelihoods in the simplex: a spatial label map (stripes and
+    blocks) blurred with uniform noise, normalised per vertex"""
+    v = np.arange(V)
+    lab = ((v % nx) * K // nx + (v // nx) // 5) % K
+    Q = np.full((V, K), 0.0)
+    Q[v, lab] = 1.0
+    Q = (1 - noise) * Q + noise * uniform(seed, np.arange(V * K)).reshape(V, K)
+    Q /= Q.sum(axis=1, keepdims=True)
+    return Q.reshape(-1).astype(dt)
+
+
+def make_simplex_cases():
+    """cases of the simplex driver (src/CP_PFDR_graph_loss_d1_simplex.cpp):
+    linear (al = 0), quadratic (al = 1) and smoothed-KL losses, 2-D grids, a
+    k-NN multigraph, a disconnected graph with zero-weight edges"""
+    cases = {}
+    for dt, nm in ((np.float32, "f32"), (np.float64, "f64")):
+        Eu, Ev = grid_graph((24, 20), 4)
+        V = 24 * 20
+        cases["cp_simplex_linear_" + nm] = dict(
+            K=3, al=0.0, Q=_q(V, 3, 24, 31, dt), Eu=Eu, Ev=Ev,
+            La_d1=np.full(Eu.size, 0.08, dt), CP_difTol=1e-3)
+        cases["cp_simplex_quad_" + nm] = dict(
+            K=4, al=1.0, Q=_q(V, 4, 24, 32, dt), Eu=Eu, Ev=Ev,
+            La_d1=(0.02 + 0.03 * uniform(33, np.arange(Eu.size))).astype(dt), CP_difTol=1e-3)
+        cases["cp_simplex_kl_" + nm] = dict(
+            K=3, al=0.1, Q=_q(V, 3, 24, 34, dt), Eu=Eu, Ev=Ev,
+            La_d1=np.full(Eu.size, 0.05, dt), CP_difTol=1e-3)
+        Ku, Kv = knn_jitter_grid((10, 8, 6), k=6, seed=35)
+        Vk = 10 * 8 * 6
+        cases["cp_simplex_knn_kl_" + nm] = dict(
+            K=5, al=0.05, Q=_q(Vk, 5, 10, 36, dt), Eu=Ku, Ev=Kv,
+            La_d1=np.full(Ku.size, 0.03, dt), CP_difTol=1e-4)
+        Au, Av = grid_graph((12, 10), 8)
+        Bu, Bv = grid_graph((9, 7), 4)
+        Vd = 1 + 120 + 63
+        Du = np.concatenate([Au + 1, Bu + 121]).astype(np.int32)
+        Dv = np.concatenate([Av + 1, Bv + 121]).astype(np.int32)
+        La = np.full(Du.size, 0.06, dt)
+        La[::13] = 0
+        cases["cp_simplex_disconnected_" + nm] = dict(
+            K=3, al=1.0, Q=_q(Vd, 3, 12, 37, dt), Eu=Du, Ev=Dv, La_d1=La, CP_difTol=1e-3)
+    return cases
+
+
+def simplex_eps(dt, V, CP_difTol, PFDR_difTol):
+    """:214-231, as compiled: ``(ZERO < c < a)`` is ``((0 < c) < a)``, so eps
+    is the machine epsilon a unless c = min(b, c) <= 0 (b, c: CP / PFDR
+    tolerances, divided by V when >= 1)"""
+    a = float(np.finfo(dt).eps)
+    b = dt(CP_difTol) / dt(V) if CP_difTol >= 1 else dt(CP_difTol)
+    c = dt(PFDR_difTol) / dt(V) if PFDR_difTol >= 1 else dt(PFDR_difTol)
+    c = b if b < c else c
+    return float(c) if not (c > 0) else a
+
+
+SIMPLEX_PFDR_DIFTOL = 1e-3  # the step harness's PFDR difTol (oracle.CPStepRefSimplex.step)
+
+
+def cp_graph_iteration_simplex(o, maxflow, case, state, rP_new=None):
+    """One iteration of the simplex driver's graph steps with the oracle
+    around ``maxflow(tr_cap, r_cap) -> segments``: gradient and most
+    confident labels (:327-376, :525-536) -> K - 1 alpha-expansions
+    (capacities :542-595, maxflow, :600-604) -> activation (:608-618) ->
+    components -> reduced graph (:684-729) -> reduced observations
+    (:733-766) -> (given the PFDR values rP_new) merge (:782-803)."""
+    c = case
+    K, al = int(c["K"]), float(c["al"])
+    Q = c["Q"]
+    dt = Q.dtype
+    V = Q.size // K
+    eps = simplex_eps(dt.type, V, c["CP_difTol"], SIMPLEX_PFDR_DIFTOL)
+    act0 = np.asarray(state["active"], np.uint8)
+    DfS, rDi = o.cp_simplex_gradient(K, al, Q, c["Eu"], c["Ev"], c["La_d1"], act0, state["Cv"],
+                                     state["rP"], eps)
+    out = {"DfS": DfS, "rDi": rDi, "caps": [], "segments": []}
+    Djv = np.zeros(V, np.int32)
+    for n in range(1, K):
+        tr, rc = o.cp_simplex_capacities(K, n, c["Eu"], c["Ev"], c["La_d1"], act0, state["Vc"],
+                                         state["rVc"], rDi, Djv, DfS)
+        seg = maxflow(tr, rc)
+        Djv = o.cp_simplex_expand(n, seg, Djv)
+        out["caps"].append((tr, rc))
+        out["segments"].append(seg)
+    out["Djv"] = Djv
+    act, w = o.cp_simplex_activate(c["Eu"], c["Ev"], Djv, act0)
+    out["activated"] = w
+    out["active_pre"] = act
+    if w == 0:
+        return out
+    Cv, Vc, rVc = o.cp_components(V, c["Eu"], c["Ev"], act)
+    out.update(Cv=Cv, Vc=Vc, rVc=rVc)
+    out["reduced"] = o.cp_reduced_graph(V, c["Eu"], c["Ev"], c["La_d1"], None, act, Cv, Vc, rVc,
+                                        eps)
+    out["observations"] = o.cp_simplex_reduced(K, al, Q, Vc, rVc)
+    if rP_new is not None:
+        out["active_post"], out["merged"] = o.cp_simplex_merge(K, c["Eu"], c["Ev"], Cv,
+                                                               np.asarray(rP_new, dt), eps, act)
+    return out

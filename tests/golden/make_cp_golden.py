@@ -24,7 +24,9 @@ reference maxflow give the reference's last segments, and its activation,
 components, reduced graph and merge give the reference's state and reduced
 problem exactly.  Usage:  python tests/golden/make_cp_golden.py [--bounds]
 (--bounds: the cases of the bounds driver, CP_PFDR_graph_quadratic_d1_bounds,
- through oracle/_ref/libcp_step_bounds_ref.so; files cp_bounds_*.npz)
+ through oracle/_ref/libcp_step_bounds_ref.so; files cp_bounds_*.npz;
+ --simplex: the simplex driver, CP_PFDR_graph_loss_d1_simplex, through
+ oracle/_ref/libcp_step_simplex_ref.so; files cp_simplex_*.npz)
 """
 import os
 import sys
@@ -34,7 +36,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 sys.path.insert(0, HERE)
-from oracle import CPStepRef, CPStepRefBounds, Oracle  # noqa: E402
+from oracle import CPStepRef, CPStepRefBounds, CPStepRefSimplex, Oracle  # noqa: E402
 import cp_cases as CC  # noqa: E402
 
 
@@ -106,9 +108,84 @@ def main_bounds():
         print("%-26s V=%d E=%d  rV:active/rE per iteration %s" % (name, V, E, " ".join(hist)))
 
 
+def check_iteration_simplex(o, ref, c, state, new, seg_last, red):
+    """the oracle chain of the simplex driver against one reference
+    iteration; returns the derived segments of every expansion but the last"""
+    d = CC.cp_graph_iteration_simplex(o, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc),
+                                      c, state, rP_new=new["rP"])
+    assert np.array_equal(d["segments"][-1], seg_last), "last expansion segments"
+    if d["activated"] == 0:
+        assert red is None
+        for k in ("active", "Cv", "Vc", "rVc", "rP"):
+            assert np.array_equal(state[k], new[k]), k
+        return d["segments"][:-1]
+    assert red is not None
+    for k in ("Cv", "Vc", "rVc"):
+        assert np.array_equal(d[k], new[k]), k
+    rEu, rEv, rLa, _ = d["reduced"]
+    assert np.array_equal(rEu, red["rEu"]), "rEu"
+    assert np.array_equal(rEv, red["rEv"]), "rEv"
+    assert np.array_equal(rLa, red["rLa_d1"]), "rLa_d1"
+    rP0, rQ, rLa_f = d["observations"]
+    assert np.array_equal(rP0, red["rP0"]), "rP0"
+    assert np.array_equal(rQ, red["rQ"]), "rQ"
+    if rLa_f is not None:
+        assert np.array_equal(rLa_f, red["rLa_f"]), "rLa_f"
+    assert np.array_equal(d["active_post"], new["active"]), "active after merge"
+    return d["segments"][:-1]
+
+
+def main_simplex():
+    """the simplex driver (src/CP_PFDR_graph_loss_d1_simplex.cpp); per
+    iteration also ``k{k}_seg_exp{n}`` for the expansions before the last
+    (derived through the reference's BK maxflow like seg_first above)"""
+    o = Oracle("port")
+    ref = CPStepRefSimplex()
+    for name, c in CC.make_simplex_cases().items():
+        out = {}
+        for k, v in c.items():
+            if v is not None:
+                out["in_" + k] = np.asarray(v)
+        K, al = c["K"], c["al"]
+        V, E = c["Q"].size // K, c["Eu"].size
+        rP0 = ref.init(K, al, c["Q"], c["Eu"], c["Ev"], c["La_d1"])
+        state = {"active": np.zeros(E, np.uint8), "Cv": np.zeros(V, np.int32),
+                 "Vc": np.arange(V, dtype=np.int32), "rVc": np.array([0, V], np.int32),
+                 "rP": rP0}
+        # the initial values are the reduced observations of one component
+        oP, _, _ = o.cp_simplex_reduced(K, al, c["Q"], state["Vc"], state["rVc"])
+        assert np.array_equal(oP, rP0), "initial rP"
+        hist = []
+        for k in range(CC.STEPS):
+            new, seg, red = ref.step(K, al, c["Q"], c["Eu"], c["Ev"], c["La_d1"],
+                                     c["CP_difTol"], state, difTol=CC.SIMPLEX_PFDR_DIFTOL)
+            segs = check_iteration_simplex(o, ref, c, state, new, seg, red)
+            for key, val in state.items():
+                out["k%d_in_%s" % (k, key)] = val
+            for key, val in new.items():
+                out["k%d_out_%s" % (k, key)] = val
+            out["k%d_seg_last" % k] = seg
+            for n, sg in enumerate(segs, 1):
+                out["k%d_seg_exp%d" % (k, n)] = sg
+            if red is not None:
+                for key, val in red.items():
+                    if val is not None:
+                        out["k%d_red_%s" % (k, key)] = val
+            hist.append("%d:%d/%s" % (new["rVc"].size - 1, int(new["active"].sum()),
+                                       "-" if red is None else red["rEu"].size))
+            state = new
+        out["meta_steps"] = np.int32(CC.STEPS)
+        out["meta_build"] = np.str_("g++ -O3 -ffp-contract=off, no OpenMP")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+        print("%-28s V=%d E=%d K=%d rV:active/rE per iteration %s"
+              % (name, V, E, K, " ".join(hist)))
+
+
 def main():
     if "--bounds" in sys.argv:
         return main_bounds()
+    if "--simplex" in sys.argv:
+        return main_simplex()
     o = Oracle("port")
     ref = CPStepRef()
     for name, c in CC.make_cases().items():
