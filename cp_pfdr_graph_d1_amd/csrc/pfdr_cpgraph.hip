@@ -631,6 +631,185 @@ __global__ void k_cp_activate(long E, const int *__restrict__ Eu, const int *__r
     block_count(c, count);
 }
 
+
+// ------------------------------------------------- the simplex driver --
+// src/CP_PFDR_graph_loss_d1_simplex.cpp: K labels, Q[v*K + k] and the
+// component label vectors rP[rv*K + k] (the reference's layouts).
+
+// Q (V x K, vertex-major) -> Qt (K x V): each label's column contiguous,
+// for the ordered component sums of the reduced observations
+template <typename real>
+__global__ void k_sx_transpose(int V, int K, const real *__restrict__ Q, real *__restrict__ Qt) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)V * K) return;
+    const long v = i / K, k = i - v * K;
+    Qt[k * V + v] = Q[i];
+}
+
+// :739-766 from the ordered sums S[k*rV + rv]: linear loss: rQ = sums, rP =
+// the corner of the first largest sum; else rQ = rP = sums / size, rLa_f =
+// size
+template <typename real>
+__global__ void k_sx_observations(int rV, int K, int linear, const real *__restrict__ S,
+                                  const int *__restrict__ rVc, real *__restrict__ rP,
+                                  real *__restrict__ rQ, real *__restrict__ rLa_f) {
+    const int rv = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rv >= rV) return;
+    real *P = rP + (size_t)rv * K, *Qo = rQ + (size_t)rv * K;
+    if (linear) {
+        int i = 0;
+        real a = S[rv];
+        for (int k = 1; k < K; k++) {
+            const real x = S[(size_t)k * rV + rv];
+            if (x > a) { a = x; i = k; }
+        }
+        for (int k = 0; k < K; k++) {
+            Qo[k] = S[(size_t)k * rV + rv];
+            P[k] = (k == i) ? real(1) : real(0);
+        }
+    } else {
+        const int n = rVc[rv + 1] - rVc[rv];
+        for (int k = 0; k < K; k++) {
+            const real q = S[(size_t)k * rV + rv] / (real)n;
+            Qo[k] = q;
+            P[k] = q;
+        }
+        if (rLa_f) rLa_f[rv] = (real)n;
+    }
+}
+
+// :327-376, one lane per (v, k): the loss gradient at the component's label
+// vector, then the d1 term over v's active arcs, newest first (the maxflow
+// graph's list order); the adds of one (v, k) are independent of the
+// other labels
+template <typename real>
+__global__ void k_sx_gradient(int V, int K, int loss, real alK, real al1, real alKal1,
+                              const real *__restrict__ Q, const int *__restrict__ ptr,
+                              const unsigned *__restrict__ slot, const int *__restrict__ Eu,
+                              const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+                              const real *__restrict__ La, const int *__restrict__ Cv,
+                              const real *__restrict__ rP, real eps, real *__restrict__ DfS) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)V * K) return;
+    const int v = (int)(i / K), k = (int)(i - (long)v * K);
+    const real q = Q[i], p = rP[(size_t)Cv[v] * K + k];
+    real g;
+    if (loss == 0) g = -q;
+    else if (loss == 1) g = p - q;
+    else g = -(alK + al1 * q) / (alKal1 + p);
+    const int b = ptr[v];
+    for (int j = ptr[v + 1] - 1; j >= b; j--) {
+        const unsigned a = slot[j];
+        const int e = (int)(a >> 1);
+        if (!active[e]) continue;
+        const real d = p - rP[(size_t)Cv[arc_head(a, Eu, Ev)] * K + k];
+        if (d > eps) g += La[e];
+        else if (d < -eps) g -= La[e];
+    }
+    DfS[i] = g;
+}
+
+// :525-536 the most confident label of each component (first on ties)
+template <typename real>
+__global__ void k_sx_best(int rV, int K, const real *__restrict__ rP, int *__restrict__ rDi) {
+    const int rv = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rv >= rV) return;
+    const real *P = rP + (size_t)rv * K;
+    int i = 0;
+    real a = P[0];
+    for (int k = 1; k < K; k++)
+        if (P[k] > a) { a = P[k]; i = k; }
+    rDi[rv] = i;
+}
+
+// :542-595 alpha-expansion n: per vertex the source/sink capacity from its
+// component's label and its current alternative, then the d1 terms of its
+// inactive edges in edge order (incidence slots ascending: the reference's
+// sequential edge loop adds c - a at the u end and -c at the v end)
+template <typename real>
+__global__ void k_sx_trcap(int V, int K, int n, const int *__restrict__ ptr,
+                           const unsigned *__restrict__ slot, const int *__restrict__ Eu,
+                           const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+                           const real *__restrict__ La, const int *__restrict__ Cv,
+                           const int *__restrict__ rDi, const int *__restrict__ Djv,
+                           const real *__restrict__ DfS, real *__restrict__ tr) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int i = rDi[Cv[v]], j = n > i ? n : n - 1, k = Djv[v];
+    const real *D = DfS + (size_t)v * K;
+    real t;
+    if (k == 0) t = D[j] - D[i];
+    else if (k == n) t = real(0);
+    else if (k > i) t = D[j] - D[k];
+    else t = D[j] - D[k - 1];
+    for (int q = ptr[v], qe = ptr[v + 1]; q < qe; q++) {
+        const unsigned a = slot[q];
+        const int e = (int)(a >> 1);
+        if (active[e]) continue;
+        const real w = real(2) * La[e];
+        const real aa = (Djv[Eu[e]] == Djv[Ev[e]]) ? real(0) : w;
+        if (a & 1u) t -= w;
+        else t += w - aa;
+    }
+    tr[v] = t;
+}
+
+// arc 2e's capacity b + c - a (arc 2e + 1 has none, :592-593)
+template <typename real>
+__global__ void k_sx_rcap(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                          const uint8_t *__restrict__ active, const real *__restrict__ La,
+                          const int *__restrict__ Djv, real *__restrict__ rc) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    if (active[e]) { rc[e] = real(0); return; }
+    const real w = real(2) * La[e];
+    const real a = (Djv[Eu[e]] == Djv[Ev[e]]) ? real(0) : w;
+    rc[e] = w + w - a;
+}
+
+// :600-604 the sink side takes alternative n
+__global__ void k_sx_expand(int V, int n, const uint8_t *__restrict__ seg, int *__restrict__ Djv) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V && seg[v]) Djv[v] = n;
+}
+
+// :608-618 activate the inactive edges whose ends took different alternatives
+__global__ void k_sx_activate(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                              const int *__restrict__ Djv, uint8_t *__restrict__ active,
+                              int *__restrict__ count) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (e < E && !active[e] && Djv[Eu[e]] != Djv[Ev[e]]) {
+        active[e] = 1;
+        c = 1;
+    }
+    block_count(c, count);
+}
+
+// :782-803 deactivate the active edges whose components' label vectors
+// differ by at most eps in every label
+template <typename real>
+__global__ void k_sx_merge(long E, int K, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                           const int *__restrict__ Cv, const real *__restrict__ rP, real eps,
+                           uint8_t *__restrict__ active, int *__restrict__ count) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (e < E && active[e]) {
+        const real *Pu = rP + (size_t)Cv[Eu[e]] * K, *Pv = rP + (size_t)Cv[Ev[e]] * K;
+        real a = real(0);
+        for (int k = 0; k < K; k++) {
+            real d = Pu[k] - Pv[k];
+            if (d < real(0)) d = -d;
+            if (d > a) a = d;
+        }
+        if (a <= eps) {
+            active[e] = 0;
+            c = 1;
+        }
+    }
+    block_count(c, count);
+}
+
 // ================================================================ state --
 struct CpGraphBase {
     virtual ~CpGraphBase() = default;
@@ -665,6 +844,17 @@ struct CpGraphBase {
     virtual void get_reduced(int *rEu_o, int *rEv_o, void *rLa_o, void *rL1_o, int mem) = 0;
     virtual void get_dfs(void *out, int mem) = 0;
     int activate(const uint8_t *seg, int mem);
+    // the simplex driver (K labels)
+    int K = 0;
+    DevBuf<int> rDi, Djv;
+    virtual void sx_setup(int K_, double al, const void *Q, int mem) = 0;
+    virtual void sx_observations(void *rP, void *rQ, void *rLa_f, int mem) = 0;
+    virtual void sx_set_values(const void *rP, int mem) = 0;
+    virtual void sx_gradient(double eps, void *DfS, int *rDi_o, int mem) = 0;
+    virtual void sx_capacities(int n, void *tr, void *rc, int mem) = 0;
+    virtual int sx_merge(double eps) = 0;
+    void sx_expand(int n, const uint8_t *seg, int mem);
+    int sx_activate();
 };
 
 static hipMemcpyKind kind_in(int mem) {
@@ -734,6 +924,31 @@ int CpGraphBase::activate(const uint8_t *seg, int mem) {
     if (!count.p) count.alloc(1);
     PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
     if (E > 0) k_cp_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, ds, active.p, count.p);
+    PFDR_HIP(hipGetLastError());
+    return d2h_scalar(count.p, s);
+}
+
+void CpGraphBase::sx_expand(int n, const uint8_t *seg, int mem) {
+    if (!K) throw std::runtime_error("simplex: call pfdr_cpgraph_simplex_setup first");
+    if (!Djv.p) throw std::runtime_error("simplex: compute the gradient first");
+    if (n < 1 || n >= K) throw std::runtime_error("simplex: expansion n out of [1, K)");
+    DevBuf<uint8_t> bs;
+    const uint8_t *ds = seg;
+    if (mem != PFDR_MEM_DEVICE) {
+        bs.alloc(V);
+        PFDR_HIP(hipMemcpyAsync(bs.p, seg, V, hipMemcpyHostToDevice, s));
+        ds = bs.p;
+    }
+    k_sx_expand<<<grid_for(V), kBlock, 0, s>>>(V, n, ds, Djv.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipStreamSynchronize(s));
+}
+
+int CpGraphBase::sx_activate() {
+    if (!Djv.p) throw std::runtime_error("simplex: compute the gradient first");
+    if (!count.p) count.alloc(1);
+    PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
+    if (E > 0) k_sx_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Djv.p, active.p, count.p);
     PFDR_HIP(hipGetLastError());
     return d2h_scalar(count.p, s);
 }
@@ -924,6 +1139,126 @@ struct CpGraph : CpGraphBase {
                 PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
         }
         PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    // ---- the simplex driver
+    real sal = real(0);
+    DevBuf<real> Q, Qt, rP, DfSK, S;
+
+    void sx_setup(int K_, double al, const void *q, int mem) override {
+        if (K_ < 2 || !q) throw std::runtime_error("simplex_setup: K >= 2 and Q required");
+        if (!(al >= 0.0 && al <= 1.0)) throw std::runtime_error("simplex_setup: al in [0, 1]");
+        K = K_;
+        sal = (real)al;
+        const size_t n = (size_t)V * K;
+        Q.alloc(n);
+        Qt.alloc(n);
+        PFDR_HIP(hipMemcpyAsync(Q.p, q, sizeof(real) * n, kind_in(mem), s));
+        k_sx_transpose<real><<<grid_for((long)n), kBlock, 0, s>>>(V, K, Q.p, Qt.p);
+        PFDR_HIP(hipGetLastError());
+        rP.release();
+        DfSK.release();
+        Djv.release();
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void need_k(const char *fn) const {
+        if (!K) throw std::runtime_error(std::string(fn) + ": call pfdr_cpgraph_simplex_setup first");
+    }
+
+    // :733-766 (and initialize() :96-108): per label the ordered sums of Qt
+    // over each component's vertices in Vc order, then the observations;
+    // rP becomes the component values
+    void sx_observations(void *rPo, void *rQo, void *rLafo, int mem) override {
+        need_k("simplex_observations");
+        S.alloc((size_t)rV * K);
+        for (int k = 0; k < K; k++)
+            segsum<real>(rV, rVc.p, Vc.p, Qt.p + (size_t)k * V, S.p + (size_t)k * rV, longs, nlong, s);
+        rP.alloc((size_t)rV * K);
+        DevBuf<real> bQ((size_t)rV * K), bL(rV);
+        const int linear = sal == real(0);
+        k_sx_observations<real><<<grid_for(rV), kBlock, 0, s>>>(rV, K, linear, S.p, rVc.p, rP.p,
+                                                                bQ.p, linear ? nullptr : bL.p);
+        PFDR_HIP(hipGetLastError());
+        const auto ko = kind_out(mem);
+        if (rPo) PFDR_HIP(hipMemcpyAsync(rPo, rP.p, sizeof(real) * rV * K, ko, s));
+        if (rQo) PFDR_HIP(hipMemcpyAsync(rQo, bQ.p, sizeof(real) * rV * K, ko, s));
+        if (rLafo && !linear) PFDR_HIP(hipMemcpyAsync(rLafo, bL.p, sizeof(real) * rV, ko, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void sx_set_values(const void *x, int mem) override {
+        need_k("simplex_set_values");
+        rP.alloc((size_t)rV * K);
+        PFDR_HIP(hipMemcpyAsync(rP.p, x, sizeof(real) * rV * K, kind_in(mem), s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    // :327-376 DfS[V*K]; :523-536 rDi, Djv = 0
+    void sx_gradient(double eps, void *out, int *rDio, int mem) override {
+        need_k("simplex_gradient");
+        if (!rP.p) throw std::runtime_error("simplex_gradient: set the component values first");
+        const size_t n = (size_t)V * K;
+        DfSK.alloc(n);
+        real alK = real(0), al1 = real(0), alKal1 = real(0);
+        if (real(0) < sal && sal < real(1)) {  // :208-212
+            alK = sal / (real)K;
+            al1 = real(1) - sal;
+            alKal1 = alK / al1;
+        }
+        const int loss = sal == real(0) ? 0 : sal == real(1) ? 1 : 2;
+        k_sx_gradient<real><<<grid_for((long)n), kBlock, 0, s>>>(
+            V, K, loss, alK, al1, alKal1, Q.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p, La.p,
+            Cv.p, rP.p, (real)eps, DfSK.p);
+        rDi.alloc(rV);
+        k_sx_best<real><<<grid_for(rV), kBlock, 0, s>>>(rV, K, rP.p, rDi.p);
+        Djv.alloc(V);
+        PFDR_HIP(hipMemsetAsync(Djv.p, 0, sizeof(int) * V, s));
+        PFDR_HIP(hipGetLastError());
+        const auto ko = kind_out(mem);
+        if (out) PFDR_HIP(hipMemcpyAsync(out, DfSK.p, sizeof(real) * n, ko, s));
+        if (rDio) PFDR_HIP(hipMemcpyAsync(rDio, rDi.p, sizeof(int) * rV, ko, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    void sx_capacities(int n, void *tr, void *rc, int mem) override {
+        need_k("simplex_capacities");
+        if (!DfSK.p || !Djv.p) throw std::runtime_error("simplex_capacities: compute the gradient first");
+        if (n < 1 || n >= K) throw std::runtime_error("simplex_capacities: n out of [1, K)");
+        DevBuf<real> btr, brc;
+        real *dtr = (real *)tr, *drc = (real *)rc;
+        if (mem != PFDR_MEM_DEVICE) {
+            btr.alloc(V);
+            brc.alloc(E > 0 ? E : 1);
+            dtr = btr.p;
+            drc = brc.p;
+        }
+        if (tr)
+            k_sx_trcap<real><<<grid_for(V), kBlock, 0, s>>>(V, K, n, inc.ptr.p, inc.idx.p, Eu.p,
+                                                            Ev.p, active.p, La.p, Cv.p, rDi.p,
+                                                            Djv.p, DfSK.p, dtr);
+        if (rc && E > 0)
+            k_sx_rcap<real><<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, active.p, La.p, Djv.p,
+                                                           drc);
+        PFDR_HIP(hipGetLastError());
+        if (mem != PFDR_MEM_DEVICE) {
+            if (tr) PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost, s));
+            if (rc && E > 0)
+                PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
+        }
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    int sx_merge(double eps) override {
+        need_k("simplex_merge");
+        if (!rP.p) throw std::runtime_error("simplex_merge: set the component values first");
+        if (!count.p) count.alloc(1);
+        PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
+        if (E > 0)
+            k_sx_merge<real><<<grid_for(E), kBlock, 0, s>>>(E, K, Eu.p, Ev.p, Cv.p, rP.p,
+                                                            (real)eps, active.p, count.p);
+        PFDR_HIP(hipGetLastError());
+        return d2h_scalar(count.p, s);
     }
 };
 
@@ -1138,5 +1473,67 @@ extern "C" int pfdr_cpgraph_activate(pfdr_cpgraph *h, const uint8_t *segment, in
     CPG_TRY("pfdr_cpgraph_activate", {
         const int n = h->g->activate(segment, mem);
         if (activated) *activated = n;
+    })
+}
+
+// ------------------------------------------------- the simplex driver --
+extern "C" int pfdr_cpgraph_simplex_setup(pfdr_cpgraph *h, int K, double al, const void *Q,
+                                          int mem) {
+    if (!h || !Q || K < 2) return report_error("pfdr_cpgraph_simplex_setup", "invalid arguments");
+    CPG_TRY("pfdr_cpgraph_simplex_setup", h->g->sx_setup(K, al, Q, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_observations(pfdr_cpgraph *h, void *rP, void *rQ,
+                                                 void *rLa_f, int mem) {
+    if (!h) return report_error("pfdr_cpgraph_simplex_observations", "null graph");
+    CPG_TRY("pfdr_cpgraph_simplex_observations", h->g->sx_observations(rP, rQ, rLa_f, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_set_values(pfdr_cpgraph *h, const void *rP, int mem) {
+    if (!h || !rP) return report_error("pfdr_cpgraph_simplex_set_values", "null argument");
+    CPG_TRY("pfdr_cpgraph_simplex_set_values", h->g->sx_set_values(rP, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_gradient(pfdr_cpgraph *h, double eps, void *DfS, int *rDi,
+                                             int mem) {
+    if (!h) return report_error("pfdr_cpgraph_simplex_gradient", "null graph");
+    CPG_TRY("pfdr_cpgraph_simplex_gradient", h->g->sx_gradient(eps, DfS, rDi, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_capacities(pfdr_cpgraph *h, int n, void *tr_cap, void *r_cap,
+                                               int mem) {
+    if (!h) return report_error("pfdr_cpgraph_simplex_capacities", "null graph");
+    CPG_TRY("pfdr_cpgraph_simplex_capacities", h->g->sx_capacities(n, tr_cap, r_cap, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_expand(pfdr_cpgraph *h, int n, const uint8_t *segment,
+                                           int mem) {
+    if (!h || !segment) return report_error("pfdr_cpgraph_simplex_expand", "null argument");
+    CPG_TRY("pfdr_cpgraph_simplex_expand", h->g->sx_expand(n, segment, mem))
+}
+
+extern "C" int pfdr_cpgraph_simplex_activate(pfdr_cpgraph *h, int *activated) {
+    if (!h) return report_error("pfdr_cpgraph_simplex_activate", "null graph");
+    CPG_TRY("pfdr_cpgraph_simplex_activate", {
+        const int n = h->g->sx_activate();
+        if (activated) *activated = n;
+    })
+}
+
+extern "C" int pfdr_cpgraph_simplex_merge(pfdr_cpgraph *h, double eps, int *deactivated) {
+    if (!h) return report_error("pfdr_cpgraph_simplex_merge", "null graph");
+    CPG_TRY("pfdr_cpgraph_simplex_merge", {
+        const int n = h->g->sx_merge(eps);
+        if (deactivated) *deactivated = n;
+    })
+}
+
+extern "C" int pfdr_cpgraph_simplex_labels(pfdr_cpgraph *h, int *Djv, int mem) {
+    if (!h || !Djv) return report_error("pfdr_cpgraph_simplex_labels", "null argument");
+    CPG_TRY("pfdr_cpgraph_simplex_labels", {
+        auto *g = h->g;
+        if (!g->Djv.p) throw std::runtime_error("simplex_labels: compute the gradient first");
+        PFDR_HIP(hipMemcpyAsync(Djv, g->Djv.p, sizeof(int) * g->V, pfdr::kind_out(mem), g->s));
+        PFDR_HIP(hipStreamSynchronize(g->s));
     })
 }

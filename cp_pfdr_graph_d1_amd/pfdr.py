@@ -44,6 +44,10 @@ EXPORTED = (
     "pfdr_cpgraph_set_values", "pfdr_cpgraph_components", "pfdr_cpgraph_reduced_graph",
     "pfdr_cpgraph_get_reduced", "pfdr_cpgraph_merge", "pfdr_cpgraph_gradient",
     "pfdr_cpgraph_capacities", "pfdr_cpgraph_capacities_bounds", "pfdr_cpgraph_activate",
+    "pfdr_cpgraph_simplex_setup", "pfdr_cpgraph_simplex_observations",
+    "pfdr_cpgraph_simplex_set_values", "pfdr_cpgraph_simplex_gradient",
+    "pfdr_cpgraph_simplex_capacities", "pfdr_cpgraph_simplex_expand",
+    "pfdr_cpgraph_simplex_activate", "pfdr_cpgraph_simplex_merge", "pfdr_cpgraph_simplex_labels",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling", "pfdr_session_profile_filter",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -826,6 +830,71 @@ class CPGraph:
         seg = np.ascontiguousarray(segment, np.uint8)
         n = C.c_int()
         self._call("pfdr_cpgraph_activate", self._p(seg), PFDR_MEM_HOST, C.byref(n))
+        return n.value
+
+    # ---- the simplex driver (src/CP_PFDR_graph_loss_d1_simplex.cpp); P
+    # layouts vertex-major [v*K + k]
+    def simplex_setup(self, K, al, Q):
+        """K labels, loss al (0 linear, 1 quadratic, else smoothed KL), Q[V*K]"""
+        self.K = int(K)
+        self.al = float(al)
+        self._Q = np.ascontiguousarray(Q, self.dtype).reshape(-1)
+        if self._Q.size != self.V * self.K:
+            raise ValueError("Q must hold V*K values")
+        self._call("pfdr_cpgraph_simplex_setup", C.c_int(self.K), C.c_double(self.al),
+                   self._p(self._Q), PFDR_MEM_HOST)
+
+    def simplex_observations(self):
+        """:733-766 -> (rP[rV*K], rQ[rV*K], rLa_f[rV] or None when al == 0);
+        rP becomes the component values"""
+        n = self.rV * self.K
+        rP = np.empty(n, self.dtype)
+        rQ = np.empty(n, self.dtype)
+        rLa_f = np.empty(self.rV, self.dtype) if self.al != 0 else None
+        self._call("pfdr_cpgraph_simplex_observations", self._p(rP), self._p(rQ),
+                   self._p(rLa_f), PFDR_MEM_HOST)
+        return rP, rQ, rLa_f
+
+    def simplex_set_values(self, rP):
+        x = np.ascontiguousarray(rP, self.dtype).reshape(-1)
+        if x.size != self.rV * self.K:
+            raise ValueError("rP must hold rV*K values")
+        self._call("pfdr_cpgraph_simplex_set_values", self._p(x), PFDR_MEM_HOST)
+
+    def simplex_gradient(self, eps):
+        """:327-376, :525-536 -> (DfS[V*K], rDi[rV])"""
+        DfS = np.empty(self.V * self.K, self.dtype)
+        rDi = np.empty(self.rV, np.int32)
+        self._call("pfdr_cpgraph_simplex_gradient", C.c_double(eps), self._p(DfS),
+                   rDi.ctypes.data_as(C.POINTER(C.c_int)), PFDR_MEM_HOST)
+        return DfS, rDi
+
+    def simplex_capacities(self, n):
+        """:542-595 -> (tr_cap[V], r_cap[E] of arc 2e; arc 2e + 1 has none)"""
+        tr = np.empty(self.V, self.dtype)
+        rc = np.empty(self.E, self.dtype)
+        self._call("pfdr_cpgraph_simplex_capacities", C.c_int(n), self._p(tr), self._p(rc),
+                   PFDR_MEM_HOST)
+        return tr, rc
+
+    def simplex_expand(self, n, segment):
+        seg = np.ascontiguousarray(segment, np.uint8)
+        self._call("pfdr_cpgraph_simplex_expand", C.c_int(n), self._p(seg), PFDR_MEM_HOST)
+
+    def simplex_labels(self):
+        D = np.empty(self.V, np.int32)
+        self._call("pfdr_cpgraph_simplex_labels", D.ctypes.data_as(C.POINTER(C.c_int)),
+                   PFDR_MEM_HOST)
+        return D
+
+    def simplex_activate(self):
+        n = C.c_int()
+        self._call("pfdr_cpgraph_simplex_activate", C.byref(n))
+        return n.value
+
+    def simplex_merge(self, eps):
+        n = C.c_int()
+        self._call("pfdr_cpgraph_simplex_merge", C.c_double(eps), C.byref(n))
         return n.value
 
     def close(self):

@@ -299,6 +299,43 @@ int pfdr_cpgraph_capacities_bounds(pfdr_cpgraph *g, int cut, double min, double 
 int pfdr_cpgraph_activate(pfdr_cpgraph *g, const uint8_t *segment, int mem,
     int *activated);
 
+/* The simplex driver, CP_PFDR_graph_loss_d1_simplex (graph created
+ * without La_l1): K >= 2 labels, Q[V*K] and the component label vectors
+ * rP[rV*K] vertex-major like the reference (P[v*K + k]); al = 0 linear,
+ * 1 quadratic, (0, 1) smoothed-KL loss.  One CP iteration: gradient ->
+ * for n = 1 .. K-1 { capacities(n) -> caller's maxflow -> expand(n,
+ * segments) } -> activate -> pfdr_cpgraph_components -> reduced_graph ->
+ * observations (the reduced problem's rQ, rLa_f and warm start rP) ->
+ * PFDR_graph_loss_d1_simplex -> set_values -> merge.  eps: the driver's
+ * finite-difference precision (src/CP_PFDR_graph_loss_d1_simplex.cpp:214-231).
+ * Replaces :327-376 (gradient), :525-536 (most confident labels),
+ * :542-604 (alpha-expansion capacities and labels), :608-618 (activation),
+ * :733-766 (reduced observations) and :782-803 (merge). */
+int pfdr_cpgraph_simplex_setup(pfdr_cpgraph *g, int K, double al, const void *Q, int mem);
+/* per component the sums of Q in Vc order; linear: rQ = sums, rP = corner
+ * of the first largest; else rQ = rP = sums / size, rLa_f[rV] = size.  The
+ * component values become rP.  Any output may be NULL; also gives the
+ * initial values of the one-component state (:96-108) */
+int pfdr_cpgraph_simplex_observations(pfdr_cpgraph *g, void *rP, void *rQ, void *rLa_f,
+    int mem);
+/* rP[rV*K]: the label vectors of the current components (PFDR's output) */
+int pfdr_cpgraph_simplex_set_values(pfdr_cpgraph *g, const void *rP, int mem);
+/* DfS[V*K] and rDi[rV] (most confident label per component), kept on the
+ * device (copied out when not NULL); resets every vertex's alternative */
+int pfdr_cpgraph_simplex_gradient(pfdr_cpgraph *g, double eps, void *DfS, int *rDi, int mem);
+/* alpha-expansion n in [1, K): tr_cap[V] and r_cap[E], the capacity of arc
+ * 2e (Eu -> Ev); arc 2e + 1 has none (:563-595) */
+int pfdr_cpgraph_simplex_capacities(pfdr_cpgraph *g, int n, void *tr_cap, void *r_cap,
+    int mem);
+/* the SINK side of expansion n's maxflow takes alternative n (:600-604) */
+int pfdr_cpgraph_simplex_expand(pfdr_cpgraph *g, int n, const uint8_t *segment, int mem);
+int pfdr_cpgraph_simplex_activate(pfdr_cpgraph *g, int *activated);
+/* deactivate the active edges whose components' label vectors differ by
+ * at most eps in every label */
+int pfdr_cpgraph_simplex_merge(pfdr_cpgraph *g, double eps, int *deactivated);
+/* Djv[V]: every vertex's alternative after the expansions so far */
+int pfdr_cpgraph_simplex_labels(pfdr_cpgraph *g, int *Djv, int mem);
+
 /* ------------------------------------------------------ multi-GPU comm -- */
 /* Partitioned sessions (quadratic solvers, identity or diagonal A): every
  * rank passes its owned vertices (V of them, global ids [vtx_begin,

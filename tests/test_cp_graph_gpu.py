@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 
 import cp_cases as CC
-from test_cp_graph_oracle import BNAMES, NAMES, iteration_state, load_case
+from test_cp_graph_oracle import (BNAMES, NAMES, SNAMES, expansion_segments, iteration_state,
+                                  load_case)
 
 pytestmark = pytest.mark.gpu
 
@@ -234,4 +235,124 @@ def test_gpu_dense_gradients_match_oracle(cpgraph_cls, oracle_port, dt):
     D = g.gradient(-V, AtA, AtY)
     oD = o.cp_gradient(-V, V, AtA, AtY, None, Eu, Ev, La, None, act, Cv, Vc, rVc, rX)
     _eq(D, oD, "DfS N=-V")
+    g.close()
+
+
+# ------------------------------------------------- the simplex driver --
+@pytest.mark.parametrize("name", SNAMES)
+def test_gpu_replays_reference_simplex_cp(cpgraph_cls, oracle_port, name):
+    """every recorded iteration of the reference's simplex cut pursuit:
+    gradient, most confident labels and each alpha-expansion's capacities
+    against the oracle, the expansions with the iteration's segments,
+    activation, components, reduced graph, reduced observations (rQ, rLa_f,
+    barycentre warm start) and merge against the reference: bit for bit"""
+    c, d = load_case(name)
+    o = oracle_port
+    K, al, Q = c["K"], c["al"], c["Q"]
+    dt = Q.dtype
+    V = Q.size // K
+    eps = CC.simplex_eps(dt.type, V, c["CP_difTol"], CC.SIMPLEX_PFDR_DIFTOL)
+    g = cpgraph_cls(V, c["Eu"], c["Ev"], c["La_d1"])
+    g.simplex_setup(K, al, Q)
+    rP0, _, _ = g.simplex_observations()  # one component: initialize() (:96-108)
+    _eq(rP0, d["k0_in_rP"], "initial rP")
+    for k in range(int(d["meta_steps"])):
+        st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
+        g.set_active(st["active"])
+        g.set_components(st["Cv"], st["Vc"], st["rVc"])
+        g.simplex_set_values(st["rP"])
+        DfS, rDi = g.simplex_gradient(eps)
+        oD, orDi = o.cp_simplex_gradient(K, al, Q, c["Eu"], c["Ev"], c["La_d1"], st["active"],
+                                         st["Cv"], st["rP"], eps)
+        _eq(DfS, oD, "DfS")
+        _eq(rDi, orDi, "rDi")
+        Djv = np.zeros(V, np.int32)
+        for n, seg in enumerate(expansion_segments(d, K, k), 1):
+            tr, rc = g.simplex_capacities(n)
+            otr, orc = o.cp_simplex_capacities(K, n, c["Eu"], c["Ev"], c["La_d1"], st["active"],
+                                               st["Vc"], st["rVc"], orDi, Djv, oD)
+            _eq(tr, otr, "tr_cap expansion %d" % n)
+            _eq(rc, orc, "r_cap expansion %d" % n)
+            g.simplex_expand(n, seg)
+            Djv = o.cp_simplex_expand(n, seg, Djv)
+            _eq(g.simplex_labels(), Djv, "Djv after expansion %d" % n)
+        w = g.simplex_activate()
+        act, ow = o.cp_simplex_activate(c["Eu"], c["Ev"], Djv, st["active"])
+        assert w == ow
+        _eq(g.active(), act, "active before merge")
+        if w == 0:
+            assert ("k%d_red_rEu" % k) not in d.files
+            continue
+        Cv, Vc, rVc = g.components()
+        _eq(Cv, new["Cv"], "Cv")
+        _eq(Vc, new["Vc"], "Vc")
+        _eq(rVc, new["rVc"], "rVc")
+        rEu, rEv, rLa, _ = g.reduced_graph(eps)
+        _eq(rEu, d["k%d_red_rEu" % k], "rEu")
+        _eq(rEv, d["k%d_red_rEv" % k], "rEv")
+        _eq(rLa, d["k%d_red_rLa_d1" % k], "rLa_d1")
+        rP, rQ, rLa_f = g.simplex_observations()
+        _eq(rP, d["k%d_red_rP0" % k], "rP0")
+        _eq(rQ, d["k%d_red_rQ" % k], "rQ")
+        if rLa_f is not None:
+            _eq(rLa_f, d["k%d_red_rLa_f" % k], "rLa_f")
+        g.simplex_set_values(new["rP"])
+        g.simplex_merge(eps)
+        _eq(g.active(), new["active"], "active after merge")
+    g.close()
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("kind,K,al", [("grid3d", 4, 0.1), ("knn", 3, 1.0), ("chain", 5, 0.0),
+                                       ("grid2d8", 6, 0.3)])
+def test_gpu_simplex_steps_match_oracle(cpgraph_cls, oracle_port, kind, K, al, dt):
+    """larger graphs, random label likelihoods, activity and label vectors
+    (ties on purpose, zero-weight edges): every simplex step against the
+    oracle, through all K - 1 expansions with random segments"""
+    o = oracle_port
+    V, Eu, Ev = _graph(kind)
+    rng = np.random.default_rng(11 + K)
+    La = (0.01 + rng.random(Eu.size)).astype(dt)
+    La[rng.random(Eu.size) < 0.02] = 0
+    Q = rng.random((V, K))
+    Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
+    act = _activity(kind, V, Eu, Ev, 9)
+    g = cpgraph_cls(V, Eu, Ev, La)
+    g.simplex_setup(K, al, Q)
+    g.set_active(act)
+    Cv, Vc, rVc = g.components()
+    rV = rVc.size - 1
+    oP, oQ, oL = o.cp_simplex_reduced(K, al, Q, Vc, rVc)
+    rP, rQ, rL = g.simplex_observations()
+    _eq(rP, oP, "rP")
+    _eq(rQ, oQ, "rQ")
+    if oL is not None:
+        _eq(rL, oL, "rLa_f")
+    P = np.round(rng.random((rV, K)), 1)  # ties -> merges, equal labels
+    P[rng.random(rV) < 0.3] = P[0]
+    P = (P / np.maximum(P.sum(axis=1, keepdims=True), 1e-9)).reshape(-1).astype(dt)
+    g.simplex_set_values(P)
+    eps = float(np.finfo(dt).eps)
+    D, rDi = g.simplex_gradient(eps)
+    oD, orDi = o.cp_simplex_gradient(K, al, Q, Eu, Ev, La, act, Cv, P, eps)
+    _eq(D, oD, "DfS")
+    _eq(rDi, orDi, "rDi")
+    Djv = np.zeros(V, np.int32)
+    for n in range(1, K):
+        tr, rc = g.simplex_capacities(n)
+        otr, orc = o.cp_simplex_capacities(K, n, Eu, Ev, La, act, Vc, rVc, orDi, Djv, oD)
+        _eq(tr, otr, "tr %d" % n)
+        _eq(rc, orc, "rc %d" % n)
+        seg = (rng.random(V) < 0.3).astype(np.uint8)
+        g.simplex_expand(n, seg)
+        Djv = o.cp_simplex_expand(n, seg, Djv)
+    _eq(g.simplex_labels(), Djv, "Djv")
+    w = g.simplex_activate()
+    oact, ow = o.cp_simplex_activate(Eu, Ev, Djv, act)
+    assert w == ow
+    _eq(g.active(), oact, "activate")
+    m = g.simplex_merge(eps)
+    oact2, om = o.cp_simplex_merge(K, Eu, Ev, Cv, P, eps, oact)
+    assert m == om
+    _eq(g.active(), oact2, "merge")
     g.close()
