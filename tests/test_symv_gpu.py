@@ -4,6 +4,8 @@ PFDR_SYMV) against the reference's golden iterates, against the column-dot
 path (k_col_dot, which reads the whole matrix as given) and against the C
 restatement (oracle/) on larger, ragged sizes.
 
+(The sequential-order path that small dense problems take by default,
+PFDR_DENSE_EXACT, is turned off here; test_parity_gpu.py covers it.)
 Both dense paths regroup the reference's dot products
 (src/PFDR_graph_quadratic_d1_l1.cpp:368-376, :432-440, :462-464), so they
 are held to the dense tolerance of test_parity_gpu.py: relative l2 <= 2e-5
@@ -18,6 +20,14 @@ import golden_io as G
 pytestmark = pytest.mark.gpu
 
 ATA = [n for n in G.names() if "AtA" in n]
+
+
+@pytest.fixture(autouse=True)
+def _tree_reduced_products(monkeypatch):
+    """these problems are small enough for the sequential-order dense path
+    (PFDR_DENSE_EXACT, default up to a chain of 8192): off here, so the
+    tree-reduced products under test (upper triangle vs column dots) run"""
+    monkeypatch.setenv("PFDR_DENSE_EXACT", "0")
 
 
 class _env:

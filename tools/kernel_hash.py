@@ -1,20 +1,28 @@
-"""sha256 over the HIP sources the bench's kernels are compiled from
-(cp_pfdr_graph_d1_amd/csrc/*.hip, *.hpp, sorted by name): recorded by
-tools/pmc_traffic.py next to the PMC traffic it summarises, compared by
-bench.py before it reports that traffic (a stale summary reports null)."""
-import glob
+"""sha256 over the HIP sources the quadratic solver's kernels (the headline
+workload's: edge / vertex sweeps, reductions, setup kernels) are compiled
+from -- pfdr_quadratic.hip and every header it includes, plus the incidence
+(pfdr_graph.hip), relabelling (pfdr_order.hip) and sequential-sum
+(pfdr_monosum.hip) translation units its setup launches -- sorted by name.
+Recorded by tools/pmc_traffic.py next to the PMC traffic it summarises and
+compared by bench.py before it reports that traffic (a summary taken on
+other kernel sources reports null).  Sources of unrelated kernels (CP graph
+steps, Gram, simplex, halo transport) and the C ABI declarations
+(include/pfdr_mi355x.h, no device code) do not enter: changing them leaves
+the headline's kernels, and so their traffic, as they were."""
 import hashlib
 import os
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+SOURCES = ("pfdr_dev.hpp", "pfdr_graph.hip", "pfdr_graph.hpp", "pfdr_halo.hpp",
+           "pfdr_monosum.hip", "pfdr_monosum.hpp", "pfdr_order.hip", "pfdr_order.hpp",
+           "pfdr_quadratic.hip", "pfdr_quadratic_kernels.hpp", "pfdr_session.hpp")
 
 
 def kernel_source_sha256():
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(ROOT, "cp_pfdr_graph_d1_amd", "csrc", "*.hip")) +
-                    glob.glob(os.path.join(ROOT, "cp_pfdr_graph_d1_amd", "csrc", "*.hpp"))):
-        h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
+    for name in sorted(SOURCES):
+        h.update(name.encode())
+        h.update(open(os.path.join(ROOT, "cp_pfdr_graph_d1_amd", "csrc", name), "rb").read())
     return h.hexdigest()
 
 
