@@ -810,6 +810,49 @@ __global__ void k_sx_merge(long E, int K, const int *__restrict__ Eu, const int 
     block_count(c, count);
 }
 
+
+// the duplex driver's two-layer cut (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp:469-527,
+// non-differentiable case): directional derivatives up / down per vertex
+// (:473-502; without La_l1 both are DfS -- the reference leaves them unset
+// there), m = MAX(0, MAX(-up, down)) with the reference's macro,
+// tr_cap[v1] = -down + m, tr_cap[v2] = -(up + m), arc v1 -> v2 of capacity m
+template <typename real>
+__global__ void k_cp_trcap_duplex(int V, int positivity, const real *__restrict__ L1,
+                                  const int *__restrict__ Cv, const real *__restrict__ rX,
+                                  const real *__restrict__ DfS, real *__restrict__ tr,
+                                  real *__restrict__ link) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const real x = rX[Cv[v]], g = DfS[v];
+    real up = g, dn = g;
+    if (L1 && x == real(0)) {
+        up = g + L1[v];
+        dn = g - L1[v];
+    }
+    if (positivity && x == real(0)) dn = -Lim<real>::huge;
+    const real in = ((-up) > (dn)) ? (-up) : (dn);
+    const real m = (real(0) > in) ? real(0) : in;
+    tr[v] = -dn + m;
+    tr[V + v] = -(up + m);
+    link[v] = m;
+}
+
+// :531-545 activate the inactive edges the cut separates in either layer
+__global__ void k_cp_activate_duplex(int V, long E, const int *__restrict__ Eu,
+                                     const int *__restrict__ Ev, const uint8_t *__restrict__ seg,
+                                     uint8_t *__restrict__ active, int *__restrict__ count) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (e < E && !active[e]) {
+        const int u = Eu[e], v = Ev[e];
+        if (seg[u] != seg[v] || seg[V + u] != seg[V + v]) {
+            active[e] = 1;
+            c = 1;
+        }
+    }
+    block_count(c, count);
+}
+
 // ================================================================ state --
 struct CpGraphBase {
     virtual ~CpGraphBase() = default;
@@ -855,6 +898,9 @@ struct CpGraphBase {
     virtual int sx_merge(double eps) = 0;
     void sx_expand(int n, const uint8_t *seg, int mem);
     int sx_activate();
+    // the duplex driver's two-layer cut
+    virtual void capacities_duplex(int positivity, void *tr, void *link, void *rc, int mem) = 0;
+    int activate_duplex(const uint8_t *seg, int mem);
 };
 
 static hipMemcpyKind kind_in(int mem) {
@@ -949,6 +995,22 @@ int CpGraphBase::sx_activate() {
     if (!count.p) count.alloc(1);
     PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
     if (E > 0) k_sx_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Djv.p, active.p, count.p);
+    PFDR_HIP(hipGetLastError());
+    return d2h_scalar(count.p, s);
+}
+
+int CpGraphBase::activate_duplex(const uint8_t *seg, int mem) {
+    DevBuf<uint8_t> bs;
+    const uint8_t *ds = seg;
+    if (mem != PFDR_MEM_DEVICE) {
+        bs.alloc(2 * (size_t)V);
+        PFDR_HIP(hipMemcpyAsync(bs.p, seg, 2 * (size_t)V, hipMemcpyHostToDevice, s));
+        ds = bs.p;
+    }
+    if (!count.p) count.alloc(1);
+    PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
+    if (E > 0)
+        k_cp_activate_duplex<<<grid_for(E), kBlock, 0, s>>>(V, E, Eu.p, Ev.p, ds, active.p, count.p);
     PFDR_HIP(hipGetLastError());
     return d2h_scalar(count.p, s);
 }
@@ -1135,6 +1197,39 @@ struct CpGraph : CpGraphBase {
         PFDR_HIP(hipGetLastError());
         if (mem != PFDR_MEM_DEVICE) {
             if (tr) PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost, s));
+            if (rc && E > 0)
+                PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
+        }
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+
+    // ---- the duplex driver's two-layer cut
+    void capacities_duplex(int positivity, void *tr, void *link, void *rc, int mem) override {
+        if (!DfS.p) throw std::runtime_error("capacities_duplex: compute the gradient first");
+        if (!has_l1 && !positivity)
+            throw std::runtime_error("capacities_duplex: differentiable problem (one-layer cut)");
+        DevBuf<real> btr, bln, brc;
+        real *dtr = (real *)tr, *dln = (real *)link, *drc = (real *)rc;
+        if (mem != PFDR_MEM_DEVICE) {
+            btr.alloc(2 * (size_t)V);
+            bln.alloc(V);
+            brc.alloc(E > 0 ? E : 1);
+            dtr = btr.p;
+            dln = bln.p;
+            drc = brc.p;
+        }
+        if (tr || link) {
+            if (!tr) { btr.alloc(2 * (size_t)V); dtr = btr.p; }
+            if (!link) { bln.alloc(V); dln = bln.p; }
+            k_cp_trcap_duplex<real><<<grid_for(V), kBlock, 0, s>>>(
+                V, positivity, has_l1 ? L1.p : nullptr, Cv.p, rX.p, DfS.p, dtr, dln);
+        }
+        if (rc && E > 0) k_cp_rcap<real><<<grid_for(E), kBlock, 0, s>>>(E, active.p, La.p, drc);
+        PFDR_HIP(hipGetLastError());
+        if (mem != PFDR_MEM_DEVICE) {
+            if (tr)
+                PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * 2 * V, hipMemcpyDeviceToHost, s));
+            if (link) PFDR_HIP(hipMemcpyAsync(link, dln, sizeof(real) * V, hipMemcpyDeviceToHost, s));
             if (rc && E > 0)
                 PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
         }
@@ -1535,5 +1630,22 @@ extern "C" int pfdr_cpgraph_simplex_labels(pfdr_cpgraph *h, int *Djv, int mem) {
         if (!g->Djv.p) throw std::runtime_error("simplex_labels: compute the gradient first");
         PFDR_HIP(hipMemcpyAsync(Djv, g->Djv.p, sizeof(int) * g->V, pfdr::kind_out(mem), g->s));
         PFDR_HIP(hipStreamSynchronize(g->s));
+    })
+}
+
+// ---------------------------------------------------- the duplex driver --
+extern "C" int pfdr_cpgraph_capacities_duplex(pfdr_cpgraph *h, int positivity, void *tr_cap,
+                                              void *r_link, void *r_cap, int mem) {
+    if (!h) return report_error("pfdr_cpgraph_capacities_duplex", "null graph");
+    CPG_TRY("pfdr_cpgraph_capacities_duplex",
+            h->g->capacities_duplex(positivity, tr_cap, r_link, r_cap, mem))
+}
+
+extern "C" int pfdr_cpgraph_activate_duplex(pfdr_cpgraph *h, const uint8_t *segment, int mem,
+                                            int *activated) {
+    if (!h || !segment) return report_error("pfdr_cpgraph_activate_duplex", "null argument");
+    CPG_TRY("pfdr_cpgraph_activate_duplex", {
+        const int n = h->g->activate_duplex(segment, mem);
+        if (activated) *activated = n;
     })
 }

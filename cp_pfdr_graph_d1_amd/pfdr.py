@@ -48,6 +48,7 @@ EXPORTED = (
     "pfdr_cpgraph_simplex_set_values", "pfdr_cpgraph_simplex_gradient",
     "pfdr_cpgraph_simplex_capacities", "pfdr_cpgraph_simplex_expand",
     "pfdr_cpgraph_simplex_activate", "pfdr_cpgraph_simplex_merge", "pfdr_cpgraph_simplex_labels",
+    "pfdr_cpgraph_capacities_duplex", "pfdr_cpgraph_activate_duplex",
     "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling", "pfdr_session_profile_filter",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
@@ -830,6 +831,25 @@ class CPGraph:
         seg = np.ascontiguousarray(segment, np.uint8)
         n = C.c_int()
         self._call("pfdr_cpgraph_activate", self._p(seg), PFDR_MEM_HOST, C.byref(n))
+        return n.value
+
+    # ---- the duplex driver's two-layer cut (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp)
+    def capacities_duplex(self, positivity=0):
+        """:469-527 -> (tr_cap[2V]: v1 then v2 nodes, r_link[V], r_cap[E])"""
+        tr = np.empty(2 * self.V, self.dtype)
+        link = np.empty(self.V, self.dtype)
+        rc = np.empty(self.E, self.dtype)
+        self._call("pfdr_cpgraph_capacities_duplex", C.c_int(int(positivity)), self._p(tr),
+                   self._p(link), self._p(rc), PFDR_MEM_HOST)
+        return tr, link, rc
+
+    def activate_duplex(self, segment):
+        """:531-545, segment[2V] -> how many edges were activated"""
+        seg = np.ascontiguousarray(segment, np.uint8)
+        if seg.size != 2 * self.V:
+            raise ValueError("segment must hold 2V entries")
+        n = C.c_int()
+        self._call("pfdr_cpgraph_activate_duplex", self._p(seg), PFDR_MEM_HOST, C.byref(n))
         return n.value
 
     # ---- the simplex driver (src/CP_PFDR_graph_loss_d1_simplex.cpp); P

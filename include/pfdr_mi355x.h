@@ -299,6 +299,22 @@ int pfdr_cpgraph_capacities_bounds(pfdr_cpgraph *g, int cut, double min, double 
 int pfdr_cpgraph_activate(pfdr_cpgraph *g, const uint8_t *segment, int mem,
     int *activated);
 
+/* The duplex driver, CP_PFDR_graph_quadratic_d1_l1_duplex, in its
+ * non-differentiable case (graph created with La_l1; positivity optional):
+ * one cut per iteration on a two-layer maxflow graph, node v (v1) and node
+ * V + v (v2) per vertex (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp:101-116).
+ * The gradient is pfdr_cpgraph_gradient's.  tr_cap[2V] (v1 nodes, then v2),
+ * r_link[V] (arc v1 -> v2; v2 -> v1 has none), r_cap[E] (every arc of edge
+ * e, both layers) from the activity before the cut (:469-527); any may be
+ * NULL.  Activation: edges separated in either layer, segment[2V]
+ * (:531-545).  The components, reduced graph and merge are the l1 driver's.
+ * (Its differentiable case indexes La_d1 as if its one-layer graph had four
+ * arcs per edge, :407 / :628 -- not reproduced.) */
+int pfdr_cpgraph_capacities_duplex(pfdr_cpgraph *g, int positivity, void *tr_cap,
+    void *r_link, void *r_cap, int mem);
+int pfdr_cpgraph_activate_duplex(pfdr_cpgraph *g, const uint8_t *segment, int mem,
+    int *activated);
+
 /* The simplex driver, CP_PFDR_graph_loss_d1_simplex (graph created
  * without La_l1): K >= 2 labels, Q[V*K] and the component label vectors
  * rP[rV*K] vertex-major like the reference (P[v*K + k]); al = 0 linear,

@@ -464,3 +464,57 @@ int oracle_cp_simplex_activate(int E, const int *Eu, const int *Ev, const int *D
     return s;
 }
 #endif
+
+/* ------------------------------------------------------------------------
+ * The duplex driver (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp), its
+ * non-differentiable case (La_l1 or positivity): a two-layer maxflow graph,
+ * node v (v1) and node V + v (v2) per vertex (:101-116).  One cut per
+ * iteration (:469-545): directional derivatives up / down (:473-502), then
+ * m = MAX(0, MAX(-up, down)), tr_cap[v1] = -down + m, tr_cap[v2] =
+ * -(up + m), the arc v1 -> v2 of capacity m (v2 -> v1 none), and every arc
+ * of an inactive edge in both layers La_d1[e] (:504-527).  With positivity
+ * and no La_l1 the reference leaves up / down of the nonzero components
+ * uninitialised (:470-502, malloc): they are DfS here, the evident intent.
+ * Its gradient is the l1 driver's (:363-433, oracle_cp_gradient).
+ * ------------------------------------------------------------------------ */
+void FN(oracle_cp_capacities_duplex)(int V, int E, const REAL *La_d1, const REAL *La_l1,
+                                     int positivity, const uint8_t *active, const int *Cv,
+                                     const REAL *rX, const REAL *DfS, REAL *tr_cap,
+                                     REAL *r_link, REAL *r_cap)
+{
+    int v, e;
+    for (v = 0; v < V; v++) {
+        const REAL x = rX[Cv[v]];
+        REAL up = DfS[v], dn = DfS[v], in, m;
+        if (La_l1 && x == (REAL)0) {
+            up = DfS[v] + La_l1[v];
+            dn = DfS[v] - La_l1[v];
+        }
+        if (positivity && x == (REAL)0) dn = -ORACLE_HUGE;
+        in = ((-up) > (dn)) ? (-up) : (dn);
+        m = (((REAL)0) > (in)) ? ((REAL)0) : (in);
+        tr_cap[v] = -dn + m;
+        tr_cap[V + v] = -(up + m);
+        r_link[v] = m;
+    }
+    for (e = 0; e < E; e++) r_cap[e] = active[e] ? (REAL)0 : La_d1[e];
+}
+
+#ifndef ORACLE_CPG_DUPLEX_INT_DEFINED
+#define ORACLE_CPG_DUPLEX_INT_DEFINED
+/* :531-545 activate the inactive edges whose ends the cut separates in
+ * either layer (segment[2V]); returns how many */
+int oracle_cp_activate_duplex(int V, int E, const int *Eu, const int *Ev, const uint8_t *segment,
+                              uint8_t *active)
+{
+    int e, w = 0;
+    for (e = 0; e < E; e++) {
+        if (!active[e] && (segment[Eu[e]] != segment[Ev[e]] ||
+                           segment[Eu[e] + V] != segment[Ev[e] + V])) {
+            active[e] = 1;
+            w++;
+        }
+    }
+    return w;
+}
+#endif

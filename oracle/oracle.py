@@ -755,3 +755,137 @@ class CPStepRefSimplex:
             _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int), _ptr(tr_cap, ct),
             _ptr(np.ascontiguousarray(r_cap, tr_cap.dtype), ct), _ptr(seg, C.c_uint8))
         return seg
+
+
+# ---- the duplex driver's cut (oracle/cp_graph_body.h, port only),
+# src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp:469-545
+def _dx_capacities(self, La_d1, La_l1, positivity, active, Cv, rX, DfS):
+    """-> (tr_cap[2V]: v1 then v2 nodes, r_link[V]: arc v1 -> v2, r_cap[E]:
+    every arc of edge e in both layers)"""
+    self._port_only("cp_capacities_duplex")
+    DfS = np.ascontiguousarray(DfS)
+    dt = DfS.dtype
+    ct, sfx = _real(dt)
+    La_d1 = np.ascontiguousarray(La_d1, dt)
+    L1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+    V, E = DfS.size, La_d1.size
+    tr = np.empty(2 * V, dt)
+    link = np.empty(V, dt)
+    rc = np.empty(E, dt)
+    self._fn("cp_capacities_duplex", sfx)(
+        C.c_int(V), C.c_int(E), _ptr(La_d1, ct), _ptr(L1, ct), C.c_int(int(positivity)),
+        _ptr(np.ascontiguousarray(active, np.uint8), C.c_uint8),
+        _ptr(np.ascontiguousarray(Cv, np.int32), C.c_int),
+        _ptr(np.ascontiguousarray(rX, dt), ct), _ptr(DfS, ct), _ptr(tr, ct), _ptr(link, ct),
+        _ptr(rc, ct))
+    return tr, link, rc
+
+
+def _dx_activate(self, V, Eu, Ev, segment, active):
+    """-> (new active, count); segment[2V]"""
+    self._port_only("cp_activate_duplex")
+    act = np.array(active, np.uint8, copy=True)
+    fn = self.lib.oracle_cp_activate_duplex
+    fn.restype = C.c_int
+    w = fn(C.c_int(V), C.c_int(len(Eu)), _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+           _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+           _ptr(np.ascontiguousarray(segment, np.uint8), C.c_uint8), _ptr(act, C.c_uint8))
+    return act, int(w)
+
+
+Oracle.cp_capacities_duplex = _dx_capacities
+Oracle.cp_activate_duplex = _dx_activate
+
+
+class CPStepRefDuplex:
+    """The REFERENCE's duplex cut pursuit (non-differentiable case), one
+    iteration at a time (oracle/_ref/libcp_step_duplex_ref.so,
+    harness/cp_step_duplex.cpp; only where the reference exists).  N = 0."""
+
+    PATH = os.path.join(HERE, "_ref", "libcp_step_duplex_ref.so")
+
+    @staticmethod
+    def available():
+        return os.path.exists(CPStepRefDuplex.PATH)
+
+    def __init__(self):
+        if CPStepRefDuplex.PATH not in _CACHE:
+            _CACHE[CPStepRefDuplex.PATH] = C.CDLL(CPStepRefDuplex.PATH)
+        self.lib = _CACHE[CPStepRefDuplex.PATH]
+
+    def init(self, Y, A, Eu, Ev, La_d1, La_l1, positivity):
+        Y = np.ascontiguousarray(Y)
+        ct, sfx = _real(Y.dtype)
+        A = None if A is None else np.ascontiguousarray(A, Y.dtype)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, Y.dtype)
+        rX0 = np.zeros(1, Y.dtype)
+        getattr(self.lib, "cp_refd_init_" + sfx)(
+            C.c_int(Y.size), C.c_int(Eu.size), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, Y.dtype), ct), _ptr(La_l1, ct),
+            C.c_int(int(positivity)), _ptr(rX0, ct))
+        return rX0
+
+    def step(self, Y, A, Eu, Ev, La_d1, La_l1, positivity, CP_difTol, state, rho=1.5,
+             condMin=1e-3, difRcd=0.0, difTol=1e-4, itMax=1000):
+        """-> (new state, segments of the 2V nodes, reduced problem or None)"""
+        Y = np.ascontiguousarray(Y)
+        dt = Y.dtype
+        ct, sfx = _real(dt)
+        V, E = Y.size, Eu.size
+        A = None if A is None else np.ascontiguousarray(A, dt)
+        La_l1 = None if La_l1 is None else np.ascontiguousarray(La_l1, dt)
+        act = np.array(state["active"], np.uint8, copy=True)
+        Cv = np.array(state["Cv"], np.int32, copy=True)
+        Vc = np.array(state["Vc"], np.int32, copy=True)
+        rV = C.c_int(int(state["rVc"].size - 1))
+        rVc = np.zeros(V + 1, np.int32)
+        rVc[:rV.value + 1] = state["rVc"]
+        rX = np.zeros(V, dt)
+        rX[:rV.value] = state["rX"]
+        seg = np.zeros(2 * V, np.uint8)
+        called, rE = C.c_int(0), C.c_int(0)
+        rEu = np.zeros(E + V, np.int32)
+        rEv = np.zeros(E + V, np.int32)
+        rLa = np.zeros(E + V, dt)
+        rL1 = np.zeros(V, dt)
+        rY = np.zeros(V, dt)
+        rAA = np.zeros(V, dt)
+        getattr(self.lib, "cp_refd_step_" + sfx)(
+            C.c_int(V), C.c_int(E), _ptr(Y, ct), _ptr(A, ct),
+            _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int),
+            _ptr(np.ascontiguousarray(La_d1, dt), ct), _ptr(La_l1, ct), C.c_int(int(positivity)),
+            ct(CP_difTol), ct(rho), ct(condMin), ct(difRcd), ct(difTol), C.c_int(itMax),
+            _ptr(act, C.c_uint8), _ptr(Cv, C.c_int), _ptr(Vc, C.c_int), _ptr(rVc, C.c_int),
+            C.byref(rV), _ptr(rX, ct), _ptr(seg, C.c_uint8), C.byref(called), C.byref(rE),
+            _ptr(rEu, C.c_int), _ptr(rEv, C.c_int), _ptr(rLa, ct), _ptr(rL1, ct), _ptr(rY, ct),
+            _ptr(rAA, ct))
+        n = rV.value
+        new = {"active": act, "Cv": Cv, "Vc": Vc, "rVc": rVc[:n + 1].copy(),
+               "rX": rX[:n].copy()}
+        red = None
+        if called.value:
+            m = rE.value
+            red = {"rEu": rEu[:m].copy(), "rEv": rEv[:m].copy(), "rLa_d1": rLa[:m].copy(),
+                   "rLa_l1": rL1[:n].copy() if La_l1 is not None else None,
+                   "rY": rY[:n].copy(), "rAA": rAA[:n].copy()}
+        return new, seg, red
+
+
+def _refd_maxflow(self, V, Eu, Ev, tr_cap, r_link, r_cap):
+    """Segments of the 2V nodes: the reference's BK maxflow on the duplex
+    graph with the cut's capacities (tr_cap[2V], r_link[V], r_cap[E])."""
+    tr_cap = np.ascontiguousarray(tr_cap)
+    ct, sfx = _real(tr_cap.dtype)
+    seg = np.zeros(2 * V, np.uint8)
+    getattr(self.lib, "cp_refd_maxflow_" + sfx)(
+        C.c_int(V), C.c_int(len(Eu)), _ptr(np.ascontiguousarray(Eu, np.int32), C.c_int),
+        _ptr(np.ascontiguousarray(Ev, np.int32), C.c_int), _ptr(tr_cap, ct),
+        _ptr(np.ascontiguousarray(r_link, tr_cap.dtype), ct),
+        _ptr(np.ascontiguousarray(r_cap, tr_cap.dtype), ct), _ptr(seg, C.c_uint8))
+    return seg
+
+
+CPStepRefDuplex.maxflow = _refd_maxflow

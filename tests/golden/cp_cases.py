@@ -305,3 +305,64 @@ def cp_graph_iteration_simplex(o, maxflow, case, state, rP_new=None):
         out["active_post"], out["merged"] = o.cp_simplex_merge(K, c["Eu"], c["Ev"], Cv,
                                                                np.asarray(rP_new, dt), eps, act)
     return out
+
+
+# ------------------------------------------------- the duplex driver --
+def make_duplex_cases():
+    """cases of the duplex driver (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp)
+    in its non-differentiable case (La_l1 or positivity: the two-layer
+    graph): the l1 cases with an l1 term or positivity, renamed"""
+    out = {}
+    for name, c in make_cases().items():
+        # differentiable (no La_l1, no positivity): the l1 driver's one-layer
+        # graph, indexed as if it had four arcs per edge (La_d1[e / 2],
+        # :407, :628; DESIGN §11) -- not reproduced; positivity without
+        # La_l1: the reference reads its up / down directions of the
+        # nonzero components from uninitialised memory (:470-502)
+        if c["La_l1"] is None:
+            continue
+        out[name.replace("cp_", "cp_duplex_", 1)] = dict(c)
+    # positivity together with an l1 term; the disconnected graph with an l1
+    # term (isolated components' eps self-loops)
+    for dt, nm in ((np.float32, "f32"), (np.float64, "f64")):
+        d = dict(make_cases()["cp_disconnected_" + nm])
+        d["La_l1"] = np.full(d["Y"].size, 0.15, dt)
+        out["cp_duplex_disconnected_l1_" + nm] = d
+        Eu, Ev = grid_graph((24, 20), 4)
+        V = 24 * 20
+        out["cp_duplex_grid2d_l1pos_" + nm] = dict(
+            Y=_y(V, 24, 19, dt), A=None, Eu=Eu, Ev=Ev,
+            La_d1=np.full(Eu.size, 0.03, dt), La_l1=np.full(V, 0.1, dt), positivity=1,
+            CP_difTol=1e-3, eps=float(np.finfo(dt).eps))
+    return out
+
+
+def cp_graph_iteration_duplex(o, maxflow, case, state, rX_new=None):
+    """One iteration of the duplex driver's graph steps with the oracle: the
+    l1 driver's gradient -> the two-layer cut's capacities (:469-527) ->
+    ``maxflow(tr_cap[2V], r_link[V], r_cap[E]) -> segments[2V]`` ->
+    activation in either layer (:531-545) -> components -> reduced graph ->
+    merge (the l1 driver's, :599-661 / :863-886 as in the duplex source)"""
+    c = case
+    V = c["Y"].size
+    dt = c["Y"].dtype
+    act0 = np.asarray(state["active"], np.uint8)
+    DfS = o.cp_gradient(0, V, c["A"], c["Y"], None, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                        act0, state["Cv"], state["Vc"], state["rVc"], state["rX"])
+    tr, link, rc = o.cp_capacities_duplex(c["La_d1"], c["La_l1"], c["positivity"], act0,
+                                          state["Cv"], state["rX"], DfS)
+    seg = maxflow(tr, link, rc)
+    act, w = o.cp_activate_duplex(V, c["Eu"], c["Ev"], seg, act0)
+    out = {"DfS": DfS, "caps": [(tr, link, rc)], "segments": [seg], "activated": w,
+           "active_pre": act}
+    if w == 0:
+        return out
+    Cv, Vc, rVc = o.cp_components(V, c["Eu"], c["Ev"], act)
+    out.update(Cv=Cv, Vc=Vc, rVc=rVc)
+    eps = cp_eps(dt, c["CP_difTol"])
+    out["reduced"] = o.cp_reduced_graph(V, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"], act, Cv,
+                                        Vc, rVc, eps)
+    if rX_new is not None:
+        out["active_post"], out["merged"] = o.cp_merge(
+            c["Eu"], c["Ev"], Cv, np.asarray(rX_new, dt), eps, c["CP_difTol"], act)
+    return out

@@ -26,7 +26,9 @@ problem exactly.  Usage:  python tests/golden/make_cp_golden.py [--bounds]
 (--bounds: the cases of the bounds driver, CP_PFDR_graph_quadratic_d1_bounds,
  through oracle/_ref/libcp_step_bounds_ref.so; files cp_bounds_*.npz;
  --simplex: the simplex driver, CP_PFDR_graph_loss_d1_simplex, through
- oracle/_ref/libcp_step_simplex_ref.so; files cp_simplex_*.npz)
+ oracle/_ref/libcp_step_simplex_ref.so; files cp_simplex_*.npz;
+ --duplex: the duplex driver's two-layer cut, CP_PFDR_graph_quadratic_d1_l1_duplex,
+ through oracle/_ref/libcp_step_duplex_ref.so; files cp_duplex_*.npz)
 """
 import os
 import sys
@@ -36,7 +38,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 sys.path.insert(0, HERE)
-from oracle import CPStepRef, CPStepRefBounds, CPStepRefSimplex, Oracle  # noqa: E402
+from oracle import CPStepRef, CPStepRefBounds, CPStepRefDuplex, CPStepRefSimplex, Oracle  # noqa: E402
 import cp_cases as CC  # noqa: E402
 
 
@@ -181,9 +183,65 @@ def main_simplex():
               % (name, V, E, K, " ".join(hist)))
 
 
+def main_duplex():
+    """the duplex driver's non-differentiable case
+    (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp): one two-layer cut per
+    iteration, whose 2V segments the reference records (k{k}_seg_last)"""
+    o = Oracle("port")
+    ref = CPStepRefDuplex()
+    for name, c in CC.make_duplex_cases().items():
+        out = {}
+        for k, v in c.items():
+            if v is not None:
+                out["in_" + k] = np.asarray(v)
+        V, E = c["Y"].size, c["Eu"].size
+        rX0 = ref.init(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                       c["positivity"])
+        state = {"active": np.zeros(E, np.uint8), "Cv": np.zeros(V, np.int32),
+                 "Vc": np.arange(V, dtype=np.int32), "rVc": np.array([0, V], np.int32),
+                 "rX": rX0}
+        hist = []
+        for k in range(CC.STEPS):
+            new, seg, red = ref.step(c["Y"], c["A"], c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                                     c["positivity"], c["CP_difTol"], state)
+            mf = lambda tr, link, rc: ref.maxflow(V, c["Eu"], c["Ev"], tr, link, rc)
+            d = CC.cp_graph_iteration_duplex(o, mf, c, state, rX_new=new["rX"])
+            assert np.array_equal(d["segments"][0], seg), "segments"
+            if d["activated"] == 0:
+                assert red is None
+            else:
+                for key in ("Cv", "Vc", "rVc"):
+                    assert np.array_equal(d[key], new[key]), key
+                rEu, rEv, rLa, rL1 = d["reduced"]
+                assert np.array_equal(rEu, red["rEu"]), "rEu"
+                assert np.array_equal(rEv, red["rEv"]), "rEv"
+                assert np.array_equal(rLa, red["rLa_d1"]), "rLa_d1"
+                if rL1 is not None:
+                    assert np.array_equal(rL1, red["rLa_l1"]), "rLa_l1"
+                assert np.array_equal(d["active_post"], new["active"]), "active after merge"
+            for key, val in state.items():
+                out["k%d_in_%s" % (k, key)] = val
+            for key, val in new.items():
+                out["k%d_out_%s" % (k, key)] = val
+            out["k%d_seg_last" % k] = seg
+            if red is not None:
+                for key, val in red.items():
+                    if val is not None:
+                        out["k%d_red_%s" % (k, key)] = val
+            hist.append("%d:%d/%s" % (new["rVc"].size - 1, int(new["active"].sum()),
+                                       "-" if red is None else red["rEu"].size))
+            state = new
+        out["meta_steps"] = np.int32(CC.STEPS)
+        out["meta_build"] = np.str_("g++ -O3 -ffp-contract=off, no OpenMP")
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+        print("%-30s V=%d E=%d  rV:active/rE per iteration %s" % (name, V, E, " ".join(hist)))
+
+
 def main():
     if "--bounds" in sys.argv:
         return main_bounds()
+    if "--duplex" in sys.argv:
+        return main_duplex()
     if "--simplex" in sys.argv:
         return main_simplex()
     o = Oracle("port")

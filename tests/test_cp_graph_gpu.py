@@ -14,8 +14,8 @@ import numpy as np
 import pytest
 
 import cp_cases as CC
-from test_cp_graph_oracle import (BNAMES, NAMES, SNAMES, expansion_segments, iteration_state,
-                                  load_case)
+from test_cp_graph_oracle import (BNAMES, DNAMES, NAMES, SNAMES, expansion_segments,
+                                  iteration_state, load_case)
 
 pytestmark = pytest.mark.gpu
 
@@ -355,4 +355,87 @@ def test_gpu_simplex_steps_match_oracle(cpgraph_cls, oracle_port, kind, K, al, d
     oact2, om = o.cp_simplex_merge(K, Eu, Ev, Cv, P, eps, oact)
     assert m == om
     _eq(g.active(), oact2, "merge")
+    g.close()
+
+
+# -------------------------------------------------- the duplex driver --
+@pytest.mark.parametrize("name", DNAMES)
+def test_gpu_replays_reference_duplex_cp(cpgraph_cls, oracle_port, name):
+    """every recorded iteration of the reference's duplex cut pursuit: the
+    gradient and the two-layer cut's capacities against the oracle, the
+    activation with the recorded 2V segments, components, reduced graph and
+    merge against the reference: bit for bit"""
+    c, d = load_case(name)
+    o = oracle_port
+    dt = c["Y"].dtype
+    V = c["Y"].size
+    eps = CC.cp_eps(dt, c["CP_difTol"])
+    g = cpgraph_cls(V, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"])
+    for k in range(int(d["meta_steps"])):
+        st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
+        g.set_active(st["active"])
+        g.set_components(st["Cv"], st["Vc"], st["rVc"])
+        g.set_values(st["rX"])
+        DfS = g.gradient(0, c["A"], c["Y"])
+        oD = o.cp_gradient(0, V, c["A"], c["Y"], None, c["Eu"], c["Ev"], c["La_d1"], c["La_l1"],
+                           st["active"], st["Cv"], st["Vc"], st["rVc"], st["rX"])
+        _eq(DfS, oD, "DfS")
+        tr, link, rc = g.capacities_duplex(c["positivity"])
+        otr, olink, orc = o.cp_capacities_duplex(c["La_d1"], c["La_l1"], c["positivity"],
+                                                 st["active"], st["Cv"], st["rX"], oD)
+        _eq(tr, otr, "tr_cap")
+        _eq(link, olink, "r_link")
+        _eq(rc, orc, "r_cap")
+        seg = d["k%d_seg_last" % k]
+        w = g.activate_duplex(seg)
+        act, ow = o.cp_activate_duplex(V, c["Eu"], c["Ev"], seg, st["active"])
+        assert w == ow
+        _eq(g.active(), act, "active before merge")
+        if w == 0:
+            continue
+        Cv, Vc, rVc = g.components()
+        _eq(Cv, new["Cv"], "Cv")
+        _eq(Vc, new["Vc"], "Vc")
+        _eq(rVc, new["rVc"], "rVc")
+        rEu, rEv, rLa, rL1 = g.reduced_graph(eps)
+        _eq(rEu, d["k%d_red_rEu" % k], "rEu")
+        _eq(rEv, d["k%d_red_rEv" % k], "rEv")
+        _eq(rLa, d["k%d_red_rLa_d1" % k], "rLa_d1")
+        _eq(rL1, d["k%d_red_rLa_l1" % k], "rLa_l1")
+        g.set_values(new["rX"])
+        g.merge(eps, c["CP_difTol"])
+        _eq(g.active(), new["active"], "active after merge")
+    g.close()
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("kind", ["grid3d", "knn", "grid2d8"])
+def test_gpu_duplex_cut_matches_oracle(cpgraph_cls, oracle_port, kind, dt):
+    """the two-layer cut on larger graphs, zero components (l1, positivity)"""
+    o = oracle_port
+    V, Eu, Ev = _graph(kind)
+    rng = np.random.default_rng(17)
+    La = (0.01 + rng.random(Eu.size)).astype(dt)
+    L1 = (0.05 * rng.random(V)).astype(dt)
+    act = _activity(kind, V, Eu, Ev, 3)
+    g = cpgraph_cls(V, Eu, Ev, La, L1)
+    g.set_active(act)
+    Cv, Vc, rVc = g.components()
+    rV = rVc.size - 1
+    rX = np.round(rng.standard_normal(rV), 1).astype(dt)
+    rX[rng.random(rV) < 0.3] = 0
+    g.set_values(rX)
+    Y = rng.standard_normal(V).astype(dt)
+    D = g.gradient(0, None, Y)
+    for pos in (0, 1):
+        tr, link, rc = g.capacities_duplex(pos)
+        otr, olink, orc = o.cp_capacities_duplex(La, L1, pos, act, Cv, rX, D)
+        _eq(tr, otr, "tr")
+        _eq(link, olink, "link")
+        _eq(rc, orc, "rc")
+    seg = (rng.random(2 * V) < 0.5).astype(np.uint8)
+    n = g.activate_duplex(seg)
+    oact, on = o.cp_activate_duplex(V, Eu, Ev, seg, act)
+    assert n == on
+    _eq(g.active(), oact, "activate")
     g.close()

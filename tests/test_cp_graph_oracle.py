@@ -20,18 +20,22 @@ import numpy as np
 import pytest
 
 import cp_cases as CC
-from oracle import CPStepRef, CPStepRefSimplex
+from oracle import CPStepRef, CPStepRefDuplex, CPStepRefSimplex
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 FILES = sorted(glob.glob(os.path.join(GOLDEN, "cp_*.npz")))
 _ALL = [os.path.basename(f)[:-4] for f in FILES]
 # the l1 driver's iterations; the bounds driver's (cp_bounds_*); the dense
 # reduced problems are test_cp_reduce.py's (cp_dense_*)
-NAMES = [n for n in _ALL if not n.startswith(("cp_bounds_", "cp_dense_", "cp_simplex_"))]
+NAMES = [n for n in _ALL
+         if not n.startswith(("cp_bounds_", "cp_dense_", "cp_simplex_", "cp_duplex_"))]
 BNAMES = [n for n in _ALL if n.startswith("cp_bounds_")]
 # the simplex driver's (src/CP_PFDR_graph_loss_d1_simplex.cpp): K - 1
 # alpha-expansions per iteration, label vectors rP
 SNAMES = [n for n in _ALL if n.startswith("cp_simplex_")]
+# the duplex driver's (src/CP_PFDR_graph_quadratic_d1_l1_duplex.cpp): one
+# two-layer cut per iteration, 2V segments
+DNAMES = [n for n in _ALL if n.startswith("cp_duplex_")]
 
 
 def load_case(name):
@@ -66,6 +70,7 @@ def test_fixtures_present():
     assert len(NAMES) >= 10, NAMES
     assert len(BNAMES) >= 10, BNAMES
     assert len(SNAMES) >= 10, SNAMES
+    assert len(DNAMES) >= 8, DNAMES
 
 
 @pytest.mark.parametrize("name", NAMES + BNAMES)
@@ -170,3 +175,44 @@ def test_oracle_simplex_capacities_through_reference_maxflow(oracle_port, name):
             oracle_port, lambda tr, rc: ref.maxflow(c["Eu"], c["Ev"], tr, rc), c, st)
         for n, (a, b) in enumerate(zip(r["segments"], expansion_segments(d, K, k)), 1):
             assert np.array_equal(a, b), (k, n)
+
+
+@pytest.mark.parametrize("name", DNAMES)
+def test_oracle_replays_reference_duplex_cp(oracle_port, name):
+    """the duplex driver: gradient -> two-layer capacities -> (the recorded
+    2V segments) -> activation in either layer -> components -> reduced
+    graph -> merge; rY / rAA through the CP builder restatement"""
+    c, d = load_case(name)
+    o = oracle_port
+    for k in range(int(d["meta_steps"])):
+        st, new = iteration_state(d, k, "in"), iteration_state(d, k, "out")
+        seg = d["k%d_seg_last" % k]
+        r = CC.cp_graph_iteration_duplex(o, lambda tr, link, rc: seg, c, st, rX_new=new["rX"])
+        if r["activated"] == 0:
+            assert ("k%d_red_rEu" % k) not in d.files
+            continue
+        for key in ("Cv", "Vc", "rVc"):
+            assert np.array_equal(r[key], new[key]), key
+        rEu, rEv, rLa, rL1 = r["reduced"]
+        assert np.array_equal(rEu, d["k%d_red_rEu" % k])
+        assert np.array_equal(rEv, d["k%d_red_rEv" % k])
+        assert np.array_equal(rLa, d["k%d_red_rLa_d1" % k])
+        assert np.array_equal(rL1, d["k%d_red_rLa_l1" % k])
+        assert np.array_equal(r["active_post"], new["active"])
+        red = o.cp_reduce(0, c["A"], c["Y"], new["rVc"], new["Vc"])
+        assert np.array_equal(red["rY"], d["k%d_red_rY" % k])
+        assert np.array_equal(red["rAA"], d["k%d_red_rAA" % k])
+
+
+@pytest.mark.skipif(not CPStepRefDuplex.available(), reason="reference harness not built here")
+@pytest.mark.parametrize("name", DNAMES)
+def test_oracle_duplex_capacities_through_reference_maxflow(oracle_port, name):
+    c, d = load_case(name)
+    ref = CPStepRefDuplex()
+    V = c["Y"].size
+    for k in range(int(d["meta_steps"])):
+        st = iteration_state(d, k, "in")
+        r = CC.cp_graph_iteration_duplex(
+            oracle_port, lambda tr, link, rc: ref.maxflow(V, c["Eu"], c["Ev"], tr, link, rc), c,
+            st)
+        assert np.array_equal(r["segments"][0], d["k%d_seg_last" % k])
