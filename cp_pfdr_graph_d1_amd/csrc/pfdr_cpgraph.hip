@@ -117,17 +117,20 @@ constexpr int kSegShort = kWave;
 template <typename real>
 __global__ void k_segsum_short(int G, const int *__restrict__ off, const int *__restrict__ idx,
                                const real *__restrict__ val, real *__restrict__ out,
-                               int *__restrict__ longs, int *__restrict__ nlong) {
+                               int *__restrict__ longs, int *__restrict__ nlong, long vstride) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const int a = off[g], b = off[g + 1];
     if (b - a > kSegShort) {
-        longs[atomicAdd(nlong, 1)] = g;
+        if (blockIdx.y == 0) longs[atomicAdd(nlong, 1)] = g;
         return;
     }
+    // grid.y = several value arrays val + y * vstride (the same segments),
+    // results at out + y * G
+    const real *vv = val + (long)blockIdx.y * vstride;
     real s = real(0);
-    for (int i = a; i < b; i++) s += val[idx ? idx[i] : i];
-    out[g] = s;
+    for (int i = a; i < b; i++) s += vv[idx ? idx[i] : i];
+    out[(long)blockIdx.y * G + g] = s;
 }
 
 // one workgroup per long segment: waves 1-3 stage the next chunk in LDS
@@ -137,11 +140,14 @@ template <typename real, bool GATHER>
 __global__ __launch_bounds__(kBlock) void k_segsum_long(int n, const int *__restrict__ longs,
                                                        const int *__restrict__ off,
                                                        const int *__restrict__ idx,
-                                                       const real *__restrict__ val,
-                                                       real *__restrict__ out) {
+                                                       const real *__restrict__ val_,
+                                                       real *__restrict__ out_, int G,
+                                                       long vstride) {
     constexpr int CH = 4096;
     __shared__ alignas(16) real buf[2][CH];
     if ((int)blockIdx.x >= n) return;
+    const real *__restrict__ val = val_ + (long)blockIdx.y * vstride;
+    real *__restrict__ out = out_ + (long)blockIdx.y * G;
     const int g = longs[blockIdx.x];
     const long a = off[g], b = off[g + 1];
     const int t = threadIdx.x;
@@ -182,17 +188,26 @@ __global__ __launch_bounds__(kBlock) void k_segsum_long(int n, const int *__rest
     if (t == 0) out[g] = s;
 }
 
+// nv value arrays val + j * vstride (j < nv) over the same segments, all
+// in one launch pair: out[j * G + g]
 template <typename real>
 static void segsum(int G, const int *off, const int *idx, const real *val, real *out,
-                   DevBuf<int> &longs, DevBuf<int> &nlong, hipStream_t s) {
-    if (G <= 0) return;
+                   DevBuf<int> &longs, DevBuf<int> &nlong, hipStream_t s, int nv = 1,
+                   long vstride = 0) {
+    if (G <= 0 || nv <= 0) return;
+    if (nv > 65535) throw std::runtime_error("segsum: too many value arrays");
     if (longs.n < (size_t)G) longs.alloc(G);
     if (!nlong.p) nlong.alloc(1);
     PFDR_HIP(hipMemsetAsync(nlong.p, 0, sizeof(int), s));
-    k_segsum_short<real><<<grid_for(G), kBlock, 0, s>>>(G, off, idx, val, out, longs.p, nlong.p);
+    k_segsum_short<real><<<dim3(grid_for(G), nv), kBlock, 0, s>>>(G, off, idx, val, out, longs.p,
+                                                                  nlong.p, vstride);
     const int nl = d2h_scalar(nlong.p, s);
-    if (nl && idx) k_segsum_long<real, true><<<nl, kBlock, 0, s>>>(nl, longs.p, off, idx, val, out);
-    else if (nl) k_segsum_long<real, false><<<nl, kBlock, 0, s>>>(nl, longs.p, off, idx, val, out);
+    if (nl && idx)
+        k_segsum_long<real, true><<<dim3(nl, nv), kBlock, 0, s>>>(nl, longs.p, off, idx, val, out,
+                                                                   G, vstride);
+    else if (nl)
+        k_segsum_long<real, false><<<dim3(nl, nv), kBlock, 0, s>>>(nl, longs.p, off, idx, val, out,
+                                                                    G, vstride);
     PFDR_HIP(hipGetLastError());
 }
 
@@ -1267,8 +1282,8 @@ struct CpGraph : CpGraphBase {
     void sx_observations(void *rPo, void *rQo, void *rLafo, int mem) override {
         need_k("simplex_observations");
         S.alloc((size_t)rV * K);
-        for (int k = 0; k < K; k++)
-            segsum<real>(rV, rVc.p, Vc.p, Qt.p + (size_t)k * V, S.p + (size_t)k * rV, longs, nlong, s);
+        // every label in one launch pair: (component, label) segments side by side
+        segsum<real>(rV, rVc.p, Vc.p, Qt.p, S.p, longs, nlong, s, K, (long)V);
         rP.alloc((size_t)rV * K);
         DevBuf<real> bQ((size_t)rV * K), bL(rV);
         const int linear = sal == real(0);

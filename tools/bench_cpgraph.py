@@ -11,7 +11,8 @@ Each step is timed on that state (median of --reps, device-resident
 inputs and outputs; activity restored between repetitions):
 
     gradient (N = 0, identity), capacities (cut 1 and 2), activate,
-    components, reduced graph, merge
+    components, reduced graph, merge; and the duplex driver's two-layer cut
+    (capacities, activation)
 
 plus the PCIe-inclusive capacities -> host copy a host maxflow needs.
 CPU: oracle/liboracle_pfdr.so (single-threaded restatement of the same
@@ -77,6 +78,11 @@ def main():
     drc = torch.empty(E, dtype=torch.float32, device="cuda")
     dDf = torch.empty(V, dtype=torch.float32, device="cuda")
     dseg = torch.from_numpy(seg ^ (rng.random(V) < 0.01).astype(np.uint8)).cuda()
+    # the duplex driver's two-layer cut (2V nodes)
+    dtr2 = torch.empty(2 * V, dtype=torch.float32, device="cuda")
+    dlink = torch.empty(V, dtype=torch.float32, device="cuda")
+    seg2 = np.concatenate([seg, seg ^ (rng.random(V) < 0.01).astype(np.uint8)])
+    dseg2 = torch.from_numpy(seg2).cuda()
     DEV = pfdr.PFDR_MEM_DEVICE
     rE = C.c_int()
     n = C.c_int()
@@ -95,6 +101,10 @@ def main():
                                         vp(dtr), vp(drc), DEV),
         "activate": lambda: call("pfdr_cpgraph_activate", C.c_void_p(dseg.data_ptr()), DEV,
                                  C.byref(n)),
+        "capacities_duplex": lambda: call("pfdr_cpgraph_capacities_duplex", C.c_int(0),
+                                          vp(dtr2), vp(dlink), vp(drc), DEV),
+        "activate_duplex": lambda: call("pfdr_cpgraph_activate_duplex",
+                                        C.c_void_p(dseg2.data_ptr()), DEV, C.byref(n)),
         "components": lambda: call("pfdr_cpgraph_components", C.byref(C.c_int())),
         "reduced_graph": lambda: call("pfdr_cpgraph_reduced_graph", C.c_double(eps),
                                       C.byref(rE)),
@@ -107,7 +117,7 @@ def main():
         for r in range(args.reps + 1):
             restore()
             if name in ("reduced_graph", "merge", "gradient", "capacities_cut1",
-                        "capacities_cut2"):
+                        "capacities_cut2", "capacities_duplex"):
                 call("pfdr_cpgraph_set_components", C.c_int(rV), C.c_void_p(Cv.ctypes.data),
                      C.c_void_p(Vc.ctypes.data), C.c_void_p(rVc.ctypes.data), pfdr.PFDR_MEM_HOST)
                 g.set_values(rX)
@@ -139,7 +149,8 @@ def main():
          C.c_void_p(Vc.ctypes.data), C.c_void_p(rVc.ctypes.data), pfdr.PFDR_MEM_HOST)
     rEu, rEv, rLa, rL1 = g.reduced_graph(eps)
     g.close()
-    total = sum(v for k, v in res.items() if not k.endswith("_to_host"))
+    total = sum(v for k, v in res.items()
+                if not k.endswith("_to_host") and not k.endswith("_duplex"))
     out = {
         "what": "CP graph steps (pfdr_cpgraph_*), one MI355X, device-resident",
         "graph": "jittered %dx%dx%d 6-NN (V=%d, E=%d)" % (nx, ny, nz, V, E),
@@ -147,6 +158,8 @@ def main():
                   "components": rV, "reduced_edges": int(rEu.size)},
         "gpu_ms": res,
         "gpu_ms_iteration_graph_steps": round(total, 3),
+        "iteration_note": "the l1 driver's two-cut iteration; *_duplex: the duplex driver's "
+                          "one two-layer cut instead of the two cuts",
         "input_generation_s": round(gen_s, 2),
     }
     if args.cpu:
@@ -168,6 +181,12 @@ def main():
         o.cp_activate(Eu, Ev, sg, act0)
         cpu["activate"] = time.perf_counter() - t
         t = time.perf_counter()
+        o.cp_capacities_duplex(La, L1, 0, act0, Cv, rX, D)
+        cpu["capacities_duplex"] = time.perf_counter() - t
+        t = time.perf_counter()
+        o.cp_activate_duplex(V, Eu, Ev, seg2, act0)
+        cpu["activate_duplex"] = time.perf_counter() - t
+        t = time.perf_counter()
         oCv, oVc, orVc = o.cp_components(V, Eu, Ev, act0)
         cpu["components"] = time.perf_counter() - t
         t = time.perf_counter()
@@ -177,7 +196,8 @@ def main():
         o.cp_merge(Eu, Ev, oCv, rX, eps, 1e-3, act0)
         cpu["merge"] = time.perf_counter() - t
         out["cpu_ms"] = {k: round(v * 1e3, 1) for k, v in cpu.items()}
-        out["cpu_ms_iteration_graph_steps"] = round(sum(cpu.values()) * 1e3, 1)
+        out["cpu_ms_iteration_graph_steps"] = round(
+            sum(v for k, v in cpu.items() if not k.endswith("_duplex")) * 1e3, 1)
         out["cpu"] = {"kind": "port", "cores": 1,
                       "note": "single-threaded C restatement (oracle/cp_graph_body.h); "
                               "components / reduced graph / gradient rebuild the maxflow "
