@@ -11,7 +11,6 @@
 //    stable LSD radix sort (rocPRIM) keyed by vertex.
 //  * deterministic host-side synthetic generators (splitmix64), the native
 //    twins of cp_pfdr_graph_d1_amd/graphs.py.
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -21,6 +20,7 @@
 #include <vector>
 
 #include "pfdr_graph.hpp"
+#include "pfdr_sort.hpp"
 
 namespace pfdr {
 
@@ -108,14 +108,7 @@ void build_incidence(const int *dEu, const int *dEv, int V, long E,
     PFDR_HIP(hipGetLastError());
     unsigned bits = 1;
     while (bits < 32 && ((1ull << bits) < (unsigned long long)V)) bits++;
-    size_t tmp_bytes = 0;
-    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key.p, skey.p,
-                                       val.p, inc.idx.p, (size_t)n, 0, bits,
-                                       s));
-    DevBuf<char> tmp(tmp_bytes > 0 ? tmp_bytes : 1);
-    PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, key.p,
-                                       skey.p, val.p, inc.idx.p, (size_t)n, 0,
-                                       bits, s));
+    radix_sort_pairs_stable<unsigned>(key.p, skey.p, val.p, inc.idx.p, n, (int)bits, s);
     k_incidence_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey.p, n, V,
                                                        inc.ptr.p);
     PFDR_HIP(hipGetLastError());
@@ -133,12 +126,7 @@ void build_incidence_rows(const unsigned *rows, unsigned *srows, const unsigned 
     inc.idx.alloc((size_t)(n > 0 ? n : 1));
     unsigned bits = 1;
     while (bits < 32 && ((1ull << bits) <= (unsigned long long)V)) bits++;
-    size_t tmp_bytes = 0;
-    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, rows, srows, vals, inc.idx.p,
-                                       (size_t)n, 0, bits, s));
-    DevBuf<char> tmp(tmp_bytes > 0 ? tmp_bytes : 1);
-    PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, rows, srows, vals, inc.idx.p,
-                                       (size_t)n, 0, bits, s));
+    radix_sort_pairs_stable<unsigned>(rows, srows, vals, inc.idx.p, n, (int)bits, s);
     k_incidence_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(srows, n, V, inc.ptr.p);
     PFDR_HIP(hipGetLastError());  // temporaries: see build_incidence
 }
@@ -173,12 +161,8 @@ void build_incidence_keyed(unsigned long long *keys, unsigned *vals, long n, int
     unsigned vbits = 1;
     while (vbits < 31 && ((1ull << vbits) <= (unsigned long long)V)) vbits++;
     DevBuf<unsigned long long> skey(n);
-    size_t tmp_bytes = 0;
-    PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, skey.p, vals, inc.idx.p,
-                                       (size_t)n, 0, 32 + vbits + 1, s));
-    DevBuf<char> tmp(tmp_bytes > 0 ? tmp_bytes : 1);
-    PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tmp_bytes, keys, skey.p, vals, inc.idx.p,
-                                       (size_t)n, 0, 32 + vbits + 1, s));
+    radix_sort_pairs_stable<unsigned long long>(keys, skey.p, vals, inc.idx.p, n,
+                                                (int)(32 + vbits + 1), s);
     k_keyed_ptr<<<grid_for(n + 1), kBlock, 0, s>>>(skey.p, n, V, inc.ptr.p);
     PFDR_HIP(hipGetLastError());  // temporaries: see build_incidence
 }

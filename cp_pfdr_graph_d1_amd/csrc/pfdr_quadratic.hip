@@ -7,11 +7,11 @@
 #include <map>
 #include <stdexcept>
 
-#include <rocprim/rocprim.hpp>
 
 #include "pfdr_halo.hpp"
 #include "pfdr_order.hpp"
 #include "pfdr_quadratic_kernels.hpp"
+#include "pfdr_sort.hpp"
 
 namespace pfdr {
 
@@ -481,10 +481,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         eorig_.alloc(E);
         k_edge_order_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, where_.p, k.p, v.p);
         PFDR_HIP(hipGetLastError());
-        size_t tb = 0;
-        PFDR_HIP(rocprim::radix_sort_pairs(nullptr, tb, k.p, ks.p, v.p, eorig_.p, E, 0, 64, s));
-        DevBuf<char> tmp(tb ? tb : 1);
-        PFDR_HIP(rocprim::radix_sort_pairs((void *)tmp.p, tb, k.p, ks.p, v.p, eorig_.p, E, 0, 64, s));
+        radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, eorig_.p, (long)E, 64, s);
         DevBuf<int> nu(E), nv(E);
         emap_.alloc(E);
         k_edge_relabel<<<grid_for(E), kBlock, 0, s>>>(E_, eorig_.p, Eu_.p, Ev_.p, where_.p, nu.p,

@@ -38,6 +38,7 @@ EXPORTED = (
     "pfdr_proj_simplex_metric_f32", "pfdr_proj_simplex_metric_f64",
     "pfdr_gram_f32", "pfdr_gram_f64", "pfdr_operator_norm_f32", "pfdr_operator_norm_f64",
     "pfdr_sequential_sum_f32", "pfdr_sequential_sum_f64",
+    "pfdr_radix_sort_pairs_u32", "pfdr_radix_sort_pairs_u64",
     "pfdr_cp_reduce_f32", "pfdr_cp_reduce_f64",
     "pfdr_cpgraph_create", "pfdr_cpgraph_destroy", "pfdr_cpgraph_set_active",
     "pfdr_cpgraph_get_active", "pfdr_cpgraph_set_components", "pfdr_cpgraph_get_components",

@@ -212,6 +212,12 @@ int pfdr_sequential_sum_f32(int64_t n, const float *a, int mem, float seed, int 
                             float *out, double *ms);
 int pfdr_sequential_sum_f64(int64_t n, const double *a, int mem, double seed, int method,
                             double *out, double *ms);
+/* The stable LSD radix sort the library builds its incidence lists with
+ * (pairs sorted by the low `bits` bits of the key, equal keys in input
+ * order), on host arrays, in place; *ms (may be NULL) receives the sort's
+ * GPU time.  n < 2^31.  Exposed for its tests. */
+int pfdr_radix_sort_pairs_u32(int64_t n, uint32_t *keys, uint32_t *vals, int bits, double *ms);
+int pfdr_radix_sort_pairs_u64(int64_t n, uint64_t *keys, uint32_t *vals, int bits, double *ms);
 /* Squared operator norm ||A||^2 by the power method (reference
  * operator_norm_matrix<real>, include/operator_norm_matrix.hpp:12-14, same
  * argument meaning; deterministic starts).  *gram_ms (may be NULL): time of
