@@ -154,7 +154,7 @@ class QuadSession final : public SessionBase {
     void forward_dense(int gate);
     void gradient();
     void objective();
-    void body();
+    void body(int i, int n);  // i-th of n bodies of a chunk
     void push_ctrl();
     void pull_ctrl();
     void wait_stream();
@@ -172,7 +172,7 @@ class QuadSession final : public SessionBase {
     void plan_overlap();
     // one launch over [ebeg, eend) and, if not empty, [ebeg2, eend2)
     void edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name,
-                    long ebeg2 = 0, long eend2 = 0);
+                    long ebeg2 = 0, long eend2 = 0, const FuseDecide<real> *fd = nullptr);
     // one launch over the blocks [bbeg, bend) and, if not empty, [bbeg2, bend2)
     void vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, const char *name,
                       int bbeg2 = 0, int bend2 = 0);
@@ -216,6 +216,14 @@ class QuadSession final : public SessionBase {
     // L2s are not coherent), once per workgroup, which costs more than the
     // kernel boundary it replaces
     static constexpr long kCoopBlocks = 0;
+    // small graphs (<= kFuseBlocks vertex blocks, dif tracked, one GPU):
+    // the loop decision on iteration t taken inside the edge sweep of t + 1,
+    // two launches per iteration instead of three (FuseDecide in
+    // pfdr_quadratic_kernels.hpp); the decisions alternate between ctrl_
+    // (even bodies of a chunk) and ctrl2_ (odd), the chunk's closing
+    // decision lands in ctrl_.  PFDR_FUSE = 0 off.
+    bool fuse_ = false;
+    DevBuf<Ctrl<real>> ctrl2_;
     template <int EPI> void col_product(ColArgs<real> ca);
     DevBuf<real> spart_;
     void plan_symv();
@@ -440,6 +448,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (!coop_) plan_pipeline();
         const char *g = getenv("PFDR_GRAPH");
         graphs_ok_ = !(g && g[0] == '0') && itMax_ >= 2 * chunk_;
+        const char *f = getenv("PFDR_FUSE");
+        // (an edgeless graph has no edge sweep to carry the decision)
+        fuse_ = !(f && f[0] == '0') && !coop_ && pblk_.empty() && track_ && !rec_obj_ &&
+                (mode_ == A_IDENT || mode_ == A_DIAG) && nbv_ <= kFuseBlocks && E_ > 0;
+        if (fuse_) ctrl2_.alloc(1);
+        fused = fuse_ ? 1 : 0;
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
 }
@@ -827,7 +841,7 @@ void QuadSession<real>::objective() {
 
 template <typename real>
 void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, const char *name,
-                                   long ebeg2, long eend2) {
+                                   long ebeg2, long eend2, const FuseDecide<real> *fd) {
     constexpr int EPT = Vec<real>::kPer16B;
     if (eend <= ebeg) { ebeg = ebeg2; eend = eend2; ebeg2 = eend2 = 0; }
     if (eend <= ebeg) return;
@@ -836,13 +850,16 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     ERange rg{ebeg, eend, ebeg2, eend2, grid_for(eend - ebeg, EPT)};
     const int nb = rg.nb0 + (eend2 > ebeg2 ? grid_for(eend2 - ebeg2, EPT) : 0);
     const int xm = xcd_fit(nb, xcd_e_), g = xcd_grid(nb, xm);
-    if (us_ && uptr_.p)
-        k_edge_sweep_us<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p,
-                                                   cw_, gi_.p, La_d1_.p, wz_.p, rho_, c, nb,
-                                                   xm, rg);
-    else
-        k_edge_sweep<real><<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
-                                                La_d1_.p, wz_.p, rho_, c, nb, xm, rg);
+    const FuseDecide<real> f = fd ? *fd : FuseDecide<real>{};
+    if (us_ && uptr_.p) {
+        auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
+        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
+                               La_d1_.p, wz_.p, rho_, c, nb, xm, rg, f);
+    } else {
+        auto k = fuse_ ? k_edge_sweep<real, true> : k_edge_sweep<real, false>;
+        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p, La_d1_.p, wz_.p,
+                               rho_, c, nb, xm, rg, f);
+    }
 }
 
 template <typename real>
@@ -908,6 +925,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
     a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
+    a.late = fuse_ ? 1 : 0;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
     a.bsplit = a.nb; a.bjump = 0;
     return a;
@@ -933,10 +951,30 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
 }
 
 template <typename real>
-void QuadSession<real>::body() {
+void QuadSession<real>::body(int i, int n) {
     hipStream_t s = stream;
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
+    if (fuse_) {
+        // E(i) decides iteration i - 1 (from cb[(i-1)&1] into cb[i&1]), V(i)
+        // reads cb[i&1]; the last body closes the chunk with k_reduce_decide's
+        // arithmetic, its decision into ctrl_
+        Ctrl<real> *cb[2] = {ctrl_.p, ctrl2_.p};
+        FuseDecide<real> fd{};
+        if (i > 0) {
+            fd.src = cb[(i - 1) & 1]; fd.dst = cb[i & 1]; fd.part = vpart_.p;
+            fd.red = red_.p; fd.Dif = rec_dif_ ? Dif_.p : nullptr; fd.nparts = nbv_;
+        }
+        edge_sweep(0, E_, cb[0], "edge_sweep", 0, 0, &fd);
+        vertex_sweep(0, nbv_, cb[i & 1], "vertex_sweep");
+        if (i == n - 1) {
+            FuseDecide<real> fl{cb[i & 1], cb[0], vpart_.p, red_.p, rec_dif_ ? Dif_.p : nullptr,
+                                nbv_};
+            k_decide_fused<real><<<1, kBlock, 0, s>>>(fl);
+        }
+        PFDR_HIP(hipGetLastError());
+        return;
+    }
     if (overlap_) {
         // pull ghosts (comm) || interior edges; boundary edges; push (comm)
         // || interior vertices; boundary vertices
@@ -1086,7 +1124,7 @@ void QuadSession<real>::plan_overlap() {
 template <typename real>
 void QuadSession<real>::run_bodies(int n) {
     if (!graphs_ok_ || prof.on) {
-        for (int i = 0; i < n; i++) body();
+        for (int i = 0; i < n; i++) body(i, n);
         return;
     }
     auto it = graphs_.find(n);
@@ -1095,7 +1133,7 @@ void QuadSession<real>::run_bodies(int n) {
         hipGraphExec_t ge = nullptr;
         PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         try {
-            for (int i = 0; i < n; i++) body();
+            for (int i = 0; i < n; i++) body(i, n);
         } catch (...) {
             (void)hipStreamEndCapture(stream, &g);
             if (g) (void)hipGraphDestroy(g);

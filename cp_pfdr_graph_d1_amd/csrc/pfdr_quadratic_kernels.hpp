@@ -961,6 +961,104 @@ __device__ __forceinline__ void edge_full(const R2<real> &pu, const R2<real> &pv
     ov = wv * zv;
 }
 
+// iterate evolution and loop control (ref :514-529, :424-429, :447-460);
+// red[0..1] = (sum (X - X_)^2, sum X^2) over all ranks
+template <typename real>
+__device__ __forceinline__ void decide_step(Ctrl<real> *ctrl, real num, real den,
+                                            real *__restrict__ Dif, int track) {
+    int it = ctrl->it;
+    if (track) {
+        const real eps = ctrl->eps;
+        const real dif = (den > eps) ? num / den : num / eps;
+        ctrl->dif = dif;
+        if (Dif) Dif[it] = dif;
+    }
+    it++;
+    ctrl->it = it;
+    const real dif = ctrl->dif;
+    if (it >= ctrl->itMax || dif < ctrl->difTol) {
+        ctrl->stop = 1;
+        ctrl->halt = 1;
+    } else if (dif < ctrl->difRcd) {
+        ctrl->recond = 1;
+        ctrl->halt = 1;
+    }
+}
+
+// Loop control of small single-GPU graphs (at most kFuseBlocks vertex
+// blocks, dif tracked, no objective record), two launches per iteration
+// instead of three (the sweeps' FD = true instances):
+//  * the decision on iteration t is taken by the edge sweep of iteration
+//    t + 1: EVERY workgroup sums the vertex sweep's partials with
+//    k_reduce_decide's loop and tree and runs decide_step on its own copy
+//    of the control block `src`; the workgroup of logical block 0 alone
+//    writes the result (and Dif, red) to `dst`, a DIFFERENT control block
+//    (the readers of this launch never see the update; the host alternates
+//    the two blocks), and every workgroup skips its stores when the
+//    decision halts -- so the iterates, iteration counts and Dif are those
+//    of the three-launch loop, bit for bit;
+//  * the halt flag (or the decision) is tested before the sweep's first
+//    store instead of ahead of everything: one dependent round trip less at
+//    the start of each launch (a halted launch then reads its operands
+//    once, which only small launches can afford).
+// The partials are loaded into registers before the sweep's own loads and
+// added only after them, so their latency hides under the edge streams.
+constexpr int kFuseBlocks = 1024;
+constexpr int kFusePer = kFuseBlocks / kBlock;  // partial pairs per lane
+
+template <typename real>
+struct FuseDecide {
+    const Ctrl<real> *src;  // null: no decision in this launch (halt of `ctrl` tested late)
+    Ctrl<real> *dst;
+    const real *part;       // 2 per vertex block
+    real *red, *Dif;
+    int nparts;             // <= kFuseBlocks
+};
+
+template <typename real>
+struct FdRegs {
+    real a[kFusePer], b[kFusePer];
+    Ctrl<real> c;  // src, loaded with the partials (no dependent load later)
+};
+
+// a lane's operands of k_reduce_decide's fixed-order loop (i = tid + k kBlock)
+template <typename real>
+__device__ __forceinline__ void fd_load(const FuseDecide<real> &fd, FdRegs<real> &r) {
+    r.c = *fd.src;
+#pragma unroll
+    for (int k = 0; k < kFusePer; k++) {
+        const int i = threadIdx.x + k * kBlock;
+        r.a[k] = i < fd.nparts ? fd.part[2 * i] : real(0);
+        r.b[k] = i < fd.nparts ? fd.part[2 * i + 1] : real(0);
+    }
+}
+
+// the loop's adds, block sums (k_reduce_decide's tree), the decision on a
+// copy of src, the writer's stores; returns the (block-uniform) halt flag.
+// Every lane calls.
+template <typename real>
+__device__ __forceinline__ int fd_decide(const FuseDecide<real> &fd, const FdRegs<real> &r,
+                                         bool writer, real (*red)[kBlock / kWave], int *s_halt) {
+    real a = real(0), b = real(0);
+#pragma unroll
+    for (int k = 0; k < kFusePer; k++)
+        if ((int)threadIdx.x + k * kBlock < fd.nparts) { a += r.a[k]; b += r.b[k]; }
+    a = block_sum(a, red[0]);
+    b = block_sum(b, red[1]);
+    if (threadIdx.x == 0) {
+        Ctrl<real> c = r.c;
+        const int was = c.halt;
+        if (!was) decide_step(&c, a, b, writer ? fd.Dif : nullptr, 1);
+        if (writer) {
+            *fd.dst = c;
+            if (!was) { fd.red[0] = a; fd.red[1] = b; }
+        }
+        *s_halt = c.halt;
+    }
+    __syncthreads();
+    return *s_halt;
+}
+
 // One or two edge ranges of one launch: logical blocks [0, nb0) sweep
 // [b0, e0), the others [b1, e1) (a partitioned session's two boundary
 // ranges, before and after the interior run, in a single launch)
@@ -1027,16 +1125,27 @@ __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int 
     }
 }
 
-template <typename real>
+template <typename real, bool FD>
 __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
-    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg) {
-    if (ctrl && ctrl->halt) return;
+    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg, FuseDecide<real> fd) {
+    if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;
+    if (FD) {
+        __shared__ real red[2][kBlock / kWave];
+        __shared__ int s_halt;
+        if (fd.src) {
+            FdRegs<real> r;
+            fd_load(fd, r);
+            if (fd_decide(fd, r, blk == 0, red, &s_halt)) return;
+        } else if (ctrl && ctrl->halt) {
+            return;
+        }
+    }
     long ebeg, eend;
     rg.pick(blk, ebeg, eend);
     const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
@@ -1055,21 +1164,31 @@ template <typename real> struct USpan { static constexpr int v = 1024; };
 // Occupancy: 86 VGPRs (f32) = 5 waves/SIMD.  Forcing 6 (80 VGPRs) or 7 (68)
 // waves was slower on the headline (0.442 -> 0.450 / 0.462 ms): more loads
 // in flight per SIMD only adds cache pressure here.
-template <typename real>
+template <typename real, bool FD>
 __global__ __launch_bounds__(256) void k_edge_sweep_us(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
     const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
     const real *__restrict__ La_d1, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
-    int nb, int xcd, ERange rg) {
-    if (ctrl && ctrl->halt) return;
+    int nb, int xcd, ERange rg, FuseDecide<real> fd) {
+    if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int CAP = USpan<real>::v;
     __shared__ int s_ptr[CAP + 1];
     __shared__ R2<real> s_xp[CAP];
     __shared__ R2<real> s_gi[CAP];
+    __shared__ real s_red[2][kBlock / kWave];
+    __shared__ int s_halt;
     int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
+    const bool writer = blk == 0;
+    // loop control (FD): its loads in flight under the edge streams
+    FdRegs<real> fr;
+    int halt = 0;
+    if (FD) {
+        if (fd.src) fd_load(fd, fr);
+        else if (ctrl) halt = ctrl->halt;
+    }
     long ebeg, eend;
     rg.pick(blk, ebeg, eend);
     const int tid = threadIdx.x;
@@ -1104,6 +1223,8 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
         }
     }
     __syncthreads();
+    if (FD && fd.src) halt = fd_decide(fd, fr, writer, s_red, &s_halt);
+    if (FD && halt) return;  // block-uniform
     if (e0 >= eend) return;
     if (full) {
         if (staged) {
@@ -1173,6 +1294,7 @@ struct VArgs {
     int track;      // iterate-evolution partials
     real *part;     // 2 per block
     const Ctrl<real> *ctrl;
+    int late;       // halt of ctrl tested after the sum, before the stores (small launches)
 };
 
 // DR average (ordered), prox on the iterate, evolution partials, next
@@ -1252,7 +1374,8 @@ __device__ __forceinline__ void vertex_finish(const VArgs<real> &a, int v, real 
 // one vertex block `blk` (all 256 lanes of the calling block take part)
 template <typename real, int GB>
 __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
-                                             real (*red)[kBlock / kWave], int *scan) {
+                                             real (*red)[kBlock / kWave], int *scan,
+                                             int halt = 0) {
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
@@ -1261,6 +1384,7 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
         x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+    if (halt) return;  // block-uniform (a.late)
     real num, den;
     vertex_finish(a, v, x, o, num, den);
     if (a.track) {
@@ -1275,14 +1399,21 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
 
 template <typename real, int GB>
 __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs<real> a) {
-    if (a.ctrl && a.ctrl->halt) return;
+    int halt = 0;
+    if (a.ctrl) {
+        if (!a.late) {
+            if (a.ctrl->halt) return;
+        } else {
+            halt = a.ctrl->halt;  // waited for only after the sum's loads
+        }
+    }
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
     __shared__ int scan[kBlock / kWave];
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;
-    vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan);
+    vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan, halt);
 }
 
 // fixed-order sum of per-block partial pairs into out[0..1]
@@ -1298,30 +1429,6 @@ __global__ __launch_bounds__(256) void k_reduce_pairs(int nparts, const real *__
     a = block_sum(a, red[0]);
     b = block_sum(b, red[1]);
     if (threadIdx.x == 0) { out[0] = a; out[stride] = b; }
-}
-
-// iterate evolution and loop control (ref :514-529, :424-429, :447-460);
-// red[0..1] = (sum (X - X_)^2, sum X^2) over all ranks
-template <typename real>
-__device__ __forceinline__ void decide_step(Ctrl<real> *ctrl, real num, real den,
-                                            real *__restrict__ Dif, int track) {
-    int it = ctrl->it;
-    if (track) {
-        const real eps = ctrl->eps;
-        const real dif = (den > eps) ? num / den : num / eps;
-        ctrl->dif = dif;
-        if (Dif) Dif[it] = dif;
-    }
-    it++;
-    ctrl->it = it;
-    const real dif = ctrl->dif;
-    if (it >= ctrl->itMax || dif < ctrl->difTol) {
-        ctrl->stop = 1;
-        ctrl->halt = 1;
-    } else if (dif < ctrl->difRcd) {
-        ctrl->recond = 1;
-        ctrl->halt = 1;
-    }
 }
 
 // single GPU: the fixed-order partial sums of k_reduce_pairs and the
@@ -1541,6 +1648,17 @@ __global__ __launch_bounds__(256) void k_coop_iterate(CoopArgs<real> t) {
         __syncthreads();
         if (c.halt) break;  // the same decision in every workgroup
     }
+}
+
+// the decision closing a chunk of fused bodies (FuseDecide): one workgroup,
+// k_reduce_decide's loop and tree, from fd.src into fd.dst
+template <typename real>
+__global__ __launch_bounds__(256) void k_decide_fused(FuseDecide<real> fd) {
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int s_halt;
+    FdRegs<real> r;
+    fd_load(fd, r);
+    (void)fd_decide(fd, r, true, red, &s_halt);
 }
 
 template <typename real>

@@ -188,8 +188,10 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
 /* Session facts by name: "reordered" (1 when the internal locality
  * relabelling is active), "device_bytes", "split_blocks", "ustaged",
  * "symv", "tiny", "coop" (workgroups of the persistent mid-size-graph
- * launch, 0 when off), "dense_exact" (1: the dense products run in the
- * reference's sequential order, bit-exact; small single-GPU problems). */
+ * launch, 0 when off), "fused" (1: the loop decision of a small graph is
+ * taken inside the next edge sweep, two launches per iteration),
+ * "dense_exact" (1: the dense products run in the reference's sequential
+ * order, bit-exact; small single-GPU problems). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 
