@@ -269,9 +269,18 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (xv && atoi(xv) >= 2) xcd_v_ = atoi(xv);
         const char *g = getenv("PFDR_GB");  // 8 (default), 4 or 16
         if (g && (atoi(g) == 16 || atoi(g) == 4)) gb_ = atoi(g);
-        // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us)
+        // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us).
+        // PFDR_USTAGE = 0 / 1 forces it; by default it is taken for graphs of
+        // at least 4 edges per vertex and for small (latency-bound) graphs.
+        // Measured (r2zf, paired, ms per edge sweep): headline 6 edges per
+        // vertex 0.457 staged vs 0.472, shuffled headline 0.468 vs 0.500, C1
+        // (130K edges) 0.008-0.010 vs 0.019; but 3 edges per vertex C2 0.450
+        // vs 0.394 and C5 6.55 vs 5.81 -- with few edges per u end the block's
+        // staging barrier and search cost more than the Eu stream and the
+        // (cache-served) u-end gathers they replace.
         const char *u = getenv("PFDR_USTAGE");
-        us_ = !(u && u[0] == '0');
+        if (u && (u[0] == '0' || u[0] == '1')) us_ = u[0] == '1';
+        else us_ = E_ >= 4L * V_ || E_ < (1L << 22);
         // amplitude sum: workgroup binade scan (default) or the one-lane loop
         const char *q = getenv("PFDR_SEQSUM");
         seq_lane_ = q && strcmp(q, "lane") == 0;
