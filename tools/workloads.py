@@ -150,11 +150,12 @@ class C2(Workload):
     grid; weak: one 256^3 per GPU)"""
     name = "c2"
     metric = "PFDR_graph_quadratic_d1_l1<float> 256^3 6-NN: Medge-updates/s"
+    SHAPE = (256, 256, 256)
 
     def inputs(self, rank, world, strong=True):
-        g, V_all, v0, v1, Eu, Ev = _grid_slab((256, 256, 256), rank, world, 6, strong=strong)
+        g, V_all, v0, v1, Eu, Ev = _grid_slab(self.SHAPE, rank, world, 6, strong=strong)
         V = v1 - v0
-        Y = pfdr.gen_piecewise(256, V_all, 2, np.float32, 0.2, (v0, v1))
+        Y = pfdr.gen_piecewise(self.SHAPE[0], V_all, 2, np.float32, 0.2, (v0, v1))
         E = Eu.size
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
                   Y=Y, La_l1=np.full(V, 0.01, np.float32), rho=1.5, condMin=1e-3)
@@ -240,13 +241,14 @@ class C4(Workload):
     kind = pfdr.PFDR_KIND_SIMPLEX
     dominant = "sx_edge_sweep"
     K = 10
+    SIDE = 2236
     edge_bytes = 8 + 9 * 10 * 4
     vertex_bytes = 10 * 4 * 4
     steps = 20
 
     def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
-        n = 2236
+        n = self.SIDE
         if strong:
             g = (n, n)
             r0, r1 = (n * rank) // world, (n * (rank + 1)) // world
@@ -277,11 +279,12 @@ class C5(Workload):
     scaling = "strong"
     vertex_bytes = 16
     steps = 10
+    SHAPE = (640, 640, 640)
 
     def inputs(self, rank, world, strong=True):
-        g, V_all, v0, v1, Eu, Ev = _grid_slab((640, 640, 640), rank, world, 6, strong=True)
+        g, V_all, v0, v1, Eu, Ev = _grid_slab(self.SHAPE, rank, world, 6, strong=True)
         V = v1 - v0
-        Y = pfdr.gen_piecewise(640, V_all, 5, np.float32, 0.2, (v0, v1))
+        Y = pfdr.gen_piecewise(self.SHAPE[0], V_all, 5, np.float32, 0.2, (v0, v1))
         E = Eu.size
         e0 = pfdr.grid_edge_count(g, 6, v0)
         kw = dict(Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.1, np.float32), X0=np.zeros(V, np.float32),
