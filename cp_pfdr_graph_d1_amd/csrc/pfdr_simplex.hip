@@ -624,7 +624,7 @@ struct SxVArgs {
     const real *wz, *Ga, *GaQ, *Q;
     const real *Zu, *Zv;  // !WZ: contributions W*Z formed in the sweep from
     const real *A1, *La_d1;  // the factors of W (sx_a) and the vertex's invAux
-    const SxR2<real> *GI;
+    const real *invAux;      // (read alone: GI's Ga half is the edge sweep's)
     real *P, *FP, *lab;
     int track;
     real *part;
@@ -647,7 +647,7 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     const bool live = vl < vb && v < a.V;
     const long i = v * K + k;
     if (live) {
-        const real inv = WZ ? real(0) : a.GI[i].y;  // 1/Aux of this (v, k)
+        const real inv = WZ ? real(0) : a.invAux[i];  // 1/Aux of this (v, k)
         const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
         const real *__restrict__ wz = a.wz;
         real s = real(0);
@@ -719,7 +719,8 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
             dif += d;
         }
         a.P[i] = p;
-        a.FP[i] = sx_explicit(a.c, p, a.GaQ[i], a.Q[i]);
+        // Q enters the quadratic loss's step only (no load otherwise)
+        a.FP[i] = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
     }
     if (a.track) {
         dif = wave_sum(dif);
@@ -1227,7 +1228,7 @@ void SimplexSession<real>::body() {
         a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.FP = FP_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
-        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.GI = GI_.p;
+        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
         if (sx_nt_ == 256) {
