@@ -16,8 +16,12 @@
 //                                                               :567-587
 //     (K > 64: k_sx_average then k_sx_project, the same two halves)
 //     k_sx_finalize     : stop / recondition flags (when tracked)
-// Layouts: P, Q, Ga, GaQ, FP are K-by-V (index v*K + k) as in the reference;
-// edge state is K-by-E; the DR contributions are wz[side][e][k].
+// Layouts: P, Q, Ga, GaQ are K-by-V (index v*K + k) as in the reference; the
+// explicit step FP lives next to P in (P, FP) pairs PF[v*K + k] and the
+// splitting-weight factors in (Ga, 1/Aux) pairs GI[v*K + k], so the edge
+// sweep (bound by its texture-address work, not by bytes) gathers each end
+// with one 16-byte access per operand pair; edge state is K-by-E; the DR
+// contributions are wz[side][e][k].
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -400,10 +404,13 @@ __global__ void k_sx_explicit(long VK, SxConst<real> c,
                               const real *__restrict__ P,
                               const real *__restrict__ GaQ,
                               const real *__restrict__ Q,
-                              real *__restrict__ FP) {
+                              SxR2<real> *__restrict__ PF) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= VK) return;
-    FP[i] = sx_explicit(c, P[i], GaQ[i], Q[i]);
+    SxR2<real> q;
+    q.x = P[i];
+    q.y = sx_explicit(c, q.x, GaQ[i], Q[i]);
+    PF[i] = q;
 }
 
 // labels of the maximum-likelihood class (ref :447-466)
@@ -474,8 +481,8 @@ __device__ __forceinline__ void sx_st(T *p, const Pk<T, N> &x) { *reinterpret_ca
 template <typename real, int L>
 __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     long EK, SxConst<real> c, const int *__restrict__ Eu,
-    const int *__restrict__ Ev, const real *__restrict__ FP,
-    const real *__restrict__ P, real *__restrict__ Zu, real *__restrict__ Zv,
+    const int *__restrict__ Ev, const SxR2<real> *__restrict__ PF,
+    real *__restrict__ Zu, real *__restrict__ Zv,
     const real *__restrict__ A1, const real *__restrict__ La_d1,
     const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
     const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
@@ -498,8 +505,15 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     }
     const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
     Pk<real, L> zu = sx_ld<real, L>(Zu + i), zv = sx_ld<real, L>(Zv + i);
-    const Pk<real, L> fpu = sx_ld<real, L>(FP + u), fpv = sx_ld<real, L>(FP + v);
-    const Pk<real, L> pu = sx_ld<real, L>(P + u), pv = sx_ld<real, L>(P + v);
+    // (P, explicit step) of both entries in one access per end: the sweep
+    // is bound by its texture-address work (profiles/r2/r2zj_c4_counters)
+    const Pk<SxR2<real>, L> qu = sx_ld<SxR2<real>, L>(PF + u), qv = sx_ld<SxR2<real>, L>(PF + v);
+    Pk<real, L> fpu, fpv, pu, pv;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+        pu.v[j] = qu.v[j].x; fpu.v[j] = qu.v[j].y;
+        pv.v[j] = qv.v[j].x; fpv.v[j] = qv.v[j].y;
+    }
     // splitting weights from their factors (prox weights: non-linear losses
     // without stored ones; contributions: only when this sweep stores W*Z)
     real wsu[L], wsv[L], gpu[L], gpv[L], la = real(0);
@@ -507,10 +521,15 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     for (int j = 0; j < L; j++) { wsu[j] = wsv[j] = real(0); gpu[j] = gpv[j] = real(1); }
     if ((c.loss != LOSS_LINEAR && !Th) || wz) {
         la = La_d1[e];
+        // (Ga, 1/Aux) of both entries of a pair in one access at each end
+        // (u, v even: K is even when L = 2) -- the sweep is bound by its
+        // texture-address work, not by bytes (profiles/r2/r2zj_c4_counters)
+        const Pk<SxR2<real>, L> gpu_ = sx_ld<SxR2<real>, L>(GI + u);
+        const Pk<SxR2<real>, L> gpv_ = sx_ld<SxR2<real>, L>(GI + v);
 #pragma unroll
         for (int j = 0; j < L; j++) {
             const real an = A1 ? A1[i + j] : la;
-            const SxR2<real> gu = GI[u + j], gv = GI[v + j];
+            const SxR2<real> gu = gpu_.v[j], gv = gpv_.v[j];
             wsu[j] = an * gu.y;
             wsv[j] = an * gv.y;
             gpu[j] = gu.x;
@@ -560,7 +579,8 @@ struct SxProjArgs {
     int V;
     SxConst<real> c;
     const real *Pavg, *Ga, *GaQ, *Q;
-    real *P, *FP, *lab;
+    real *P, *lab;
+    SxR2<real> *PF;  // (P, explicit step) pairs: the edge sweep's operands
     int track;   // 0 none, 1 l1 evolution, 2 label changes
     real *part;
     const Ctrl<real> *ctrl;
@@ -594,7 +614,10 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
         for (int k = 0; k < K; k++) {
             const real p = x[k];
             a.P[b + k] = p;
-            a.FP[b + k] = sx_explicit(a.c, p, a.GaQ[b + k], a.Q[b + k]);
+            SxR2<real> q;
+            q.x = p;
+            q.y = sx_explicit(a.c, p, a.GaQ[b + k], a.Q[b + k]);
+            a.PF[b + k] = q;
         }
     }
     if (a.track) {
@@ -625,7 +648,8 @@ struct SxVArgs {
     const real *Zu, *Zv;  // !WZ: contributions W*Z formed in the sweep from
     const real *A1, *La_d1;  // the factors of W (sx_a) and the vertex's invAux
     const real *invAux;      // (read alone: GI's Ga half is the edge sweep's)
-    real *P, *FP, *lab;
+    real *P, *lab;
+    SxR2<real> *PF;          // (P, explicit step) pairs: the edge sweep's operands
     int track;
     real *part;
     const Ctrl<real> *ctrl;
@@ -720,7 +744,10 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
         }
         a.P[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
-        a.FP[i] = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
+        SxR2<real> q;
+        q.x = p;
+        q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
+        a.PF[i] = q;
     }
     if (a.track) {
         dif = wave_sum(dif);
@@ -961,7 +988,10 @@ class SimplexSession final : public SessionBase {
     bool rec_obj_, rec_dif_;
     int track_;  // 0, 1 (l1 evolution), 2 (labels)
     DevBuf<int> Eu_, Ev_;
-    DevBuf<real> La_d1_, La_f_, Q_, P_, FP_, Pavg_, Ga_, GaQ_, invAux_, lab_;
+    DevBuf<real> La_d1_, La_f_, Q_, P_, Pavg_, Ga_, GaQ_, invAux_, lab_;
+    // (P, explicit step) pairs per (v, k), ghosts included: written with P
+    // by the vertex sweep, one access per edge end in the edge sweep
+    DevBuf<SxR2<real>> PF_;
     DevBuf<real> Zu_, Zv_, A1_, wz_, part_, opart_, Obj_, Dif_;
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
     // stored prox weights/thresholds of the non-linear losses (else
@@ -995,6 +1025,9 @@ class SimplexSession final : public SessionBase {
     // K-wide ghost rows of a [Vg][K] array from their owners
     void pullK(DevBuf<real> &b) {
         if (halo_) halo_->pull(b.p, K_ * (int)sizeof(real), stream);
+    }
+    void pullPF() {
+        if (halo_) halo_->pull(PF_.p, K_ * (int)sizeof(SxR2<real>), stream);
     }
     void push_wz();
 };
@@ -1088,7 +1121,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     } else {
         Pavg_.alloc(VK_);
     }
-    FP_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
+    PF_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
     const size_t EKn = EK_ ? EK_ : 1;
     // Zv carries the received contributions (the senders' W*Z) after its
     // E*K entries for the fused vertex sweep
@@ -1128,19 +1161,19 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
 
     if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, Zv_.p);
     precondition(true);
-    k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
+    k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
     PFDR_HIP(hipGetLastError());
-    pullK(FP_);
+    pullPF();
     if (rec_obj_) objective();
     PFDR_HIP(hipStreamSynchronize(s));
     pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
-    for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &FP_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
+    for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
                             &Dif_})
         device_bytes += (int64_t)(b->n * sizeof(real));
-    device_bytes += (int64_t)(GI_.n * sizeof(SxR2<real>));
+    device_bytes += (int64_t)((GI_.n + PF_.n) * sizeof(SxR2<real>));
 }
 
 // ref :64-370
@@ -1206,13 +1239,13 @@ void SimplexSession<real>::body() {
         const int nb = grid_for(EK_ / pair);
         const int xm = xcd_fit(nb, sx_xcd_e_);
         if (pair == 2)
-            k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+            k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
                                                                rho_, c, nb, xm);
         else
-            k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, FP_.p, P_.p,
+            k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                (vb_ && !sx_wz_) ? nullptr : wz_.p,
@@ -1225,7 +1258,7 @@ void SimplexSession<real>::body() {
     if (vb_) {
         SxVArgs<real> a{};
         a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
-        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.FP = FP_.p;
+        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
@@ -1246,14 +1279,14 @@ void SimplexSession<real>::body() {
         }
         SxProjArgs<real> a{};
         a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
-        a.P = P_.p; a.FP = FP_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        a.P = P_.p; a.PF = PF_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         ProfScope ps(prof, "sx_project", s);
         launch_project(a);
     }
     if (halo_) {
         ProfScope ps(prof, "halo_pull", s);
         pullK(P_);
-        pullK(FP_);
+        pullPF();
     }
     const int nparts = vb_ ? nbs_ : nbv_;
     if (gated && halo_) {
@@ -1307,9 +1340,9 @@ int SimplexSession<real>::run(int iters) {
             } else if (hctrl_->recond) {
                 if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
                 precondition(false);
-                k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, FP_.p);
+                k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
                 PFDR_HIP(hipGetLastError());
-                pullK(FP_);
+                pullPF();
                 difRcd_ *= real(0.1);  // ref :563
                 hctrl_->difRcd = difRcd_;
                 hctrl_->recond = 0;

@@ -1,5 +1,5 @@
 set -u
-cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r2zi; mkdir -p $O
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/${TAG:-r2zi}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -k "simplex or sx or partition or dropin" -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do
