@@ -224,6 +224,18 @@ class QuadSession final : public SessionBase {
     // decision lands in ctrl_.  PFDR_FUSE = 0 off.
     bool fuse_ = false;
     DevBuf<Ctrl<real>> ctrl2_;
+    // fused sessions whose vertex blocks have at most kPadPer * kBlock CSR
+    // entries: the edge sweep stores each contribution at its slot sl_[2e +
+    // side] of its block's list in wzp_ (stride pad_nmax_), and the vertex
+    // sweep (k_vertex_sweep_pad) stages its block's list with one dependent
+    // round trip instead of three.  PFDR_PAD = 0 off.
+    bool pad_ = false;
+    static constexpr int kPadBlocks = 512;
+    int pad_nmax_ = 0;
+    DevBuf<int> sl_;
+    DevBuf<real> wzp_;
+    void plan_pad();
+    PadOut<real> pad_out() const { return PadOut<real>{pad_ ? sl_.p : nullptr, wzp_.p}; }
     template <int EPI> void col_product(ColArgs<real> ca);
     DevBuf<real> spart_;
     void plan_symv();
@@ -463,8 +475,43 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
                 (mode_ == A_IDENT || mode_ == A_DIAG) && nbv_ <= kFuseBlocks && E_ > 0;
         if (fuse_) ctrl2_.alloc(1);
         fused = fuse_ ? 1 : 0;
+        if (fuse_) plan_pad();
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
+    acc(sl_.n * 4 + wzp_.n * sizeof(real));
+}
+
+template <typename real>
+void QuadSession<real>::plan_pad() {
+    // by default up to kPadBlocks vertex blocks: at 1024 blocks (512^2 grid,
+    // f32) the scattered contribution stores cost more than the round trips
+    // they save (profiles/r2/r2zp_exp_pad.log, r2zq_exp_pad.log); PFDR_PAD = 0 off, 1 whole range
+    const char *e = getenv("PFDR_PAD");
+    if ((e && e[0] == '0') || halo_ || !E_) return;
+    if (!(e && e[0] == '1') && nbv_ > kPadBlocks) return;
+    hipStream_t s = stream;
+    int *hm = static_cast<int *>(pinned_small_get());
+    struct Put {
+        hipStream_t s;
+        int *h;
+        ~Put() { (void)hipStreamSynchronize(s); pinned_small_put(h); }
+    } put{s, hm};
+    DevBuf<int> dm(1);
+    PFDR_HIP(hipMemsetAsync(dm.p, 0, sizeof(int), s));
+    k_pad_nmax<<<grid_for(nbv_), kBlock, 0, s>>>(V_, nbv_, inc_.ptr.p, dm.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipMemcpyAsync(hm, dm.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    const int nmax = std::max(kBlock, (*hm + kBlock - 1) / kBlock * kBlock);
+    if (nmax > kPadPer * kBlock) return;
+    sl_.alloc(2 * (size_t)E_);
+    wzp_.alloc((size_t)nbv_ * nmax);
+    PFDR_HIP(hipMemsetAsync(wzp_.p, 0, wzp_.n * sizeof(real), s));
+    k_pad_slots<<<nbv_, kBlock, 0, s>>>(V_, E_, inc_.ptr.p, inc_.idx.p, nmax, sl_.p);
+    PFDR_HIP(hipGetLastError());
+    pad_nmax_ = nmax;
+    pad_ = true;
+    padded = 1;
 }
 
 // endpoints (local ids), partition plan, incidence CSR keyed by global edge id
@@ -863,11 +910,11 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
-                               La_d1_.p, wz_.p, rho_, c, nb, xm, rg, f);
+                               La_d1_.p, wz_.p, rho_, c, nb, xm, rg, f, pad_out());
     } else {
         auto k = fuse_ ? k_edge_sweep<real, true> : k_edge_sweep<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p, La_d1_.p, wz_.p,
-                               rho_, c, nb, xm, rg, f);
+                               rho_, c, nb, xm, rg, f, pad_out());
     }
 }
 
@@ -954,6 +1001,10 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
         a.xcd = xcd_fit(a.nb, xcd_v_);
     }
     ProfScope ps(prof, name, s);
+    if (pad_ && bend2 <= bbeg2) {
+        k_vertex_sweep_pad<real><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a, wzp_.p, pad_nmax_);
+        return;
+    }
     if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
     else if (gb_ == 4) k_vertex_sweep<real, 4><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
     else k_vertex_sweep<real, 16><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);

@@ -1071,6 +1071,16 @@ struct ERange {
     }
 };
 
+// Contributions of a small graph stored where its vertex sweep reads them
+// (k_vertex_sweep_pad): the contribution of (e, side) goes to wzp[sl[2e +
+// side]], the slot of that entry in its vertex block's CSR list, each block's
+// list at a fixed stride.  Null sl: side-major wz as below.
+template <typename real>
+struct PadOut {
+    const int *sl;
+    real *wzp;
+};
+
 // Edge sweep over the edges [ebeg, eend) (ebeg a multiple of the lane
 // width); writes the DR contributions W*Z side-major: wz[e] (u end),
 // wz[E + e] (v end), so the u-side run of a vertex is contiguous.  Streams
@@ -1083,12 +1093,15 @@ template <typename real>
 __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int *__restrict__ Eu,
                                           const int *__restrict__ Ev, const R2<real> *xp,
                                           real *Z2, const real *A1, real cw, const R2<real> *gi,
-                                          const real *__restrict__ La_d1, real *wz, real rho) {
+                                          const real *__restrict__ La_d1, real *wz, real rho,
+                                          PadOut<real> pd = PadOut<real>{nullptr, nullptr}) {
     constexpr int EPT = Vec<real>::kPer16B;
     if (e0 >= eend) return;
     if (e0 + EPT <= eend) {
         const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
         const Pk<int, EPT> iv = ldv<int, EPT>(Ev + e0);
+        Pk<int, 2 * EPT> sv{};
+        if (pd.sl) sv = ldv<int, 2 * EPT>(pd.sl + 2 * e0);
         R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
@@ -1109,8 +1122,16 @@ __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int 
             edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
                             z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
         stv<real, 2 * EPT>(Z2 + 2 * e0, z);
-        stv<real, EPT>(wz + e0, ou);
-        stv<real, EPT>(wz + E + e0, ov);
+        if (pd.sl) {
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                pd.wzp[sv.v[2 * j]] = ou.v[j];
+                pd.wzp[sv.v[2 * j + 1]] = ov.v[j];
+            }
+        } else {
+            stv<real, EPT>(wz + e0, ou);
+            stv<real, EPT>(wz + E + e0, ov);
+        }
     } else {
         for (long e = e0; e < eend; e++) {
             const int u = Eu[e], v = Ev[e];
@@ -1119,8 +1140,13 @@ __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int 
                             zv, ou, ov, rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
-            wz[e] = ou;
-            wz[E + e] = ov;
+            if (pd.sl) {
+                pd.wzp[pd.sl[2 * e]] = ou;
+                pd.wzp[pd.sl[2 * e + 1]] = ov;
+            } else {
+                wz[e] = ou;
+                wz[E + e] = ov;
+            }
         }
     }
 }
@@ -1130,9 +1156,11 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
-    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg, FuseDecide<real> fd) {
+    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg, FuseDecide<real> fd,
+    PadOut<real> pdx) {
     if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
+    const PadOut<real> pd = FD ? pdx : PadOut<real>{nullptr, nullptr};
     int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;
     if (FD) {
@@ -1149,7 +1177,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     long ebeg, eend;
     rg.pick(blk, ebeg, eend);
     const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
-    edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, wz, rho);
+    edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, wz, rho, pd);
 }
 
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
@@ -1170,10 +1198,11 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
     const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
     const real *__restrict__ La_d1, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
-    int nb, int xcd, ERange rg, FuseDecide<real> fd) {
+    int nb, int xcd, ERange rg, FuseDecide<real> fd, PadOut<real> pdx) {
     if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int CAP = USpan<real>::v;
+    const PadOut<real> pd = FD ? pdx : PadOut<real>{nullptr, nullptr};
     __shared__ int s_ptr[CAP + 1];
     __shared__ R2<real> s_xp[CAP];
     __shared__ R2<real> s_gi[CAP];
@@ -1203,12 +1232,14 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     Pk<int, EPT> iv{};
     Pk<real, 2 * EPT> z{};
     Pk<real, EPT> la{}, a{};
+    Pk<int, 2 * EPT> sv{};
     R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
     if (full) {
         iv = ldv<int, EPT>(Ev + e0);
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
         la = ldv<real, EPT>(La_d1 + e0);
         if (A1) a = ldv<real, EPT>(A1 + e0);
+        if (pd.sl) sv = ldv<int, 2 * EPT>(pd.sl + 2 * e0);
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             pv[j] = xp[iv.v[j]];
@@ -1258,8 +1289,16 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
             edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
                             z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
         stv<real, 2 * EPT>(Z2 + 2 * e0, z);
-        stv<real, EPT>(wz + e0, ou);
-        stv<real, EPT>(wz + E + e0, ov);
+        if (pd.sl) {
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                pd.wzp[sv.v[2 * j]] = ou.v[j];
+                pd.wzp[sv.v[2 * j + 1]] = ov.v[j];
+            }
+        } else {
+            stv<real, EPT>(wz + e0, ou);
+            stv<real, EPT>(wz + E + e0, ov);
+        }
     } else {
         for (long e = e0; e < eend; e++) {
             const int u = Eu[e], v = Ev[e];
@@ -1268,8 +1307,13 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
                             zv, ou, ov, rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
-            wz[e] = ou;
-            wz[E + e] = ov;
+            if (pd.sl) {
+                pd.wzp[pd.sl[2 * e]] = ou;
+                pd.wzp[pd.sl[2 * e + 1]] = ov;
+            } else {
+                wz[e] = ou;
+                wz[E + e] = ov;
+            }
         }
     }
 }
@@ -1414,6 +1458,83 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan, halt);
+}
+
+// Vertex sweep of a small graph (the fused-decision range) whose edge sweep
+// stores the contributions block by block (PadOut): vertex block b's CSR
+// entries are wzp[b * nmax ...) in CSR order, so the block stages them with
+// loads whose addresses depend on nothing loaded, issued together with the
+// per-vertex operands and the CSR pointers -- one dependent round trip
+// instead of three (pointers -> other-entry addresses -> gathered
+// contributions), which is what a latency-bound launch pays for.  Each lane
+// then adds its vertex's entries in CSR order from LDS (the sums of
+// split_sum / gather_sum, bit for bit) and finishes as vertex_block does.
+constexpr int kPadPer = 16;  // staged entries per lane: nmax <= kPadPer * kBlock
+template <typename real>
+__global__ __launch_bounds__(256) void k_vertex_sweep_pad(VArgs<real> a,
+                                                          const real *__restrict__ wzp, int nmax) {
+    static_assert(kPadPer * kBlock <= GatherCap<real>::v, "staged list fits the LDS chunk");
+    int halt = 0;
+    if (a.ctrl) {
+        if (!a.late) {
+            if (a.ctrl->halt) return;
+        } else {
+            halt = a.ctrl->halt;  // waited for only after the sum's loads
+        }
+    }
+    __shared__ real lds[kPadPer * kBlock];
+    __shared__ real red[2][kBlock / kWave];
+    const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (lb >= a.nb) return;
+    const int blk = a.bbeg + lb;
+    const int tid = threadIdx.x, v0 = blk * kBlock, v = v0 + tid;
+    const VOps<real> o = vertex_ops(a, v);
+    const int p0 = a.ptr[v0];
+    const int my0 = v < a.V ? a.ptr[v] : 0, my1 = v < a.V ? a.ptr[v + 1] : 0;
+    const real *src = wzp + (long)blk * nmax;
+    const int per = nmax / kBlock;  // block-uniform
+    real w[kPadPer];
+#pragma unroll
+    for (int k = 0; k < kPadPer; k++)
+        if (k < per) w[k] = src[k * kBlock + tid];
+#pragma unroll
+    for (int k = 0; k < kPadPer; k++)
+        if (k < per) lds[k * kBlock + tid] = w[k];
+    __syncthreads();
+    real x = real(0);
+    for (int j = my0; j < my1; j++) x += lds[j - p0];
+    if (halt) return;  // block-uniform
+    real num, den;
+    vertex_finish(a, v, x, o, num, den);
+    if (a.track) {
+        num = block_sum(num, red[0]);
+        den = block_sum(den, red[1]);
+        if (tid == 0) {
+            a.part[2 * blk] = num;
+            a.part[2 * blk + 1] = den;
+        }
+    }
+}
+
+// largest CSR entry count of a vertex block (atomicMax into *out)
+static __global__ void k_pad_nmax(int V, int nb, const int *__restrict__ ptr, int *out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    atomicMax(out, ptr[min(V, (b + 1) * kBlock)] - ptr[b * kBlock]);
+}
+
+// slot of every contribution (e, side) in its vertex block's padded list:
+// sl[2e + side] = b * nmax + (CSR position - first position of block b)
+static __global__ void k_pad_slots(int V, long E, const int *__restrict__ ptr,
+                                   const unsigned *__restrict__ idx, int nmax, int *__restrict__ sl) {
+    const int v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= V) return;
+    const int b = v / kBlock, base = ptr[b * kBlock];
+    for (int j = ptr[v]; j < ptr[v + 1]; j++) {
+        const long addr = idx[j];
+        const long side = addr >= E ? 1 : 0;
+        sl[2 * (addr - side * E) + side] = b * nmax + (j - base);
+    }
 }
 
 // fixed-order sum of per-block partial pairs into out[0..1]

@@ -494,6 +494,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
     else if (!strcmp(what, "coop")) *value = s->impl->coop;
     else if (!strcmp(what, "fused")) *value = s->impl->fused;
+    else if (!strcmp(what, "padded")) *value = s->impl->padded;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "pipeline_chunks")) *value = s->impl->pipeline_chunks;
     else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;

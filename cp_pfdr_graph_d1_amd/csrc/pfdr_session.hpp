@@ -65,6 +65,7 @@ class SessionBase {
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch
     int64_t coop = 0;          // mid-size graph: workgroups of the persistent launch (0: off)
     int64_t fused = 0;         // small graph: loop decision inside the next edge sweep
+    int64_t padded = 0;        // fused graph: contributions stored in per-block lists
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
     int64_t pipeline_chunks = 0;  // pipelined iteration: vertex chunks per iteration
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)

@@ -189,7 +189,9 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
  * relabelling is active), "device_bytes", "split_blocks", "ustaged",
  * "symv", "tiny", "coop" (workgroups of the persistent mid-size-graph
  * launch, 0 when off), "fused" (1: the loop decision of a small graph is
- * taken inside the next edge sweep, two launches per iteration),
+ * taken inside the next edge sweep, two launches per iteration), "padded"
+ * (1: such a graph's contributions are stored in per-vertex-block lists, so
+ * its vertex sweep stages them without dependent address loads),
  * "dense_exact" (1: the dense products run in the reference's sequential
  * order, bit-exact; small single-GPU problems). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);

@@ -10,7 +10,10 @@ converged, reconditioning where the case has it) and on grids across the
 fused range (16 to 1024 vertex blocks, just past it: not fused), stopping
 at a tolerance, at itMax inside a chunk, after reconditionings, with the
 run split into calls of odd and even lengths, with and without hipGraph
-replay."""
+replay.  Fused sessions of at most 512 vertex blocks, each holding at most
+4096 CSR entries, also store their contributions in per-block lists
+(k_vertex_sweep_pad; PFDR_PAD = 0 off, 1 on across the fused range):
+identical as well, and a block past that cap keeps the gathered sweep."""
 import os
 
 import numpy as np
@@ -46,7 +49,8 @@ def test_fused_golden_identical(gpu_lib, name, fixed):
     c, g = G.load(name)
     res = []
     for env in ({"PFDR_TINY": "0", "PFDR_FUSE": "1"}, {"PFDR_TINY": "0", "PFDR_FUSE": "0"},
-                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_GRAPH": "0"}):
+                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_GRAPH": "0"},
+                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_PAD": "0"}):
         with _env(**env):
             res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
     X0, it0, _, D0 = res[0]
@@ -92,11 +96,15 @@ def test_fused_sessions_identical(gpu_lib, case):
     V = int(np.prod(shape))
     fusable = (V + 255) // 256 <= 1024
     res = []
-    for env in ({"PFDR_FUSE": "1"}, {"PFDR_FUSE": "0"}, {"PFDR_FUSE": "1", "PFDR_GRAPH": "0"}):
+    for env in ({"PFDR_FUSE": "1"}, {"PFDR_FUSE": "0"}, {"PFDR_FUSE": "1", "PFDR_GRAPH": "0"},
+                {"PFDR_FUSE": "1", "PFDR_PAD": "0"}, {"PFDR_FUSE": "1", "PFDR_PAD": "1"}):
         with _env(PFDR_TINY="0", **env):
             s = _session(pfdr, shape, dt, kind, diag, itMax, difTol, difRcd)
         try:
-            assert s.query("fused") == (1 if fusable and env["PFDR_FUSE"] == "1" else 0)
+            fused = fusable and env["PFDR_FUSE"] == "1"
+            assert s.query("fused") == (1 if fused else 0)
+            pad = env.get("PFDR_PAD", "1" if (V + 255) // 256 <= 512 else "0")  # kPadBlocks
+            assert s.query("padded") == (1 if fused and pad == "1" else 0)
             for n in runs:
                 s.run(n)
             res.append(s.result())
@@ -108,3 +116,39 @@ def test_fused_sessions_identical(gpu_lib, case):
         assert it1 == it0
         assert np.array_equal(X1, X0)
         assert np.array_equal(D1[:it1], D0[:it0])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_padded_cap(gpu_lib, dt):
+    """A vertex block past the per-block list cap (a hub with 5000 incident
+    edges) keeps the gathered vertex sweep; smaller graphs of the same law
+    are padded.  Both equal the unfused three-launch loop bit for bit."""
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation
+    for hub in (5000, 1000):
+        Eu, Ev = grid_graph((96, 96), 4)
+        V = 96 * 96
+        extra = np.arange(1, hub + 1, dtype=np.int32) * 7 % V
+        extra[extra == 0] = 1
+        Eu = np.concatenate([np.zeros(hub, np.int32), Eu.astype(np.int32)])
+        Ev = np.concatenate([extra, Ev.astype(np.int32)])
+        Y = piecewise_observation((96, 96), 1, dt)
+        res = []
+        for env in ({"PFDR_FUSE": "1"}, {"PFDR_FUSE": "0"}):
+            with _env(PFDR_TINY="0", **env):
+                s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev,
+                                 np.full(Eu.size, 0.1, dt), np.zeros(V, dt), Y,
+                                 La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3,
+                                 difRcd=1e-2, difTol=1e-6, itMax=600, record_dif=True)
+            try:
+                if env["PFDR_FUSE"] == "1":
+                    assert s.query("fused") == 1
+                    assert s.query("padded") == (0 if hub > 4096 else 1)
+                s.run(600)
+                res.append(s.result())
+            finally:
+                s.close()
+        (X0, it0, _, D0), (X1, it1, _, D1) = res
+        assert it0 == it1 and 0 < it0
+        assert np.array_equal(X0, X1)
+        assert np.array_equal(D0[:it0], D1[:it1])
