@@ -449,6 +449,187 @@ __global__ void k_bfs_take(int lo, int hi, const int *__restrict__ ptr,
     if (!EMIT && l == 0) cnt[i - lo] = c;
 }
 
+// ---- the same levels driven from the device: the frontier bounds live in a
+// control block (lo, hi, done, overflow), every kernel of a level reads
+// them, fixed grids loop over the frontier, and a one-lane kernel advances
+// the bounds; the host enqueues levels in batches (one hipGraph replay each)
+// and reads the control block once per batch instead of once per level
+// (each host round trip cost ~40 us of a ~60 us level).
+// The claims, counts and emission order are those of the per-level kernels
+// above, so L, Cv and Vc are identical.
+struct BfsCtl {
+    int lo, hi, done, overflow;
+};
+
+__device__ __forceinline__ void bfs_chunk(int n, int nblk, int b, int &c0, int &c1) {
+    // frontier positions [c0, c1) of block b: whole steps of kBlock / kSub vertices
+    constexpr int step = kBlock / kSub;
+    const int per = ((n + nblk - 1) / nblk + step - 1) / step * step;
+    c0 = min(n, b * per);
+    c1 = min(n, c0 + per);
+}
+
+__global__ void k_bfsd_claim(const BfsCtl *__restrict__ ctl, const int *__restrict__ L,
+                             const int *__restrict__ ptr, const unsigned *__restrict__ slot,
+                             const int *__restrict__ Eu, const int *__restrict__ Ev,
+                             const uint8_t *__restrict__ active, const int *__restrict__ Cv,
+                             unsigned long long *claim) {
+    const BfsCtl c = *ctl;
+    if (c.done) return;
+    const long nt = (long)(c.hi - c.lo) * kSub;
+    for (long gt = (long)blockIdx.x * blockDim.x + threadIdx.x; gt < nt;
+         gt += (long)gridDim.x * blockDim.x) {
+        const int i = c.lo + (int)(gt / kSub), l = (int)(gt % kSub);
+        const int v = L[i];
+        const int top = ptr[v + 1] - 1, deg = top + 1 - ptr[v];
+        for (int j = l; j < deg; j += kSub) {
+            const unsigned a = slot[top - j];
+            if (active[a >> 1]) continue;
+            const int w = arc_head(a, Eu, Ev);
+            if (Cv[w] != -1) continue;
+            atomicMin(claim + w, claim_key(i, j));
+        }
+    }
+}
+
+// claims won by frontier vertex i (the whole subgroup returns the count;
+// EMIT: appended in arc order at base, Cv set)
+template <bool EMIT>
+__device__ __forceinline__ int bfs_take_one(int i, int l, int sh, const int *__restrict__ L,
+                                            const int *__restrict__ ptr,
+                                            const unsigned *__restrict__ slot,
+                                            const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                            const uint8_t *__restrict__ active,
+                                            const unsigned long long *__restrict__ claim,
+                                            bool valid, int base, int *Lo, int *Cv) {
+    int v = 0, deg = 0, top = 0, cv = 0;
+    if (valid) {
+        v = L[i];
+        top = ptr[v + 1] - 1;
+        deg = top + 1 - ptr[v];
+        if (EMIT) cv = Cv[v];
+    }
+    int c = 0;
+    // every lane of the wave runs the same number of ballots
+    int dmax = deg;
+    for (int o = 1; o < kWave; o <<= 1) dmax = max(dmax, __shfl_xor(dmax, o, kWave));
+    for (int j0 = 0; j0 < dmax; j0 += kSub) {
+        const int j = j0 + l;
+        bool win = false;
+        int w = 0;
+        if (j < deg) {
+            const unsigned a = slot[top - j];
+            if (!active[a >> 1]) {
+                w = arc_head(a, Eu, Ev);
+                win = claim[w] == claim_key(i, j);
+            }
+        }
+        const unsigned long long m = __ballot(win);
+        const unsigned mine = (unsigned)(m >> sh) & ((1u << kSub) - 1);
+        if (EMIT && win) {
+            Lo[base + c + __builtin_popcount(mine & ((1u << l) - 1))] = w;
+            Cv[w] = cv;
+        }
+        c += __builtin_popcount(mine);
+    }
+    return c;
+}
+
+// counts of the block's chunk into cnt[i - lo], the chunk's total into bsum[b]
+__global__ __launch_bounds__(kBlock) void k_bfsd_count(
+    const BfsCtl *__restrict__ ctl, const int *__restrict__ L, const int *__restrict__ ptr,
+    const unsigned *__restrict__ slot, const int *__restrict__ Eu, const int *__restrict__ Ev,
+    const uint8_t *__restrict__ active, const unsigned long long *__restrict__ claim,
+    int *__restrict__ cnt, int *__restrict__ bsum) {
+    __shared__ int red[kBlock / kWave];
+    const BfsCtl c = *ctl;
+    if (c.done) return;
+    int c0, c1;
+    bfs_chunk(c.hi - c.lo, gridDim.x, blockIdx.x, c0, c1);
+    const int t = threadIdx.x, l = t % kSub, sh = (t & (kWave - 1)) & ~(kSub - 1);
+    if (c0 >= c1) {  // past the frontier (block-uniform)
+        if (t == 0) bsum[blockIdx.x] = 0;
+        return;
+    }
+    int tot = 0;
+    for (int q = c0; q < c1; q += kBlock / kSub) {
+        const int fi = q + t / kSub;
+        const bool valid = fi < c1;
+        const int k = bfs_take_one<false>(c.lo + fi, l, sh, L, ptr, slot, Eu, Ev, active, claim,
+                                          valid, 0, nullptr, nullptr);
+        if (valid && l == 0) {
+            cnt[fi] = k;
+            tot += k;
+        }
+    }
+    tot = block_sum(tot, red);
+    if (t == 0) bsum[blockIdx.x] = tot;
+}
+
+// emission: the block's base is the sum of the earlier blocks' totals, each
+// step's 16 vertices are offset by an exclusive scan of their counts
+__global__ __launch_bounds__(kBlock) void k_bfsd_emit(
+    const BfsCtl *__restrict__ ctl, const int *__restrict__ ptr, const unsigned *__restrict__ slot,
+    const int *__restrict__ Eu, const int *__restrict__ Ev, const uint8_t *__restrict__ active,
+    const unsigned long long *__restrict__ claim, const int *__restrict__ cnt,
+    const int *__restrict__ bsum, int *L, int *Cv) {
+    constexpr int step = kBlock / kSub;
+    __shared__ int red[kBlock / kWave];
+    __shared__ int off[step + 1];
+    __shared__ int s_pre;
+    const BfsCtl c = *ctl;
+    if (c.done) return;
+    const int t = threadIdx.x, l = t % kSub, sh = (t & (kWave - 1)) & ~(kSub - 1);
+    int c0, c1;
+    bfs_chunk(c.hi - c.lo, gridDim.x, blockIdx.x, c0, c1);
+    if (c0 >= c1) return;  // past the frontier (block-uniform)
+    int pre = 0;
+    for (int b = t; b < (int)blockIdx.x; b += kBlock) pre += bsum[b];
+    pre = block_sum(pre, red);  // valid in thread 0
+    if (t == 0) s_pre = pre;
+    __syncthreads();
+    int base = c.hi + s_pre;
+    for (int q = c0; q < c1; q += step) {
+        __syncthreads();
+        if (t == 0) {
+            int a = 0;
+            for (int k = 0; k < step; k++) {
+                off[k] = a;
+                if (q + k < c1) a += cnt[q + k];
+            }
+            off[step] = a;
+        }
+        __syncthreads();
+        const int fi = q + t / kSub;
+        const bool valid = fi < c1;
+        (void)bfs_take_one<true>(c.lo + fi, l, sh, L, ptr, slot, Eu, Ev, active, claim, valid,
+                                 base + off[t / kSub], L, Cv);
+        base += off[step];
+    }
+}
+
+// lo <- hi, hi += this level's total; done when it is 0 or every vertex is queued
+__global__ void k_bfsd_advance(BfsCtl *ctl, const int *__restrict__ bsum, int nblk, int V) {
+    __shared__ int red[kBlock / kWave];
+    const BfsCtl c = *ctl;
+    if (c.done) return;
+    int tot = 0;
+    for (int b = threadIdx.x; b < nblk; b += kBlock) tot += bsum[b];
+    tot = block_sum(tot, red);
+    if (threadIdx.x == 0) {
+        BfsCtl n = c;
+        if (tot > V - c.hi) {
+            n.overflow = 1;
+            n.done = 1;
+        } else {
+            n.lo = c.hi;
+            n.hi = c.hi + tot;
+            n.done = (tot == 0 || n.hi >= V) ? 1 : 0;
+        }
+        *ctl = n;
+    }
+}
+
 __global__ void k_gather_keys(int V, const int *__restrict__ L, const int *__restrict__ Cv,
                               unsigned *__restrict__ key) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -987,6 +1168,7 @@ struct CpGraphBase {
     DevBuf<int> longs, nlong;
 
     void components();
+    void bfs_device();  // the BFS levels of components(), driven from the device
     virtual void reduced_graph(double eps) = 0;
     virtual int merge(double eps, double difTol) = 0;
     virtual void gradient(int N, const void *A, const void *Y, const void *R, int mem) = 0;
@@ -1038,6 +1220,10 @@ void CpGraphBase::components() {
     rV = d2h_scalar(i2.p + Vn, s);
     k_bfs_roots<<<grid_for(Vn), kBlock, 0, s>>>(Vn, i1.p, i2.p, L.p, Cv.p, claim.p);
     PFDR_HIP(hipGetLastError());
+    const char *bd = getenv("PFDR_BFS_HOST");  // A/B: 1 = one host round trip per level
+    if (!(bd && bd[0] == '1')) {
+        bfs_device();
+    } else {
     // levels; i1/i2 reused as per-frontier counts / offsets
     int lo = 0, hi = rV;
     while (hi > lo && hi < Vn) {
@@ -1059,6 +1245,7 @@ void CpGraphBase::components() {
         hi += add;
     }
     if (hi != Vn) throw std::runtime_error("components: BFS did not reach every vertex");
+    }
     // Vc = the concatenated levels stably sorted by component
     DevBuf<unsigned> key(Vn), skey(Vn);
     Vc.alloc(Vn);
@@ -1068,6 +1255,71 @@ void CpGraphBase::components() {
     k_comp_ptr<<<grid_for(Vn + 1), kBlock, 0, s>>>(Vn, rV, skey.p, rVc.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipStreamSynchronize(s));
+}
+
+// levels after the roots (L[0, rV)): batches of device-driven levels, the
+// first few launched directly, the rest as replays of one captured batch
+void CpGraphBase::bfs_device() {
+    const int Vn = V;
+    if (rV >= Vn) return;
+    DevBuf<BfsCtl> ctl(1);
+    BfsCtl *h = static_cast<BfsCtl *>(pinned_small_get());
+    struct Put {
+        hipStream_t s;
+        void *h;
+        ~Put() { (void)hipStreamSynchronize(s); pinned_small_put(h); }
+    } put{s, h};
+    *h = BfsCtl{0, rV, 0, 0};
+    PFDR_HIP(hipMemcpyAsync(ctl.p, h, sizeof(BfsCtl), hipMemcpyHostToDevice, s));
+    constexpr int step = kBlock / kSub;
+    const int gc = std::min(2048, grid_for((long)Vn * kSub));
+    const int ge = std::max(1, std::min(1024, (Vn + step - 1) / step));
+    DevBuf<int> bsum(ge);
+    auto level = [&]() {
+        k_bfsd_claim<<<gc, kBlock, 0, s>>>(ctl.p, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p,
+                                           Cv.p, claim.p);
+        k_bfsd_count<<<ge, kBlock, 0, s>>>(ctl.p, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p,
+                                           claim.p, i1.p, bsum.p);
+        k_bfsd_emit<<<ge, kBlock, 0, s>>>(ctl.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p, active.p,
+                                          claim.p, i1.p, bsum.p, L.p, Cv.p);
+        k_bfsd_advance<<<1, kBlock, 0, s>>>(ctl.p, bsum.p, ge, Vn);
+    };
+    auto poll = [&]() {
+        PFDR_HIP(hipMemcpyAsync(h, ctl.p, sizeof(BfsCtl), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        return h->done != 0;
+    };
+    constexpr int kFirst = 8, kBatch = 32;
+    for (int i = 0; i < kFirst; i++) level();
+    PFDR_HIP(hipGetLastError());
+    if (!poll()) {
+        hipGraph_t gr = nullptr;
+        hipGraphExec_t ge_ = nullptr;
+        PFDR_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            for (int i = 0; i < kBatch; i++) level();
+        } catch (...) {
+            (void)hipStreamEndCapture(s, &gr);
+            if (gr) (void)hipGraphDestroy(gr);
+            throw;
+        }
+        PFDR_HIP(hipStreamEndCapture(s, &gr));
+        const hipError_t e = hipGraphInstantiate(&ge_, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        PFDR_HIP(e);
+        struct Exec {
+            hipStream_t s;
+            hipGraphExec_t g;
+            ~Exec() { (void)hipStreamSynchronize(s); (void)hipGraphExecDestroy(g); }
+        } ex{s, ge_};
+        // a level adds at least one vertex until done: at most V batches
+        for (long b = 0; b <= (long)Vn; b++) {
+            PFDR_HIP(hipGraphLaunch(ge_, s));
+            if (poll()) break;
+        }
+    }
+    if (h->overflow) throw std::runtime_error("components: BFS overflow");
+    if (h->hi != Vn) throw std::runtime_error("components: BFS did not reach every vertex");
 }
 
 int CpGraphBase::activate(const uint8_t *seg, int mem) {
