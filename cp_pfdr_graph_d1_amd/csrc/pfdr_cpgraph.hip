@@ -1558,10 +1558,11 @@ struct CpGraph : CpGraphBase {
                                                             DfS.p, dtr);
         if (rc && E > 0) k_cp_rcap<real><<<grid_for(E), kBlock, 0, s>>>(E, active.p, La.p, drc);
         PFDR_HIP(hipGetLastError());
-        if (mem != PFDR_MEM_DEVICE) {
-            if (tr) PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost, s));
-            if (rc && E > 0)
-                PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
+        if (mem != PFDR_MEM_DEVICE) {  // the caller's arrays pinned for the DMA (HostPins)
+            HostPins hp(s);
+            if (tr) hp.copy(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost);
+            if (rc && E > 0) hp.copy(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost);
+            hp.release();
         }
         PFDR_HIP(hipStreamSynchronize(s));
     }
@@ -1699,10 +1700,11 @@ struct CpGraph : CpGraphBase {
             k_sx_rcap<real><<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, active.p, La.p, Djv.p,
                                                            drc);
         PFDR_HIP(hipGetLastError());
-        if (mem != PFDR_MEM_DEVICE) {
-            if (tr) PFDR_HIP(hipMemcpyAsync(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost, s));
-            if (rc && E > 0)
-                PFDR_HIP(hipMemcpyAsync(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost, s));
+        if (mem != PFDR_MEM_DEVICE) {  // the caller's arrays pinned for the DMA (HostPins)
+            HostPins hp(s);
+            if (tr) hp.copy(tr, dtr, sizeof(real) * V, hipMemcpyDeviceToHost);
+            if (rc && E > 0) hp.copy(rc, drc, sizeof(real) * E, hipMemcpyDeviceToHost);
+            hp.release();
         }
         PFDR_HIP(hipStreamSynchronize(s));
     }
