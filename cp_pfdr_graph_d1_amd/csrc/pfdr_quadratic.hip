@@ -312,16 +312,18 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
 
     // small single-GPU graphs iterate in one 1024-lane workgroup
-    // (k_tiny_iterate, four vertex blocks at a time): faster than two
-    // launches per iteration up to ~10 vertex blocks (r3u, us/iteration:
-    // 256 vertices 8.2 -> 2.2, 1024: 9.8 -> 4.6, 2025: 9.8 -> 8.4, 4096:
-    // 10.2 -> 16), so up to 8 blocks and 8192 edges.  The split incidence is
-    // not built for them (one setup round trip less).
+    // (k_tiny_iterate, four vertex blocks at a time): against the two-launch
+    // loop (fused decision, per-block lists) on 4-NN grids, us/iteration
+    // (profiles/r2/r2zv_exp_tiny.log): f32 1 block 4.4 vs 8.9, 4: 6.6 vs
+    // 10.8, 8: 10.5 vs 10.8, 16: 19.3 vs 11.1; f64 4: 8.0 vs 10.0, 8: 13.5
+    // vs 9.8 -- so up to 8 blocks in f32, 5 in f64, and 8192 edges.  The
+    // split incidence is not built for them (one setup round trip less).
     if (!(p->nranks > 1 || p->comm) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
         E_ > 0) {
         const char *t = getenv("PFDR_TINY");
         const long maxE = t ? atol(t) : 8192;
-        tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= (t ? 32 : 8);
+        const int maxB = t ? kTinyMaxBlocks : (sizeof(real) == 4 ? 8 : 5);
+        tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= maxB;
         tiny = tiny_ ? 1 : 0;
         coop_ok_ = !tiny_;
     }

@@ -1616,29 +1616,36 @@ struct TinyArgs {
 // (wave_sum, then the block's 4 wave sums in order).
 constexpr int kTiny = 1024;
 
+// Memory-level parallelism inside the one workgroup (everything it touches
+// sits in its XCD's L2, so each dependent round trip is an L2 latency): the
+// edge pass runs k_edge_sweep's lane body (EPT edges per lane, 16-byte
+// streams, the endpoint gathers of all EPT edges issued together), the
+// vertex pass loads 8 CSR addresses, then 8 contributions, at a time and
+// adds them in order, and the loop control stays in registers / LDS (the
+// control block is stored each iteration, never re-read; the per-block
+// partials are summed from LDS).
+constexpr int kTinyMaxBlocks = 32;
+
 template <typename real>
 __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
+    constexpr int EPT = Vec<real>::kPer16B;
     __shared__ real wred[2][kTiny / kWave];
+    __shared__ real bpart[2][kTinyMaxBlocks];
     __shared__ int halt;
     const int tid = threadIdx.x;
     const VArgs<real> &a = t.va;
     R2<real> *xp = a.xp;
+    Ctrl<real> c{};
+    if (tid == 0) {
+        if (t.ctrl) c = *t.ctrl;
+        halt = t.ctrl ? c.halt : 0;
+    }
+    __syncthreads();
     for (int it = 0; it < t.iters; it++) {
-        if (t.ctrl) {
-            if (tid == 0) halt = t.ctrl->halt;
-            __syncthreads();
-            if (halt) break;  // uniform
-        }
-        for (long e = tid; e < t.E; e += kTiny) {
-            const int u = t.Eu[e], v = t.Ev[e];
-            real zu = t.Z2[2 * e], zv = t.Z2[2 * e + 1], ou, ov;
-            edge_full<real>(xp[u], xp[v], t.gi[u], t.gi[v], edge_a(e, t.A1, t.La_d1, t.cw),
-                            t.La_d1[e], zu, zv, ou, ov, t.rho);
-            t.Z2[2 * e] = zu;
-            t.Z2[2 * e + 1] = zv;
-            t.wz[e] = ou;
-            t.wz[t.E + e] = ov;
-        }
+        if (halt) break;  // uniform (set by lane 0 before the last barrier)
+        for (long e0 = (long)tid * EPT; e0 < t.E; e0 += (long)kTiny * EPT)
+            edge_lane<real>(e0, t.E, t.E, t.Eu, t.Ev, xp, t.Z2, t.A1, t.cw, t.gi, t.La_d1, t.wz,
+                            t.rho);
         __syncthreads();
         for (int b0 = 0; b0 < a.nb; b0 += kTiny / kBlock) {
             const int blk = b0 + tid / kBlock;
@@ -1647,8 +1654,20 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
             if (blk < a.nb) {
                 const VOps<real> o = vertex_ops(a, v);
                 real x = real(0);
-                if (v < a.V)
-                    for (int j = a.ptr[v]; j < a.ptr[v + 1]; j++) x += a.wz[a.idx[j]];
+                if (v < a.V) {
+                    const int j1 = a.ptr[v + 1];
+                    for (int j = a.ptr[v]; j < j1; j += 8) {
+                        unsigned id[8];
+                        real w[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) id[q] = j + q < j1 ? a.idx[j + q] : 0u;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) w[q] = j + q < j1 ? a.wz[id[q]] : real(0);
+#pragma unroll
+                        for (int q = 0; q < 8; q++)
+                            if (j + q < j1) x += w[q];
+                    }
+                }
                 vertex_finish(a, v, x, o, num, den);
             }
             if (a.track) {
@@ -1660,6 +1679,8 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
                     real sn = real(0), sd = real(0);
                     const int w0 = tid / kWave;
                     for (int i = 0; i < kBlock / kWave; i++) { sn += wred[0][w0 + i]; sd += wred[1][w0 + i]; }
+                    bpart[0][blk] = sn;
+                    bpart[1][blk] = sd;
                     a.part[2 * blk] = sn;
                     a.part[2 * blk + 1] = sd;
                 }
@@ -1670,7 +1691,7 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
         if (t.ctrl) {  // k_reduce_decide on the first 256 lanes, its tree exactly
             real sa = real(0), sb = real(0);
             if (t.track && tid < kBlock)
-                for (int i = tid; i < a.nb; i += kBlock) { sa += a.part[2 * i]; sb += a.part[2 * i + 1]; }
+                for (int i = tid; i < a.nb; i += kBlock) { sa += bpart[0][i]; sb += bpart[1][i]; }
             sa = wave_sum(sa);
             sb = wave_sum(sb);
             if ((tid & (kWave - 1)) == 0 && tid < kBlock) { wred[0][tid / kWave] = sa; wred[1][tid / kWave] = sb; }
@@ -1680,7 +1701,9 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
                 if (t.track)
                     for (int i = 0; i < kBlock / kWave; i++) { na += wred[0][i]; nb += wred[1][i]; }
                 if (t.track) { t.red[0] = na; t.red[1] = nb; }
-                decide_step(t.ctrl, na, nb, t.Dif, t.track);
+                decide_step(&c, na, nb, t.Dif, t.track);
+                *t.ctrl = c;
+                halt = c.halt;
             }
         }
         __syncthreads();

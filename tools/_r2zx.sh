@@ -1,0 +1,6 @@
+set -u
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r2zx; mkdir -p $O
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc $(tail -1 $O/pytest.log)"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+echo "smoke $(tail -1 $O/smoke.log)"
