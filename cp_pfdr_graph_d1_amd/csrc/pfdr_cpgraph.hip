@@ -1263,12 +1263,8 @@ void CpGraphBase::bfs_device() {
     const int Vn = V;
     if (rV >= Vn) return;
     DevBuf<BfsCtl> ctl(1);
-    BfsCtl *h = static_cast<BfsCtl *>(pinned_small_get());
-    struct Put {
-        hipStream_t s;
-        void *h;
-        ~Put() { (void)hipStreamSynchronize(s); pinned_small_put(h); }
-    } put{s, h};
+    PinnedSmall pin(s);
+    BfsCtl *h = static_cast<BfsCtl *>(pin.p);
     *h = BfsCtl{0, rV, 0, 0};
     PFDR_HIP(hipMemcpyAsync(ctl.p, h, sizeof(BfsCtl), hipMemcpyHostToDevice, s));
     constexpr int step = kBlock / kSub;

@@ -492,12 +492,8 @@ void QuadSession<real>::plan_pad() {
     if ((e && e[0] == '0') || halo_ || !E_) return;
     if (!(e && e[0] == '1') && nbv_ > kPadBlocks) return;
     hipStream_t s = stream;
-    int *hm = static_cast<int *>(pinned_small_get());
-    struct Put {
-        hipStream_t s;
-        int *h;
-        ~Put() { (void)hipStreamSynchronize(s); pinned_small_put(h); }
-    } put{s, hm};
+    PinnedSmall pin(s);
+    int *hm = static_cast<int *>(pin.p);
     DevBuf<int> dm(1);
     PFDR_HIP(hipMemsetAsync(dm.p, 0, sizeof(int), s));
     k_pad_nmax<<<grid_for(nbv_), kBlock, 0, s>>>(V_, nbv_, inc_.ptr.p, dm.p);
