@@ -234,6 +234,16 @@ class QuadSession final : public SessionBase {
     int pad_nmax_ = 0;
     DevBuf<int> sl_;
     DevBuf<real> wzp_;
+    // and, in f32 up to kEndsBlocks, the endpoint data as per-edge copies: (X, P)
+    // and (Ga, 1/Aux) of both ends at xpe_ / gie_ [2e + side], scattered by
+    // the vertex sweep through pidx_ (the end of each list entry), so the
+    // edge sweep (k_edge_sweep_ends) streams everything: one dependent
+    // round trip.  PFDR_PAD_ENDS = 0 off, 1 on for every padded session.
+    bool ends_ = false;
+    static constexpr int kEndsBlocks = 512;
+    DevBuf<int> pidx_;
+    DevBuf<R2<real>> xpe_, gie_;
+    void refresh_ends();
     void plan_pad();
     PadOut<real> pad_out() const { return PadOut<real>{pad_ ? sl_.p : nullptr, wzp_.p}; }
     template <int EPI> void col_product(ColArgs<real> ca);
@@ -480,7 +490,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         if (fuse_) plan_pad();
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
-    acc(sl_.n * 4 + wzp_.n * sizeof(real));
+    acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
 }
 
 template <typename real>
@@ -505,11 +515,33 @@ void QuadSession<real>::plan_pad() {
     sl_.alloc(2 * (size_t)E_);
     wzp_.alloc((size_t)nbv_ * nmax);
     PFDR_HIP(hipMemsetAsync(wzp_.p, 0, wzp_.n * sizeof(real), s));
-    k_pad_slots<<<nbv_, kBlock, 0, s>>>(V_, E_, inc_.ptr.p, inc_.idx.p, nmax, sl_.p);
+    const char *en = getenv("PFDR_PAD_ENDS");
+    // default: f32 up to kEndsBlocks (f32 us/iter 11.2 -> 9.6 at 9 blocks,
+    // 11.5 -> 10.5 at 256, 12.7 -> 12.2 at 507; f64 slower: 10.4 -> 11.0 at 9
+    // blocks, 12.5 -> 26 at 256; profiles/r2/r2zz_exp_ends.log, r2zz2)
+    ends_ = !(en && en[0] == '0') &&
+            ((sizeof(real) == 4 && nbv_ <= kEndsBlocks) || (en && en[0] == '1'));
+    if (ends_) {
+        pidx_.alloc((size_t)nbv_ * nmax);
+        PFDR_HIP(hipMemsetAsync(pidx_.p, 0, pidx_.n * sizeof(int), s));
+        xpe_.alloc(2 * (size_t)E_);
+        gie_.alloc(2 * (size_t)E_);
+    }
+    k_pad_slots<<<nbv_, kBlock, 0, s>>>(V_, E_, inc_.ptr.p, inc_.idx.p, nmax, sl_.p,
+                                        ends_ ? pidx_.p : nullptr);
     PFDR_HIP(hipGetLastError());
     pad_nmax_ = nmax;
     pad_ = true;
     padded = 1;
+    refresh_ends();
+}
+
+template <typename real>
+void QuadSession<real>::refresh_ends() {
+    if (!ends_) return;
+    k_pad_ends<real><<<grid_for(E_), kBlock, 0, stream>>>(E_, Eu_.p, Ev_.p, xp_.p, gi_.p, xpe_.p,
+                                                          gie_.p);
+    PFDR_HIP(hipGetLastError());
 }
 
 // endpoints (local ids), partition plan, incidence CSR keyed by global edge id
@@ -905,6 +937,11 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     const int nb = rg.nb0 + (eend2 > ebeg2 ? grid_for(eend2 - ebeg2, EPT) : 0);
     const int xm = xcd_fit(nb, xcd_e_), g = xcd_grid(nb, xm);
     const FuseDecide<real> f = fd ? *fd : FuseDecide<real>{};
+    if (ends_ && fuse_) {  // the whole edge range (fused sessions sweep [0, E) in one launch)
+        k_edge_sweep_ends<real><<<g, kBlock, 0, s>>>(E_, xpe_.p, gie_.p, Z2_.p, A1_.p, cw_,
+                                                     La_d1_.p, rho_, c, nb, xm, f, pad_out());
+        return;
+    }
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
@@ -1000,7 +1037,8 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
     }
     ProfScope ps(prof, name, s);
     if (pad_ && bend2 <= bbeg2) {
-        k_vertex_sweep_pad<real><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a, wzp_.p, pad_nmax_);
+        k_vertex_sweep_pad<real><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(
+            a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
         return;
     }
     if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
@@ -1236,6 +1274,7 @@ int QuadSession<real>::run(int iters) {
             } else if (hctrl_->recond) {
                 if (verbose_) { print_progress(); printf("Reconditioning... "); fflush(stdout); }
                 precondition(false);
+                refresh_ends();  // (X, P) and (Ga, 1/Aux) rewritten
                 drop_graphs();  // A1_ now holds the splitting weights' factors
                 difRcd2_ *= real(0.01);  // ref :458
                 hctrl_->difRcd = difRcd2_;

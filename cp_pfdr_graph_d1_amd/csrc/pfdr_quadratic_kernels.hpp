@@ -1371,8 +1371,8 @@ __device__ __forceinline__ VOps<real> vertex_ops(const VArgs<real> &a, int v) {
 // after the ordered sum x of vertex v: prox, evolution terms, next forward
 // step (ref :499-529 then :355-464 of the next iteration)
 template <typename real>
-__device__ __forceinline__ void vertex_finish(const VArgs<real> &a, int v, real x,
-                                              const VOps<real> &o, real &num, real &den) {
+__device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, real x,
+                                                  const VOps<real> &o, real &num, real &den) {
     num = real(0);
     den = real(0);
     R2<real> q = o.q;
@@ -1413,6 +1413,7 @@ __device__ __forceinline__ void vertex_finish(const VArgs<real> &a, int v, real 
         }
         a.xp[v] = q;
     }
+    return q;
 }
 
 // one vertex block `blk` (all 256 lanes of the calling block take part)
@@ -1472,7 +1473,9 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
 constexpr int kPadPer = 16;  // staged entries per lane: nmax <= kPadPer * kBlock
 template <typename real>
 __global__ __launch_bounds__(256) void k_vertex_sweep_pad(VArgs<real> a,
-                                                          const real *__restrict__ wzp, int nmax) {
+                                                          const real *__restrict__ wzp, int nmax,
+                                                          const int *__restrict__ pidx,
+                                                          R2<real> *__restrict__ xpe) {
     static_assert(kPadPer * kBlock <= GatherCap<real>::v, "staged list fits the LDS chunk");
     int halt = 0;
     if (a.ctrl) {
@@ -1483,6 +1486,7 @@ __global__ __launch_bounds__(256) void k_vertex_sweep_pad(VArgs<real> a,
         }
     }
     __shared__ real lds[kPadPer * kBlock];
+    __shared__ int sidx[kPadPer * kBlock];
     __shared__ real red[2][kBlock / kWave];
     const int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
@@ -1494,18 +1498,29 @@ __global__ __launch_bounds__(256) void k_vertex_sweep_pad(VArgs<real> a,
     const real *src = wzp + (long)blk * nmax;
     const int per = nmax / kBlock;  // block-uniform
     real w[kPadPer];
+    int pe[kPadPer];
 #pragma unroll
     for (int k = 0; k < kPadPer; k++)
-        if (k < per) w[k] = src[k * kBlock + tid];
+        if (k < per) {
+            w[k] = src[k * kBlock + tid];
+            if (xpe) pe[k] = pidx[(long)blk * nmax + k * kBlock + tid];
+        }
 #pragma unroll
     for (int k = 0; k < kPadPer; k++)
-        if (k < per) lds[k * kBlock + tid] = w[k];
+        if (k < per) {
+            lds[k * kBlock + tid] = w[k];
+            if (xpe) sidx[k * kBlock + tid] = pe[k];
+        }
     __syncthreads();
     real x = real(0);
     for (int j = my0; j < my1; j++) x += lds[j - p0];
     if (halt) return;  // block-uniform
     real num, den;
-    vertex_finish(a, v, x, o, num, den);
+    const R2<real> q = vertex_finish(a, v, x, o, num, den);
+    // (X, P) to the copies the next edge sweep streams: entry j of this
+    // vertex is the end (e, side) = pidx of the edge that contributed it
+    if (xpe && v < a.V)
+        for (int j = my0; j < my1; j++) xpe[sidx[j - p0]] = q;
     if (a.track) {
         num = block_sum(num, red[0]);
         den = block_sum(den, red[1]);
@@ -1514,6 +1529,90 @@ __global__ __launch_bounds__(256) void k_vertex_sweep_pad(VArgs<real> a,
             a.part[2 * blk + 1] = den;
         }
     }
+}
+
+// Edge sweep of a padded session whose endpoint data arrive as per-edge
+// copies (written by the previous vertex sweep / k_pad_ends): (X, P) and
+// (Ga, 1/Aux) of both ends of edge e at xpe / gie [2e + side], so every
+// load of the sweep is a stream (no endpoint index, no gather: one
+// dependent round trip); contributions stored through sl as in PadOut.
+// Fused decision as k_edge_sweep<real, true>.
+template <typename real>
+__global__ __launch_bounds__(256) void k_edge_sweep_ends(
+    long E, const R2<real> *__restrict__ xpe, const R2<real> *__restrict__ gie,
+    real *__restrict__ Z2, const real *__restrict__ A1, real cw,
+    const real *__restrict__ La_d1, real rho, const Ctrl<real> *ctrl, int nb, int xcd,
+    FuseDecide<real> fd, PadOut<real> pd) {
+    constexpr int EPT = Vec<real>::kPer16B;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int s_halt;
+    FdRegs<real> fr;
+    int halt = 0;
+    if (fd.src) fd_load(fd, fr);
+    else if (ctrl) halt = ctrl->halt;
+    const long e0 = ((long)blk * blockDim.x + threadIdx.x) * EPT;
+    const bool full = e0 + EPT <= E;
+    R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
+    Pk<real, 2 * EPT> z{};
+    Pk<real, EPT> la{}, a{};
+    Pk<int, 2 * EPT> sv{};
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            pu[j] = xpe[2 * (e0 + j)]; pv[j] = xpe[2 * (e0 + j) + 1];
+            gu[j] = gie[2 * (e0 + j)]; gv[j] = gie[2 * (e0 + j) + 1];
+        }
+        z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
+        la = ldv<real, EPT>(La_d1 + e0);
+        if (A1) a = ldv<real, EPT>(A1 + e0);
+        sv = ldv<int, 2 * EPT>(pd.sl + 2 * e0);
+    }
+    if (fd.src) halt = fd_decide(fd, fr, blk == 0, red, &s_halt);
+    if (halt || e0 >= E) return;  // halt is block-uniform
+    if (full) {
+        if (!A1) {
+#pragma unroll
+            for (int j = 0; j < EPT; j++) a.v[j] = cw * la.v[j];
+        }
+        Pk<real, EPT> ou, ov;
+#pragma unroll
+        for (int j = 0; j < EPT; j++)
+            edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
+                            z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            pd.wzp[sv.v[2 * j]] = ou.v[j];
+            pd.wzp[sv.v[2 * j + 1]] = ov.v[j];
+        }
+    } else {
+        for (long e = e0; e < E; e++) {
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            edge_full<real>(xpe[2 * e], xpe[2 * e + 1], gie[2 * e], gie[2 * e + 1],
+                            edge_a(e, A1, La_d1, cw), La_d1[e], zu, zv, ou, ov, rho);
+            Z2[2 * e] = zu;
+            Z2[2 * e + 1] = zv;
+            pd.wzp[pd.sl[2 * e]] = ou;
+            pd.wzp[pd.sl[2 * e + 1]] = ov;
+        }
+    }
+}
+
+// the per-edge endpoint copies from the vertex arrays (setup, and after a
+// reconditioning rewrote (X, P) and (Ga, 1/Aux))
+template <typename real>
+__global__ void k_pad_ends(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                           const R2<real> *__restrict__ xp, const R2<real> *__restrict__ gi,
+                           R2<real> *__restrict__ xpe, R2<real> *__restrict__ gie) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int u = Eu[e], v = Ev[e];
+    xpe[2 * e] = xp[u];
+    xpe[2 * e + 1] = xp[v];
+    gie[2 * e] = gi[u];
+    gie[2 * e + 1] = gi[v];
 }
 
 // largest CSR entry count of a vertex block (atomicMax into *out)
@@ -1525,15 +1624,19 @@ static __global__ void k_pad_nmax(int V, int nb, const int *__restrict__ ptr, in
 
 // slot of every contribution (e, side) in its vertex block's padded list:
 // sl[2e + side] = b * nmax + (CSR position - first position of block b)
+// and, with pidx, the end 2e + side of each list entry
 static __global__ void k_pad_slots(int V, long E, const int *__restrict__ ptr,
-                                   const unsigned *__restrict__ idx, int nmax, int *__restrict__ sl) {
+                                   const unsigned *__restrict__ idx, int nmax, int *__restrict__ sl,
+                                   int *__restrict__ pidx) {
     const int v = blockIdx.x * kBlock + threadIdx.x;
     if (v >= V) return;
     const int b = v / kBlock, base = ptr[b * kBlock];
     for (int j = ptr[v]; j < ptr[v + 1]; j++) {
         const long addr = idx[j];
         const long side = addr >= E ? 1 : 0;
-        sl[2 * (addr - side * E) + side] = b * nmax + (j - base);
+        const long end = 2 * (addr - side * E) + side;
+        sl[end] = b * nmax + (j - base);
+        if (pidx) pidx[(long)b * nmax + (j - base)] = (int)end;
     }
 }
 

@@ -13,7 +13,10 @@ run split into calls of odd and even lengths, with and without hipGraph
 replay.  Fused sessions of at most 512 vertex blocks, each holding at most
 4096 CSR entries, also store their contributions in per-block lists
 (k_vertex_sweep_pad; PFDR_PAD = 0 off, 1 on across the fused range):
-identical as well, and a block past that cap keeps the gathered sweep."""
+identical as well, and a block past that cap keeps the gathered sweep; with
+the endpoint data streamed as per-edge copies (k_edge_sweep_ends; f32 up to
+512 blocks by default, PFDR_PAD_ENDS = 0 off, 1 on for every padded session)
+as well."""
 import os
 
 import numpy as np
@@ -50,7 +53,9 @@ def test_fused_golden_identical(gpu_lib, name, fixed):
     res = []
     for env in ({"PFDR_TINY": "0", "PFDR_FUSE": "1"}, {"PFDR_TINY": "0", "PFDR_FUSE": "0"},
                 {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_GRAPH": "0"},
-                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_PAD": "0"}):
+                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_PAD": "0"},
+                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_PAD_ENDS": "0"},
+                {"PFDR_TINY": "0", "PFDR_FUSE": "1", "PFDR_PAD_ENDS": "1"}):
         with _env(**env):
             res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
     X0, it0, _, D0 = res[0]
@@ -97,7 +102,9 @@ def test_fused_sessions_identical(gpu_lib, case):
     fusable = (V + 255) // 256 <= 1024
     res = []
     for env in ({"PFDR_FUSE": "1"}, {"PFDR_FUSE": "0"}, {"PFDR_FUSE": "1", "PFDR_GRAPH": "0"},
-                {"PFDR_FUSE": "1", "PFDR_PAD": "0"}, {"PFDR_FUSE": "1", "PFDR_PAD": "1"}):
+                {"PFDR_FUSE": "1", "PFDR_PAD": "0"}, {"PFDR_FUSE": "1", "PFDR_PAD": "1"},
+                {"PFDR_FUSE": "1", "PFDR_PAD_ENDS": "0"},
+                {"PFDR_FUSE": "1", "PFDR_PAD": "1", "PFDR_PAD_ENDS": "1"}):
         with _env(PFDR_TINY="0", **env):
             s = _session(pfdr, shape, dt, kind, diag, itMax, difTol, difRcd)
         try:
