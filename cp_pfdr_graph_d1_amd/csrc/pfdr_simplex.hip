@@ -970,6 +970,7 @@ class SimplexSession final : public SessionBase {
             (void)hipStreamSynchronize(stream);  // no control-block copy in flight
             pinned_small_put(hctrl_);
         }
+        drop_graphs();
     }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
@@ -1017,6 +1018,17 @@ class SimplexSession final : public SessionBase {
     bool stopped_ = false;
     int chunk_ = 32;
     int next_print_ = 0;
+    // hipGraph of a chunk of bodies (single GPU, no objective record,
+    // unprofiled; re-captured after a reconditioning): small problems --
+    // cut pursuit's reduced ones -- are otherwise bound by the host's three
+    // launches per iteration.  PFDR_GRAPH=0 launches directly.
+    bool graphs_ok_ = false;
+    std::map<int, hipGraphExec_t> graphs_;
+    void run_bodies(int n);
+    void drop_graphs() {
+        for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+        graphs_.clear();
+    }
 
     void precondition(bool init);
     void objective();
@@ -1168,6 +1180,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     PFDR_HIP(hipStreamSynchronize(s));
     pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
+    {
+        const char *g = getenv("PFDR_GRAPH");
+        graphs_ok_ = !(g && g[0] == '0') && !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
+    }
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
@@ -1325,12 +1341,39 @@ void SimplexSession<real>::push_wz() {
 }
 
 template <typename real>
+void SimplexSession<real>::run_bodies(int n) {
+    if (!graphs_ok_ || prof.on) {
+        for (int i = 0; i < n; i++) body();
+        return;
+    }
+    auto it = graphs_.find(n);
+    if (it == graphs_.end()) {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        try {
+            for (int i = 0; i < n; i++) body();
+        } catch (...) {
+            (void)hipStreamEndCapture(stream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        PFDR_HIP(hipStreamEndCapture(stream, &g));
+        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        PFDR_HIP(e);
+        it = graphs_.emplace(n, ge).first;
+    }
+    PFDR_HIP(hipGraphLaunch(it->second, stream));
+}
+
+template <typename real>
 int SimplexSession<real>::run(int iters) {
     const bool gated = track_ || rec_obj_;
     const int target = (int)std::min<long>((long)it_ + std::max(iters, 0), (long)itMax_);
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
-        for (int i = 0; i < n; i++) body();
+        run_bodies(n);
         if (gated) {
             PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
             wait_stream();
@@ -1340,6 +1383,7 @@ int SimplexSession<real>::run(int iters) {
             } else if (hctrl_->recond) {
                 if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
                 precondition(false);
+                drop_graphs();  // kernel arguments (A1_, stored weights) may have changed
                 k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
                 PFDR_HIP(hipGetLastError());
                 pullPF();
