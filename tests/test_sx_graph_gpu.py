@@ -1,0 +1,94 @@
+"""GPU: single-GPU simplex sessions replay their iteration chunks as
+hipGraphs (re-captured after a reconditioning; PFDR_GRAPH = 0 launches
+directly).  Iterates, iteration counts and the evolution record must be
+identical bit for bit to the directly launched loop on
+every simplex golden case (fixed-k and converged: l1 and label-count
+evolution, reconditioning, La_f, self-loops) -- and, at the fixed iteration
+count, to the reference's golden iterates -- and on grids stopped at a
+tolerance, at itMax inside a chunk, after reconditionings, with the run
+split into calls of odd and even lengths."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+SX = [n for n in G.names() if n.startswith("simplex_")]
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("name", SX)
+@pytest.mark.parametrize("fixed", [True, False], ids=["fixk", "conv"])
+def test_sx_graph_golden_identical(gpu_lib, name, fixed):
+    c, g = G.load(name)
+    res = []
+    for env in ({"PFDR_GRAPH": "1"}, {"PFDR_GRAPH": "0"}):
+        with _env(**env):
+            res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
+    X0, it0, _, D0 = res[0]
+    for X1, it1, _, D1 in res[1:]:
+        assert it1 == it0
+        assert np.array_equal(X1, X0)
+        assert np.array_equal(D1[:it1], D0[:it0])
+    if fixed:
+        assert np.array_equal(X0, g["fixk_X"])
+
+
+CASES = [  # shape, dtype, K, al, itMax, difTol, difRcd, run() lengths
+    ((40, 40), np.float32, 4, 0.1, 3000, 1e-5, 1e-2, (3000,)),
+    ((40, 40), np.float64, 3, 0.0, 400, 1e-4, 0.0, (400,)),            # linear loss
+    ((64, 48), np.float32, 6, 1.0, 70, 0.0, 1e-1, (70,)),              # itMax inside a chunk
+    ((30, 30), np.float32, 5, 0.3, 500, 2.0, 20.0, (7, 33, 1, 64, 500)),  # label counts
+    ((100, 100), np.float64, 4, 0.1, 200, 1e-9, 1e-3, (31, 200)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%d-%s-K%d-al%g" % (
+    c[0][0], c[0][1], np.dtype(c[1]).name, c[2], c[3]))
+def test_sx_graph_sessions_identical(gpu_lib, case):
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    shape, dt, K, al, itMax, difTol, difRcd, runs = case
+    Eu, Ev = grid_graph(shape, 8)
+    V = int(np.prod(shape))
+    rng = np.random.default_rng(V + K)
+    Q = rng.random((V, K))
+    Q[: V // 2, 0] += 2.0
+    Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
+    res = []
+    for env in ({"PFDR_GRAPH": "1"}, {"PFDR_GRAPH": "0"}):
+        with _env(**env):
+            s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev,
+                             np.full(Eu.size, 0.05, dt), Q.copy(), Q, K=K, al=al, rho=1.0,
+                             condMin=0.1, difRcd=difRcd, difTol=difTol, itMax=itMax,
+                             record_dif=True)
+        try:
+            for n in runs:
+                s.run(n)
+            res.append(s.result())
+        finally:
+            s.close()
+    X0, it0, _, D0 = res[0]
+    assert 0 < it0 <= itMax
+    for X1, it1, _, D1 in res[1:]:
+        assert it1 == it0
+        assert np.array_equal(X1, X0)
+        assert np.array_equal(D1[:it1], D0[:it0])

@@ -1,8 +1,8 @@
 """Small simplex problems (cut pursuit's reduced ones): microseconds per
 iteration of PFDR_graph_loss_d1_simplex sessions on 8-neighbour grids, K = 4
 smoothed KL, f32 / f64, difTol tiny (runs to itMax), with and without the
-hipGraph replay of iteration chunks (PFDR_GRAPH = 1 / 0).
-Usage: python tools/exp_sx_small.py"""
+hipGraph replay of iteration chunks (PFDR_GRAPH = 1 / 0) or the fused
+loop decision (PFDR_FUSE).  Usage: python tools/exp_sx_small.py [KNOB]"""
 import os
 import sys
 import time
@@ -15,15 +15,18 @@ from cp_pfdr_graph_d1_amd import pfdr  # noqa: E402
 from cp_pfdr_graph_d1_amd.graphs import grid_graph  # noqa: E402
 
 
+KNOB = sys.argv[1] if len(sys.argv) > 1 else "PFDR_GRAPH"  # or PFDR_FUSE
+
+
 def us_per_it(shape, dt, graph, K=4, it=1000):
-    os.environ["PFDR_GRAPH"] = graph
+    os.environ[KNOB] = graph
     Eu, Ev = grid_graph(shape, 8)
     V = int(np.prod(shape))
     rng = np.random.default_rng(V)
     Q = rng.random((V, K))
     Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
     s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.05, dt),
-                     Q.copy(), Q, K=K, al=0.1, rho=1.0, condMin=0.1, difRcd=0.0, difTol=1e-30,
+                     Q.copy(), Q, K=K, al=0.1, rho=1.0, condMin=0.1, difRcd=0.0, difTol=1e-12,
                      itMax=it + 100)
     try:
         s.run(100)
@@ -40,5 +43,5 @@ torch.cuda.init()
 for dt in (np.float32, np.float64):
     for shape in ((16, 16), (40, 40), (100, 100), (300, 300)):
         r = {g: [us_per_it(shape, dt, g) for _ in range(2)] for g in ("1", "0")}
-        print("%-4s %-8s graph %7.2f %7.2f   direct %7.2f %7.2f us/it" % (
-            np.dtype(dt).name[5:], "%dx%d" % shape, *r["1"], *r["0"]), flush=True)
+        print("%-4s %-8s %s on %7.2f %7.2f   off %7.2f %7.2f us/it" % (
+            np.dtype(dt).name[5:], "%dx%d" % shape, KNOB, *r["1"], *r["0"]), flush=True)
