@@ -95,6 +95,11 @@ static T d2h_scalar(const T *p, hipStream_t s) {
     return h;
 }
 
+// grid of the counting edge kernels (activation, merge): a grid-stride loop
+// and one atomic per block -- one block per 256 edges put 234K atomics on
+// one word at the headline size (2.3 ms of serialised adds)
+inline int count_grid(long n) { return std::min(grid_for(n), 2048); }
+
 // per-block partial count -> one atomicAdd (integer: order-free)
 __device__ __forceinline__ void block_count(int c, int *total) {
     __shared__ int red[kBlock / kWave];
@@ -776,9 +781,10 @@ template <typename real>
 __global__ void k_cp_merge(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                            const int *__restrict__ Cv, const real *__restrict__ rX, real eps,
                            real difTol, uint8_t *__restrict__ active, int *__restrict__ count) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     int c = 0;
-    if (e < E && active[e]) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x) {
+        if (!active[e]) continue;
         real a = rX[Cv[Eu[e]]], b = rX[Cv[Ev[e]]], d = a - b;
         if (a < real(0)) a = -a;
         if (b < real(0)) b = -b;
@@ -787,7 +793,7 @@ __global__ void k_cp_merge(long E, const int *__restrict__ Eu, const int *__rest
         d = (a > eps) ? d / a : d / eps;
         if (d <= difTol) {
             active[e] = 0;
-            c = 1;
+            c++;
         }
     }
     block_count(c, count);
@@ -914,12 +920,13 @@ __global__ void k_cp_rcap(long E, const uint8_t *__restrict__ active, const real
 __global__ void k_cp_activate(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                               const uint8_t *__restrict__ seg, uint8_t *__restrict__ active,
                               int *__restrict__ count) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     int c = 0;
-    if (e < E && seg[Eu[e]] != seg[Ev[e]] && !active[e]) {
-        active[e] = 1;
-        c = 1;
-    }
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x)
+        if (seg[Eu[e]] != seg[Ev[e]] && !active[e]) {
+            active[e] = 1;
+            c++;
+        }
     block_count(c, count);
 }
 
@@ -1069,12 +1076,13 @@ __global__ void k_sx_expand(int V, int n, const uint8_t *__restrict__ seg, int *
 __global__ void k_sx_activate(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                               const int *__restrict__ Djv, uint8_t *__restrict__ active,
                               int *__restrict__ count) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     int c = 0;
-    if (e < E && !active[e] && Djv[Eu[e]] != Djv[Ev[e]]) {
-        active[e] = 1;
-        c = 1;
-    }
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x)
+        if (!active[e] && Djv[Eu[e]] != Djv[Ev[e]]) {
+            active[e] = 1;
+            c++;
+        }
     block_count(c, count);
 }
 
@@ -1084,9 +1092,10 @@ template <typename real>
 __global__ void k_sx_merge(long E, int K, const int *__restrict__ Eu, const int *__restrict__ Ev,
                            const int *__restrict__ Cv, const real *__restrict__ rP, real eps,
                            uint8_t *__restrict__ active, int *__restrict__ count) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     int c = 0;
-    if (e < E && active[e]) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x) {
+        if (!active[e]) continue;
         const real *Pu = rP + (size_t)Cv[Eu[e]] * K, *Pv = rP + (size_t)Cv[Ev[e]] * K;
         real a = real(0);
         for (int k = 0; k < K; k++) {
@@ -1096,7 +1105,7 @@ __global__ void k_sx_merge(long E, int K, const int *__restrict__ Eu, const int 
         }
         if (a <= eps) {
             active[e] = 0;
-            c = 1;
+            c++;
         }
     }
     block_count(c, count);
@@ -1133,13 +1142,14 @@ __global__ void k_cp_trcap_duplex(int V, int positivity, const real *__restrict_
 __global__ void k_cp_activate_duplex(int V, long E, const int *__restrict__ Eu,
                                      const int *__restrict__ Ev, const uint8_t *__restrict__ seg,
                                      uint8_t *__restrict__ active, int *__restrict__ count) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     int c = 0;
-    if (e < E && !active[e]) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+         e += (long)gridDim.x * blockDim.x) {
+        if (active[e]) continue;
         const int u = Eu[e], v = Ev[e];
         if (seg[u] != seg[v] || seg[V + u] != seg[V + v]) {
             active[e] = 1;
-            c = 1;
+            c++;
         }
     }
     block_count(c, count);
@@ -1328,7 +1338,7 @@ int CpGraphBase::activate(const uint8_t *seg, int mem) {
     }
     if (!count.p) count.alloc(1);
     PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
-    if (E > 0) k_cp_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, ds, active.p, count.p);
+    if (E > 0) k_cp_activate<<<count_grid(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, ds, active.p, count.p);
     PFDR_HIP(hipGetLastError());
     return d2h_scalar(count.p, s);
 }
@@ -1353,7 +1363,7 @@ int CpGraphBase::sx_activate() {
     if (!Djv.p) throw std::runtime_error("simplex: compute the gradient first");
     if (!count.p) count.alloc(1);
     PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
-    if (E > 0) k_sx_activate<<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Djv.p, active.p, count.p);
+    if (E > 0) k_sx_activate<<<count_grid(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Djv.p, active.p, count.p);
     PFDR_HIP(hipGetLastError());
     return d2h_scalar(count.p, s);
 }
@@ -1369,7 +1379,7 @@ int CpGraphBase::activate_duplex(const uint8_t *seg, int mem) {
     if (!count.p) count.alloc(1);
     PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
     if (E > 0)
-        k_cp_activate_duplex<<<grid_for(E), kBlock, 0, s>>>(V, E, Eu.p, Ev.p, ds, active.p, count.p);
+        k_cp_activate_duplex<<<count_grid(E), kBlock, 0, s>>>(V, E, Eu.p, Ev.p, ds, active.p, count.p);
     PFDR_HIP(hipGetLastError());
     return d2h_scalar(count.p, s);
 }
@@ -1477,7 +1487,7 @@ struct CpGraph : CpGraphBase {
         if (!count.p) count.alloc(1);
         PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
         if (E > 0)
-            k_cp_merge<real><<<grid_for(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Cv.p, rX.p, (real)eps,
+            k_cp_merge<real><<<count_grid(E), kBlock, 0, s>>>(E, Eu.p, Ev.p, Cv.p, rX.p, (real)eps,
                                                             (real)difTol, active.p, count.p);
         PFDR_HIP(hipGetLastError());
         return d2h_scalar(count.p, s);
@@ -1711,7 +1721,7 @@ struct CpGraph : CpGraphBase {
         if (!count.p) count.alloc(1);
         PFDR_HIP(hipMemsetAsync(count.p, 0, sizeof(int), s));
         if (E > 0)
-            k_sx_merge<real><<<grid_for(E), kBlock, 0, s>>>(E, K, Eu.p, Ev.p, Cv.p, rP.p,
+            k_sx_merge<real><<<count_grid(E), kBlock, 0, s>>>(E, K, Eu.p, Ev.p, Cv.p, rP.p,
                                                             (real)eps, active.p, count.p);
         PFDR_HIP(hipGetLastError());
         return d2h_scalar(count.p, s);
