@@ -142,6 +142,7 @@ class QuadSession final : public SessionBase {
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
+    hipGraphExec_t chunk_graph();
     void drop_graphs() {
         for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
         graphs_.clear();
@@ -491,6 +492,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }
     acc(where_.n * 4 + amp_orig_.n * sizeof(real));
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
+    // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
+    // which a small solve timed to tolerance would otherwise pay in its loop)
+    if (graphs_ok_) (void)chunk_graph();
 }
 
 template <typename real>
@@ -1217,31 +1221,39 @@ void QuadSession<real>::plan_overlap() {
     (void)s;
 }
 
+// the captured graph of a whole chunk (chunk_ bodies), instantiated once --
+// at the end of the setup, and again after a reconditioning dropped it
+template <typename real>
+hipGraphExec_t QuadSession<real>::chunk_graph() {
+    auto it = graphs_.find(chunk_);
+    if (it != graphs_.end()) return it->second;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+        for (int i = 0; i < chunk_; i++) body(i, chunk_);
+    } catch (...) {
+        (void)hipStreamEndCapture(stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+    }
+    PFDR_HIP(hipStreamEndCapture(stream, &g));
+    const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    PFDR_HIP(e);
+    graphs_.emplace(chunk_, ge);
+    return ge;
+}
+
+// whole chunks replay the captured graph; a partial chunk (the tail of a
+// run) is launched directly rather than captured for one use
 template <typename real>
 void QuadSession<real>::run_bodies(int n) {
-    if (!graphs_ok_ || prof.on) {
+    if (!graphs_ok_ || prof.on || n != chunk_) {
         for (int i = 0; i < n; i++) body(i, n);
         return;
     }
-    auto it = graphs_.find(n);
-    if (it == graphs_.end()) {
-        hipGraph_t g = nullptr;
-        hipGraphExec_t ge = nullptr;
-        PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        try {
-            for (int i = 0; i < n; i++) body(i, n);
-        } catch (...) {
-            (void)hipStreamEndCapture(stream, &g);
-            if (g) (void)hipGraphDestroy(g);
-            throw;
-        }
-        PFDR_HIP(hipStreamEndCapture(stream, &g));
-        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        PFDR_HIP(e);
-        it = graphs_.emplace(n, ge).first;
-    }
-    PFDR_HIP(hipGraphLaunch(it->second, stream));
+    PFDR_HIP(hipGraphLaunch(chunk_graph(), stream));
 }
 
 template <typename real>

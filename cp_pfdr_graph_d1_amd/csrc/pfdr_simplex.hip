@@ -1025,6 +1025,7 @@ class SimplexSession final : public SessionBase {
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
+    hipGraphExec_t chunk_graph();
     void drop_graphs() {
         for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
         graphs_.clear();
@@ -1184,6 +1185,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         const char *g = getenv("PFDR_GRAPH");
         graphs_ok_ = !(g && g[0] == '0') && !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
     }
+    if (graphs_ok_) (void)chunk_graph();  // instantiated with the setup
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
@@ -1340,31 +1342,39 @@ void SimplexSession<real>::push_wz() {
     halo_->push_packed(buf, Zv_.p + EK_, eb, stream);  // the tail of Zv (vertex sweep)
 }
 
+// the captured graph of a whole chunk (chunk_ bodies), instantiated once --
+// at the end of the setup, and again after a reconditioning dropped it
+template <typename real>
+hipGraphExec_t SimplexSession<real>::chunk_graph() {
+    auto it = graphs_.find(chunk_);
+    if (it != graphs_.end()) return it->second;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+        for (int i = 0; i < chunk_; i++) body();
+    } catch (...) {
+        (void)hipStreamEndCapture(stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+    }
+    PFDR_HIP(hipStreamEndCapture(stream, &g));
+    const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    PFDR_HIP(e);
+    graphs_.emplace(chunk_, ge);
+    return ge;
+}
+
+// whole chunks replay the captured graph; a partial chunk (the tail of a
+// run) is launched directly rather than captured for one use
 template <typename real>
 void SimplexSession<real>::run_bodies(int n) {
-    if (!graphs_ok_ || prof.on) {
+    if (!graphs_ok_ || prof.on || n != chunk_) {
         for (int i = 0; i < n; i++) body();
         return;
     }
-    auto it = graphs_.find(n);
-    if (it == graphs_.end()) {
-        hipGraph_t g = nullptr;
-        hipGraphExec_t ge = nullptr;
-        PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        try {
-            for (int i = 0; i < n; i++) body();
-        } catch (...) {
-            (void)hipStreamEndCapture(stream, &g);
-            if (g) (void)hipGraphDestroy(g);
-            throw;
-        }
-        PFDR_HIP(hipStreamEndCapture(stream, &g));
-        const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        PFDR_HIP(e);
-        it = graphs_.emplace(n, ge).first;
-    }
-    PFDR_HIP(hipGraphLaunch(it->second, stream));
+    PFDR_HIP(hipGraphLaunch(chunk_graph(), stream));
 }
 
 template <typename real>
