@@ -478,20 +478,15 @@ __device__ __forceinline__ void sx_st(T *p, const Pk<T, N> &x) { *reinterpret_ca
 // pair shares its edge, so every stream and the four K-run gathers move as
 // 8-byte (f32) / 16-byte (f64) accesses, and the endpoint loads and the
 // index division are paid once per pair)
+// one lane's L entries [i, i + L) of the (edge, label) sweep, i < EK: the
+// body of k_sx_edge_sweep, shared with the one-workgroup k_sx_tiny_iterate
 template <typename real, int L>
-__global__ __launch_bounds__(256) void k_sx_edge_sweep(
-    long EK, SxConst<real> c, const int *__restrict__ Eu,
-    const int *__restrict__ Ev, const SxR2<real> *__restrict__ PF,
-    real *__restrict__ Zu, real *__restrict__ Zv,
+__device__ __forceinline__ void sx_edge_lane(
+    long i, long EK, const SxConst<real> &c, const int *__restrict__ Eu,
+    const int *__restrict__ Ev, const SxR2<real> *PF, real *Zu, real *Zv,
     const real *__restrict__ A1, const real *__restrict__ La_d1,
     const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
-    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
-    const Ctrl<real> *ctrl, int nb, int xcd) {
-    if (ctrl && ctrl->halt) return;
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
-    if (blk >= nb) return;
-    const long i = ((long)blk * blockDim.x + threadIdx.x) * L;
-    if (i >= EK) return;
+    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *wz, real rho) {
     const int K = c.K;
     long e;
     int k;
@@ -561,6 +556,23 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
             wz[EK + i + j] = wsv[j] * zv.v[j];
         }
     }
+}
+
+template <typename real, int L>
+__global__ __launch_bounds__(256) void k_sx_edge_sweep(
+    long EK, SxConst<real> c, const int *__restrict__ Eu,
+    const int *__restrict__ Ev, const SxR2<real> *__restrict__ PF,
+    real *__restrict__ Zu, real *__restrict__ Zv,
+    const real *__restrict__ A1, const real *__restrict__ La_d1,
+    const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
+    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
+    const Ctrl<real> *ctrl, int nb, int xcd) {
+    if (ctrl && ctrl->halt) return;
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;
+    const long i = ((long)blk * blockDim.x + threadIdx.x) * L;
+    if (i >= EK) return;
+    sx_edge_lane<real, L>(i, EK, c, Eu, Ev, PF, Zu, Zv, A1, La_d1, GI, Wd1u, Wd1v, Th, wz, rho);
 }
 
 template <typename real>
@@ -655,20 +667,21 @@ struct SxVArgs {
     const Ctrl<real> *ctrl;
 };
 
+// One block of the fused vertex sweep: NT lanes (t = the lane within
+// them) with their own xs / ms / red in LDS.  Every lane of the calling
+// workgroup reaches the same barriers (a block past the last, blk >= nb, has
+// no live lane); the block's evolution partial goes to *part_out (lane 0).
+// The body of k_sx_vertex_sweep, shared with the one-workgroup
+// k_sx_tiny_iterate (four blocks side by side).
 template <typename real, int NT, bool WZ>
-__global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
-    if (a.ctrl && a.ctrl->halt) return;
-    __shared__ real xs[NT], ms[NT];
-    __shared__ real red[NT / kWave];
+__device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
+                                                real *ms, real *red, real *part_out) {
     const int K = a.c.K, vb = a.vb;
-    const int t = threadIdx.x;
     const int vl = t / K;
     const int k = t - vl * K;
-    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
-    if (blk >= a.nb) return;
     const long v0 = (long)blk * vb;
     const long v = v0 + vl;
-    const bool live = vl < vb && v < a.V;
+    const bool live = blk < a.nb && vl < vb && v < a.V;
     const long i = v * K + k;
     if (live) {
         const real inv = WZ ? real(0) : a.invAux[i];  // 1/Aux of this (v, k)
@@ -723,7 +736,7 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     }
     __syncthreads();
     real dif = real(0);
-    if (t < vb && v0 + t < a.V) {
+    if (blk < a.nb && t < vb && v0 + t < a.V) {
         real *x = xs + t * K;
         proj_simplex_column<real, 1>(x, ms + t * K, K, real(1));
         if (a.track == 2) {
@@ -756,7 +769,120 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
             __syncthreads();
             if (t == 0) for (int q = 1; q < NT / kWave; q++) dif += red[q];
         }
-        if (t == 0) a.part[blk] = dif;
+        if (t == 0 && blk < a.nb) *part_out = dif;
+    }
+}
+
+template <typename real, int NT, bool WZ>
+__global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real xs[NT], ms[NT];
+    __shared__ real red[NT / kWave];
+    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (blk >= a.nb) return;
+    sx_vertex_block<real, NT, WZ>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+}
+
+// ------------------------------------------ small problems, one launch --
+// Up to `iters` whole iterations of a small single-GPU simplex problem in ONE
+// workgroup of 1024 lanes: the edge pass (sx_edge_lane over the (edge,
+// label) entries), the vertex pass four 256-lane blocks side by side
+// (sx_vertex_block, the fused vertex sweep's blocks with their partials in
+// LDS), then k_sx_finalize's reduction and decision on a register copy of
+// the control block.  The same device code and operation order as the
+// three-launch loop, so the iterates, iteration counts and the evolution
+// record are identical bit for bit; what goes is the launches that bound
+// cut pursuit's reduced problems.
+constexpr int kSxTiny = 1024;
+constexpr int kSxTinyMaxBlocks = 32;
+// default limits (PFDR_SX_TINY widens the entry limit and the block cap to
+// 32): against the three launches (graph-replayed), us/iteration on 8-nbr
+// grids, K = 4 (profiles/r2/r3m_exp_sx_tiny.log): f32 1 block 6.6 vs 11.0,
+// 4 blocks 11.1 vs 11.9, 9 blocks 25 vs 11.8; f64 1 block 8.0 vs 12.4, 4
+// blocks 14.2 vs 12.7 -- one CU's throughput loses beyond a few blocks
+template <typename real> struct SxTinyBlocks { static constexpr int v = 4; };
+template <> struct SxTinyBlocks<double> { static constexpr int v = 2; };
+constexpr long kSxTinyEK = 1L << 16;
+
+template <typename real>
+struct SxTinyArgs {
+    long EK;
+    SxConst<real> c;
+    const int *Eu, *Ev;
+    real *Zu, *Zv;
+    const real *A1, *La_d1, *Wd1u, *Wd1v, *Th;
+    const SxR2<real> *GI;
+    real rho;
+    SxVArgs<real> va;   // every block of the fused vertex sweep
+    Ctrl<real> *ctrl;   // null: no tracking, run exactly `iters`
+    real *Dif;
+    long V;             // vertices (the l1 evolution's normalisation)
+    int iters;
+};
+
+template <typename real, int L>
+__global__ __launch_bounds__(kSxTiny) void k_sx_tiny_iterate(SxTinyArgs<real> t) {
+    constexpr int NB = kSxTiny / kBlock;  // vertex blocks side by side
+    __shared__ real xs[kSxTiny], ms[kSxTiny];
+    __shared__ real red[kSxTiny / kWave];
+    __shared__ real bpart[kSxTinyMaxBlocks + NB];
+    __shared__ real wred[kBlock / kWave];
+    __shared__ int halt;
+    const int tid = threadIdx.x, sub = tid / kBlock, lt = tid & (kBlock - 1);
+    const SxVArgs<real> &a = t.va;
+    Ctrl<real> c{};
+    if (tid == 0) {
+        if (t.ctrl) c = *t.ctrl;
+        halt = t.ctrl ? c.halt : 0;
+    }
+    __syncthreads();
+    for (int it = 0; it < t.iters; it++) {
+        if (halt) break;  // uniform (set by lane 0 before the last barrier)
+        for (long i = (long)tid * L; i < t.EK; i += (long)kSxTiny * L)
+            sx_edge_lane<real, L>(i, t.EK, t.c, t.Eu, t.Ev, a.PF, t.Zu, t.Zv, t.A1, t.La_d1, t.GI,
+                                  t.Wd1u, t.Wd1v, t.Th, nullptr, t.rho);
+        __syncthreads();
+        for (int b0 = 0; b0 < a.nb; b0 += NB) {
+            const int blk = b0 + sub;
+            sx_vertex_block<real, kBlock, false>(a, blk, lt, xs + sub * kBlock, ms + sub * kBlock,
+                                                 red + sub * (kBlock / kWave), bpart + blk);
+            __syncthreads();  // xs / ms / red reused by the next four blocks
+        }
+        if (t.ctrl) {  // k_sx_finalize on the first 256 lanes: its loop and block_sum's tree
+            real sm = real(0);
+            if (a.track) {
+                if (tid < kBlock)
+                    for (int i = tid; i < a.nb; i += kBlock) sm += bpart[i];
+                sm = wave_sum(sm);
+                if ((tid & (kWave - 1)) == 0 && tid < kBlock) wred[tid / kWave] = sm;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                real s = real(0);
+                if (a.track)
+                    for (int i = 0; i < kBlock / kWave; i++) s += wred[i];
+                int itc = c.it;
+                if (a.track) {
+                    real dif = s;
+                    if (a.track == 1) dif /= t.V;  // relative l1 evolution (ref :688)
+                    c.dif = dif;
+                    if (t.Dif) t.Dif[itc] = dif;
+                }
+                itc++;
+                c.it = itc;
+                const real dif = c.dif;
+                if (itc >= c.itMax || dif < c.difTol) {
+                    c.stop = 1;
+                    c.halt = 1;
+                } else if (dif < c.difRcd) {
+                    c.recond = 1;
+                    c.halt = 1;
+                }
+                *t.ctrl = c;
+                halt = c.halt;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -1025,6 +1151,10 @@ class SimplexSession final : public SessionBase {
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
+    // small single-GPU problems: a chunk of iterations in one workgroup
+    // (k_sx_tiny_iterate; PFDR_SX_TINY = most (edge, label) entries, 0 off)
+    bool tiny_ = false;
+    void tiny_chunk(int n);
     hipGraphExec_t chunk_graph();
     void drop_graphs() {
         for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
@@ -1185,6 +1315,14 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         const char *g = getenv("PFDR_GRAPH");
         graphs_ok_ = !(g && g[0] == '0') && !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
     }
+    {
+        const char *t = getenv("PFDR_SX_TINY");
+        const long maxEK = t ? atol(t) : kSxTinyEK;
+        tiny_ = maxEK > 0 && !halo_ && !rec_obj_ && vb_ && sx_nt_ == kBlock && !sx_wz_ &&
+                EK_ > 0 && EK_ <= maxEK && nbs_ <= (t ? kSxTinyMaxBlocks : SxTinyBlocks<real>::v);
+        tiny = tiny_ ? 1 : 0;
+        if (tiny_) graphs_ok_ = false;
+    }
     if (graphs_ok_) (void)chunk_graph();  // instantiated with the setup
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
@@ -1342,6 +1480,29 @@ void SimplexSession<real>::push_wz() {
     halo_->push_packed(buf, Zv_.p + EK_, eb, stream);  // the tail of Zv (vertex sweep)
 }
 
+template <typename real>
+void SimplexSession<real>::tiny_chunk(int n) {
+    const bool gated = track_ || rec_obj_;
+    SxTinyArgs<real> t{};
+    t.EK = EK_; t.c = c_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Zu = Zu_.p; t.Zv = Zv_.p;
+    t.A1 = A1_.p; t.La_d1 = La_d1_.p; t.Wd1u = Wd1u_.p; t.Wd1v = Wd1v_.p; t.Th = Th_.p;
+    t.GI = GI_.p; t.rho = rho_;
+    SxVArgs<real> &a = t.va;
+    a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
+    a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
+    a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = nullptr;
+    a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
+    a.nb = nbs_; a.xcd = 0;
+    t.ctrl = gated ? ctrl_.p : nullptr;
+    t.Dif = rec_dif_ ? Dif_.p : nullptr;
+    t.V = Vglob_;
+    t.iters = n;
+    ProfScope ps(prof, "sx_tiny_iterate", stream);
+    if (K_ % 2 == 0 && sx_pair_) k_sx_tiny_iterate<real, 2><<<1, kSxTiny, 0, stream>>>(t);
+    else k_sx_tiny_iterate<real, 1><<<1, kSxTiny, 0, stream>>>(t);
+    PFDR_HIP(hipGetLastError());
+}
+
 // the captured graph of a whole chunk (chunk_ bodies), instantiated once --
 // at the end of the setup, and again after a reconditioning dropped it
 template <typename real>
@@ -1383,7 +1544,8 @@ int SimplexSession<real>::run(int iters) {
     const int target = (int)std::min<long>((long)it_ + std::max(iters, 0), (long)itMax_);
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
-        run_bodies(n);
+        if (tiny_) tiny_chunk(n);
+        else run_bodies(n);
         if (gated) {
             PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
             wait_stream();

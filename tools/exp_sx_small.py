@@ -15,7 +15,8 @@ from cp_pfdr_graph_d1_amd import pfdr  # noqa: E402
 from cp_pfdr_graph_d1_amd.graphs import grid_graph  # noqa: E402
 
 
-KNOB = sys.argv[1] if len(sys.argv) > 1 else "PFDR_GRAPH"  # or PFDR_FUSE
+KNOB = sys.argv[1] if len(sys.argv) > 1 else "PFDR_GRAPH"  # or PFDR_SX_TINY
+ON = sys.argv[2] if len(sys.argv) > 2 else "1"  # the knob's "on" value
 
 
 def us_per_it(shape, dt, graph, K=4, it=1000):
@@ -41,7 +42,7 @@ def us_per_it(shape, dt, graph, K=4, it=1000):
 
 torch.cuda.init()
 for dt in (np.float32, np.float64):
-    for shape in ((16, 16), (40, 40), (100, 100), (300, 300)):
-        r = {g: [us_per_it(shape, dt, g) for _ in range(2)] for g in ("1", "0")}
+    for shape in ((8, 8), (16, 16), (24, 24), (32, 32), (40, 40), (64, 64), (100, 100)):
+        r = {g: [us_per_it(shape, dt, g) for _ in range(2)] for g in (ON, "0")}
         print("%-4s %-8s %s on %7.2f %7.2f   off %7.2f %7.2f us/it" % (
-            np.dtype(dt).name[5:], "%dx%d" % shape, KNOB, *r["1"], *r["0"]), flush=True)
+            np.dtype(dt).name[5:], "%dx%d" % shape, KNOB, *r[ON], *r["0"]), flush=True)
