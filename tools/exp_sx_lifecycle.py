@@ -2,7 +2,8 @@
 iterations: session create / run / result copy-out / close, in ms, for
 grid sizes like cut pursuit's reduced simplex problems (copy_ms
 ~1.3 ms a call), with and without the chunk graph (PFDR_GRAPH).
-Usage: python tools/exp_sx_lifecycle.py"""
+Usage: python tools/exp_sx_lifecycle.py [SHAPES]   (e.g. 60x60,120x120;
+other knobs, e.g. PFDR_SX_NT=64, from the environment)"""
 import os
 import sys
 import time
@@ -40,7 +41,8 @@ def phases(shape, graph, K=4, it=223, dt=np.float32):
 
 torch.cuda.init()
 phases((16, 16), "1")
-for shape in ((120, 120), (240, 240)):
+SHAPES = sys.argv[1] if len(sys.argv) > 1 else "120x120,240x240"
+for shape in [tuple(int(n) for n in t.split("x")) for t in SHAPES.split(",")]:
     for g in ("1", "0"):
         for rep in range(3):
             c, r, o, d = phases(shape, g)
