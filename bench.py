@@ -20,10 +20,12 @@ updates / max-over-ranks time.  The ranks bootstrap over a gloo (host)
 process group; the one RCCL communicator of the process is the library's
 (halo exchanges, scalar all-reduces, the max-over-ranks timing reduction).
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
-(HIP events on the session stream over the timed region; PMC traffic from
-profiles/pmc_traffic.json) and the reference CPU path timed on this host
-(bounded sample, its own process, before this process touches the GPU).
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel and
+of every sweep beside it (HIP events on the session stream over the timed
+region; SURVEY.md §8(d)'s bytes split per sweep as tools/workloads.py states;
+PMC traffic from profiles/pmc/<workload>.json), the whole iteration's
+fraction, and the reference CPU path timed on this host (bounded sample, its
+own process, before this process touches the GPU).
 `--workload c1..c5` selects the other BASELINE.json configs
 (tools/workloads.py), measured for DESIGN.md; the driver's line is the
 default headline.
@@ -153,21 +155,29 @@ def run_cpu_baseline(args):
         return {"value": None, "error": repr(ex)[:300]}
 
 
-def pmc_traffic(kernel, E):
-    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
-    when it was taken on this workload size AND on the kernel sources built
-    into this library (sha256 of csrc/*.hip, *.hpp); else (None, reason)."""
+def pmc_summary(wl, E):
+    """The committed rocprofv3 PMC summary of this workload
+    (profiles/pmc/<workload>.json, written by tools/pmc_traffic.py) when it
+    was taken on this size AND on the kernel sources built into this library
+    (sha256 of the solver's csrc sources); else (None, reason)."""
     try:
         from kernel_hash import kernel_source_sha256
-        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc", wl.name + ".json")))
         if d.get("workload_E") != E:
-            return None, "PMC summary taken on another workload"
-        if d.get("kernel_source_sha256") != kernel_source_sha256():
+            return None, "PMC summary taken on another size"
+        if d.get("kernel_source_sha256") != kernel_source_sha256(wl.pmc):
             return None, "stale: PMC summary taken on other kernel sources"
-        return d["kernels"][kernel]["hbm_bytes_per_launch"], None
+        return d["kernels"], None
     except Exception as ex:
         return None, "no PMC summary (%s)" % type(ex).__name__
+
+
+# every launch of a kernel family once per iteration: a partitioned session's
+# boundary launches (edge_sweep_b, vertex_sweep_b) complete the interior ones
+FAMILIES = {"edge_sweep": ("edge_sweep", "edge_sweep_b"),
+            "vertex_sweep": ("vertex_sweep", "vertex_sweep_b"),
+            "sx_edge_sweep": ("sx_edge_sweep",), "sx_vertex_sweep": ("sx_vertex_sweep",),
+            "gemv_cols": ("gemv_cols",), "gemv_rows": ("gemv_rows",), "symv": ("symv",)}
 
 
 def main():
@@ -286,7 +296,7 @@ def main():
         del kw
     names = (wl.dominant, "edge_sweep", "edge_sweep_b", "vertex_sweep", "vertex_sweep_b",
              "sx_edge_sweep", "sx_vertex_sweep", "sx_average", "sx_project", "gemv_rows",
-             "gemv_cols", "halo_pull", "halo_push")
+             "gemv_cols", "halo_pull", "halo_push", "seq_evolution")
     stats = {k: sess.kernel_stats(k) for k in names}
     res = res_timed if converge else sess.result()
     finite = bool(np.all(np.isfinite(res[0])))
@@ -294,17 +304,14 @@ def main():
     reordered = bool(sess.query("reordered"))
     quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
     split_blocks = sess.query("split_blocks") if quad else 0
-    chunks = sess.query("pipeline_chunks") if quad else 0
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
-    # partitioned with halo overlap: the timed "edge_sweep" launch covers the
-    # interior edges only (the boundary edges run after the halo pull)
-    E_dom = sess.query("interior_edges") if quad else E
-    # the edge sweep's kernel: u ends staged in LDS for u-sorted edges
-    kname = "k_" + wl.dominant
-    if wl.dominant == "edge_sweep" and quad and sess.query("ustaged"):
-        kname = "k_edge_sweep_us"
-    if wl.dominant == "symv" and symv:
-        kname = "k_symv_tiles+k_symv_finish"
+    seqdif = sess.query("seqdif")
+    # kernel names behind each family (rocprof / PMC summaries)
+    knames = {f: ["k_" + f] for f in FAMILIES}
+    if quad and sess.query("ustaged"):  # u ends staged in LDS for u-sorted edges
+        knames["edge_sweep"] = ["k_edge_sweep_us"]
+    if symv:
+        knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
     sess.close()
     if comm:
         from cp_pfdr_graph_d1_amd import partition
@@ -314,10 +321,28 @@ def main():
     if rank != 0:
         return
     ms_step = el_max / max(done, 1) * 1e3
-    traffic, traffic_note = pmc_traffic(kname, E)
-    n_dom, ms_dom = stats[wl.dominant]
-    alg = wl.dominant_bytes(V, E_dom)
-    achieved = alg / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
+    # per kernel family: SURVEY.md 8(d)'s bytes of that sweep (tools/workloads.py
+    # kernel_bytes) over its mean time per iteration (HIP events, timed region)
+    pmc, pmc_note = pmc_summary(wl, E)
+    kbytes = wl.kernel_bytes(V, E)
+    kernels = {}
+    for fam, alg_b in kbytes.items():
+        ms = sum(stats[k][1] for k in FAMILIES[fam] if k in stats and stats[k][0])
+        if ms <= 0:
+            continue
+        gbs = alg_b / (ms * 1e-3) / 1e9
+        row = {"kernel": "+".join(knames[fam]), "algorithmic_bytes": int(alg_b),
+               "mean_ms": round(ms, 5), "achieved_GBps": round(gbs, 1),
+               "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if pmc is not None and all(k in pmc for k in knames[fam]):
+            t = sum(pmc[k]["hbm_bytes_per_launch"] for k in knames[fam])
+            row["pmc_bytes"] = int(t)
+            row["pmc_over_algorithmic"] = round(t / alg_b, 3)
+            row["pmc_GBps"] = round(t / (ms * 1e-3) / 1e9, 1)
+        kernels[fam] = row
+    dom = kernels.get(wl.dominant, {})
+    it_bytes = wl.iteration_bytes(V, E)
+    it_gbs = it_bytes / (ms_step * 1e-3) / 1e9
     out = {
         "metric": wl.metric,
         "value": round(E_all * done / el_max / 1e6, 2),
@@ -342,34 +367,31 @@ def main():
             "device_bytes": dev_bytes,
             "relabelled": reordered,
             "split_incidence_blocks": split_blocks,
-            "pipeline_chunks": chunks,
+            "sequential_evolution": bool(seqdif),
             **({"symv_upper_triangle": bool(symv)} if wl.dominant == "symv" else {}),
             "finite": finite,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": kname,
-            "achieved": None if achieved is None else round(achieved, 1),
+            "kernel": dom.get("kernel"),
+            "achieved": dom.get("achieved_GBps"),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            **({"traffic_note": traffic_note} if traffic_note else {}),
-            "algorithmic_bytes_per_launch": int(alg),
+            "frac": dom.get("frac"),
+            "traffic": dom.get("pmc_bytes"),
+            **({"traffic_note": pmc_note} if pmc_note else {}),
+            "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes"),
             "timed_launches": "every %d-th launch of %s" % (period, ", ".join(
                 k for k in timed if stats.get(k, (0,))[0])),
-            "launches": n_dom,
-            "mean_ms": round(ms_dom, 5),
+            "launches": stats[wl.dominant][0],
+            "mean_ms": dom.get("mean_ms"),
+            "kernels": kernels,
             "kernels_mean_ms": {k: round(v[1], 5) for k, v in stats.items() if v[0]},
-            "iteration_algorithmic_GBps": round(wl.iteration_bytes(V, E) / (ms_step * 1e-3) / 1e9, 1),
+            "iteration": {"algorithmic_bytes": int(it_bytes), "achieved_GBps": round(it_gbs, 1),
+                          "frac": round(it_gbs / HBM_PEAK_GBS, 4)},
         },
         "cpu_baseline": cpu,
     }
-    if achieved is not None and achieved > HBM_PEAK_GBS:
-        out["roofline"]["frac_note"] = (
-            "above 1: SURVEY.md 8(d)'s per-unit figure counts the reference's array layout "
-            "(every per-edge weight array streamed); this kernel recomputes the weights from "
-            "their factors and moves fewer bytes (DESIGN.md section 4)")
     if extra:
         out["extra"] = extra
     if converge:

@@ -3,12 +3,33 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <mutex>
+#include <set>
 
-#include "pfdr_dev.hpp"
+#include "pfdr_halo.hpp"
 
 namespace pfdr {
 int report_rccl(const char *fn, ncclResult_t r);
+
+// Communicators the watchdog aborted.  The handle belongs to the caller
+// (pfdr_comm_init made it), so a timed-out session cannot simply free it:
+// ncclCommAbort releases the communicator, and the caller's normal clean-up
+// (pfdr_comm_destroy in a finally block) must then not destroy it again.
+static std::mutex g_aborted_m;
+static std::set<void *> g_aborted;
+
+void comm_abort(void *comm) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    if (!comm || g_aborted.count(comm)) return;
+    (void)ncclCommAbort((ncclComm_t)comm);
+    g_aborted.insert(comm);
 }
+
+bool comm_aborted(void *comm) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    return g_aborted.count(comm) != 0;
+}
+}  // namespace pfdr
 
 int pfdr::report_rccl(const char *fn, ncclResult_t r) {
     char msg[256];
@@ -42,6 +63,10 @@ extern "C" int pfdr_comm_init(void **comm_out, int nranks, int rank, const void 
 
 extern "C" int pfdr_comm_destroy(void *comm) {
     if (!comm) return PFDR_OK;
+    {   // aborted by the watchdog: already released, forget the handle
+        std::lock_guard<std::mutex> l(pfdr::g_aborted_m);
+        if (pfdr::g_aborted.erase(comm)) return PFDR_OK;
+    }
     ncclResult_t r = ncclCommDestroy((ncclComm_t)comm);
     if (r != ncclSuccess) return pfdr::report_rccl("pfdr_comm_destroy", r);
     return PFDR_OK;
@@ -50,6 +75,9 @@ extern "C" int pfdr_comm_destroy(void *comm) {
 // max-reduce one host double over the ranks (timing: max over ranks)
 extern "C" int pfdr_comm_allreduce_max_f64(void *comm, double *value) {
     if (!comm || !value) return pfdr::report_error("pfdr_comm_allreduce_max_f64", "null argument");
+    if (pfdr::comm_aborted(comm))
+        return pfdr::report_error("pfdr_comm_allreduce_max_f64",
+                                  "communicator aborted by the watchdog (PFDR_COMM_TIMEOUT)");
     try {
         hipStream_t s = pfdr::lib_stream();
         pfdr::DevBuf<double> d(1);

@@ -238,8 +238,7 @@ static void segsum(int G, const int *off, const int *idx, const real *val, real 
     k_segsum_short<real><<<dim3(grid_for(G), nv), kBlock, 0, s>>>(G, off, idx, val, out, longs.p,
                                                                   nlong.p, vstride);
     int nl = d2h_scalar(nlong.p, s);
-    const char *mo = getenv("PFDR_SEGMONO");  // A/B: 0 keeps one workgroup per long segment
-    if (nl && !(mo && mo[0] == '0')) {
+    if (nl) {
         std::vector<int> hl(nl), hb(2 * (size_t)nl);
         DevBuf<int> db(2 * (size_t)nl);
         k_seg_bounds<<<grid_for(nl), kBlock, 0, s>>>(nl, longs.p, off, db.p);
@@ -391,77 +390,16 @@ __device__ __forceinline__ unsigned long long claim_key(int i, int j) {
 // after the other.
 constexpr int kSub = 16;
 
-// frontier L[lo, hi): every unvisited neighbour through an inactive edge is
-// claimed by its first visit in the reference's order (queue position i,
-// then the arc's rank j in the maxflow graph's list: slots descending)
-__global__ void k_bfs_claim(int lo, int hi, const int *__restrict__ L, const int *__restrict__ ptr,
-                            const unsigned *__restrict__ slot, const int *__restrict__ Eu,
-                            const int *__restrict__ Ev, const uint8_t *__restrict__ active,
-                            const int *__restrict__ Cv, unsigned long long *claim) {
-    const long gt = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = lo + (int)(gt / kSub), l = (int)(gt % kSub);
-    if (i >= hi) return;
-    const int v = L[i];
-    const int top = ptr[v + 1] - 1, deg = top + 1 - ptr[v];
-    for (int j = l; j < deg; j += kSub) {
-        const unsigned a = slot[top - j];
-        if (active[a >> 1]) continue;
-        const int w = arc_head(a, Eu, Ev);
-        if (Cv[w] != -1) continue;
-        atomicMin(claim + w, claim_key(i, j));
-    }
-}
-
-// EMIT = false: cnt[i - lo] = claims won by L[i]; true: append them in
-// arc order at hi + cnt[i - lo] (the exclusive scan of the counts)
-template <bool EMIT>
-__global__ void k_bfs_take(int lo, int hi, const int *__restrict__ ptr,
-                           const unsigned *__restrict__ slot, const int *__restrict__ Eu,
-                           const int *__restrict__ Ev, const uint8_t *__restrict__ active,
-                           const unsigned long long *__restrict__ claim, int *__restrict__ cnt,
-                           int *L, int *Cv) {
-    const long gt = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = lo + (int)(gt / kSub), l = (int)(gt % kSub);
-    const int sh = (threadIdx.x & (kWave - 1)) & ~(kSub - 1);  // subgroup's first lane
-    if (i >= hi) return;
-    const int v = L[i];
-    const int top = ptr[v + 1] - 1, deg = top + 1 - ptr[v];
-    int c = 0, base = 0, cv = 0;
-    if (EMIT) {
-        base = hi + cnt[i - lo];
-        cv = Cv[v];
-    }
-    for (int j0 = 0; j0 < deg; j0 += kSub) {
-        const int j = j0 + l;
-        bool win = false;
-        int w = 0;
-        if (j < deg) {
-            const unsigned a = slot[top - j];
-            if (!active[a >> 1]) {
-                w = arc_head(a, Eu, Ev);
-                win = claim[w] == claim_key(i, j);
-            }
-        }
-        const unsigned long long m = __ballot(win);
-        const unsigned mine = (unsigned)(m >> sh) & ((1u << kSub) - 1);
-        if (EMIT && win) {
-            const int p = base + c + __builtin_popcount(mine & ((1u << l) - 1));
-            L[p] = w;
-            Cv[w] = cv;
-        }
-        c += __builtin_popcount(mine);
-    }
-    if (!EMIT && l == 0) cnt[i - lo] = c;
-}
-
-// ---- the same levels driven from the device: the frontier bounds live in a
-// control block (lo, hi, done, overflow), every kernel of a level reads
-// them, fixed grids loop over the frontier, and a one-lane kernel advances
-// the bounds; the host enqueues levels in batches (one hipGraph replay each)
-// and reads the control block once per batch instead of once per level
-// (each host round trip cost ~40 us of a ~60 us level).
-// The claims, counts and emission order are those of the per-level kernels
-// above, so L, Cv and Vc are identical.
+// ---- breadth-first levels driven from the device.  Frontier L[lo, hi):
+// every unvisited neighbour through an inactive edge is claimed by its first
+// visit in the reference's order (queue position i, then the arc's rank j in
+// the maxflow graph's list: slots descending); the winners are counted,
+// scanned and appended in arc order.  The frontier bounds live in a control
+// block (lo, hi, done, overflow), every kernel of a level reads them, fixed
+// grids loop over the frontier, and a one-lane kernel advances the bounds;
+// the host enqueues levels in batches (one hipGraph replay each) and reads
+// the control block once per batch instead of once per level (a host round
+// trip per level cost ~40 us of a ~60 us level).
 struct BfsCtl {
     int lo, hi, done, overflow;
 };
@@ -1230,32 +1168,7 @@ void CpGraphBase::components() {
     rV = d2h_scalar(i2.p + Vn, s);
     k_bfs_roots<<<grid_for(Vn), kBlock, 0, s>>>(Vn, i1.p, i2.p, L.p, Cv.p, claim.p);
     PFDR_HIP(hipGetLastError());
-    const char *bd = getenv("PFDR_BFS_HOST");  // A/B: 1 = one host round trip per level
-    if (!(bd && bd[0] == '1')) {
-        bfs_device();
-    } else {
-    // levels; i1/i2 reused as per-frontier counts / offsets
-    int lo = 0, hi = rV;
-    while (hi > lo && hi < Vn) {
-        const int n = hi - lo;
-        const int gb = grid_for((long)n * kSub);
-        k_bfs_claim<<<gb, kBlock, 0, s>>>(lo, hi, L.p, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
-                                                   active.p, Cv.p, claim.p);
-        k_bfs_take<false><<<gb, kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
-                                                         active.p, claim.p, i1.p, L.p, Cv.p);
-        PFDR_HIP(hipMemsetAsync(i1.p + n, 0, sizeof(int), s));
-        excl_scan(tmp, i1.p, i2.p, n + 1, s);
-        const int add = d2h_scalar(i2.p + n, s);
-        if (add == 0) break;
-        if (add > Vn - hi) throw std::runtime_error("components: BFS overflow");
-        k_bfs_take<true><<<gb, kBlock, 0, s>>>(lo, hi, inc.ptr.p, inc.idx.p, Eu.p, Ev.p,
-                                                        active.p, claim.p, i2.p, L.p, Cv.p);
-        PFDR_HIP(hipGetLastError());
-        lo = hi;
-        hi += add;
-    }
-    if (hi != Vn) throw std::runtime_error("components: BFS did not reach every vertex");
-    }
+    bfs_device();
     // Vc = the concatenated levels stably sorted by component
     DevBuf<unsigned> key(Vn), skey(Vn);
     Vc.alloc(Vn);

@@ -103,33 +103,6 @@ __device__ __forceinline__ T block_sum(T v, T *lds /* >= kBlock/64 */) {
     return s;
 }
 
-// Grid-wide barrier of a persistent launch whose workgroups are all
-// resident (hipLaunchCooperativeKernel).  bar[0] counts arrivals, bar[1] is
-// the generation: the last workgroup to arrive resets the count and bumps
-// the generation the others wait on.  The agent-scope fences on both sides
-// publish this workgroup's writes to the other XCDs (their L2s are not
-// coherent with ours) and drop stale lines from our caches afterwards.
-// Device-scope atomics and vector stores only.
-__device__ __forceinline__ void grid_sync(unsigned *bar, unsigned nblocks) {
-    __syncthreads();  // every wave's stores are in L2 (L1 writes through)
-    if (threadIdx.x == 0) {
-        // one L2 write-back per workgroup, then arrive
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            nblocks - 1) {
-            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
-                __builtin_amdgcn_s_sleep(1);
-        }
-        // drop stale lines (the CU's L1 for all its waves, and L2)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-}
-
 // packed vector of N T (16-byte accesses)
 template <typename T, int N>
 struct alignas(sizeof(T) * N) Pk { T v[N]; };

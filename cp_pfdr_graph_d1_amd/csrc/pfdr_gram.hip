@@ -299,147 +299,6 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
         }
 }
 
-// f32, wide tile (opt-in, PFDR_GRAM_WIDE=1): one block = a 256 x 256 tile,
-// 8 waves (512 threads) 2 x 4 over it, each wave a 128 x 64 quadrant = 4 x 2
-// tiles of v_mfma_f32_32x32x2_f32 (128 accumulators per lane), so every
-// operand fragment read from LDS feeds 2-4 MFMAs and each staged K slice
-// carries twice k_gram_v's matrix work per byte fetched.  One block per CU
-// (registers, 99 KB of LDS): the K slices are double-buffered in LDS (one
-// barrier per slice) with the next slice's 16-byte global loads in flight
-// during the MFMAs.  Requires ld % 4 == 0 and a 16-byte aligned A.
-// Measured no faster than k_gram_v (r2j, r2k).
-struct GramW {
-    static constexpr int BT = 256, BK = 16, T = 32, WI = 128, WJ = 64, NI = 4, NJ = 2, VW = 4;
-    static constexpr int NTH = 512;
-    static constexpr int NL = BT * BK / (NTH * VW);  // 16-byte loads per operand per lane
-};
-
-template <int LAYOUT>
-__global__ __launch_bounds__(512, 1) void k_gram_w(int P, long K, const float *__restrict__ A,
-                                                   long ld, long kchunk, int nchunk,
-                                                   float *__restrict__ Gpart) {
-    using M = Mfma<float>;
-    using W = GramW;
-    constexpr int BT = W::BT, BK = W::BK, T = W::T, VW = W::VW, NL = W::NL, NTH = W::NTH;
-    constexpr int WI = W::WI, WJ = W::WJ, NI = W::NI, NJ = W::NJ;
-    constexpr int PADC = LAYOUT == GRAM_TN ? 1 : VW;
-    int bi, bj, z;
-    if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
-    const long k0 = (long)z * kchunk;
-    const long k1 = min(K, k0 + kchunk);
-    float *G = Gpart + (size_t)z * P * P;
-    __shared__ alignas(16) float Ls[2][BK][BT + PADC], Rs[2][BK][BT + PADC];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wi = w & 1, wj = w >> 1;  // 2 x 4 waves
-    const long i0 = (long)bi * BT, j0 = (long)bj * BT;
-    M::acc_t acc[NI][NJ];
-#pragma unroll
-    for (int a = 0; a < NI; a++)
-#pragma unroll
-        for (int b = 0; b < NJ; b++)
-#pragma unroll
-            for (int r = 0; r < M::NR; r++) acc[a][b][r] = 0.f;
-    Pk<float, VW> lr[NL], rr[NL];
-    auto load = [&](long kb) {
-#pragma unroll
-        for (int q = 0; q < NL; q++) {
-            const int f = t + NTH * q;
-            int i, k;
-            if (LAYOUT == GRAM_NT) { k = f / (BT / VW); i = (f - k * (BT / VW)) * VW; }
-            else { i = f / (BK / VW); k = (f - i * (BK / VW)) * VW; }
-            const long kk = kb + k;
-#pragma unroll
-            for (int side = 0; side < 2; side++) {
-                const long base = side ? j0 : i0;
-                Pk<float, VW> &o = side ? rr[q] : lr[q];
-                const bool full = LAYOUT == GRAM_NT ? (kk < k1 && base + i + VW <= P)
-                                                    : (kk + VW <= k1 && base + i < P);
-                if (full) {
-                    o = LAYOUT == GRAM_NT ? ldv<float, VW>(A + (base + i) + kk * ld)
-                                          : ldv<float, VW>(A + kk + (base + i) * ld);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < VW; u++) {
-                        const long ii = LAYOUT == GRAM_NT ? base + i + u : base + i;
-                        const long ku = LAYOUT == GRAM_NT ? kk : kk + u;
-                        o.v[u] = (ii < P && ku < k1) ? gram_elem<float, LAYOUT>(A, ld, ii, ku)
-                                                     : 0.f;
-                    }
-                }
-            }
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < NL; q++) {
-            const int f = t + NTH * q;
-            if (LAYOUT == GRAM_NT) {
-                const int k = f / (BT / VW), i = (f - k * (BT / VW)) * VW;
-                stv<float, VW>(&Ls[buf][k][i], lr[q]);
-                stv<float, VW>(&Rs[buf][k][i], rr[q]);
-            } else {
-                const int i = f / (BK / VW), k = (f - i * (BK / VW)) * VW;
-#pragma unroll
-                for (int u = 0; u < VW; u++) {
-                    Ls[buf][k + u][i] = lr[q].v[u];
-                    Rs[buf][k + u][i] = rr[q].v[u];
-                }
-            }
-        }
-    };
-    if (k0 < k1) load(k0);
-    int buf = 0;
-    for (long kb = k0; kb < k1; kb += BK, buf ^= 1) {
-        store(buf);
-        __syncthreads();  // also: every wave is done with this buffer's previous slice
-        if (kb + BK < k1) load(kb + BK);
-        // operand fragments of the next K step read from LDS while the
-        // matrix cores work on this one (one wave per SIMD: nothing else
-        // hides the LDS latency)
-        const int c = lane % T;
-        float a[2][NI], b[2][NJ];
-#pragma unroll
-        for (int q = 0; q < NI; q++) a[0][q] = Ls[buf][lane / T][wi * WI + q * T + c];
-#pragma unroll
-        for (int q = 0; q < NJ; q++) b[0][q] = Rs[buf][lane / T][wj * WJ + q * T + c];
-#pragma unroll
-        for (int ks = 0; ks < BK; ks += M::KS) {
-            const int cur = (ks / M::KS) & 1;
-            if (ks + M::KS < BK) {
-                const int kr = ks + M::KS + lane / T;
-#pragma unroll
-                for (int q = 0; q < NI; q++) a[cur ^ 1][q] = Ls[buf][kr][wi * WI + q * T + c];
-#pragma unroll
-                for (int q = 0; q < NJ; q++) b[cur ^ 1][q] = Rs[buf][kr][wj * WJ + q * T + c];
-            }
-#pragma unroll
-            for (int x = 0; x < NI; x++)
-#pragma unroll
-                for (int y = 0; y < NJ; y++) acc[x][y] = M::mma(a[cur][x], b[cur][y], acc[x][y]);
-        }
-    }
-    // epilogue as k_gram_v: each 32 x 32 accumulator tile through LDS, whole
-    // column segments of G and of its mirror
-    __shared__ float Os[8][T][T + 1];
-    float(*O)[T + 1] = Os[w];
-    constexpr int JS = 64 / T;
-    const int li = lane % T, lj = lane / T;
-#pragma unroll
-    for (int x = 0; x < NI; x++)
-#pragma unroll
-        for (int y = 0; y < NJ; y++) {
-            const long ib = i0 + wi * WI + x * T, jb = j0 + wj * WJ + y * T;
-#pragma unroll
-            for (int r = 0; r < M::NR; r++) O[M::row(lane, r)][M::col(lane, r)] = acc[x][y][r];
-            __syncthreads();
-            for (int j = lj; j < T; j += JS)
-                if (ib + li < P && jb + j < P) G[(ib + li) + (jb + j) * P] = O[li][j];
-            if (bi != bj)
-                for (int i = lj; i < T; i += JS)
-                    if (jb + li < P && ib + i < P) G[(jb + li) + (ib + i) * P] = O[i][li];
-            __syncthreads();
-        }
-}
 
 // G = sum of the chunk partials, in chunk order
 template <typename real>
@@ -458,17 +317,10 @@ template <typename real>
 void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t s) {
     using M = Mfma<real>;
     if (P <= 0) return;
-    const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0 &&
-                     !(getenv("PFDR_GRAM_SCALAR") && getenv("PFDR_GRAM_SCALAR")[0] == '1');
-    // f32 with 16-byte operands: the wide tile on request (PFDR_GRAM_WIDE=1);
-    // measured no faster than k_gram_v (r2k: C3 23.4 vs 22.3 ms, A^tA 12.1
-    // vs 12.2-12.4 ms with the tail-free chunk count), so k_gram_v by default
-    const char *gw = getenv("PFDR_GRAM_WIDE");
-    const bool wide = sizeof(real) == 4 && vec && gw && gw[0] == '1';
-    const int BT = wide ? GramW::BT : M::BT, BK = wide ? GramW::BK : M::BK;
-    // blocks to aim for: the wide tile runs one block per CU
-    const char *gt = getenv("PFDR_GRAM_TARGET");
-    const long target = gt && atol(gt) > 0 ? atol(gt) : wide ? 1024 : 2048;
+    // 16-byte operand loads when the layout allows (k_gram_v), else k_gram
+    const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0;
+    const int BT = M::BT, BK = M::BK;
+    const long target = 2048;  // blocks to aim for
     const int nb = (P + BT - 1) / BT;
     const long tiles = (long)nb * (nb + 1) / 2;
     long nchunk = std::max(1L, std::min((target + tiles - 1) / tiles, (K + 4 * BK - 1) / (4 * BK)));
@@ -485,14 +337,7 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     const long nblk = gram_slots(nb, nchunk);  // see gram_block
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
-    if (wide) {
-        if (which == 0)
-            k_gram_w<GRAM_TN><<<grid, GramW::NTH, 0, s>>>(P, K, (const float *)A, ld, kchunk,
-                                                         (int)nchunk, (float *)out);
-        else
-            k_gram_w<GRAM_NT><<<grid, GramW::NTH, 0, s>>>(P, K, (const float *)A, ld, kchunk,
-                                                         (int)nchunk, (float *)out);
-    } else if (vec) {
+    if (vec) {
         if (which == 0) k_gram_v<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
         else k_gram_v<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
     } else {

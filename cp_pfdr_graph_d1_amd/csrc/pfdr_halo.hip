@@ -178,8 +178,9 @@ class RcclTransport final : public Transport {
   public:
     RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) { nranks = n; rank = r; }
     // a stalled communicator cannot be used again: abort it so the peers'
-    // operations fail too instead of waiting on this rank
-    void on_timeout() override { (void)ncclCommAbort(comm_); }
+    // operations fail too instead of waiting on this rank (recorded, so the
+    // owner's pfdr_comm_destroy skips the freed handle)
+    void on_timeout() override { comm_abort(comm_); }
     void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
                   hipStream_t s) override {
@@ -217,6 +218,9 @@ class RcclTransport final : public Transport {
 };
 
 std::unique_ptr<Transport> make_rccl_transport(void *comm, int n, int r) {
+    if (comm_aborted(comm))
+        throw std::runtime_error("RCCL communicator aborted by the watchdog (PFDR_COMM_TIMEOUT); "
+                                 "destroy it and create a new one");
     return std::unique_ptr<Transport>(new RcclTransport(comm, n, r));
 }
 

@@ -65,6 +65,10 @@ class Transport {
 };
 
 std::unique_ptr<Transport> make_rccl_transport(void *comm, int nranks, int rank);
+// watchdog abort of a caller-owned communicator (pfdr_comm.hip): aborted
+// once, remembered so that pfdr_comm_destroy does not free it a second time
+void comm_abort(void *comm);
+bool comm_aborted(void *comm);
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
 // wake every rank waiting on the hub with an error (a rank failed)
 void loopback_abort(void *hub, const char *reason);

@@ -299,12 +299,22 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_sum(long n, const real *_
 // one workgroup then chains the summaries and scans term by term only the
 // tiles where the sum leaves its binade or the prediction missed.
 //
+// Every kernel below runs gridDim.y independent sums at once (sum y over
+// a + y * astride, its scratch at y times the one-sum offsets): the
+// iterate evolution needs two per iteration (sum (X_ - X)^2 and sum X^2).
+// `halt` (may be null): a nonzero flag there makes every kernel return at
+// once (a halted chunk of captured iterations).
+//
 // 1. per-tile sums in f64 (only to predict the binade of the running sum)
 template <typename real>
 __global__ __launch_bounds__(256) void k_mono_tile_sums(long n, const real *__restrict__ a,
-                                                        double *__restrict__ tsum) {
+                                                        long astride, double *__restrict__ tsum,
+                                                        const int *__restrict__ halt) {
     constexpr long TILE = MonoTile<real>::TILE;
     __shared__ double red[kBlock / kWave];
+    if (halt && *halt) return;
+    a += blockIdx.y * astride;
+    tsum += (long)blockIdx.y * gridDim.x;
     const long b = (long)blockIdx.x * TILE;
     double z = 0.0;
     for (long i = b + threadIdx.x; i < min(b + TILE, n); i += 256) z += (double)a[i];
@@ -316,9 +326,13 @@ __global__ __launch_bounds__(256) void k_mono_tile_sums(long n, const real *__re
 template <typename real>
 __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double *__restrict__ tsum,
                                                        const real *__restrict__ seed,
-                                                       int *__restrict__ ebase) {
+                                                       int *__restrict__ ebase,
+                                                       const int *__restrict__ halt) {
     __shared__ double wsum[1024 / kWave];
     __shared__ double carry;
+    if (halt && *halt) return;
+    tsum += (long)blockIdx.y * ntiles;
+    ebase += (long)blockIdx.y * ntiles;
     const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
     if (t == 0) carry = seed ? (double)*seed : 0.0;
     __syncthreads();
@@ -341,58 +355,74 @@ __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double 
     }
 }
 
-// 3. summaries (d0, d1) of tile blockIdx.x / kMonoCand on the grid
-//    2^(ebase - 1 + blockIdx.x % kMonoCand)
+// 3. summaries (d0, d1) of tile blockIdx.x on the grids 2^(ebase - 1 + c),
+//    c = 0 .. kMonoCand - 1, from one load of the tile
 template <typename real>
 __global__ __launch_bounds__(kMonoThreads) void k_mono_summaries(long n, const real *__restrict__ a,
+                                                                 long astride,
                                                                  const int *__restrict__ ebase,
-                                                                 long long *__restrict__ summ) {
+                                                                 long long *__restrict__ summ,
+                                                                 const int *__restrict__ halt) {
     constexpr int J = MonoTile<real>::J, NW = kMonoThreads / kWave;
-    __shared__ long long w0[NW], w1[NW];
-    const int tile = blockIdx.x / kMonoCand, c = blockIdx.x % kMonoCand;
+    __shared__ long long w0[kMonoCand][NW], w1[kMonoCand][NW];
+    if (halt && *halt) return;
+    const long nt = gridDim.x;
+    a += blockIdx.y * astride;
+    ebase += (long)blockIdx.y * nt;
+    summ += (long)blockIdx.y * nt * 2 * kMonoCand;
+    const int tile = blockIdx.x;
     const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-    const int ue = ebase[tile] - 1 + c;
     real x[J];
     mono_load(x, a, n, (long)tile * MonoTile<real>::TILE, t);
-    long long i0, i1;
-    mono_run(x, ue, i0, i1);
-    mono_wave_scan<real>(i0, i1, lane);
-    if (lane == kWave - 1) {
-        w0[w] = i0;
-        w1[w] = i1;
+    const int e0 = ebase[tile] - 1;
+#pragma unroll
+    for (int c = 0; c < kMonoCand; c++) {
+        long long i0, i1;
+        mono_run(x, e0 + c, i0, i1);
+        mono_wave_scan<real>(i0, i1, lane);
+        if (lane == kWave - 1) {
+            w0[c][w] = i0;
+            w1[c][w] = i1;
+        }
     }
     __syncthreads();
-    if (t == 0) {
+    if (t < kMonoCand) {
         long long q0 = 0, q1 = 0;
         for (int k = 0; k < NW; k++) {
-            long long b0 = w0[k], b1 = w1[k];
+            long long b0 = w0[t][k], b1 = w1[t][k];
             compose<real>(q0, q1, b0, b1);
             q0 = b0;
             q1 = b1;
         }
-        summ[2 * blockIdx.x] = q0;
-        summ[2 * blockIdx.x + 1] = q1;
+        summ[2 * ((long)tile * kMonoCand + t)] = q0;
+        summ[2 * ((long)tile * kMonoCand + t) + 1] = q1;
     }
 }
 
-// 4. one workgroup: wave 0 chains the summaries of 64 tiles at a time on the
-//    current binade; the first tile that would leave it (or has no summary
-//    for it) is scanned term by term by the workgroup (mono_range).
+// 4. one workgroup per sum: wave 0 chains the summaries of 64 tiles at a
+//    time on the current binade; the first tile that would leave it (or has
+//    no summary for it) is scanned term by term by the workgroup (mono_range).
 template <typename real>
 __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *__restrict__ a,
-                                                            int ntiles,
+                                                            long astride, int ntiles,
                                                             const int *__restrict__ ebase,
                                                             const long long *__restrict__ summ,
                                                             const real *__restrict__ seed,
                                                             int nparts,
                                                             const int *__restrict__ cnt_part,
                                                             real *__restrict__ sum_out,
-                                                            long long *__restrict__ cnt_out) {
+                                                            long long *__restrict__ cnt_out,
+                                                            const int *__restrict__ halt) {
     constexpr long TILE = MonoTile<real>::TILE;
     constexpr long long TOP = 1ll << FpGrid<real>::p, CAP = TOP + 1;
     __shared__ MonoShared sh;
+    if (halt && *halt) return;
+    a += blockIdx.y * astride;
+    ebase += (long)blockIdx.y * ntiles;
+    summ += (long)blockIdx.y * ntiles * 2 * kMonoCand;
+    sum_out += blockIdx.y;
     const int t = threadIdx.x, lane = t & (kWave - 1);
-    if (cnt_out) mono_count<real>(nparts, cnt_part, cnt_out, sh);
+    if (cnt_out && blockIdx.y == 0) mono_count<real>(nparts, cnt_part, cnt_out, sh);
     if (t == 0) sh.exit_at = INT_MAX;
     __syncthreads();
     real s = seed ? *seed : real(0);
@@ -435,31 +465,35 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *
     if (t == 0) *sum_out = s;
 }
 
-// n terms at a (device), seed (device, may be nullptr) -> *out (device);
+// nsum sums of n terms each, sum y at a + y * astride (device), seed
+// (device, may be nullptr; the same for every sum) -> out[y] (device);
 // cnt_out (may be nullptr) receives the sum of cnt_part[0..nparts).
-// ws: scratch of mono_ws_bytes(n) bytes.
+// ws: scratch of mono_ws_bytes(n, nsum) bytes.  halt: see above.
 template <typename real>
-inline size_t mono_ws_bytes(long n) {
+inline size_t mono_ws_bytes(long n, int nsum = 1) {
     const long nt = (n + MonoTile<real>::TILE - 1) / MonoTile<real>::TILE;
-    return (size_t)nt * (sizeof(double) + sizeof(int) + 2 * kMonoCand * sizeof(long long)) + 64;
+    return (size_t)nsum * nt * (sizeof(double) + sizeof(int) + 2 * kMonoCand * sizeof(long long)) +
+           64;
 }
 template <typename real>
 void mono_sum(long n, const real *a, const real *seed, int nparts, const int *cnt_part, real *out,
-              long long *cnt_out, void *ws, hipStream_t s) {
+              long long *cnt_out, void *ws, hipStream_t s, int nsum = 1, long astride = 0,
+              const int *halt = nullptr) {
     constexpr long TILE = MonoTile<real>::TILE;
     const long nt = (n + TILE - 1) / TILE;
-    if (nt <= 4) {
+    if (nt <= 4 && nsum == 1 && !halt) {
         k_mono_sum<real><<<1, kMonoThreads, 0, s>>>(n, a, seed, nparts, cnt_part, out, cnt_out);
         return;
     }
     long long *summ = static_cast<long long *>(ws);
-    double *tsum = reinterpret_cast<double *>(summ + 2 * kMonoCand * nt);
-    int *ebase = reinterpret_cast<int *>(tsum + nt);
-    k_mono_tile_sums<real><<<(int)nt, 256, 0, s>>>(n, a, tsum);
-    k_mono_predict<real><<<1, 1024, 0, s>>>((int)nt, tsum, seed, ebase);
-    k_mono_summaries<real><<<(int)(nt * kMonoCand), kMonoThreads, 0, s>>>(n, a, ebase, summ);
-    k_mono_walk<real><<<1, kMonoThreads, 0, s>>>(n, a, (int)nt, ebase, summ, seed, nparts,
-                                                 cnt_part, out, cnt_out);
+    double *tsum = reinterpret_cast<double *>(summ + 2 * kMonoCand * nt * nsum);
+    int *ebase = reinterpret_cast<int *>(tsum + nt * nsum);
+    const dim3 gt((unsigned)nt, (unsigned)nsum), g1(1, (unsigned)nsum);
+    k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, tsum, halt);
+    k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, seed, ebase, halt);
+    k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, summ, halt);
+    k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ, seed,
+                                                  nparts, cnt_part, out, cnt_out, halt);
 }
 
 // The same sum by one lane (PFDR_SEQSUM=lane, and the A/B tests): all lanes

@@ -92,11 +92,32 @@ class QuadSession final : public SessionBase {
     // XCD-aware block order (xcd_block): runs of 64 edge blocks / 16 vertex
     // blocks per XCD, so the neighbour bands a run gathers share one L2
     // (paired A/B on the headline: 0.754 -> 0.727 ms/iter; profiles/r1/r1zk)
-    int xcd_e_ = 64, xcd_v_ = 16;
-    int gb_ = 8;                 // gathers in flight per lane in the vertex sweep
-    bool us_ = true;             // edge sweep stages the u ends of u-sorted edges
-    bool seq_lane_ = false;      // amplitude sum by one lane (k_seq_sum) instead of mono_sum
+    static constexpr int xcd_e_ = 64, xcd_v_ = 16;
+    // the edge sweep stages the u ends of u-sorted edges in LDS (k_edge_sweep_us)
+    // for graphs of at least 4 edges per vertex and for small (latency-bound)
+    // graphs.  Measured (r2zf, paired, ms per edge sweep): headline 6 edges
+    // per vertex 0.457 staged vs 0.472, shuffled headline 0.468 vs 0.500, C1
+    // (130K edges) 0.008-0.010 vs 0.019; but 3 edges per vertex C2 0.450 vs
+    // 0.394 and C5 6.55 vs 5.81 -- with few edges per u end the block's
+    // staging barrier and search cost more than the Eu stream and the
+    // (cache-served) u-end gathers they replace.
+    bool us_ = true;
     DevBuf<char> mono_ws_;       // mono_sum scratch (tile summaries)
+    // uniform La_d1 (k_uniform_check at setup): the iteration kernels take
+    // the one value la0_ instead of streaming the array (4 B per edge)
+    bool la_uniform_ = false;
+    real la0_ = real(0);
+    const real *la_it() const { return la_uniform_ ? nullptr : La_d1_.p; }
+    // iterate evolution with the reference's sequential rounding
+    // (PFDR_EVOLUTION_*, include/pfdr_mi355x.h): the vertex sweep stores the
+    // terms (X_ - X)^2 and X^2 in the caller's vertex order, two binade-scan
+    // sums (mono_sum) replace the tree of k_reduce_decide, k_decide decides
+    int evo_ = PFDR_EVOLUTION_AUTO;
+    bool seqdif_ = false;
+    long tstride_ = 0;
+    DevBuf<real> terms_;
+    DevBuf<char> dws_;
+    static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
     // emap_[edge position] = original edge id (setup only)
@@ -138,7 +159,7 @@ class QuadSession final : public SessionBase {
     // kernel boundary costs ~1.6 us of GPU time, a launched one ~2.8 us
     // (profiles/r2/r2d_launch_gap.log) -- the difference is a large share of
     // an iteration of a small graph.  Re-captured after a reconditioning
-    // (new kernel arguments).  PFDR_GRAPH=0 launches directly.
+    // (new kernel arguments).
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
@@ -182,24 +203,6 @@ class QuadSession final : public SessionBase {
     // (k_tiny_iterate; PFDR_TINY = max edges, 0 = off)
     bool tiny_ = false;
     void tiny_chunk(int n);
-    // mid-size single-GPU graphs: a chunk of iterations in one persistent
-    // launch of coopG_ resident workgroups with grid barriers
-    // (k_coop_iterate; PFDR_COOP = most vertex blocks, 0 = off, the
-    // default: slower than graph-replayed launches, see kCoopBlocks;
-    // PFDR_COOP_G = most workgroups)
-    bool coop_ok_ = false, coop_ = false;
-    int coopG_ = 0;
-    DevBuf<unsigned> bar_;
-    void plan_coop();
-    void coop_chunk(int n);
-    // pipelined iteration (single GPU, u-sorted edges, label bandwidth below
-    // the chunk size): vertex chunks k = 0..C-1 run as edge sweep of chunk
-    // k+1, then vertex sweep of chunk k, so each chunk's DR contributions are
-    // read back while they are still in the 256 MB Infinity Cache
-    // (PFDR_CHUNKS = C; 0 off)
-    std::vector<int> pblk_;    // vertex-block boundaries of the chunks (C + 1)
-    std::vector<long> pedge_;  // edge boundaries (C + 1), multiples of the lane width
-    void plan_pipeline();
     const real *full_x();  // X of every vertex (A^tA mode), gathered over the ranks
     // A^tA mode on one GPU with an exactly symmetric matrix: products from the
     // block upper triangle (k_symv_tiles / k_symv_finish, half the bytes)
@@ -207,29 +210,23 @@ class QuadSession final : public SessionBase {
     int snb_ = 0;
     // small dense problems on one GPU (CP's reduced problems): every dot
     // product in the reference's sequential order (k_col_seq, k_rows_seq),
-    // bit-exact; PFDR_DENSE_EXACT = 0 off, 1 always (one GPU), default when
-    // the longest chain (max(N, V) direct, V for A^tA) is <= kExactChain
+    // bit-exact, when the longest chain (max(N, V) direct, V for A^tA) is
+    // <= kExactChain
     bool exact_ = false;
     static constexpr long kExactChain = 8192;
-    // default PFDR_COOP: off.  Measured on C1 (r2m/r2n): 37 us per iteration
-    // with 256 workgroups against 14.6 for the graph-replayed launches -- a
-    // grid barrier must write back and invalidate the L2 of every XCD (their
-    // L2s are not coherent), once per workgroup, which costs more than the
-    // kernel boundary it replaces
-    static constexpr long kCoopBlocks = 0;
     // small graphs (<= kFuseBlocks vertex blocks, dif tracked, one GPU):
     // the loop decision on iteration t taken inside the edge sweep of t + 1,
     // two launches per iteration instead of three (FuseDecide in
     // pfdr_quadratic_kernels.hpp); the decisions alternate between ctrl_
     // (even bodies of a chunk) and ctrl2_ (odd), the chunk's closing
-    // decision lands in ctrl_.  PFDR_FUSE = 0 off.
+    // decision lands in ctrl_.
     bool fuse_ = false;
     DevBuf<Ctrl<real>> ctrl2_;
     // fused sessions whose vertex blocks have at most kPadPer * kBlock CSR
     // entries: the edge sweep stores each contribution at its slot sl_[2e +
     // side] of its block's list in wzp_ (stride pad_nmax_), and the vertex
     // sweep (k_vertex_sweep_pad) stages its block's list with one dependent
-    // round trip instead of three.  PFDR_PAD = 0 off.
+    // round trip instead of three.
     bool pad_ = false;
     static constexpr int kPadBlocks = 512;
     int pad_nmax_ = 0;
@@ -239,7 +236,7 @@ class QuadSession final : public SessionBase {
     // and (Ga, 1/Aux) of both ends at xpe_ / gie_ [2e + side], scattered by
     // the vertex sweep through pidx_ (the end of each list entry), so the
     // edge sweep (k_edge_sweep_ends) streams everything: one dependent
-    // round trip.  PFDR_PAD_ENDS = 0 off, 1 on for every padded session.
+    // round trip.
     bool ends_ = false;
     static constexpr int kEndsBlocks = 512;
     DevBuf<int> pidx_;
@@ -282,32 +279,15 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     rec_obj_ = p->record_obj != 0;
     rec_dif_ = p->record_dif != 0;
     track_ = (difTol_ > real(0)) || (difRcd > real(0)) || rec_dif_;
+    evo_ = p->evolution;
+    if (evo_ < PFDR_EVOLUTION_AUTO || evo_ > PFDR_EVOLUTION_TREE)
+        throw std::runtime_error("evolution must be PFDR_EVOLUTION_AUTO, _SEQUENTIAL or _TREE");
+    if (evo_ == PFDR_EVOLUTION_SEQUENTIAL && (p->nranks > 1 || p->comm))
+        throw std::runtime_error("PFDR_EVOLUTION_SEQUENTIAL needs a single GPU (a partitioned "
+                                 "session sums the evolution statistic in a tree)");
+    const bool want_seq = track_ && evo_ == PFDR_EVOLUTION_SEQUENTIAL;
     Ldiag_ = (p->Ltype == PFDR_LIPSCHITZ_DIAG) && p->L;
-    {   // tuning knobs for A/B runs: PFDR_XCD = <edge mode><vertex mode> (0 / 1)
-        const char *x = getenv("PFDR_XCD");
-        if (x && strlen(x) == 2) { xcd_e_ = x[0] == '1'; xcd_v_ = x[1] == '1'; }
-        const char *xc = getenv("PFDR_XCD_CHUNK");  // edge sweep: runs of C blocks per XCD
-        if (xc && atoi(xc) >= 2) xcd_e_ = atoi(xc);
-        const char *xv = getenv("PFDR_XCD_CHUNK_V");  // vertex sweep: idem
-        if (xv && atoi(xv) >= 2) xcd_v_ = atoi(xv);
-        const char *g = getenv("PFDR_GB");  // 8 (default), 4 or 16
-        if (g && (atoi(g) == 16 || atoi(g) == 4)) gb_ = atoi(g);
-        // u-sorted edges: u ends staged in LDS, no Eu stream (k_edge_sweep_us).
-        // PFDR_USTAGE = 0 / 1 forces it; by default it is taken for graphs of
-        // at least 4 edges per vertex and for small (latency-bound) graphs.
-        // Measured (r2zf, paired, ms per edge sweep): headline 6 edges per
-        // vertex 0.457 staged vs 0.472, shuffled headline 0.468 vs 0.500, C1
-        // (130K edges) 0.008-0.010 vs 0.019; but 3 edges per vertex C2 0.450
-        // vs 0.394 and C5 6.55 vs 5.81 -- with few edges per u end the block's
-        // staging barrier and search cost more than the Eu stream and the
-        // (cache-served) u-end gathers they replace.
-        const char *u = getenv("PFDR_USTAGE");
-        if (u && (u[0] == '0' || u[0] == '1')) us_ = u[0] == '1';
-        else us_ = E_ >= 4L * V_ || E_ < (1L << 22);
-        // amplitude sum: workgroup binade scan (default) or the one-lane loop
-        const char *q = getenv("PFDR_SEQSUM");
-        seq_lane_ = q && strcmp(q, "lane") == 0;
-    }
+    us_ = E_ >= 4L * V_ || E_ < (1L << 22);
     // prox selection (ref l1 :499-512, bounds :472-490)
     positivity_ = 0;
     lo_ = hi_ = real(0);
@@ -330,13 +310,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     // vs 9.8 -- so up to 8 blocks in f32, 5 in f64, and 8192 edges.  The
     // split incidence is not built for them (one setup round trip less).
     if (!(p->nranks > 1 || p->comm) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
-        E_ > 0) {
+        E_ > 0 && !want_seq) {
         const char *t = getenv("PFDR_TINY");
         const long maxE = t ? atol(t) : 8192;
         const int maxB = t ? kTinyMaxBlocks : (sizeof(real) == 4 ? 8 : 5);
         tiny_ = E_ <= maxE && (V_ + kBlock - 1) / kBlock <= maxB;
         tiny = tiny_ ? 1 : 0;
-        coop_ok_ = !tiny_;
     }
     // graph, partition plan, incidence CSR
     setup_graph(p);
@@ -348,9 +327,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         throw std::runtime_error("N < 0 requires A = A^tA (columns of the owned vertices, "
                                  "length V) and N = -V (V over all ranks)");
     if ((mode_ == A_DIRECT || mode_ == A_ATA) && !halo_) {
-        const char *x = getenv("PFDR_DENSE_EXACT");
         const long chain = mode_ == A_DIRECT ? std::max<long>(N_, V_) : (long)V_;
-        exact_ = x ? (x[0] == '1') : chain <= kExactChain;
+        exact_ = chain <= kExactChain;
         dense_exact = exact_ ? 1 : 0;
     }
     const int mem = p->mem;
@@ -444,6 +422,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         k_diag<real><<<grid_for(V), kBlock, 0, s>>>(V_, mode_, A_.p, Vglob_, v0_, diag_.p);
     }
     PFDR_HIP(hipGetLastError());
+    // uniform La_d1? (read back with c below)
+    DevBuf<int> ubad(1);
+    PFDR_HIP(hipMemsetAsync(ubad.p, 0, sizeof(int), s));
+    if (E_) k_uniform_check<real><<<grid_for(E), kBlock, 0, s>>>(E_, La_d1_.p, ubad.p);
     // Z = X at both ends, first preconditioning, first forward step
     if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p);
     precondition(true);
@@ -460,6 +442,13 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     PFDR_HIP(hipStreamSynchronize(s));
     // c of the first conditioning: a_e = cw_ La_d1[e] in the edge sweeps
     PFDR_HIP(hipMemcpy(&cw_, &ctrl_.p->c, sizeof(real), hipMemcpyDeviceToHost));
+    if (E_) {
+        int bad = 1;
+        PFDR_HIP(hipMemcpy(&bad, ubad.p, sizeof(int), hipMemcpyDeviceToHost));
+        PFDR_HIP(hipMemcpy(&la0_, La_d1_.p, sizeof(real), hipMemcpyDeviceToHost));
+        la_uniform_ = bad == 0;
+        la_uniform = la_uniform_ ? 1 : 0;
+    }
     pins_.release();
     stopped_ = (itMax_ <= 0);
     interior_edges = E_;
@@ -473,24 +462,28 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
-    order_.release();  // inputs are in the internal labels now
     if (halo_) {
-        const char *o = getenv("PFDR_OVERLAP");  // A/B: PFDR_OVERLAP=0 serialises the halo
-        if (!(o && o[0] == '0')) plan_overlap();
+        plan_overlap();
     } else if (!tiny_) {
-        if (coop_ok_) plan_coop();
-        if (!coop_) plan_pipeline();
-        const char *g = getenv("PFDR_GRAPH");
-        graphs_ok_ = !(g && g[0] == '0') && itMax_ >= 2 * chunk_;
-        const char *f = getenv("PFDR_FUSE");
+        graphs_ok_ = itMax_ >= 2 * chunk_;
         // (an edgeless graph has no edge sweep to carry the decision)
-        fuse_ = !(f && f[0] == '0') && !coop_ && pblk_.empty() && track_ && !rec_obj_ &&
-                (mode_ == A_IDENT || mode_ == A_DIAG) && nbv_ <= kFuseBlocks && E_ > 0;
+        fuse_ = track_ && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
+                nbv_ <= kFuseBlocks && E_ > 0 && !want_seq;
         if (fuse_) ctrl2_.alloc(1);
         fused = fuse_ ? 1 : 0;
         if (fuse_) plan_pad();
     }
-    acc(where_.n * 4 + amp_orig_.n * sizeof(real));
+    // sequential evolution statistic: the plain multi-launch loop on one GPU
+    seqdif_ = track_ && !halo_ && !tiny_ && !fuse_ &&
+              (want_seq || (evo_ == PFDR_EVOLUTION_AUTO && (long)V_ >= kSeqDifMin));
+    if (seqdif_) {
+        tstride_ = ((long)V_ + 3) / 4 * 4;  // 16-byte aligned second array
+        terms_.alloc(2 * (size_t)tstride_);
+        dws_.alloc(mono_ws_bytes<real>(V_, 2));
+        seqdif = 1;
+    }
+    if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
+    acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
     // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
     // which a small solve timed to tolerance would otherwise pay in its loop)
@@ -499,12 +492,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
 
 template <typename real>
 void QuadSession<real>::plan_pad() {
-    // by default up to kPadBlocks vertex blocks: at 1024 blocks (512^2 grid,
-    // f32) the scattered contribution stores cost more than the round trips
-    // they save (profiles/r2/r2zp_exp_pad.log, r2zq_exp_pad.log); PFDR_PAD = 0 off, 1 whole range
-    const char *e = getenv("PFDR_PAD");
-    if ((e && e[0] == '0') || halo_ || !E_) return;
-    if (!(e && e[0] == '1') && nbv_ > kPadBlocks) return;
+    // up to kPadBlocks vertex blocks: at 1024 blocks (512^2 grid, f32) the
+    // scattered contribution stores cost more than the round trips they save
+    // (profiles/r2/r2zp_exp_pad.log, r2zq_exp_pad.log)
+    if (halo_ || !E_ || nbv_ > kPadBlocks) return;
     hipStream_t s = stream;
     PinnedSmall pin(s);
     int *hm = static_cast<int *>(pin.p);
@@ -519,12 +510,10 @@ void QuadSession<real>::plan_pad() {
     sl_.alloc(2 * (size_t)E_);
     wzp_.alloc((size_t)nbv_ * nmax);
     PFDR_HIP(hipMemsetAsync(wzp_.p, 0, wzp_.n * sizeof(real), s));
-    const char *en = getenv("PFDR_PAD_ENDS");
-    // default: f32 up to kEndsBlocks (f32 us/iter 11.2 -> 9.6 at 9 blocks,
-    // 11.5 -> 10.5 at 256, 12.7 -> 12.2 at 507; f64 slower: 10.4 -> 11.0 at 9
-    // blocks, 12.5 -> 26 at 256; profiles/r2/r2zz_exp_ends.log, r2zz2)
-    ends_ = !(en && en[0] == '0') &&
-            ((sizeof(real) == 4 && nbv_ <= kEndsBlocks) || (en && en[0] == '1'));
+    // f32 up to kEndsBlocks (f32 us/iter 11.2 -> 9.6 at 9 blocks, 11.5 ->
+    // 10.5 at 256, 12.7 -> 12.2 at 507; f64 slower: 10.4 -> 11.0 at 9 blocks,
+    // 12.5 -> 26 at 256; profiles/r2/r2zz_exp_ends.log, r2zz2)
+    ends_ = sizeof(real) == 4 && nbv_ <= kEndsBlocks;
     if (ends_) {
         pidx_.alloc((size_t)nbv_ * nmax);
         PFDR_HIP(hipMemsetAsync(pidx_.p, 0, pidx_.n * sizeof(int), s));
@@ -628,8 +617,6 @@ void QuadSession<real>::build_split() {
     k_uptr<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, V_, Eu_.p, uptr_.p);
     PFDR_HIP(hipGetLastError());
     ustaged = us_ ? 1 : 0;
-    const char *sp = getenv("PFDR_SPLIT");  // A/B: PFDR_SPLIT=0 keeps the CSR gather everywhere
-    if (sp && sp[0] == '0') return;
     mask_.alloc(V_);
     oidx_.alloc(ototal ? ototal : 1);
     blkok_.alloc(nb);
@@ -767,16 +754,14 @@ void QuadSession<real>::col_product(ColArgs<real> ca) {
     PFDR_HIP(hipGetLastError());
 }
 
-// symmetric products (PFDR_SYMV: 0 off, 1 whenever valid, default for
-// V >= 4 T): one GPU, V a multiple of the 16-byte vector, A 16-byte aligned,
-// and the caller's matrix exactly symmetric (k_sym_check, one pass at setup;
-// a matrix that is not keeps the column dots, which read it as given)
+// symmetric products for V >= 4 T: one GPU, V a multiple of the 16-byte
+// vector, A 16-byte aligned, and the caller's matrix exactly symmetric
+// (k_sym_check, one pass at setup; a matrix that is not keeps the column
+// dots, which read it as given)
 template <typename real>
 void QuadSession<real>::plan_symv() {
     using S = SymT<real>;
-    const char *e = getenv("PFDR_SYMV");
-    const int want = e ? atoi(e) : 2;
-    if (halo_ || exact_ || !want || (want == 2 && V_ < 4 * S::T)) return;
+    if (halo_ || exact_ || V_ < 4 * S::T) return;
     if (V_ % S::VW || ((uintptr_t)A_.p % 16)) return;
     hipStream_t s = stream;
     DevBuf<int> flag(1);
@@ -836,14 +821,9 @@ void QuadSession<real>::amplitude(bool init) {
         k_gather<real><<<nbv_, kBlock, 0, s>>>(V_, absval_.p, where_.p, amp_orig_.p);
         amp = amp_orig_.p;
     }
-    if (seq_lane_)
-        k_seq_sum<real><<<1, kBlock, 0, s>>>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_,
-                                             cnt_part_.p, csum_.p, ccnt_.p);
-    else {
-        if (mono_ws_.n < mono_ws_bytes<real>(V_)) mono_ws_.alloc(mono_ws_bytes<real>(V_));
-        mono_sum<real>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_, cnt_part_.p, csum_.p,
-                       ccnt_.p, mono_ws_.p, s);
-    }
+    if (mono_ws_.n < mono_ws_bytes<real>(V_)) mono_ws_.alloc(mono_ws_bytes<real>(V_));
+    mono_sum<real>(V_, amp, seeded ? red_.p + 3 : nullptr, nbv_, cnt_part_.p, csum_.p, ccnt_.p,
+                   mono_ws_.p, s);
     PFDR_HIP(hipGetLastError());
     if (halo_) {
         Transport &tr = *halo_->tr;
@@ -943,17 +923,17 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     const FuseDecide<real> f = fd ? *fd : FuseDecide<real>{};
     if (ends_ && fuse_) {  // the whole edge range (fused sessions sweep [0, E) in one launch)
         k_edge_sweep_ends<real><<<g, kBlock, 0, s>>>(E_, xpe_.p, gie_.p, Z2_.p, A1_.p, cw_,
-                                                     La_d1_.p, rho_, c, nb, xm, f, pad_out());
+                                                     la_it(), la0_, rho_, c, nb, xm, f, pad_out());
         return;
     }
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
-                               La_d1_.p, wz_.p, rho_, c, nb, xm, rg, f, pad_out());
+                               la_it(), la0_, wz_.p, rho_, c, nb, xm, rg, f, pad_out());
     } else {
         auto k = fuse_ ? k_edge_sweep<real, true> : k_edge_sweep<real, false>;
-        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p, La_d1_.p, wz_.p,
-                               rho_, c, nb, xm, rg, f, pad_out());
+        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p, la_it(), la0_,
+                               wz_.p, rho_, c, nb, xm, rg, f, pad_out());
     }
 }
 
@@ -961,54 +941,14 @@ template <typename real>
 void QuadSession<real>::tiny_chunk(int n) {
     const bool gated = track_ || rec_obj_;
     TinyArgs<real> t{};
-    t.E = E_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Z2 = Z2_.p; t.A1 = A1_.p; t.La_d1 = La_d1_.p;
-    t.cw = cw_; t.rho = rho_; t.gi = gi_.p; t.wz = wz_.p;
+    t.E = E_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Z2 = Z2_.p; t.A1 = A1_.p; t.La_d1 = la_it();
+    t.la0 = la0_; t.cw = cw_; t.rho = rho_; t.gi = gi_.p; t.wz = wz_.p;
     t.va = vargs(0, nbv_, nullptr);
     t.red = red_.p; t.ctrl = gated ? ctrl_.p : nullptr; t.Dif = rec_dif_ ? Dif_.p : nullptr;
     t.track = track_ ? 1 : 0; t.iters = n;
     ProfScope ps(prof, "tiny_iterate", stream);
     k_tiny_iterate<real><<<1, kTiny, 0, stream>>>(t);
     PFDR_HIP(hipGetLastError());
-}
-
-// persistent launch for mid-size graphs: every workgroup must be resident
-// (grid barriers), so the grid is capped by the occupancy of the kernel and
-// by the CUs; the runtime's cooperative launch checks it again
-template <typename real>
-void QuadSession<real>::plan_coop() {
-    const char *e = getenv("PFDR_COOP");
-    const long maxb = e ? atol(e) : kCoopBlocks;
-    if (maxb <= 0 || nbv_ > maxb) return;
-    int cus = 0, occ = 0;
-    PFDR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    PFDR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void *>(k_coop_iterate<real, 8>), kBlock, 0));
-    const char *g = getenv("PFDR_COOP_G");
-    constexpr long EB = (long)kBlock * Vec<real>::kPer16B;  // edges per workgroup chunk
-    long G = std::max<long>(nbv_, (E_ + EB - 1) / EB);
-    G = std::min<long>(G, (long)cus * std::max(occ, 1));
-    G = std::min<long>(G, g && atol(g) > 0 ? atol(g) : cus);
-    if (G < 1) return;
-    coopG_ = (int)G;
-    bar_.alloc(2);
-    PFDR_HIP(hipMemsetAsync(bar_.p, 0, 2 * sizeof(unsigned), stream));
-    coop_ = true;
-    coop = coopG_;
-}
-
-template <typename real>
-void QuadSession<real>::coop_chunk(int n) {
-    const bool gated = track_ || rec_obj_;
-    CoopArgs<real> t{};
-    t.E = E_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Z2 = Z2_.p; t.A1 = A1_.p; t.La_d1 = La_d1_.p;
-    t.cw = cw_; t.rho = rho_; t.gi = gi_.p; t.wz = wz_.p;
-    t.va = vargs(0, nbv_, nullptr);
-    t.red = red_.p; t.ctrl = gated ? ctrl_.p : nullptr; t.Dif = rec_dif_ ? Dif_.p : nullptr;
-    t.track = track_ ? 1 : 0; t.iters = n; t.bar = bar_.p;
-    void *args[] = {&t};
-    ProfScope ps(prof, "coop_iterate", stream);
-    PFDR_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_coop_iterate<real, 8>),
-                                        dim3(coopG_), dim3(kBlock), args, 0, stream));
 }
 
 template <typename real>
@@ -1021,6 +961,9 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
     a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
     a.late = fuse_ ? 1 : 0;
+    a.terms = seqdif_ ? terms_.p : nullptr;
+    a.tmap = (seqdif_ && reordered_) ? order_.p : nullptr;
+    a.tstride = tstride_;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
     a.bsplit = a.nb; a.bjump = 0;
     return a;
@@ -1045,9 +988,7 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
             a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
         return;
     }
-    if (gb_ == 8) k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
-    else if (gb_ == 4) k_vertex_sweep<real, 4><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
-    else k_vertex_sweep<real, 16><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
+    k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }
 
 template <typename real>
@@ -1098,14 +1039,6 @@ void QuadSession<real>::body(int i, int n) {
         vertex_sweep(blo_, bhi_, c, "vertex_sweep");
         PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
         vertex_sweep(0, blo_, c, "vertex_sweep_b", bhi_, nbv_);
-    } else if (pblk_.size() > 1) {
-        // chunked: E(0), then E(k+1), V(k) for every chunk k
-        const int C = (int)pblk_.size() - 1;
-        edge_sweep(pedge_[0], pedge_[1], c, "edge_sweep");
-        for (int k = 0; k < C; k++) {
-            if (k + 1 < C) edge_sweep(pedge_[k + 1], pedge_[k + 2], c, "edge_sweep");
-            vertex_sweep(pblk_[k], pblk_[k + 1], c, "vertex_sweep");
-        }
     } else {
         if (halo_) {
             ProfScope ps(prof, "halo_pull", s);
@@ -1118,7 +1051,13 @@ void QuadSession<real>::body(int i, int n) {
         }
         vertex_sweep(0, nbv_, c, "vertex_sweep");
     }
-    if (gated && !halo_) {
+    if (seqdif_) {
+        // the reference's two sequential sums (ref :518-526), then its decision
+        ProfScope ps(prof, "seq_evolution", s);
+        mono_sum<real>(V_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
+                       &ctrl_.p->halt);
+        k_decide<real><<<1, 64, 0, s>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
+    } else if (gated && !halo_) {
         k_reduce_decide<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, ctrl_.p,
                                                    rec_dif_ ? Dif_.p : nullptr, track_ ? 1 : 0);
     } else if (gated) {  // the partial sums are all-reduced before the decision
@@ -1131,45 +1070,6 @@ void QuadSession<real>::body(int i, int n) {
     PFDR_HIP(hipGetLastError());
     if (mode_ == A_DIRECT || mode_ == A_ATA) forward_dense(gated ? GATE_ACTIVE : GATE_NONE);
     if (rec_obj_) objective();
-}
-
-// chunk plan of the pipelined iteration: C chunks of whole vertex blocks,
-// each at least the label bandwidth + 1 vertices, so that the edges of chunk
-// k + 1 (u ends in it) only touch chunks k..k+2 and every edge touching
-// chunk k is swept before its vertex sweep; edge boundaries rounded UP to
-// the lane width (the few edges moved into the previous range have their u
-// end at its last vertex's successor and touch no chunk before it)
-template <typename real>
-void QuadSession<real>::plan_pipeline() {
-    const char *e = getenv("PFDR_CHUNKS");
-    const int want = e ? atoi(e) : 0;
-    if (want < 2 || !uptr_.p || !E_ || rec_obj_) return;
-    hipStream_t s = stream;
-    constexpr int EPT = Vec<real>::kPer16B;
-    DevBuf<int> d(1);
-    PFDR_HIP(hipMemsetAsync(d.p, 0, sizeof(int), s));
-    k_bandwidth<<<std::min(grid_for(E_), 4096), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, d.p);
-    PFDR_HIP(hipGetLastError());
-    int bw = 0;
-    PFDR_HIP(hipMemcpyAsync(&bw, d.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    PFDR_HIP(hipStreamSynchronize(s));
-    const int minb = (bw + 1 + kBlock - 1) / kBlock;  // blocks per chunk at least
-    const int C = std::min(want, nbv_ / std::max(minb, 1));
-    if (C < 2) return;
-    std::vector<int> up((size_t)V_ + 1);
-    PFDR_HIP(hipMemcpy(up.data(), uptr_.p, sizeof(int) * ((size_t)V_ + 1), hipMemcpyDeviceToHost));
-    pblk_.assign(C + 1, 0);
-    pedge_.assign(C + 1, 0);
-    for (int k = 0; k <= C; k++) {
-        pblk_[k] = (int)((long)nbv_ * k / C);
-        const long ev = up[std::min((long)V_, (long)pblk_[k] * kBlock)];
-        pedge_[k] = std::min((long)E_, (ev + EPT - 1) / EPT * EPT);
-    }
-    pedge_[0] = 0;
-    pedge_[C] = E_;
-    for (int k = 0; k < C; k++)
-        if (pblk_[k + 1] - pblk_[k] < minb) { pblk_.clear(); pedge_.clear(); return; }
-    pipeline_chunks = C;
 }
 
 // interior edge range and vertex-block range of a partitioned session (the
@@ -1276,7 +1176,6 @@ int QuadSession<real>::run(int iters) {
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
         if (tiny_) tiny_chunk(n);
-        else if (coop_) coop_chunk(n);
         else run_bodies(n);
         if (gated) {
             pull_ctrl();

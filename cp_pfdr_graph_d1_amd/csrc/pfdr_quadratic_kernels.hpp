@@ -33,6 +33,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 
 #include "pfdr_graph.hpp"
 #include "pfdr_monosum.hpp"
@@ -221,23 +222,6 @@ static __global__ void k_uptr(long E, int V, const int *__restrict__ Eu, int *__
     const int lo = e == 0 ? 0 : Eu[e - 1] + 1;
     const int hi = e == E ? V : Eu[e];
     for (int v = lo; v <= hi; v++) uptr[v] = (int)e;
-}
-
-// max |Eu[e] - Ev[e]| (the graph's label bandwidth; atomicMax of block maxima)
-static __global__ void k_bandwidth(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
-                                   int *__restrict__ bw) {
-    __shared__ int red[kBlock / kWave];
-    int m = 0;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E;
-         e += (long)gridDim.x * blockDim.x)
-        m = max(m, abs(Eu[e] - Ev[e]));
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; w++) m = max(m, red[w]);
-        atomicMax(bw, m);
-    }
 }
 
 // One lane per vertex: code (bit i: the i-th CSR entry is the vertex's next
@@ -765,6 +749,32 @@ __device__ __forceinline__ real edge_a(long e, const real *__restrict__ A1,
     return A1 ? A1[e] : cw * La_d1[e];
 }
 
+// La_d1[e] of the iteration kernels: a null array means every edge weighs
+// la0 (a uniform La_d1 detected at setup, k_uniform_check: the 4-byte
+// stream is not read; the value, and so every operation, is the same)
+template <typename real>
+__device__ __forceinline__ real la_at(long e, const real *__restrict__ La_d1, real la0) {
+    return La_d1 ? La_d1[e] : la0;
+}
+template <typename real, int N>
+__device__ __forceinline__ Pk<real, N> la_vec(long e0, const real *__restrict__ La_d1, real la0) {
+    Pk<real, N> la;
+    if (La_d1) return *reinterpret_cast<const Pk<real, N> *>(La_d1 + e0);
+#pragma unroll
+    for (int j = 0; j < N; j++) la.v[j] = la0;
+    return la;
+}
+
+// nonzero *bad when some La_d1[e] differs from La_d1[0] (bitwise)
+template <typename real>
+__global__ void k_uniform_check(long E, const real *__restrict__ La_d1, int *__restrict__ bad) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    using U = typename std::conditional<sizeof(real) == 4, unsigned, unsigned long long>::type;
+    const U x = *reinterpret_cast<const U *>(La_d1 + e), x0 = *reinterpret_cast<const U *>(La_d1);
+    if (__any(x != x0) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(bad, 1);
+}
+
 // d1 contributions a_e to the per-vertex sums (both ends through the CSR,
 // like the DR average; ref :156-192).  On reconditioning, first turn the
 // auxiliary variables into subgradients with the OLD weights and metric
@@ -1087,13 +1097,14 @@ struct PadOut {
 // per edge: Eu, Ev, Z (r/w), La_d1, the two contributions (+ A1 after a
 // reconditioning); gathers (X, P) and (Ga, invAux) of both ends.
 // one lane's EPT edges [e0, e0 + EPT) of the edges [.., eend): the lane
-// body of k_edge_sweep, shared with the persistent k_coop_iterate (whose
+// body of k_edge_sweep, shared with the one-workgroup k_tiny_iterate (whose
 // xp is rewritten between its edge passes: no __restrict__ on it)
 template <typename real>
 __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int *__restrict__ Eu,
                                           const int *__restrict__ Ev, const R2<real> *xp,
                                           real *Z2, const real *A1, real cw, const R2<real> *gi,
-                                          const real *__restrict__ La_d1, real *wz, real rho,
+                                          const real *__restrict__ La_d1, real la0, real *wz,
+                                          real rho,
                                           PadOut<real> pd = PadOut<real>{nullptr, nullptr}) {
     constexpr int EPT = Vec<real>::kPer16B;
     if (e0 >= eend) return;
@@ -1109,7 +1120,7 @@ __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int 
             gu[j] = gi[iu.v[j]]; gv[j] = gi[iv.v[j]];
         }
         Pk<real, 2 * EPT> z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        const Pk<real, EPT> la = ldv<real, EPT>(La_d1 + e0);
+        const Pk<real, EPT> la = la_vec<real, EPT>(e0, La_d1, la0);
         Pk<real, EPT> a;
         if (A1) a = ldv<real, EPT>(A1 + e0);
         else {
@@ -1136,8 +1147,9 @@ __device__ __forceinline__ void edge_lane(long e0, long eend, long E, const int 
         for (long e = e0; e < eend; e++) {
             const int u = Eu[e], v = Ev[e];
             real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
-            edge_full<real>(xp[u], xp[v], gi[u], gi[v], edge_a(e, A1, La_d1, cw), La_d1[e], zu,
-                            zv, ou, ov, rho);
+            const real l = la_at(e, La_d1, la0);
+            edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou, ov,
+                            rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
             if (pd.sl) {
@@ -1155,9 +1167,9 @@ template <typename real, bool FD>
 __global__ __launch_bounds__(256) void k_edge_sweep(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
-    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real *__restrict__ wz,
-    real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg, FuseDecide<real> fd,
-    PadOut<real> pdx) {
+    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd, ERange rg,
+    FuseDecide<real> fd, PadOut<real> pdx) {
     if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     const PadOut<real> pd = FD ? pdx : PadOut<real>{nullptr, nullptr};
@@ -1177,7 +1189,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     long ebeg, eend;
     rg.pick(blk, ebeg, eend);
     const long e0 = ebeg + ((long)blk * blockDim.x + threadIdx.x) * EPT;
-    edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, wz, rho, pd);
+    edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, la0, wz, rho, pd);
 }
 
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
@@ -1197,8 +1209,8 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
     const int *__restrict__ uptr, const R2<real> *__restrict__ xp, real *__restrict__ Z2,
     const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
-    const real *__restrict__ La_d1, real *__restrict__ wz, real rho, const Ctrl<real> *ctrl,
-    int nb, int xcd, ERange rg, FuseDecide<real> fd, PadOut<real> pdx) {
+    const real *__restrict__ La_d1, real la0, real *__restrict__ wz, real rho,
+    const Ctrl<real> *ctrl, int nb, int xcd, ERange rg, FuseDecide<real> fd, PadOut<real> pdx) {
     if (!FD && ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int CAP = USpan<real>::v;
@@ -1237,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
     if (full) {
         iv = ldv<int, EPT>(Ev + e0);
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        la = ldv<real, EPT>(La_d1 + e0);
+        la = la_vec<real, EPT>(e0, La_d1, la0);
         if (A1) a = ldv<real, EPT>(A1 + e0);
         if (pd.sl) sv = ldv<int, 2 * EPT>(pd.sl + 2 * e0);
 #pragma unroll
@@ -1303,8 +1315,9 @@ __global__ __launch_bounds__(256) void k_edge_sweep_us(
         for (long e = e0; e < eend; e++) {
             const int u = Eu[e], v = Ev[e];
             real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
-            edge_full<real>(xp[u], xp[v], gi[u], gi[v], edge_a(e, A1, La_d1, cw), La_d1[e], zu,
-                            zv, ou, ov, rho);
+            const real l = la_at(e, La_d1, la0);
+            edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou, ov,
+                            rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
             if (pd.sl) {
@@ -1339,6 +1352,13 @@ struct VArgs {
     real *part;     // 2 per block
     const Ctrl<real> *ctrl;
     int late;       // halt of ctrl tested after the sum, before the stores (small launches)
+    // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
+    // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
+    // caller's order (tmap[v] for a relabelled session, else v), summed
+    // afterwards in that order with the reference's rounding (mono_sum)
+    real *terms;
+    const int *tmap;
+    long tstride;
 };
 
 // DR average (ordered), prox on the iterate, evolution partials, next
@@ -1404,6 +1424,11 @@ __device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, r
             const real d = q.x - x;
             num = d * d;
             den = x * x;
+            if (a.terms) {
+                const long i = a.tmap ? a.tmap[v] : v;
+                a.terms[i] = num;
+                a.terms[a.tstride + i] = den;
+            }
         }
         q.x = x;
         if (a.fwd) {
@@ -1541,7 +1566,7 @@ template <typename real>
 __global__ __launch_bounds__(256) void k_edge_sweep_ends(
     long E, const R2<real> *__restrict__ xpe, const R2<real> *__restrict__ gie,
     real *__restrict__ Z2, const real *__restrict__ A1, real cw,
-    const real *__restrict__ La_d1, real rho, const Ctrl<real> *ctrl, int nb, int xcd,
+    const real *__restrict__ La_d1, real la0, real rho, const Ctrl<real> *ctrl, int nb, int xcd,
     FuseDecide<real> fd, PadOut<real> pd) {
     constexpr int EPT = Vec<real>::kPer16B;
     const int blk = xcd_block(blockIdx.x, nb, xcd);
@@ -1565,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep_ends(
             gu[j] = gie[2 * (e0 + j)]; gv[j] = gie[2 * (e0 + j) + 1];
         }
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        la = ldv<real, EPT>(La_d1 + e0);
+        la = la_vec<real, EPT>(e0, La_d1, la0);
         if (A1) a = ldv<real, EPT>(A1 + e0);
         sv = ldv<int, 2 * EPT>(pd.sl + 2 * e0);
     }
@@ -1590,8 +1615,9 @@ __global__ __launch_bounds__(256) void k_edge_sweep_ends(
     } else {
         for (long e = e0; e < E; e++) {
             real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            const real l = la_at(e, La_d1, la0);
             edge_full<real>(xpe[2 * e], xpe[2 * e + 1], gie[2 * e], gie[2 * e + 1],
-                            edge_a(e, A1, La_d1, cw), La_d1[e], zu, zv, ou, ov, rho);
+                            A1 ? A1[e] : cw * l, l, zu, zv, ou, ov, rho);
             Z2[2 * e] = zu;
             Z2[2 * e + 1] = zv;
             pd.wzp[pd.sl[2 * e]] = ou;
@@ -1702,6 +1728,7 @@ struct TinyArgs {
     const int *Eu, *Ev;
     real *Z2;
     const real *A1, *La_d1;
+    real la0;           // every edge's weight when La_d1 is null
     real cw, rho;
     const R2<real> *gi;
     real *wz;
@@ -1747,7 +1774,7 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
     for (int it = 0; it < t.iters; it++) {
         if (halt) break;  // uniform (set by lane 0 before the last barrier)
         for (long e0 = (long)tid * EPT; e0 < t.E; e0 += (long)kTiny * EPT)
-            edge_lane<real>(e0, t.E, t.E, t.Eu, t.Ev, xp, t.Z2, t.A1, t.cw, t.gi, t.La_d1, t.wz,
+            edge_lane<real>(e0, t.E, t.E, t.Eu, t.Ev, xp, t.Z2, t.A1, t.cw, t.gi, t.La_d1, t.la0, t.wz,
                             t.rho);
         __syncthreads();
         for (int b0 = 0; b0 < a.nb; b0 += kTiny / kBlock) {
@@ -1810,90 +1837,6 @@ __global__ __launch_bounds__(kTiny) void k_tiny_iterate(TinyArgs<real> t) {
             }
         }
         __syncthreads();
-    }
-}
-
-// ------------------------------------- mid-size graphs, one launch --
-// A chunk of whole iterations of a single-GPU graph in ONE launch of G
-// workgroups that are all resident (cooperative launch, G <= the CUs):
-// per iteration the edge pass (chunks of kBlock * EPT edges dealt over the
-// workgroups, each lane running k_edge_sweep's lane body), a grid barrier,
-// the vertex pass (vertex blocks dealt over the workgroups, vertex_block as
-// in k_vertex_sweep, per-block evolution partials), a grid barrier; then
-// EVERY workgroup sums the partials with k_reduce_decide's tree and takes
-// the same decision on its own copy of the control block (workgroup 0
-// alone writes it and Dif), so the loop needs no third barrier and every
-// workgroup leaves it at the same iteration.  Same device code, same
-// operation order as the multi-launch path: iterates, iteration counts and
-// Dif are identical bit for bit; what goes is 2-3 launches per iteration
-// (the latency floor of C1-sized graphs and CP's reduced problems).
-template <typename real>
-struct CoopArgs {
-    long E;
-    const int *Eu, *Ev;
-    real *Z2;
-    const real *A1, *La_d1;
-    real cw, rho;
-    const R2<real> *gi;
-    real *wz;
-    VArgs<real> va;     // nb = every vertex block, bbeg 0, no XCD order
-    real *red;          // (num, den) of the last evolution
-    Ctrl<real> *ctrl;   // null: no tracking, run exactly `iters`
-    real *Dif;
-    int track, iters;
-    unsigned *bar;      // grid barrier state (2 words, zero at first use)
-};
-
-template <typename real, int GB>
-__global__ __launch_bounds__(256) void k_coop_iterate(CoopArgs<real> t) {
-    constexpr int EPT = Vec<real>::kPer16B;
-    __shared__ real lds[GatherCap<real>::v];
-    __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[kBlock / kWave];
-    __shared__ Ctrl<real> c;
-    const unsigned G = gridDim.x;
-    const int tid = threadIdx.x;
-    const VArgs<real> &a = t.va;
-    if (t.ctrl) {
-        if (tid == 0) c = *t.ctrl;
-        __syncthreads();
-        if (c.halt) return;  // every workgroup reads the same control block
-    }
-    const long nbe = (t.E + (long)kBlock * EPT - 1) / ((long)kBlock * EPT);
-    for (int it = 0; it < t.iters; it++) {
-        for (long b = blockIdx.x; b < nbe; b += G)
-            edge_lane<real>((b * kBlock + tid) * EPT, t.E, t.E, t.Eu, t.Ev, a.xp, t.Z2, t.A1,
-                            t.cw, t.gi, t.La_d1, t.wz, t.rho);
-        grid_sync(t.bar, G);
-        for (int blk = blockIdx.x; blk < a.nb; blk += G) {
-            vertex_block<real, GB>(a, blk, lds, red, scan);
-            __syncthreads();  // lds / scan reused by the next block
-        }
-        if (!t.ctrl) {
-            if (it + 1 < t.iters) grid_sync(t.bar, G);
-            continue;
-        }
-        grid_sync(t.bar, G);
-        // k_reduce_decide, in every workgroup
-        real sa = real(0), sb = real(0);
-        if (t.track) {
-            for (int i = tid; i < a.nb; i += kBlock) {
-                sa += a.part[2 * i];
-                sb += a.part[2 * i + 1];
-            }
-            sa = block_sum(sa, red[0]);
-            sb = block_sum(sb, red[1]);
-        }
-        if (tid == 0) {
-            decide_step(&c, sa, sb, blockIdx.x == 0 ? t.Dif : nullptr, t.track);
-            if (blockIdx.x == 0) {
-                if (t.track) { t.red[0] = sa; t.red[1] = sb; }
-                t.ctrl->it = c.it; t.ctrl->dif = c.dif;
-                t.ctrl->stop = c.stop; t.ctrl->recond = c.recond; t.ctrl->halt = c.halt;
-            }
-        }
-        __syncthreads();
-        if (c.halt) break;  // the same decision in every workgroup
     }
 }
 

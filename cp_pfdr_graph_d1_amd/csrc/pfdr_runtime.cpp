@@ -377,7 +377,7 @@ using namespace pfdr;
     }
 
 extern "C" const char *pfdr_last_error(void) { return g_last_error.c_str(); }
-extern "C" int pfdr_abi_version(void) { return 2; }
+extern "C" int pfdr_abi_version(void) { return 3; }
 extern "C" int pfdr_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return -1;
@@ -492,11 +492,11 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
-    else if (!strcmp(what, "coop")) *value = s->impl->coop;
     else if (!strcmp(what, "fused")) *value = s->impl->fused;
     else if (!strcmp(what, "padded")) *value = s->impl->padded;
+    else if (!strcmp(what, "seqdif")) *value = s->impl->seqdif;
+    else if (!strcmp(what, "la_uniform")) *value = s->impl->la_uniform;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
-    else if (!strcmp(what, "pipeline_chunks")) *value = s->impl->pipeline_chunks;
     else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;
     else return report_error("pfdr_session_query", (std::string("unknown key ") + what).c_str());

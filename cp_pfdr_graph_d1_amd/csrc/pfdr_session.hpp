@@ -63,11 +63,11 @@ class SessionBase {
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
     int64_t symv = 0;          // A^tA products from the block upper triangle
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch
-    int64_t coop = 0;          // mid-size graph: workgroups of the persistent launch (0: off)
     int64_t fused = 0;         // small graph: loop decision inside the next edge sweep
     int64_t padded = 0;        // fused graph: contributions stored in per-block lists
+    int64_t seqdif = 0;        // evolution statistic with the reference's sequential rounding
+    int64_t la_uniform = 0;    // one La_d1 value for every edge: the array is not streamed
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
-    int64_t pipeline_chunks = 0;  // pipelined iteration: vertex chunks per iteration
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;

@@ -29,6 +29,7 @@
 
 #include "pfdr_graph.hpp"
 #include "pfdr_halo.hpp"
+#include "pfdr_monosum.hpp"
 #include "pfdr_session.hpp"
 
 namespace pfdr {
@@ -596,6 +597,7 @@ struct SxProjArgs {
     int track;   // 0 none, 1 l1 evolution, 2 label changes
     real *part;
     const Ctrl<real> *ctrl;
+    real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
 };
 
 // projection + evolution + next explicit step, one thread per vertex
@@ -615,6 +617,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
                 real d = a.P[b + k] - x[k];
                 if (d < real(0)) d = -d;
                 dif += d;
+                if (a.terms) a.terms[b + k] = d;
             }
         } else if (a.track == 2) {
             real mx = x[0];
@@ -622,6 +625,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
             for (int k = 1; k < K; k++) if (x[k] > mx) { mx = x[k]; l = k; }
             const real fl = (real)l;
             if (fl != a.lab[v]) { dif = real(1); a.lab[v] = fl; }
+            if (a.terms) a.terms[v] = dif;
         }
         for (int k = 0; k < K; k++) {
             const real p = x[k];
@@ -665,6 +669,7 @@ struct SxVArgs {
     int track;
     real *part;
     const Ctrl<real> *ctrl;
+    real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
 };
 
 // One block of the fused vertex sweep: NT lanes (t = the lane within
@@ -673,7 +678,7 @@ struct SxVArgs {
 // no live lane); the block's evolution partial goes to *part_out (lane 0).
 // The body of k_sx_vertex_sweep, shared with the one-workgroup
 // k_sx_tiny_iterate (four blocks side by side).
-template <typename real, int NT, bool WZ>
+template <typename real, int NT>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
                                                 real *ms, real *red, real *part_out) {
     const int K = a.c.K, vb = a.vb;
@@ -684,9 +689,8 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     const bool live = blk < a.nb && vl < vb && v < a.V;
     const long i = v * K + k;
     if (live) {
-        const real inv = WZ ? real(0) : a.invAux[i];  // 1/Aux of this (v, k)
+        const real inv = a.invAux[i];  // 1/Aux of this (v, k)
         const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
-        const real *__restrict__ wz = a.wz;
         real s = real(0);
         int j = j0;
         // 8 slots, then 8 contributions in flight per lane; summed in order
@@ -695,10 +699,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             real w[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
-            if (WZ) {
-#pragma unroll
-                for (int q = 0; q < 8; q++) w[q] = wz[(long)sl[q] * K + k];
-            } else {  // W * Z formed here (the reference's products, same rounding)
+            {   // W * Z formed here (the reference's products, same rounding)
                 // branch-free: received entries (address 2E + j) sit in the
                 // tail of Zv as the sender's W*Z (factor 1), so all 16 loads
                 // issue together
@@ -721,15 +722,11 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
         }
         for (; j < j1; j++) {
             const long ad = a.idx[j];
-            if (WZ) {
-                s += wz[ad * K + k];
-            } else {
-                const bool sv = ad >= a.E;
-                const long ea = sv ? ad - a.E : ad;
-                const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
-                if (ea >= a.E) s += z;
-                else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
-            }
+            const bool sv = ad >= a.E;
+            const long ea = sv ? ad - a.E : ad;
+            const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
+            if (ea >= a.E) s += z;
+            else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
         }
         xs[t] = s;
         ms[t] = a.Ga[i];
@@ -745,6 +742,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             for (int d = 1; d < K; d++) if (x[d] > mx) { mx = x[d]; l = d; }
             const real fl = (real)l;
             if (fl != a.lab[v0 + t]) { dif = real(1); a.lab[v0 + t] = fl; }
+            if (a.terms) a.terms[v0 + t] = dif;
         }
     }
     __syncthreads();
@@ -754,6 +752,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             real d = a.P[i] - p;
             if (d < real(0)) d = -d;
             dif += d;
+            if (a.terms) a.terms[i] = d;
         }
         a.P[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
@@ -773,14 +772,14 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     }
 }
 
-template <typename real, int NT, bool WZ>
+template <typename real, int NT>
 __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real xs[NT], ms[NT];
     __shared__ real red[NT / kWave];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
-    sx_vertex_block<real, NT, WZ>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+    sx_vertex_block<real, NT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
 }
 
 // ------------------------------------------ small problems, one launch --
@@ -844,7 +843,7 @@ __global__ __launch_bounds__(kSxTiny) void k_sx_tiny_iterate(SxTinyArgs<real> t)
         __syncthreads();
         for (int b0 = 0; b0 < a.nb; b0 += NB) {
             const int blk = b0 + sub;
-            sx_vertex_block<real, kBlock, false>(a, blk, lt, xs + sub * kBlock, ms + sub * kBlock,
+            sx_vertex_block<real, kBlock>(a, blk, lt, xs + sub * kBlock, ms + sub * kBlock,
                                                  red + sub * (kBlock / kWave), bpart + blk);
             __syncthreads();  // xs / ms / red reused by the next four blocks
         }
@@ -1070,12 +1069,6 @@ static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipS
 
 static int mask_words(int D) { return (D + 63) / 64; }
 
-// A/B switch: NAME=0 disables an optional fast path
-static bool env_flag_off(const char *name) {
-    const char *v = getenv(name);
-    return v && v[0] == '0';
-}
-
 template <typename real>
 static void launch_proj(real *X, const real *M, int D, int N, int nm,
                         const real *A, int na, hipStream_t s) {
@@ -1114,6 +1107,15 @@ class SimplexSession final : public SessionBase {
     real rho_, condMin_, difTol_, difRcd_, cap_;
     bool rec_obj_, rec_dif_;
     int track_;  // 0, 1 (l1 evolution), 2 (labels)
+    // evolution sum with the reference's sequential rounding (PFDR_EVOLUTION_*,
+    // include/pfdr_mi355x.h): the vertex sweep stores the terms in the
+    // reference's order (v K + k, or v for label changes), one binade-scan sum
+    // (mono_sum) replaces the block partials' tree
+    bool seqdif_ = false;
+    long nterms_ = 0;
+    DevBuf<real> terms_;
+    DevBuf<char> dws_;
+    static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     DevBuf<int> Eu_, Ev_;
     DevBuf<real> La_d1_, La_f_, Q_, P_, Pavg_, Ga_, GaQ_, invAux_, lab_;
     // (P, explicit step) pairs per (v, k), ghosts included: written with P
@@ -1121,25 +1123,24 @@ class SimplexSession final : public SessionBase {
     DevBuf<SxR2<real>> PF_;
     DevBuf<real> Zu_, Zv_, A1_, wz_, part_, opart_, Obj_, Dif_;
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
-    // stored prox weights/thresholds of the non-linear losses (else
-    // recomputed from the factors in every edge sweep; PFDR_SX_PW=0/1)
+    // stored prox weights/thresholds of the non-linear losses for odd K (one
+    // (e, k) per lane); even K takes two per lane and recomputes them from
+    // the factors (C4: 1.076 -> 0.950 ms, r1zw; odd K stored: 1.24 vs 1.30 ms)
     DevBuf<real> Wd1u_, Wd1v_, Th_;
     bool sx_pw_ = true;
-    bool sx_pair_ = true;  // PFDR_SX_PAIR=0: one (e, k) per lane in the edge sweep (A/B)
     DevBuf<Ctrl<real>> ctrl_;
     Ctrl<real> *hctrl_ = nullptr;
     Incidence inc_;
     HostPins pins_;  // caller arrays pinned for the setup copies
     int nbv_, nbe_;
-    int vb_ = 0, nbs_ = 0, sx_nt_ = 256;  // fused vertex sweep: vertices, blocks, threads
-    // false (default): the vertex sweep forms W*Z from the gathered Z and W
-    // (K contiguous words per incidence), so the edge sweep neither reads W
-    // nor writes contributions: 28 instead of 44 streamed bytes per (e, k)
-    // (C4: 2.42 -> 2.17 ms/iteration)
-    bool sx_wz_ = false;
-    // XCD-aware block order (PFDR_SX_XCD=<edge><vertex>, PFDR_SX_XCD_CHUNK[_V]):
-    // runs of 64 edge blocks per XCD (C4 edge sweep 1.275 -> 1.244 ms, r1zm)
-    int sx_xcd_e_ = 64, sx_xcd_v_ = 0;
+    int vb_ = 0, nbs_ = 0;  // fused vertex sweep (K <= 64): vertices per block, blocks
+    // the fused vertex sweep forms W*Z from the gathered Z and W (K contiguous
+    // words per incidence), so the edge sweep neither reads W nor writes
+    // contributions: 28 instead of 44 streamed bytes per (e, k) (C4: 2.42 ->
+    // 2.17 ms/iteration)
+    // XCD-aware block order: runs of 64 edge blocks per XCD (C4 edge sweep
+    // 1.275 -> 1.244 ms, r1zm); the vertex sweep in plain order
+    static constexpr int sx_xcd_e_ = 64, sx_xcd_v_ = 0;
     int it_ = 0;
     bool stopped_ = false;
     int chunk_ = 32;
@@ -1147,7 +1148,7 @@ class SimplexSession final : public SessionBase {
     // hipGraph of a chunk of bodies (single GPU, no objective record,
     // unprofiled; re-captured after a reconditioning): small problems --
     // cut pursuit's reduced ones -- are otherwise bound by the host's three
-    // launches per iteration.  PFDR_GRAPH=0 launches directly.
+    // launches per iteration.
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
@@ -1214,6 +1215,13 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     rec_dif_ = p->record_dif != 0;
     track_ = (difTol_ > real(0) || difRcd_ > real(0) || rec_dif_) ? (difTol_ >= real(1) ? 2 : 1) : 0;
     cap_ = real(1.9) * (real(2) - rho_);
+    const int evo = p->evolution;
+    if (evo < PFDR_EVOLUTION_AUTO || evo > PFDR_EVOLUTION_TREE)
+        throw std::runtime_error("evolution must be PFDR_EVOLUTION_AUTO, _SEQUENTIAL or _TREE");
+    if (evo == PFDR_EVOLUTION_SEQUENTIAL && (p->nranks > 1 || p->comm))
+        throw std::runtime_error("PFDR_EVOLUTION_SEQUENTIAL needs a single GPU (a partitioned "
+                                 "session sums the evolution statistic in a tree)");
+    nterms_ = track_ == 2 ? (long)V_ : (long)V_ * K_;
 
     const int mem = p->mem;
     const auto kind = mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
@@ -1248,18 +1256,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         else PFDR_HIP(hipMemcpyAsync(q.first->p, q.second, VK_ * sizeof(real), kind, s));
         pullK(*q.first);
     }
-    if (K_ <= 64 && !env_flag_off("PFDR_SX_FUSED")) {
-        const char *nt = getenv("PFDR_SX_NT");  // threads per block: 64 (default) or 256
-        sx_nt_ = (nt && atoi(nt) == 64) ? 64 : 256;
-        const char *xc = getenv("PFDR_SX_XCD");
-        if (xc && strlen(xc) == 2) { sx_xcd_e_ = xc[0] == '1'; sx_xcd_v_ = xc[1] == '1'; }
-        const char *xe = getenv("PFDR_SX_XCD_CHUNK");  // runs of C blocks per XCD (edge sweep)
-        if (xe && atoi(xe) >= 2) sx_xcd_e_ = atoi(xe);
-        const char *xv = getenv("PFDR_SX_XCD_CHUNK_V");  // idem, vertex sweep
-        if (xv && atoi(xv) >= 2) sx_xcd_v_ = atoi(xv);
-        const char *wz = getenv("PFDR_SX_WZ");  // 1: edge sweep stores W*Z (A/B)
-        sx_wz_ = wz && wz[0] == '1';
-        vb_ = sx_nt_ / K_;
+    if (K_ <= 64) {
+        vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
     } else {
         Pavg_.alloc(VK_);
@@ -1271,14 +1269,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     Zu_.alloc(EKn);
     Zv_.alloc(EKn + (size_t)R_ * K_);
     GI_.alloc(VgK);
-    {
-        const char *pr = getenv("PFDR_SX_PAIR");
-        sx_pair_ = !(pr && pr[0] == '0');
-        // prox weights: recomputed in the pair sweep (C4: 1.076 -> 0.950 ms,
-        // r1zw), stored for the one-per-lane sweep (odd K: 1.24 vs 1.30 ms)
-        const char *pw = getenv("PFDR_SX_PW");
-        sx_pw_ = pw ? pw[0] == '1' : !(sx_pair_ && K_ % 2 == 0);
-    }
+    sx_pw_ = K_ % 2 != 0;
     if (sx_pw_ && c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
@@ -1311,23 +1302,30 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     PFDR_HIP(hipStreamSynchronize(s));
     pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
-    {
-        const char *g = getenv("PFDR_GRAPH");
-        graphs_ok_ = !(g && g[0] == '0') && !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
-    }
+    graphs_ok_ = !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
     {
         const char *t = getenv("PFDR_SX_TINY");
         const long maxEK = t ? atol(t) : kSxTinyEK;
-        tiny_ = maxEK > 0 && !halo_ && !rec_obj_ && vb_ && sx_nt_ == kBlock && !sx_wz_ &&
-                EK_ > 0 && EK_ <= maxEK && nbs_ <= (t ? kSxTinyMaxBlocks : SxTinyBlocks<real>::v);
+        tiny_ = maxEK > 0 && !halo_ && !rec_obj_ && vb_ &&
+                EK_ > 0 && EK_ <= maxEK && nbs_ <= (t ? kSxTinyMaxBlocks : SxTinyBlocks<real>::v) &&
+                !(track_ && evo == PFDR_EVOLUTION_SEQUENTIAL);
         tiny = tiny_ ? 1 : 0;
         if (tiny_) graphs_ok_ = false;
+    }
+    seqdif_ = track_ && !halo_ && !tiny_ &&
+              (evo == PFDR_EVOLUTION_SEQUENTIAL ||
+               (evo == PFDR_EVOLUTION_AUTO && nterms_ >= kSeqDifMin));
+    if (seqdif_) {
+        terms_.alloc((size_t)nterms_);
+        dws_.alloc(mono_ws_bytes<real>(nterms_, 1));
+        red_.alloc(2);
+        seqdif = 1;
     }
     if (graphs_ok_) (void)chunk_graph();  // instantiated with the setup
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
-                            &Dif_})
+                            &Dif_, &terms_})
         device_bytes += (int64_t)(b->n * sizeof(real));
     device_bytes += (int64_t)((GI_.n + PF_.n) * sizeof(SxR2<real>));
 }
@@ -1391,20 +1389,20 @@ void SimplexSession<real>::body() {
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     if (EK_) {
         ProfScope ps(prof, "sx_edge_sweep", s);
-        const int pair = (K_ % 2 == 0 && sx_pair_) ? 2 : 1;  // see k_sx_edge_sweep
+        const int pair = K_ % 2 == 0 ? 2 : 1;  // see k_sx_edge_sweep
         const int nb = grid_for(EK_ / pair);
         const int xm = xcd_fit(nb, sx_xcd_e_);
         if (pair == 2)
             k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               (vb_ && !sx_wz_) ? nullptr : wz_.p,
+                                                               vb_ ? nullptr : wz_.p,
                                                                rho_, c, nb, xm);
         else
             k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               (vb_ && !sx_wz_) ? nullptr : wz_.p,
+                                                               vb_ ? nullptr : wz_.p,
                                                                rho_, c, nb, xm);
     }
     if (halo_) {
@@ -1416,17 +1414,12 @@ void SimplexSession<real>::body() {
         a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
         a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        a.terms = seqdif_ ? terms_.p : nullptr;
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
-        if (sx_nt_ == 256) {
-            if (sx_wz_) k_sx_vertex_sweep<real, 256, true><<<g, 256, 0, s>>>(a);
-            else k_sx_vertex_sweep<real, 256, false><<<g, 256, 0, s>>>(a);
-        } else {
-            if (sx_wz_) k_sx_vertex_sweep<real, 64, true><<<g, 64, 0, s>>>(a);
-            else k_sx_vertex_sweep<real, 64, false><<<g, 64, 0, s>>>(a);
-        }
+        k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
     } else {
         {
             ProfScope ps(prof, "sx_average", s);
@@ -1436,6 +1429,7 @@ void SimplexSession<real>::body() {
         SxProjArgs<real> a{};
         a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
         a.P = P_.p; a.PF = PF_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        a.terms = seqdif_ ? terms_.p : nullptr;
         ProfScope ps(prof, "sx_project", s);
         launch_project(a);
     }
@@ -1452,6 +1446,13 @@ void SimplexSession<real>::body() {
         }
         k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
                                                  rec_dif_ ? Dif_.p : nullptr, red_.p);
+    } else if (seqdif_) {
+        // the reference's sequential sum (ref :655-689), then its decision
+        ProfScope ps(prof, "seq_evolution", s);
+        mono_sum<real>(nterms_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
+                       &ctrl_.p->halt);
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
+                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
     } else if (gated) {
         k_sx_finalize<real><<<1, kBlock, 0, s>>>(nparts, part_.p, Vglob_, track_, ctrl_.p,
                                                  rec_dif_ ? Dif_.p : nullptr, nullptr);
@@ -1465,7 +1466,7 @@ template <typename real>
 void SimplexSession<real>::push_wz() {
     const int eb = K_ * (int)sizeof(real);
     real *tail = wz_.p + 2 * EK_;
-    if (!vb_ || sx_wz_) {  // the edge sweep stored W*Z
+    if (!vb_) {  // the edge sweep stored W*Z
         halo_->push(wz_.p, tail, eb, stream);
         return;
     }
@@ -1498,7 +1499,7 @@ void SimplexSession<real>::tiny_chunk(int n) {
     t.V = Vglob_;
     t.iters = n;
     ProfScope ps(prof, "sx_tiny_iterate", stream);
-    if (K_ % 2 == 0 && sx_pair_) k_sx_tiny_iterate<real, 2><<<1, kSxTiny, 0, stream>>>(t);
+    if (K_ % 2 == 0) k_sx_tiny_iterate<real, 2><<<1, kSxTiny, 0, stream>>>(t);
     else k_sx_tiny_iterate<real, 1><<<1, kSxTiny, 0, stream>>>(t);
     PFDR_HIP(hipGetLastError());
 }

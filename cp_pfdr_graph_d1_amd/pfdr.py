@@ -27,7 +27,9 @@ PFDR_MEM_HOST, PFDR_MEM_DEVICE = 0, 1
 PFDR_KIND_L1, PFDR_KIND_BOUNDS, PFDR_KIND_SIMPLEX = 0, 1, 2
 SCAL, DIAG = 0, 1
 REORDER_AUTO, REORDER_ON, REORDER_OFF = 0, 1, 2
-ABI_VERSION = 2  # pfdr_abi_version() of the matching library
+# iterate-evolution statistic (include/pfdr_mi355x.h PFDR_EVOLUTION_*)
+EVOLUTION_AUTO, EVOLUTION_SEQUENTIAL, EVOLUTION_TREE = 0, 1, 2
+ABI_VERSION = 3  # pfdr_abi_version() of the matching library
 
 # every C entry point of include/pfdr_mi355x.h
 EXPORTED = (
@@ -88,6 +90,7 @@ class Problem(C.Structure):
         ("vtx_begin", C.c_int64), ("V_global", C.c_int64),
         ("e_global", C.c_void_p), ("e_offset", C.c_int64),
         ("reorder", C.c_int),
+        ("evolution", C.c_int),
     ]
 
 
@@ -472,7 +475,7 @@ class Session:
                  difRcd=0.0, difTol=0.0, itMax=1000, record_obj=False,
                  record_dif=False, verbose=0, device=False, nranks=0, rank=0,
                  comm=None, comm_kind=0, vtx_begin=0, V_global=0, e_global=None,
-                 e_offset=0, reorder=REORDER_AUTO):
+                 e_offset=0, reorder=REORDER_AUTO, evolution=EVOLUTION_AUTO):
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
@@ -506,6 +509,7 @@ class Session:
         p.comm_kind = comm_kind
         p.vtx_begin, p.V_global, p.e_offset = vtx_begin, V_global, e_offset
         p.reorder = reorder
+        p.evolution = evolution
         if e_global is not None:
             eg = np.ascontiguousarray(e_global, np.int64)
             self._keep.append(eg)

@@ -56,7 +56,7 @@ extern "C" {
 #define PFDR_LIPSCHITZ_DIAG 1
 
 const char *pfdr_last_error(void);
-int pfdr_abi_version(void);          /* 2 (pfdr_problem.reorder added) */
+int pfdr_abi_version(void);          /* 3 (pfdr_problem.evolution added) */
 int pfdr_device_count(void);         /* visible HIP devices, <0 on error */
 
 /* ------------------------------------------------------------------ l1 -- */
@@ -126,6 +126,25 @@ int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
 #define PFDR_REORDER_ON 1
 #define PFDR_REORDER_OFF 2
 
+/* Iterate-evolution statistic (the stopping / reconditioning test and Dif;
+ * reference src/PFDR_graph_quadratic_d1_l1.cpp:514-529, simplex
+ * src/PFDR_graph_loss_d1_simplex.cpp:653-691).  The reference adds its terms
+ * one by one in `real`, and over millions of f32 terms that sum drifts by
+ * percents from the exact value -- enough to move the stopping iteration.
+ * SEQUENTIAL reproduces that rounding exactly (parallel binade scan,
+ * pfdr_monosum.hpp): Dif, the stopping iteration and the iterate are then
+ * the reference's bit for bit.  TREE sums in a fixed tree (faster; the
+ * decision may land an iteration or so away on huge f32 problems).  AUTO:
+ * SEQUENTIAL on one GPU for sums of at least 2^17 terms, except on the
+ * small-graph paths that decide inside a sweep (quadratic: identity /
+ * diagonal A, no objective record, <= 1,024 vertex blocks of 256; both
+ * solvers' one-workgroup paths), which keep TREE; a partitioned session
+ * always uses TREE (SEQUENTIAL there is refused).  SEQUENTIAL forced on a
+ * small graph takes the multi-launch loop instead of those paths. */
+#define PFDR_EVOLUTION_AUTO 0
+#define PFDR_EVOLUTION_SEQUENTIAL 1
+#define PFDR_EVOLUTION_TREE 2
+
 typedef struct pfdr_problem {
     int kind;             /* PFDR_KIND_* */
     int dtype;            /* PFDR_F32 / PFDR_F64: type of every real array */
@@ -157,6 +176,8 @@ typedef struct pfdr_problem {
     int64_t e_offset;
     /* --- internal locality reordering (quadratic solvers, one GPU) -------- */
     int reorder;          /* PFDR_REORDER_*; results are identical either way */
+    /* --- iterate-evolution statistic -------------------------------------- */
+    int evolution;        /* PFDR_EVOLUTION_* */
 } pfdr_problem;
 
 typedef struct pfdr_session pfdr_session;

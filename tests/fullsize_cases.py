@@ -13,6 +13,11 @@ with the library's native generators (splitmix64 laws, no device needed):
   c4_k2                simplex K = 10, KL al = 0.1, 2236^2 8-nbr (V 5.0M,
                        E 20.0M), f32, 2 iterations
   c5_k1                bounds [0, 1], 640^3 6-NN (V 262M, E 785M), f32, 1 it
+  headline_conv        the headline solved to difTol 1e-5 (C2's
+  c2_conv              parity tolerance), C2 to difTol 1e-5 and C4 to its
+  c4_conv              difTol 1e-4: the north star's
+                       "within 1e-5 relative l2 of the CPU reference" on
+                       converged solves, iteration counts included
 
 tests/golden/make_fullsize.py runs the REFERENCE (oracle/_ref/
 libpfdr_ref_seq.so) on each and commits digests (tests/golden/fullsize/);
@@ -26,7 +31,8 @@ from cp_pfdr_graph_d1_amd import pfdr
 # C3 scalar Lipschitz constant L = ||A||^2: computed once by
 # make_fullsize.py (power method in float64) and stored with the digest
 CASES = ("c1_fixk25", "c1_conv", "headline_k3", "c2_k2", "c3_direct_k2", "c3_ata_k3",
-         "c4_k2", "c5_k1")
+         "c4_k2", "c5_k1", "headline_conv", "c2_conv", "c4_conv")
+CONVERGED = ("c1_conv", "headline_conv", "c2_conv", "c4_conv")
 SAMPLE_SEED = 0x5EED
 DENSE = ("c3_direct_k2", "c3_ata_k3")
 
@@ -65,17 +71,21 @@ def build(name, L_c3=None):
                  positivity=0, Ltype=pfdr.DIAG, L=None, rho=1.5, condMin=1e-3, difRcd=0.0,
                  difTol=1e-6 if conv else 0.0, itMax=10000 if conv else 25)
         return dict(solver="l1", dtype=np.float64, args=a, sample_m=V)
-    if name == "headline_k3":
+    if name in ("headline_k3", "headline_conv"):
         d = _piecewise_l1((250, 200, 200), 2, 6, np.float32, knn=True)
         # headline Y: gen_piecewise(nx=250, seed 2) as tools/workloads.py
+        conv = name == "headline_conv"
         a = dict(d, A=None, N=0, positivity=0, Ltype=pfdr.SCAL, L=None, rho=1.5,
-                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=3)
-        return dict(solver="l1", dtype=np.float32, args=a, sample_m=4096)
-    if name == "c2_k2":
+                 condMin=1e-3, difRcd=0.0, difTol=1e-5 if conv else 0.0,
+                 itMax=10000 if conv else 3)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=65536 if conv else 4096)
+    if name in ("c2_k2", "c2_conv"):
         d = _piecewise_l1((256, 256, 256), 2, 6, np.float32)
+        conv = name == "c2_conv"
         a = dict(d, A=None, N=0, positivity=0, Ltype=pfdr.SCAL, L=None, rho=1.5,
-                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=2)
-        return dict(solver="l1", dtype=np.float32, args=a, sample_m=4096)
+                 condMin=1e-3, difRcd=0.0, difTol=1e-5 if conv else 0.0,
+                 itMax=10000 if conv else 2)
+        return dict(solver="l1", dtype=np.float32, args=a, sample_m=65536 if conv else 4096)
     if name == "c3_direct_k2":
         N, nx, ny = 1024, 2000, 1000
         V = nx * ny
@@ -106,7 +116,7 @@ def build(name, L_c3=None):
                  positivity=0, Ltype=pfdr.SCAL, L=np.array([2.0], np.float32), rho=1.5,
                  condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=3)
         return dict(solver="l1", dtype=np.float32, args=a, sample_m=V)
-    if name == "c4_k2":
+    if name in ("c4_k2", "c4_conv"):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
         n, K = 2236, 10
         V = n * n
@@ -115,9 +125,12 @@ def build(name, L_c3=None):
         lab = ((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)
         Q = simplex_observation(V, K, 4, lab, np.float32)
         E = Eu.size
+        conv = name == "c4_conv"
         a = dict(P0=Q.copy(), Q=Q, K=K, Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32),
-                 al=0.1, La_f=None, rho=1.0, condMin=0.1, difRcd=0.0, difTol=0.0, itMax=2)
-        return dict(solver="simplex", dtype=np.float32, args=a, sample_m=16384)
+                 al=0.1, La_f=None, rho=1.0, condMin=0.1, difRcd=0.0,
+                 difTol=1e-4 if conv else 0.0, itMax=10000 if conv else 2)
+        return dict(solver="simplex", dtype=np.float32, args=a,
+                    sample_m=65536 if conv else 16384)
     if name == "c5_k1":
         shape = (640, 640, 640)
         Eu, Ev = pfdr.gen_grid_edges(shape, 6)

@@ -70,6 +70,8 @@ def main():
         X, it, Dif = F.run(ref, case)
         t2 = time.perf_counter()
         d = F.digest(X, it, Dif, case["sample_m"])
+        if os.environ.get("PFDR_SAVE_X"):  # whole iterate, for local analysis only
+            np.save(os.path.join(os.environ["PFDR_SAVE_X"], name + ".npy"), X)
         if name in F.DENSE:
             # the same problem through the reference's double instantiation
             # (inputs widened exactly): the accuracy yardstick of the f32 runs

@@ -86,30 +86,3 @@ def test_headline_objective_decreases(gpu_lib):
     assert Obj[40] < Obj[5] and Obj[40] < Obj[0]
 
 
-def test_c3_ata_symmetric_product_full_size(gpu_lib):
-    """C3's A^tA variant at its full size (V = 32,768, A^tA = 4.3 GB formed on
-    the matrix cores): the upper-triangle product (k_symv_tiles) and the
-    full column dots (k_col_dot, PFDR_SYMV=0) regroup the same dot products
-    differently, so the iterates agree to the dense f32 tolerance of
-    test_parity_gpu.py (2e-5 relative l2) -- and the Gram output is exactly
-    symmetric, so the session must take the upper-triangle path."""
-    from workloads import WORKLOADS
-    from cp_pfdr_graph_d1_amd import pfdr
-    wl = WORKLOADS["c3_ata"]
-    inp = wl.inputs(0, 1)
-    out = []
-    for flag in ("2", "0"):
-        os.environ["PFDR_SYMV"] = flag
-        try:
-            s = pfdr.Session(wl.kind, wl.dtype, inp["V"], inp["E"], itMax=ITS, **inp["kw"])
-        finally:
-            del os.environ["PFDR_SYMV"]
-        assert s.query("symv") == (1 if flag == "2" else 0)
-        s.run(ITS)
-        out.append(s.result()[0])
-        s.close()
-    X1, X0 = out
-    assert np.all(np.isfinite(X1))
-    err = np.linalg.norm(X1.astype(np.float64) - X0) / max(np.linalg.norm(X0.astype(np.float64)), 1e-30)
-    print("c3_ata full size: symv vs column dots rel_l2 %.3e" % err)
-    assert err <= 2e-5

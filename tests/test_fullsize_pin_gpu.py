@@ -21,14 +21,17 @@ through the host-pointer C ABI that CP callers use, and:
     star's bound) and at least as close to it as the reference's f32 run;
   * converged C1: iteration count within 2 and 1e-9 relative l2 (f64) on
     every coordinate, bit-exact when the counts agree;
+  * converged headline / C2 (difTol 1e-5) and C4 (difTol 1e-4), the north
+    star's "within 1e-5 relative l2 of the CPU reference" on converged
+    solves: the same iteration count and sha256-equal X;
   * Dif: the reference accumulates the evolution statistic sequentially in
-    `real` (src/PFDR_graph_quadratic_d1_l1.cpp:514-529, simplex :677-688);
-    over millions of f32 terms that drifts far from the exact value (measured:
-    0.0843 vs 0.0884 at V = 10M, 0.00715 vs 0.00872 over C4's 50M terms),
-    while this library tree-reduces it.  At full size the GPU's f32 Dif is
-    therefore checked against the float64 recomputation from its own
-    consecutive iterates (1e-5; the reference's value is printed beside it);
-    f64 Dif against the reference's within 1e-9.
+    `real` (src/PFDR_graph_quadratic_d1_l1.cpp:514-529, simplex :653-691);
+    over millions of f32 terms that sum drifts by percents from the exact
+    value (0.0843 vs 0.0884 at V = 10M).  At these sizes the library sums the
+    terms with the same sequential rounding (PFDR_EVOLUTION_AUTO ->
+    sequential, pfdr_monosum.hpp), so Dif is the reference's bit for bit and
+    the stopping iteration is the first k with Dif[k] below the tolerance
+    (squared for the quadratic solvers), like the reference's loop.
 
 These catch size-only bugs the small fixtures cannot: int32 offsets, the
 split-incidence / staged-sweep fallbacks, CSR chunks beyond one workgroup.
@@ -50,22 +53,6 @@ def _gold(name):
     if not os.path.exists(p):
         pytest.fail("%s missing: run tests/golden/make_fullsize.py where the reference exists" % p)
     return np.load(p)
-
-
-def _dif64(case, X, k, gpu_lib):
-    """Dif[k-1] recomputed in float64 from the GPU's iterates k-1 and k"""
-    a = case["args"]
-    if k == 1:
-        Xp = (a["P0"] if case["solver"] == "simplex" else a["X0"]).astype(np.float64)
-    else:
-        a0 = a["itMax"]
-        a["itMax"] = k - 1
-        Xp = F.run(gpu_lib, case)[0].astype(np.float64)
-        a["itMax"] = a0
-    X = X.astype(np.float64)
-    if case["solver"] == "simplex":
-        return np.abs(Xp - X).sum() / (X.size // a["K"])
-    return ((Xp - X) ** 2).sum() / (X ** 2).sum()
 
 
 @pytest.mark.parametrize("name", F.CASES)
@@ -99,12 +86,17 @@ def test_fullsize_matches_reference(gpu_lib, name):
             assert exact
         return
     assert it == git
+    assert err <= 1e-5
     assert exact, "graph-mode / simplex iterate differs from the reference at full size"
-    gd = g["Dif"][:it].astype(np.float64)
+    gd = g["Dif"][:it]
     if X.dtype == np.float64:
         assert np.linalg.norm(Dif - gd) <= 1e-9 * np.linalg.norm(gd)
         return
-    d64 = _dif64(case, X, it, gpu_lib)
-    print("  Dif[%d]: GPU %.9g, float64 recomputation %.9g, reference %.9g" % (
-        it - 1, Dif[-1], d64, gd[-1]))
-    assert abs(float(Dif[-1]) - d64) <= 1e-5 * d64
+    assert np.array_equal(Dif, gd), "f32 Dif differs from the reference's sequential sums"
+    a = case["args"]
+    if name in F.CONVERGED:
+        tol = a["difTol"] if case["solver"] == "simplex" else np.float32(a["difTol"]) ** 2
+        below = np.nonzero(Dif < tol)[0]
+        print("  converged: it %d, first Dif below tolerance at %s" % (
+            it, below[0] if below.size else None))
+        assert below.size and below[0] == it - 1

@@ -39,19 +39,6 @@ def test_gram_matches_numpy(gpu_lib, dt, shape, which):
     assert err <= (2e-6 if dt == np.float32 else 1e-13)
 
 
-@pytest.mark.parametrize("shape", [(333, 129), (1000, 257), (64, 3000), (96, 4096)])
-@pytest.mark.parametrize("which", [0, 1])
-def test_gram_wide_tile(gpu_lib, shape, which, monkeypatch):
-    """the opt-in 256 x 256 f32 tile (PFDR_GRAM_WIDE=1, k_gram_w), same bar"""
-    monkeypatch.setenv("PFDR_GRAM_WIDE", "1")
-    A = _mat(*shape, seed=7 + sum(shape) + which, dt=np.float32)
-    G, _ = pfdr.gram(A, which)
-    A64 = A.astype(np.float64)
-    ref = A64.T @ A64 if which == 0 else A64 @ A64.T
-    assert np.array_equal(G, G.T)
-    assert np.linalg.norm(G - ref) / np.linalg.norm(ref) <= 2e-6
-
-
 def _spectral(M, N, s, seed, dt):
     """A = U diag(s) V^t with orthonormal U, V: ||A||^2 = max(s)^2"""
     rng = np.random.default_rng(seed)

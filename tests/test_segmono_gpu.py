@@ -2,13 +2,11 @@
 weights, a reduced edge's group of TV weights, the simplex driver's label
 sums, the CP builder's component sums) by the binade scan of
 pfdr_monosum.hpp when every term is nonnegative and finite
-(pfdr_cpgraph.hip segsum, PFDR_SEGMONO = 0 keeps one workgroup per long
-segment).  Both must equal the oracle (the reference's sequential loops,
+(pfdr_cpgraph.hip segsum; a segment with a negative or non-finite term
+keeps one workgroup).  Both must equal the oracle (the reference's sequential loops,
 oracle/cp_graph_body.h, oracle/cp_reduce_body.h) bit for bit: segments of
 75,000 terms, a segment with a negative term (falls back), a signed
 observation vector next to a positive diagonal."""
-import os
-
 import numpy as np
 import pytest
 
@@ -23,22 +21,6 @@ def _eq(a, b, what):
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), (what, np.flatnonzero(a != b)[:5])
     else:
         assert np.array_equal(a, b), (what, np.flatnonzero(a != b)[:5])
-
-
-class _env:
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 def _quadrants(nx=600, ny=500):
@@ -66,18 +48,16 @@ def test_reduced_graph_giant_components(gpu_lib, oracle_port, dt, negative):
     assert orVc.size - 1 == 4
     eps = float(np.finfo(dt).eps)
     ored = o.cp_reduced_graph(V, Eu, Ev, La, L1, act, oCv, oVc, orVc, eps)
-    for mono in ("1", "0"):
-        with _env(PFDR_SEGMONO=mono):
-            g = CPGraph(V, Eu, Ev, La, L1)
-            try:
-                g.set_active(act)
-                Cv, Vc, rVc = g.components()
-                _eq(Vc, oVc, "Vc")
-                red = g.reduced_graph(eps)
-                for a, b, nm in zip(red, ored, ("rEu", "rEv", "rLa_d1", "rLa_l1")):
-                    _eq(a, b, "%s (PFDR_SEGMONO=%s)" % (nm, mono))
-            finally:
-                g.close()
+    g = CPGraph(V, Eu, Ev, La, L1)
+    try:
+        g.set_active(act)
+        Cv, Vc, rVc = g.components()
+        _eq(Vc, oVc, "Vc")
+        red = g.reduced_graph(eps)
+        for a, b, nm in zip(red, ored, ("rEu", "rEv", "rLa_d1", "rLa_l1")):
+            _eq(a, b, nm)
+    finally:
+        g.close()
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
@@ -121,8 +101,6 @@ def test_builder_long_components(gpu_lib, oracle_port, dt):
     A = (0.5 + rng.random(V)).astype(dt)
     Y = (rng.random(V) - 0.5).astype(dt)
     o = oracle_port.cp_reduce(0, A, Y, ptr, Vc, preAt=True)
-    for mono in ("1", "0"):
-        with _env(PFDR_SEGMONO=mono):
-            g = pfdr.cp_reduce(0, A, Y, ptr, Vc, preAt=True, normTol=1e-6, normItMax=500)
-        for k in ("rAA", "rY"):
-            assert np.array_equal(g[k], o[k]), (k, mono)
+    g = pfdr.cp_reduce(0, A, Y, ptr, Vc, preAt=True, normTol=1e-6, normItMax=500)
+    for k in ("rAA", "rY"):
+        assert np.array_equal(g[k], o[k]), k

@@ -1,11 +1,12 @@
 """GPU: the split incidence of the vertex sweep (csrc/pfdr_quadratic_kernels.hpp
-split_sum) and the u-staged edge sweep (k_edge_sweep_us).  When the edges are sorted by their u end, each vertex's u-end
-contributions are a contiguous run and only the other entries are gathered;
-a per-vertex mask keeps the reference's (e, side) summation order.  The
-split and the plain CSR gather must give the same iterates bit for bit, and
-both must match the restatement of the reference (oracle)."""
-import os
-
+split_sum) and the u-staged edge sweep (k_edge_sweep_us).  When the edges
+are sorted by their u end, each vertex's u-end contributions are a
+contiguous run and only the other entries are gathered; a per-vertex code
+keeps the reference's (e, side) summation order.  Blocks that do not
+qualify (hubs, unsorted edges) keep the CSR gather.  Every path must equal
+the restatement of the reference (oracle) bit for bit: iterates, iteration
+counts and Dif (the sessions here sum the evolution sequentially, like the
+reference, so reconditioning and stopping decisions are the reference's)."""
 import numpy as np
 import pytest
 
@@ -15,55 +16,50 @@ from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, unifo
 pytestmark = pytest.mark.gpu
 
 
-KNOBS = ("PFDR_SPLIT", "PFDR_USTAGE")
-
-
-def _solve(split, V, Eu, Ev, Y, dt, it, reorder=pfdr.REORDER_OFF, **kw):
-    """split: True = split vertex sweep and u-staged edge sweep (defaults),
-    False = CSR gather and Eu stream everywhere."""
-    old = {k: os.environ.get(k) for k in KNOBS}
-    for k in KNOBS:
-        os.environ[k] = "1" if split else "0"
+def _solve(V, Eu, Ev, Y, dt, it, reorder=pfdr.REORDER_OFF, difRcd=0.0, difTol=0.0):
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                     np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3,
+                     itMax=it, reorder=reorder, difRcd=difRcd, difTol=difTol, record_dif=True,
+                     evolution=pfdr.EVOLUTION_SEQUENTIAL)
     try:
-        s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
-                         np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3,
-                         itMax=it, reorder=reorder, **kw)
+        nsplit = s.query("split_blocks")
+        s.run(it)
+        X, its, _, Dif = s.result()
     finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-    nsplit = s.query("split_blocks")
-    s.run(it)
-    X, its, _, Dif = s.result()
-    s.close()
+        s.close()
     return X, its, Dif, nsplit
 
 
+def _oracle(oracle_port, V, Eu, Ev, Y, dt, it, difRcd=0.0, difTol=0.0):
+    return oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
+                                       np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt), 0, 0,
+                                       None, 1.5, 1e-3, difRcd, difTol, it, dif=True)
+
+
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
-def test_split_equals_gather_natural_grid(gpu_lib, dt):
+def test_split_natural_grid_matches_oracle(gpu_lib, oracle_port, dt):
     """3-D 6-neighbour grid in emission order: every block takes the split
-    path; with reconditioning and a tolerance the two paths agree bit for bit
-    (iterates, iteration count, Dif)."""
+    path; with reconditioning and a tolerance, iterates, iteration count and
+    Dif equal the restatement's"""
     shape = (48, 40, 24)
     Eu, Ev = grid_graph(shape, 6)
+    Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
     V = int(np.prod(shape))
     Y = piecewise_observation(shape, 3, dt)
-    kw = dict(difRcd=1e-1, difTol=1e-5, record_dif=True)
-    Xs, its, Ds, ns = _solve(True, V, Eu, Ev, Y, dt, 400, **kw)
-    Xg, itg, Dg, ng = _solve(False, V, Eu, Ev, Y, dt, 400, **kw)
-    assert ns == (V + 255) // 256 and ng == 0
-    assert its == itg
-    assert np.array_equal(Xs, Xg)
-    assert np.array_equal(Ds[:its], Dg[:itg])
+    kw = dict(difRcd=1e-1, difTol=1e-5)
+    Xs, its, Ds, ns = _solve(V, Eu, Ev, Y, dt, 400, **kw)
+    Xo, ito, _, Do = _oracle(oracle_port, V, Eu, Ev, Y, dt, 400, **kw)
+    assert ns == (V + 255) // 256
+    assert its == ito
+    assert np.array_equal(Xs, Xo)
+    assert np.array_equal(Ds[:its], Do[:ito])
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 def test_split_mixed_blocks_with_hubs(gpu_lib, oracle_port, dt):
     """A 2-D grid plus hub vertices of degree > 32 and zero-out-degree runs:
     the hubs' blocks fall back to the CSR gather, the others split; results
-    equal the plain gather and the oracle bit for bit at a fixed k."""
+    equal the oracle bit for bit at a fixed k."""
     shape = (96, 80)
     V = int(np.prod(shape))
     Eu0, Ev0 = grid_graph(shape, 8)
@@ -82,31 +78,28 @@ def test_split_mixed_blocks_with_hubs(gpu_lib, oracle_port, dt):
     Eu, Ev = Eu[order].astype(np.int32), Ev[order].astype(np.int32)
     Y = piecewise_observation(shape, 4, dt)
     k = 25
-    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, dt, k)
-    Xg, _, _, _ = _solve(False, V, Eu, Ev, Y, dt, k)
+    Xs, _, _, ns = _solve(V, Eu, Ev, Y, dt, k)
     nb = (V + 255) // 256
     assert 0 < ns < nb
-    assert np.array_equal(Xs, Xg)
-    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
-                                                np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
-                                                0, 0, None, 1.5, 1e-3, 0.0, 0.0, k)
+    Xo, ito, _, _ = _oracle(oracle_port, V, Eu, Ev, Y, dt, k)
     assert ito == k
     assert np.array_equal(Xs, Xo)
 
 
-def test_split_unsorted_edges_keep_the_gather(gpu_lib):
-    """Edges out of u order: no split blocks, same results as sorted input
-    handled by the gather (the summation order is the edge order)."""
+def test_split_unsorted_edges_keep_the_gather(gpu_lib, oracle_port):
+    """Edges out of u order: no split blocks, the CSR gather and the Eu
+    stream everywhere (the summation order is the edge order); equal to the
+    oracle bit for bit"""
     shape = (64, 64)
     Eu, Ev = grid_graph(shape, 4)
     V = int(np.prod(shape))
     p = np.argsort(uniform(9, np.arange(Eu.size)), kind="stable")
     Eu, Ev = Eu[p].astype(np.int32), Ev[p].astype(np.int32)
     Y = piecewise_observation(shape, 6, np.float32)
-    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, np.float32, 10)
-    Xg, _, _, _ = _solve(False, V, Eu, Ev, Y, np.float32, 10)
+    Xs, _, _, ns = _solve(V, Eu, Ev, Y, np.float32, 10)
+    Xo, _, _, _ = _oracle(oracle_port, V, Eu, Ev, Y, np.float32, 10)
     assert ns == 0
-    assert np.array_equal(Xs, Xg)
+    assert np.array_equal(Xs, Xo)
 
 
 def test_split_after_relabelling(gpu_lib):
@@ -119,7 +112,7 @@ def test_split_after_relabelling(gpu_lib):
     new_of[np.argsort(uniform(11, np.arange(V)), kind="stable")] = np.arange(V)
     Eu, Ev = new_of[Eu].astype(np.int32), new_of[Ev].astype(np.int32)
     Y = piecewise_observation(shape, 7, np.float32)
-    Xs, _, _, ns = _solve(True, V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_ON)
-    Xg, _, _, ng = _solve(False, V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_OFF)
+    Xs, _, _, ns = _solve(V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_ON)
+    Xg, _, _, ng = _solve(V, Eu, Ev, Y, np.float32, 12, reorder=pfdr.REORDER_OFF)
     assert ns > 0 and ng == 0
     assert np.array_equal(Xs, Xg)

@@ -1,5 +1,5 @@
 """GPU: single-GPU simplex sessions replay their iteration chunks as
-hipGraphs (re-captured after a reconditioning; PFDR_GRAPH = 0 launches
+hipGraphs (re-captured after a reconditioning; a profiled session launches
 directly), and small ones run each chunk in one workgroup launch
 (k_sx_tiny_iterate; PFDR_SX_TINY = most (edge, label) entries, 0 off, a
 large value lifts the block cap to 32).  Iterates, iteration counts and the evolution record must be
@@ -42,8 +42,7 @@ class _env:
 def test_sx_graph_golden_identical(gpu_lib, name, fixed):
     c, g = G.load(name)
     res = []
-    for env in ({"PFDR_GRAPH": "1"}, {"PFDR_GRAPH": "0", "PFDR_SX_TINY": "0"},
-                {"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "100000000"}):
+    for env in ({}, {"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "100000000"}):
         with _env(**env):
             res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
     X0, it0, _, D0 = res[0]
@@ -77,8 +76,9 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
     Q[: V // 2, 0] += 2.0
     Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
     res = []
-    for env in ({"PFDR_SX_TINY": "0"}, {"PFDR_GRAPH": "0", "PFDR_SX_TINY": "0"},
+    for env in ({"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "0", "launch": "direct"},
                 {"PFDR_SX_TINY": "100000000"}, {}):
+        direct = env.pop("launch", None) == "direct"
         with _env(**env):
             s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev,
                              np.full(Eu.size, 0.05, dt), Q.copy(), Q, K=K, al=al, rho=1.0,
@@ -90,6 +90,8 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
                 assert s.query("tiny") == (1 if nb <= 32 else 0)
             elif env.get("PFDR_SX_TINY") == "0":
                 assert s.query("tiny") == 0
+            if direct:  # profiled: every chunk launched directly, no graph replay
+                s.profile(True)
             for n in runs:
                 s.run(n)
             res.append(s.result())

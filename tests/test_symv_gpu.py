@@ -1,17 +1,13 @@
-"""GPU: A^tA mode (N = -V) with the products taken from the block upper
-triangle of an exactly symmetric matrix (k_symv_tiles / k_symv_finish,
-PFDR_SYMV) against the reference's golden iterates, against the column-dot
-path (k_col_dot, which reads the whole matrix as given) and against the C
-restatement (oracle/) on larger, ragged sizes.
-
-(The sequential-order path that small dense problems take by default,
-PFDR_DENSE_EXACT, is turned off here; test_parity_gpu.py covers it.)
-Both dense paths regroup the reference's dot products
+"""GPU: A^tA mode (N = -V) past the sequential-order range of small dense
+problems (V > 8192, test_parity_gpu.py covers the small ones): the products
+taken from the block upper triangle of an exactly symmetric matrix
+(k_symv_tiles / k_symv_finish), or, for a matrix that is not exactly
+symmetric or a V off the 16-byte vector, by full column dots (k_col_dot,
+which reads the whole matrix as given) -- against the C restatement
+(oracle/) on ragged sizes.  Both regroup the reference's dot products
 (src/PFDR_graph_quadratic_d1_l1.cpp:368-376, :432-440, :462-464), so they
 are held to the dense tolerance of test_parity_gpu.py: relative l2 <= 2e-5
-(f32) / 1e-12 (f64) at a fixed iteration count, 1e-5 / 1e-9 converged."""
-import os
-
+(f32) / 1e-12 (f64) at a fixed iteration count."""
 import numpy as np
 import pytest
 
@@ -19,81 +15,10 @@ import golden_io as G
 
 pytestmark = pytest.mark.gpu
 
-ATA = [n for n in G.names() if "AtA" in n]
-
-
-@pytest.fixture(autouse=True)
-def _tree_reduced_products(monkeypatch):
-    """these problems are small enough for the sequential-order dense path
-    (PFDR_DENSE_EXACT, default up to a chain of 8192): off here, so the
-    tree-reduced products under test (upper triangle vs column dots) run"""
-    monkeypatch.setenv("PFDR_DENSE_EXACT", "0")
-
-
-class _env:
-    def __init__(self, **kw):
-        self.kw = kw
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kw}
-        os.environ.update(self.kw)
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-
-
 def _tol(dt, fixed):
     if fixed:
         return 2e-5 if dt == np.float32 else 1e-12
     return 1e-5 if dt == np.float32 else 1e-9
-
-
-def _session(c, **kw):
-    from cp_pfdr_graph_d1_amd import pfdr
-    kind = pfdr.PFDR_KIND_L1 if str(c["solver"]) == "l1" else pfdr.PFDR_KIND_BOUNDS
-    X0 = np.asarray(c["X0"])
-    extra = dict(La_l1=c.get("La_l1"), positivity=int(c.get("positivity", 0)))
-    if kind == pfdr.PFDR_KIND_BOUNDS:
-        extra = dict(lo=float(c["lo"]), hi=float(c["hi"]))
-    return pfdr.Session(kind, X0.dtype, X0.size, c["Eu"].size, c["Eu"], c["Ev"], c["La_d1"],
-                        X0, c["Y"], N=int(c["N"]), A=c["A"], Ltype=int(c["Ltype"]), L=c["L"],
-                        rho=float(c["rho"]), condMin=float(c["condMin"]), **extra, **kw)
-
-
-@pytest.mark.parametrize("name", ATA)
-@pytest.mark.parametrize("fixed", [True, False], ids=["fixk", "conv"])
-def test_symv_matches_reference(gpu_lib, name, fixed):
-    c, g = G.load(name)
-    tag = "fixk" if fixed else "conv"
-    gX, git = g[tag + "_X"], int(g[tag + "_it"])
-    with _env(PFDR_SYMV="1"):
-        s = _session(c, itMax=1)
-        assert s.query("symv") == 1, "golden A^tA is exactly symmetric: upper-triangle path expected"
-        s.close()
-        X1, it1, Obj1, Dif1 = G.replay(gpu_lib, c, fixed)
-    with _env(PFDR_SYMV="0"):
-        s = _session(c, itMax=1)
-        assert s.query("symv") == 0
-        s.close()
-        X0, it0, _, _ = G.replay(gpu_lib, c, fixed)
-    dt = X1.dtype
-    e1, e0 = G.rel_l2(X1, gX), G.rel_l2(X0, gX)
-    print("%s %s symv rel_l2=%.3e it=%d | col-dot %.3e it=%d | ref it=%d"
-          % (name, tag, e1, it1, e0, it0, git))
-    assert np.all(np.isfinite(X1))
-    assert e1 <= _tol(dt, fixed)
-    assert G.rel_l2(X1, X0) <= _tol(dt, fixed)
-    if fixed:
-        assert it1 == git
-        go = g["fixk_Obj"][: it1 + 1]
-        assert np.allclose(Obj1[: it1 + 1], go, rtol=(1e-4 if dt == np.float32 else 1e-10),
-                           atol=1e-6 * np.abs(go).max())
-    else:
-        assert abs(it1 - git) <= 2
 
 
 def _problem(V, dt, seed, nx):
@@ -111,41 +36,35 @@ def _problem(V, dt, seed, nx):
     return A, Y, Eu.astype(np.int32), Ev.astype(np.int32), L
 
 
-# ragged tiles (V not a multiple of the 128 / 64 tile), several tile rows
-@pytest.mark.parametrize("V,nx", [(1000, 40), (2048, 64), (1540, 44)])
-@pytest.mark.parametrize("dt", [np.float32, np.float64], ids=["f32", "f64"])
-def test_symv_matches_oracle(gpu_lib, oracle_port, V, nx, dt):
+# V = 8320 (whole 128 / 64 tiles), 8452 (ragged tiles); 8450 / 8449: V off
+# the 16-byte vector (f32 / f64) and an asymmetric matrix: column dots
+CASES = [(8320, 64, np.float32, False, 1), (8452, 2, np.float32, False, 1),
+         (8450, 2, np.float32, False, 0), (8452, 2, np.float32, True, 0),
+         (8320, 64, np.float64, False, 1), (8449, 7, np.float64, False, 0)]
+
+
+@pytest.mark.parametrize("V,nx,dt,asym,symv", CASES,
+                         ids=["%d-%s%s" % (c[0], np.dtype(c[2]).name, "-asym" if c[3] else "")
+                              for c in CASES])
+def test_dense_ata_matches_oracle(gpu_lib, oracle_port, V, nx, dt, asym, symv):
+    from cp_pfdr_graph_d1_amd import pfdr
     A, Y, Eu, Ev, L = _problem(V, dt, V, nx)
+    if asym:
+        A[3, 700] = np.nextafter(A[3, 700], dt(np.inf))
     La = np.full(Eu.size, 0.05, dt)
     L1 = np.full(V, 0.01, dt)
     X0 = np.zeros(V, dt)
+    Af = A.ravel(order="F")
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, X0, Y, N=-V, A=Af, L=L,
+                     itMax=1)
+    assert s.query("symv") == symv and s.query("dense_exact") == 0
+    s.close()
     kw = dict(La_l1=L1, positivity=0, Ltype=0, L=L, rho=1.5, condMin=1e-3, difRcd=0.0,
-              difTol=0.0, itMax=30, obj=True, dif=True)
-    ref = oracle_port.quadratic_d1_l1(X0, Y, A.ravel(order="F"), -V, Eu, Ev, La, **kw)
-    with _env(PFDR_SYMV="1"):
-        got = gpu_lib.quadratic_d1_l1(X0, Y, A.ravel(order="F"), -V, Eu, Ev, La, **kw)
-    with _env(PFDR_SYMV="0"):
-        cold = gpu_lib.quadratic_d1_l1(X0, Y, A.ravel(order="F"), -V, Eu, Ev, La, **kw)
+              difTol=0.0, itMax=20, obj=True, dif=True)
+    ref = oracle_port.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
+    got = gpu_lib.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
     e = G.rel_l2(got[0], ref[0])
-    print("V=%d %s symv vs oracle rel_l2=%.3e, col-dot %.3e" % (V, np.dtype(dt).name, e,
-                                                                  G.rel_l2(cold[0], ref[0])))
-    assert got[1] == ref[1] == 30
+    print("V=%d %s symv=%d vs oracle rel_l2=%.3e" % (V, np.dtype(dt).name, symv, e))
+    assert got[1] == ref[1] == 20
     assert e <= _tol(dt, True)
     assert np.allclose(got[2], ref[2], rtol=(1e-4 if dt == np.float32 else 1e-10))
-
-
-def test_symv_not_taken_for_asymmetric_or_ragged_vectors(gpu_lib):
-    from cp_pfdr_graph_d1_amd import pfdr
-    for V, asym in ((1000, True), (1002, False)):
-        A, Y, Eu, Ev, L = _problem(V, np.float32, 5, 2 if V == 1002 else 40)
-        if asym:
-            A[3, 700] = np.nextafter(A[3, 700], np.float32(np.inf))
-        with _env(PFDR_SYMV="1"):
-            s = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, Eu.size, Eu, Ev,
-                             np.full(Eu.size, 0.05, np.float32), np.zeros(V, np.float32), Y,
-                             N=-V, A=A.ravel(order="F"), L=L, itMax=5)
-            assert s.query("symv") == 0
-            s.run(5)
-            X, it, _, _ = s.result()
-            s.close()
-        assert it == 5 and np.all(np.isfinite(X))

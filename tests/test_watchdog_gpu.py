@@ -72,3 +72,45 @@ def test_failing_rank_wakes_its_peers(gpu_lib, monkeypatch):
     el = time.time() - t0
     print(ei.value)
     assert el < 30, "the healthy rank waited for the watchdog instead of being woken"
+
+
+def test_rccl_abort_then_destroy_is_safe(gpu_lib, monkeypatch):
+    """RCCL transport, one rank, a watchdog forced to fire (a timeout far
+    below one iteration's GPU time): the library aborts the caller's
+    communicator, the call fails with the diagnostic, a new session on the
+    aborted handle is refused, and the owner's normal clean-up
+    (pfdr_comm_destroy) returns without freeing the handle a second time"""
+    import ctypes as C
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    lib = pfdr.load()
+    idb = (C.c_char * 128)()
+    assert lib.pfdr_comm_unique_id(idb) == 0
+    comm = C.c_void_p()
+    assert lib.pfdr_comm_init(C.byref(comm), 1, 0, idb) == 0, lib.pfdr_last_error()
+    Eu, Ev = grid_graph((512, 512), 4)
+    V = 512 * 512
+    Y = pfdr.gen_piecewise(512, V, 2, np.float32)
+    La = np.full(Eu.size, 0.1, np.float32)
+    monkeypatch.setenv("PFDR_COMM_TIMEOUT", "1e-7")
+    with pytest.raises(Exception) as ei:
+        s = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, Eu.size, Eu, Ev, La,
+                         np.zeros(V, np.float32), Y, difTol=1e-9, itMax=2000,
+                         nranks=1, rank=0, comm=comm.value, comm_kind=P.COMM_RCCL,
+                         vtx_begin=0, V_global=V)
+        try:
+            s.run(2000)
+        finally:
+            s.close()
+    print(ei.value)
+    assert "stalled" in str(ei.value)
+    monkeypatch.setenv("PFDR_COMM_TIMEOUT", "60")
+    with pytest.raises(Exception) as e2:
+        pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, Eu.size, Eu, Ev, La,
+                     np.zeros(V, np.float32), Y, itMax=5, nranks=1, rank=0, comm=comm.value,
+                     comm_kind=P.COMM_RCCL, vtx_begin=0, V_global=V)
+    assert "aborted" in str(e2.value)
+    v = C.c_double(1.0)
+    assert lib.pfdr_comm_allreduce_max_f64(comm, C.byref(v)) != 0
+    assert lib.pfdr_comm_destroy(comm) == 0

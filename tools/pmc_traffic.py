@@ -8,6 +8,7 @@ correction applies to their streams; gathers are uncalibrated (the guide:
 ratios between variants of one kernel are unaffected).  Infinity-Cache hits
 are counted by these counters, not excluded.
 Usage: python tools/pmc_traffic.py <dir with fetch/ and write/> [workload E V]
+(the summary goes to stdout; bench.py reads profiles/pmc/<workload>.json)
 """
 import csv
 import glob
@@ -36,11 +37,15 @@ def main(root, workload="headline", E=60000000, V=10000000):
     fetch = counter(os.path.join(root, "fetch"), "FETCH_SIZE")
     write = counter(os.path.join(root, "write"), "WRITE_SIZE")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from kernel_hash import kernel_source_sha256
+    from workloads import WORKLOADS
+    solver = WORKLOADS[workload].pmc if workload in WORKLOADS else "quadratic"
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel "
                      "trace only), bench.py --workload %s" % workload,
            "workload": workload, "workload_E": E, "workload_V": V,
-           "kernel_source_sha256": kernel_source_sha256(), "kernels": {}}
+           "solver_sources": solver,
+           "kernel_source_sha256": kernel_source_sha256(solver), "kernels": {}}
     for k in sorted(set(fetch) & set(write)):
         if not k.startswith("k_"):
             continue

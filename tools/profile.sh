@@ -10,4 +10,4 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-forma
 echo "fetch ok"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $B --steps 5 --warmup 1 > $OUT/write.log 2>&1 || exit $?
 echo "write ok"
-python tools/pmc_traffic.py $OUT ${WL:-headline} ${E:-60000000} ${V:-10000000} > $OUT/pmc_traffic.json && cat $OUT/pmc_traffic.json
+python tools/pmc_traffic.py $OUT ${WL:-headline} ${E:-60000000} ${V:-10000000} > $OUT/pmc_traffic.json && cp $OUT/pmc_traffic.json gpurun_out/pmc_${WL:-headline}.json && cat $OUT/pmc_traffic.json

@@ -3,9 +3,15 @@ BASELINE.json, restated concretely in SURVEY.md §8(d).
 
 Each workload builds the session arguments of one rank (inputs generated
 deterministically, natively where large) and states its algorithmic bytes
- so bench.py can price the dominant kernel against the HBM
-roofline.  Only `headline` is the driver's bench line; the others are run
-with `python bench.py --workload cN` for DESIGN.md.
+ so bench.py can price each kernel against the HBM
+roofline.  SURVEY.md §8(d)'s per-iteration figure is split between the two
+sweeps by the reference loop each replaces: the edge sweep owns the TV prox
+loop's arrays (ref src/PFDR_graph_quadratic_d1_l1.cpp:466-489: Eu, Ev, Zu and
+Zv read and written, W_d1u, W_d1v, Th_d1), the vertex sweep the DR average's
+splitting weights (:491-497: Wu, Wv) and the per-vertex arrays; the
+simplex the same per (edge, label) (src/PFDR_graph_loss_d1_simplex.cpp:589-648).
+Only `headline` is the driver's bench line; the others are run with
+`python bench.py --workload cN` for DESIGN.md.
 """
 import numpy as np
 
@@ -24,6 +30,7 @@ class Workload:
     vertex_bytes = 20
     steps = 50
     itMax_extra = 0
+    pmc = "quadratic"         # kernel sources whose hash keys its PMC summary
 
     def inputs(self, rank, world, strong=True):
         """-> dict(V, E, kw (pfdr.Session kwargs), vtx_begin, e_offset, desc,
@@ -32,9 +39,22 @@ class Workload:
         copy-sized slab of a graph stacked `world` times."""
         raise NotImplementedError
 
+    def real_bytes(self):
+        return np.dtype(self.dtype).itemsize
+
+    def kernel_bytes(self, V, E):
+        """algorithmic HBM bytes of one launch of each sweep: SURVEY.md
+        §8(d)'s iteration bytes split as the module docstring says (quadratic:
+        edge sweep 8 + 7 s per edge, vertex sweep 2 s per edge + the vertex
+        term; they add up to iteration_bytes)"""
+        s = self.real_bytes()
+        e_edge = 8 + 7 * s
+        return {"edge_sweep": e_edge * E,
+                "vertex_sweep": (self.edge_bytes - e_edge) * E + self.vertex_bytes * V}
+
     def dominant_bytes(self, V, E):
         """algorithmic HBM bytes of one launch of the dominant kernel"""
-        return self.edge_bytes * E
+        return self.kernel_bytes(V, E)[self.dominant]
 
     def iteration_bytes(self, V, E):
         """algorithmic HBM bytes of one whole iteration"""
@@ -223,9 +243,11 @@ class C3(Workload):
                                              if gram_ms > 0 else None,
                                              "gram_peak_TFLOPs_f32_mfma": 157.3}})
 
-    def dominant_bytes(self, V, E):
-        # one pass over A (column dots P = -A^t R), + X, Ga, R
-        return 4 * self.N * V + 12 * V
+    def kernel_bytes(self, V, E):
+        # one pass over A each (R = Y - A X; P = -A^t R), + X, Ga, R; the graph
+        d = Workload.kernel_bytes(self, V, E)
+        d.update(gemv_cols=4 * self.N * V + 12 * V, gemv_rows=4 * self.N * V + 8 * V)
+        return d
 
     def iteration_bytes(self, V, E):
         # two passes over A (R = Y - A X, then P = -A^t R) + the graph
@@ -240,11 +262,20 @@ class C4(Workload):
     metric = "PFDR_graph_loss_d1_simplex<float> K=10 KL 5M-vertex 8-NN: Medge-updates/s"
     kind = pfdr.PFDR_KIND_SIMPLEX
     dominant = "sx_edge_sweep"
+    pmc = "simplex"
     K = 10
     SIDE = 2236
     edge_bytes = 8 + 9 * 10 * 4
     vertex_bytes = 10 * 4 * 4
     steps = 20
+
+    def kernel_bytes(self, V, E):
+        # per (edge, label): the prox loop's 7 arrays (ref :589-634) in the
+        # edge sweep, the average's Wu, Wv (ref :636-648) with the per-vertex
+        # K-wide arrays in the fused vertex sweep
+        s, K = self.real_bytes(), self.K
+        return {"sx_edge_sweep": (8 + 7 * K * s) * E,
+                "sx_vertex_sweep": 2 * K * s * E + self.vertex_bytes * V}
 
     def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
@@ -350,9 +381,11 @@ class C3AtA(Workload):
                                     "full_product_TFLOP": round(2.0 * N * V * V / 1e12, 3),
                                     "peak_TFLOPs_f32_mfma": 157.3}})
 
-    def dominant_bytes(self, V, E):
+    def kernel_bytes(self, V, E):
         # A^tA adds V(V+1)/2 unique entries per iteration
-        return 4 * V * (V + 1) // 2 + 12 * V
+        d = Workload.kernel_bytes(self, V, E)
+        d["symv"] = 4 * V * (V + 1) // 2 + 12 * V
+        return d
 
     def iteration_bytes(self, V, E):
         return 4 * V * (V + 1) // 2 + self.edge_bytes * E + self.vertex_bytes * V
