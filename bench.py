@@ -245,7 +245,8 @@ def main():
         from cp_pfdr_graph_d1_amd import partition
         comm = partition.comm_init(world, rank, lambda x: dist.broadcast(x, 0))
         dist_kw = dict(nranks=world, rank=rank, comm=comm, comm_kind=partition.COMM_RCCL,
-                       vtx_begin=inp["vtx_begin"], e_offset=inp["e_offset"])
+                       vtx_begin=inp["vtx_begin"], e_offset=inp["e_offset"],
+                       e_global=inp.get("e_global"), vtx_label=inp.get("vtx_label"))
         parallelism = "vertex-partition x%d (RCCL halo), %s scaling" % (
             world, "strong" if strong else "weak")
     elif world > 1:

@@ -14,6 +14,7 @@
 // order — so results are bit-identical with and without reordering.
 #include <climits>
 #include <cstring>
+#include <vector>
 #include <rocprim/rocprim.hpp>
 
 #include "pfdr_order.hpp"
@@ -211,3 +212,39 @@ bool bfs_order(const int *Eu, const int *Ev, long E, int V, DevBuf<int> &order,
 }
 
 }  // namespace pfdr
+
+extern "C" int pfdr_locality_order(int V, int64_t E, const int *Eu, const int *Ev, int mem,
+                                   int *order_out, int *applied) {
+    using namespace pfdr;
+    if (V <= 0 || E < 0 || (E > 0 && (!Eu || !Ev)) || !order_out)
+        return report_error("pfdr_locality_order", "invalid arguments");
+    try {
+        hipStream_t s = lib_stream();
+        DevBuf<int> du(E ? E : 1), dv(E ? E : 1), order, where;
+        const auto kind = mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        if (E) {
+            PFDR_HIP(hipMemcpyAsync(du.p, Eu, E * sizeof(int), kind, s));
+            PFDR_HIP(hipMemcpyAsync(dv.p, Ev, E * sizeof(int), kind, s));
+        }
+        check_endpoints(du.p, dv.p, E, V, s);
+        const bool ok = E > 0 && bfs_order(du.p, dv.p, E, V, order, where, s);
+        if (!ok) {
+            std::vector<int> id(V);
+            for (int v = 0; v < V; v++) id[v] = v;
+            PFDR_HIP(hipMemcpyAsync(order_out, id.data(), V * sizeof(int),
+                                    mem == PFDR_MEM_DEVICE ? hipMemcpyHostToDevice
+                                                           : hipMemcpyHostToHost, s));
+        } else {
+            PFDR_HIP(hipMemcpyAsync(order_out, order.p, V * sizeof(int),
+                                    mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                           : hipMemcpyDeviceToHost, s));
+        }
+        PFDR_HIP(hipStreamSynchronize(s));
+        if (applied) *applied = ok ? 1 : 0;
+    } catch (const HipError &h) {
+        return report_error("pfdr_locality_order", h);
+    } catch (const std::exception &ex) {
+        return report_error("pfdr_locality_order", ex.what());
+    }
+    return PFDR_OK;
+}

@@ -138,6 +138,11 @@ class QuadSession final : public SessionBase {
     real cw_ = real(0);
     DevBuf<real> R_, Rpart_, vpart_, opart_, Obj_, Dif_, red_, csum_;
     DevBuf<real> Rsum_, xfull_;  // dense A on a partition: summed A X, gathered X
+    // relabelled partition (pfdr_problem.vtx_label): the caller's label of
+    // each owned vertex; the amplitudes are all-reduced into ampg_ at those
+    // labels and summed in the caller's order on every rank
+    DevBuf<int> lab_;
+    DevBuf<real> ampg_;
     long v0_ = 0, Vglob_ = 0;
     DevBuf<long long> ccnt_;
     DevBuf<int> cnt_part_;
@@ -323,6 +328,20 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     // have the global length
     v0_ = halo_ ? (long)halo_->vtx_begin : 0;
     Vglob_ = halo_ ? (long)halo_->off.back() : V_;
+    if (p->vtx_label) {
+        if (!halo_) throw std::runtime_error("vtx_label is for partitioned sessions");
+        std::vector<int64_t> h64(V_);
+        PFDR_HIP(hipMemcpy(h64.data(), p->vtx_label, sizeof(int64_t) * V_,
+                           p->mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+        std::vector<int> h32(V_);
+        for (int v = 0; v < V_; v++) {
+            if (h64[v] < 0 || h64[v] >= Vglob_)
+                throw std::runtime_error("vtx_label outside [0, V_global)");
+            h32[v] = (int)h64[v];
+        }
+        lab_.alloc(V_);
+        PFDR_HIP(hipMemcpy(lab_.p, h32.data(), sizeof(int) * V_, hipMemcpyHostToDevice));
+    }
     if (mode_ == A_ATA && -(long)N_ != Vglob_)
         throw std::runtime_error("N < 0 requires A = A^tA (columns of the owned vertices, "
                                  "length V) and N = -V (V over all ranks)");
@@ -551,6 +570,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     if (p->nranks > 1 || p->comm) {
         partition_setup(p, V_, E_, halo_, Eu_, Ev_, eg, &e_offset, s);
         Vg_ = V_ + halo_->G;
+        ghosts = halo_->G;
     } else {
         Vg_ = V_;
         if (E && kind == hipMemcpyHostToDevice) {
@@ -814,6 +834,24 @@ void QuadSession<real>::amplitude(bool init) {
     k_amp<real><<<nbv_, kBlock, 0, s>>>(V_, init ? (mode_ == A_DIRECT ? 1 : 0) : 2, Y_.p, diag_.p,
                                         pre_.p, xp_.p, absval_.p, cnt_part_.p);
     PFDR_HIP(hipGetLastError());
+    if (halo_ && lab_.p) {
+        // relabelled partition: every rank holds the amplitudes of all
+        // vertices at the caller's labels (one writer per position, so the
+        // all-reduce adds zeros only) and sums them in that order
+        Transport &tr = *halo_->tr;
+        if (ampg_.n < (size_t)Vglob_) ampg_.alloc(Vglob_);
+        PFDR_HIP(hipMemsetAsync(ampg_.p, 0, sizeof(real) * Vglob_, s));
+        k_scatter<real><<<nbv_, kBlock, 0, s>>>(V_, absval_.p, lab_.p, ampg_.p);
+        PFDR_HIP(hipGetLastError());
+        tr.allreduce_sum(ampg_.p, (int)Vglob_, dtype_of<real>(), s);
+        if (mono_ws_.n < mono_ws_bytes<real>(Vglob_)) mono_ws_.alloc(mono_ws_bytes<real>(Vglob_));
+        mono_sum<real>(Vglob_, ampg_.p, nullptr, nbv_, cnt_part_.p, csum_.p, ccnt_.p, mono_ws_.p,
+                       s);
+        tr.allreduce_sum(ccnt_.p, 1, 2, s);
+        k_set_c<real><<<1, 64, 0, s>>>(csum_.p, ccnt_.p, init ? 1 : 0, ctrl_.p);
+        PFDR_HIP(hipGetLastError());
+        return;
+    }
     const bool seeded = halo_ && halo_->tr->rank > 0;
     if (halo_) halo_->tr->chain_recv(red_.p + 3, sizeof(real), s);
     const real *amp = absval_.p;

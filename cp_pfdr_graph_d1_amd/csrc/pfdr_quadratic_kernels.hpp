@@ -304,6 +304,14 @@ __global__ void k_gather(long n, const T *__restrict__ src, const int *__restric
     if (i < n) dst[i] = src[map[i]];
 }
 
+// dst[map[i]] = src[i] (a relabelled partition's amplitudes in the caller's order)
+template <typename T>
+__global__ void k_scatter(long n, const T *__restrict__ src, const int *__restrict__ map,
+                          T *__restrict__ dst) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[map[i]] = src[i];
+}
+
 // Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324); half-edge layout Z2[2e + side]
 template <typename real>
 __global__ void k_z_init(long E, const int *__restrict__ Eu,
@@ -759,9 +767,13 @@ __device__ __forceinline__ real la_at(long e, const real *__restrict__ La_d1, re
 template <typename real, int N>
 __device__ __forceinline__ Pk<real, N> la_vec(long e0, const real *__restrict__ La_d1, real la0) {
     Pk<real, N> la;
-    if (La_d1) return *reinterpret_cast<const Pk<real, N> *>(La_d1 + e0);
 #pragma unroll
     for (int j = 0; j < N; j++) la.v[j] = la0;
+    if (La_d1) {
+        const Pk<real, N> x = ldv<real, N>(La_d1 + e0);
+#pragma unroll
+        for (int j = 0; j < N; j++) la.v[j] = x.v[j];
+    }
     return la;
 }
 

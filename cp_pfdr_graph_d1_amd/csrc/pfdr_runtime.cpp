@@ -496,6 +496,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "padded")) *value = s->impl->padded;
     else if (!strcmp(what, "seqdif")) *value = s->impl->seqdif;
     else if (!strcmp(what, "la_uniform")) *value = s->impl->la_uniform;
+    else if (!strcmp(what, "ghosts")) *value = s->impl->ghosts;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;

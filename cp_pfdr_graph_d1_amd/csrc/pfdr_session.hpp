@@ -68,6 +68,7 @@ class SessionBase {
     int64_t seqdif = 0;        // evolution statistic with the reference's sequential rounding
     int64_t la_uniform = 0;    // one La_d1 value for every edge: the array is not streamed
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
+    int64_t ghosts = 0;        // partitioned: ghost (halo) vertices of this rank
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;

@@ -1230,6 +1230,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (p->nranks > 1 || p->comm) {  // vertex partition with K-wide halos
         partition_setup(p, V_, E_, halo_, Eu_, Ev_, eg, &e_offset, s);
         Vg_ = V_ + halo_->G;
+        ghosts = halo_->G;
         R_ = halo_->R;
         Vglob_ = (long)halo_->off.back();
         red_.alloc(2);

@@ -6,6 +6,10 @@
 * ``Plan``: the library's host-only planner (pfdr_plan_* in
   include/pfdr_mi355x.h) — what a partitioned session runs at setup, drivable
   over any transport (the CPU tests use torch.distributed/gloo).
+* ``locality_order`` / ``relabelled_split``: randomly labelled graphs are
+  relabelled (breadth-first, pfdr_locality_order) before the vertex-range
+  split, so the halos stay the size of the graph's cut surfaces
+  (SURVEY.md §8(e)); the result is unchanged bit for bit.
 * ``solve_loopback``: k ranks as k threads on one GPU (loopback transport);
   returns the concatenated result, which equals the unpartitioned solve.
 * ``comm_init``: the RCCL communicator for one process per GPU, its unique id
@@ -41,6 +45,43 @@ def split_edges(Eu, off):
     """Edge ids (ascending) owned by each rank: those whose Eu it owns."""
     owner = np.searchsorted(off, np.asarray(Eu, np.int64), side="right") - 1
     return [np.nonzero(owner == r)[0].astype(np.int64) for r in range(len(off) - 1)]
+
+
+def locality_order(V, Eu, Ev):
+    """order[new] = old label: the library's deterministic breadth-first
+    order (pfdr_locality_order, computed on the current GPU); identity for
+    path-like graphs.  Returns (order, applied)."""
+    lib = pfdr.load()
+    Eu = np.ascontiguousarray(Eu, np.int32)
+    Ev = np.ascontiguousarray(Ev, np.int32)
+    order = np.empty(V, np.int32)
+    applied = C.c_int(0)
+    pfdr._check(lib.pfdr_locality_order(C.c_int(V), C.c_int64(Eu.size),
+                                        C.c_void_p(Eu.ctypes.data), C.c_void_p(Ev.ctypes.data),
+                                        C.c_int(pfdr.PFDR_MEM_HOST),
+                                        C.c_void_p(order.ctypes.data), C.byref(applied)),
+                "pfdr_locality_order")
+    return order, bool(applied.value)
+
+
+def relabelled_split(order, off, Eu, Ev):
+    """The vertex-range split of a relabelled graph: new label of every old
+    one (where), relabelled endpoints, and per rank the original edge ids it
+    owns (relabelled Eu in its range) sorted by (relabelled Eu, edge id), so
+    every rank's edges are u-sorted for the sweeps.  The summation order
+    stays the reference's: the sessions key their sums by the original edge
+    ids (e_global)."""
+    order = np.asarray(order, np.int64)
+    where = np.empty_like(order)
+    where[order] = np.arange(order.size)
+    nEu = where[np.asarray(Eu, np.int64)]
+    nEv = where[np.asarray(Ev, np.int64)]
+    parts = []
+    owner = np.searchsorted(off, nEu, side="right") - 1
+    for r in range(len(off) - 1):
+        e = np.nonzero(owner == r)[0]
+        parts.append(e[np.argsort(nEu[e], kind="stable")].astype(np.int64))
+    return where, nEu.astype(np.int32), nEv.astype(np.int32), parts
 
 
 class Plan:
@@ -98,16 +139,36 @@ class Plan:
 def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                    positivity=0, lo=-np.inf, hi=np.inf, Ltype=0, L=None, rho=1.5,
                    condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=100, record_obj=False,
-                   record_dif=False, off=None, K=0, al=0.0, N=0):
+                   record_dif=False, off=None, K=0, al=0.0, N=0, relabel=False):
     """Partitioned solve with k ranks as k threads on the current GPU.
     Simplex (kind PFDR_KIND_SIMPLEX): X0 = P0 and Y = Q are K-by-V (v*K + k),
     La_l1 = La_f.  Dense A: N > 0 (A is N-by-V column-major, each rank gets
-    its vertices' columns, Y stays whole) or N = -V (A^tA, column blocks).  Returns (X, it, Obj, Dif, info) with X for all vertices."""
+    its vertices' columns, Y stays whole) or N = -V (A^tA, column blocks).
+    relabel (graph modes): split the locality order instead of the labels
+    (locality_order, relabelled_split).  Returns (X, it, Obj, Dif, info)
+    with X for all vertices in the caller's labels."""
     lib = pfdr.load()
     Kw = max(int(K), 1)
     V = np.asarray(X0).size // Kw
     off = vertex_offsets(V, k) if off is None else np.asarray(off, np.int64)
-    parts = split_edges(Eu, off)
+    order = None
+    if relabel:
+        if N != 0:
+            raise ValueError("relabel: graph modes only (identity / diagonal A, simplex)")
+        order, _ = locality_order(V, Eu, Ev)
+        where, Eu, Ev, parts = relabelled_split(order, off, Eu, Ev)
+        oi = np.asarray(order, np.int64)
+
+        def perm(a):  # per-vertex arrays into the new labels
+            if a is None:
+                return None
+            a = np.asarray(a)
+            if Kw > 1 and a.size == V * Kw:
+                return np.ascontiguousarray(a.reshape(V, Kw)[oi].reshape(-1))
+            return np.ascontiguousarray(a[oi]) if a.size == V else a
+        X0, Y, A, La_l1, L = perm(X0), perm(Y), perm(A), perm(La_l1), perm(L)
+    else:
+        parts = split_edges(Eu, off)
     hub = C.c_void_p()
     pfdr._check(lib.pfdr_loopback_create(C.byref(hub), C.c_int(k)), "pfdr_loopback_create")
     results, errors, queries = [None] * k, [None] * k, [None] * k
@@ -137,9 +198,11 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              Ltype=Ltype, L=vsl(L), rho=rho, condMin=condMin, difRcd=difRcd,
                              difTol=difTol, itMax=itMax, record_obj=record_obj,
                              record_dif=record_dif, K=K, al=al, nranks=k, rank=r, comm=hub.value,
-                             comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e)
+                             comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e,
+                             vtx_label=None if order is None else order[v0:v1])
+            queries[r] = {"ghosts": s.query("ghosts")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
-                queries[r] = {q: s.query(q) for q in ("split_blocks", "ustaged")}
+                queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged")})
             s.run(itMax)
             results[r] = s.result()
             s.close()
@@ -158,12 +221,19 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
     for ex in first or [ex for ex in errors if ex is not None]:
         raise ex
     X = np.concatenate([res[0] for res in results])
+    if order is not None:  # back to the caller's labels
+        Xo = np.empty_like(X)
+        if Kw > 1:
+            Xo.reshape(V, Kw)[np.asarray(order, np.int64)] = X.reshape(V, Kw)
+        else:
+            Xo[np.asarray(order, np.int64)] = X
+        X = Xo
     its = {res[1] for res in results}
     if len(its) != 1:
         raise pfdr.PFDRError("ranks disagree on the iteration count: %s" % its)
     it = its.pop()
     return X, it, results[0][2], results[0][3], {"off": off, "edges": [p.size for p in parts],
-                                                 "queries": queries}
+                                                 "queries": queries, "order": order}
 
 
 def comm_init(nranks, rank, host_broadcast):

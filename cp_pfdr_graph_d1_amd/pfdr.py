@@ -64,6 +64,7 @@ EXPORTED = (
     "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
     "pfdr_gen_uniform_f32", "pfdr_gen_uniform_f64", "pfdr_gen_matvec_f32",
     "pfdr_gen_matvec_f64", "pfdr_gen_symmetric_f32", "pfdr_gen_symmetric_f64",
+    "pfdr_locality_order",
 )
 
 
@@ -91,6 +92,7 @@ class Problem(C.Structure):
         ("e_global", C.c_void_p), ("e_offset", C.c_int64),
         ("reorder", C.c_int),
         ("evolution", C.c_int),
+        ("vtx_label", C.c_void_p),
     ]
 
 
@@ -475,7 +477,8 @@ class Session:
                  difRcd=0.0, difTol=0.0, itMax=1000, record_obj=False,
                  record_dif=False, verbose=0, device=False, nranks=0, rank=0,
                  comm=None, comm_kind=0, vtx_begin=0, V_global=0, e_global=None,
-                 e_offset=0, reorder=REORDER_AUTO, evolution=EVOLUTION_AUTO):
+                 e_offset=0, reorder=REORDER_AUTO, evolution=EVOLUTION_AUTO,
+                 vtx_label=None):
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
@@ -510,6 +513,10 @@ class Session:
         p.vtx_begin, p.V_global, p.e_offset = vtx_begin, V_global, e_offset
         p.reorder = reorder
         p.evolution = evolution
+        if vtx_label is not None:
+            vl = np.ascontiguousarray(vtx_label, np.int64)
+            self._keep.append(vl)
+            p.vtx_label = C.c_void_p(vl.ctypes.data)
         if e_global is not None:
             eg = np.ascontiguousarray(e_global, np.int64)
             self._keep.append(eg)

@@ -178,9 +178,29 @@ typedef struct pfdr_problem {
     int reorder;          /* PFDR_REORDER_*; results are identical either way */
     /* --- iterate-evolution statistic -------------------------------------- */
     int evolution;        /* PFDR_EVOLUTION_* */
+    /* --- relabelled partition (pfdr_locality_order) ----------------------- */
+    const int64_t *vtx_label; /* caller's label of each owned vertex (V of them,
+                             host or device per mem); NULL: vtx_begin + v.  Set
+                             when the ranks own ranges of a RELABELLED graph:
+                             the preconditioner's amplitude sum then runs in
+                             the caller's label order (all-reduced, then summed
+                             in that order on every rank), as the reference's
+                             one-thread loop does (quadratic solvers). */
 } pfdr_problem;
 
 typedef struct pfdr_session pfdr_session;
+
+/* Locality order of a graph's vertices for a vertex-range partition
+ * (randomly labelled k-NN graphs must be reordered before
+ * partitioning, or every edge becomes a halo edge): the deterministic
+ * breadth-first order of pfdr_order.hip, computed on the current device.
+ * order_out[new] = old label (V entries, host or device per mem).  *applied
+ * = 0 when the graph is path-like (too many levels) and the identity was
+ * returned.  Use: rank r owns new labels [off[r], off[r+1]), its edges are
+ * those whose relabelled Eu it owns (original edge ids as e_global), and
+ * vtx_label = order_out[off[r] .. off[r+1]) (see partition.py). */
+int pfdr_locality_order(int V, int64_t E, const int *Eu, const int *Ev, int mem,
+                        int *order_out, int *applied);
 
 int pfdr_session_create(pfdr_session **out, const pfdr_problem *p);
 /* Run up to `iters` more iterations (stopping early on difTol / itMax as the

@@ -8,8 +8,9 @@ GPU exchanging through the loopback hub instead of processes over RCCL (two
 RCCL ranks cannot share one GPU).  The gathered iterate after a fixed number
 of iterations must equal, bit for bit, the single-GPU session of the same
 global graph -- strong scaling at N = 2, 3 and 8 (the headline, C2, C5, and
-the simplex C4 with K-wide halos) and weak scaling at N = 3 (the stacked
-headline) -- at reduced grid sizes."""
+the simplex C4 with K-wide halos, the randomly labelled headline split in
+its locality order) and weak scaling at N = 3 (the stacked headline) -- at
+reduced grid sizes."""
 import os
 import sys
 import threading
@@ -24,6 +25,10 @@ import workloads  # noqa: E402
 
 
 class Headline(workloads.Headline):
+    SHAPE = (30, 24, 16)
+
+
+class HeadlineShuffled(workloads.HeadlineShuffled):
     SHAPE = (30, 24, 16)
 
 
@@ -77,7 +82,8 @@ def _ranks(wl, world, strong):
             inp = inps[r]
             s = _session(wl, inp, nranks=world, rank=r, comm=hub.value,
                          comm_kind=P.COMM_LOOPBACK, vtx_begin=inp["vtx_begin"],
-                         e_offset=inp["e_offset"])
+                         e_offset=inp["e_offset"], e_global=inp.get("e_global"),
+                         vtx_label=inp.get("vtx_label"))
             s.run(STEPS)
             res[r] = s.result()
             s.close()
@@ -96,12 +102,18 @@ def _ranks(wl, world, strong):
         raise ex
     assert {r[1] for r in res} == {STEPS}
     assert sum(i["E"] for i in inps) == sum(len(i["kw"]["Eu"]) for i in inps)
-    return np.concatenate([r[0] for r in res])
+    X = np.concatenate([r[0] for r in res])
+    if inps[0].get("vtx_label") is not None:  # a relabelled split: back to the caller's labels
+        lab = np.concatenate([i["vtx_label"] for i in inps])
+        Xc = np.empty_like(X)
+        Xc[lab] = X
+        X = Xc
+    return X
 
 
 CASES = [(Headline(), 2, True), (Headline(), 3, True), (Headline(), 8, True),
          (Headline(), 3, False), (C2(), 8, True), (C5(), 8, True), (C4(), 3, True),
-         (C4(), 8, True)]
+         (C4(), 8, True), (HeadlineShuffled(), 3, True), (HeadlineShuffled(), 8, True)]
 
 
 @pytest.mark.parametrize("wl,world,strong", CASES,

@@ -162,3 +162,60 @@ def test_partitioned_dense_matches_reference(gpu_lib, name, k, fixed):
     else:
         assert abs(it - git) <= 2
         assert err <= (1e-5 if X.dtype == np.float32 else 1e-9)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("kind", ["l1", "bounds", "simplex"])
+def test_relabelled_partition_random_labels(gpu_lib, k, kind):
+    """a randomly labelled graph is relabelled (breadth-first
+    locality order) before the vertex-range split.  The gathered iterate, in
+    the caller's labels, equals the single-GPU session's bit for bit (the
+    sums keep the original edge ids; the l1 / bounds preconditioner's
+    amplitude is summed in the caller's label order on every rank), and the
+    ranks hold a small fraction of the ghosts of the random-label split."""
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, uniform
+    shape = (40, 36, 30)
+    V = int(np.prod(shape))
+    Eu, Ev = grid_graph(shape, 6)
+    new_of = np.empty(V, np.int64)
+    new_of[np.argsort(uniform(13, np.arange(V)), kind="stable")] = np.arange(V)
+    Eu, Ev = new_of[Eu].astype(np.int32), new_of[Ev].astype(np.int32)
+    dt = np.float32
+    La = np.full(Eu.size, 0.1, dt)
+    its = 30
+    if kind == "simplex":
+        K = 4
+        lab = (np.arange(V) * 4) // V
+        Q = np.zeros((V, K), dt)
+        Q[np.arange(V), lab] = 1.0
+        Q = (0.7 * Q + 0.3 * uniform(5, np.arange(V * K)).reshape(V, K)).astype(dt)
+        Q = (Q / Q.sum(axis=1, keepdims=True)).astype(dt)
+        Qp = np.empty_like(Q)
+        Qp[new_of] = Q
+        Qp = Qp.reshape(-1)
+        kw = dict(K=K, al=0.1, rho=1.0, condMin=0.1, itMax=its)
+        s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, La, Qp.copy(), Qp, **kw)
+        args = (k, pfdr.PFDR_KIND_SIMPLEX, dt, Eu, Ev, La, Qp.copy(), Qp)
+    else:
+        Y0 = piecewise_observation(shape, 3, dt)
+        Y = np.empty_like(Y0)
+        Y[new_of] = Y0
+        kind_c = pfdr.PFDR_KIND_L1 if kind == "l1" else pfdr.PFDR_KIND_BOUNDS
+        kw = dict(rho=1.5, condMin=1e-3, itMax=its)
+        kw.update(dict(La_l1=np.full(V, 0.01, dt)) if kind == "l1" else dict(lo=0.0, hi=0.8))
+        s = pfdr.Session(kind_c, dt, V, Eu.size, Eu, Ev, La, np.zeros(V, dt), Y, **kw)
+        args = (k, kind_c, dt, Eu, Ev, La, np.zeros(V, dt), Y)
+    s.run(its)
+    X1, it1, _, _ = s.result()
+    s.close()
+    Xr, itr, _, _, info = P.solve_loopback(*args, relabel=True, **kw)
+    Xp, itp, _, _, info0 = P.solve_loopback(*args, **kw)
+    g_rel = sum(q["ghosts"] for q in info["queries"])
+    g_raw = sum(q["ghosts"] for q in info0["queries"])
+    print("%s k=%d ghosts: relabelled %d, random labels %d" % (kind, k, g_rel, g_raw))
+    assert it1 == itr == itp == its
+    assert np.array_equal(Xr, X1)
+    assert np.array_equal(Xp, X1)
+    assert g_rel * 5 < g_raw

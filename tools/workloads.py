@@ -121,10 +121,13 @@ class HeadlineSlab8(Headline):
 
 class HeadlineShuffled(Headline):
     """SURVEY.md §8(d) headline ordering (ii): the same graph and data with a
-    random vertex relabelling and an edge shuffle (seed 7).  Single GPU: a
-    vertex-range partition of random labels has no locality to exploit."""
+    random vertex relabelling and an edge shuffle (seed 7).  One GPU: the
+    session relabels it internally.  N > 1: every rank computes the
+    library's locality order of the whole graph (pfdr_locality_order, the
+    same on every rank) and owns a range of it (random
+    labels must be reordered before the split, or every edge is a halo
+    edge); the sums keep the original edge ids and the caller's labels."""
     name = "headline_shuffled"
-    partitionable = False
 
     def inputs(self, rank, world, strong=True):
         from cp_pfdr_graph_d1_amd.graphs import uniform
@@ -139,6 +142,20 @@ class HeadlineShuffled(Headline):
         Y[new_of] = kw["Y"]
         kw["Y"] = Y
         d["desc"] = d["desc"].replace("6-NN", "6-NN, random vertex labels + edge shuffle (seed 7)")
+        if world == 1:
+            return d
+        from cp_pfdr_graph_d1_amd import partition as P
+        order, _ = P.locality_order(V, kw["Eu"], kw["Ev"])
+        off = P.vertex_offsets(V, world)
+        _, nEu, nEv, parts = P.relabelled_split(order, off, kw["Eu"], kw["Ev"])
+        e = parts[rank]
+        v0, v1 = int(off[rank]), int(off[rank + 1])
+        oi = np.asarray(order, np.int64)[v0:v1]
+        kw.update(Eu=nEu[e], Ev=nEv[e], La_d1=kw["La_d1"][e], X0=kw["X0"][oi], Y=kw["Y"][oi],
+                  La_l1=kw["La_l1"][oi])
+        d.update(V=v1 - v0, E=e.size, kw=kw, vtx_begin=v0, e_offset=0, e_global=e,
+                 vtx_label=oi)
+        d["desc"] += ", locality order split into %d ranges" % world
         return d
 
 
