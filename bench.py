@@ -69,20 +69,21 @@ def cpu_baseline_child(args):
     from workloads import WORKLOADS
     kind = "reference" if oracle.available("ref_omp") else "port"
     lib = oracle.Oracle("ref_omp" if kind == "reference" else "port")
-    if args.workload == "c1":  # the reference's own CPU case: time to tolerance
-        inp = WORKLOADS["c1"].inputs(0, 1)
+    if args.workload in ("c1", "headline_conv"):  # time to tolerance, whole solve
+        inp = WORKLOADS[args.workload].inputs(0, 1)
         kw = inp["kw"]
         Eu, Ev = kw["Eu"].astype(np.int32), kw["Ev"].astype(np.int32)
         t = time.perf_counter()
         X, it, _, _ = lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
-                                          kw["La_l1"], 0, int(kw["Ltype"]), None, kw["rho"],
-                                          kw["condMin"], 0.0, kw["difTol"], 10000)
+                                          kw["La_l1"], 0, int(kw.get("Ltype", 0)), None,
+                                          kw["rho"], kw["condMin"], 0.0, kw["difTol"], 10000)
         el = time.perf_counter() - t
         print(json.dumps({
             "value": Eu.size * it / el / 1e6, "unit": "Medge-updates/s",
             "cores": len(cores) if kind == "reference" else 1, "kind": kind,
             "converged_iterations": it, "time_to_tolerance_s": el,
-            "sample": "whole C1 solve to difTol 1e-6 (setup included), same inputs", **host}))
+            "sample": "whole %s solve to difTol %g (setup included), same inputs" % (
+                args.workload, kw["difTol"]), **host}))
         return
     name = args.workload if args.workload in ("c2", "c3", "c4", "c5") else "headline"
     sample = "full %s graph" % name
@@ -212,7 +213,8 @@ def main():
     dist_on = world > 1 or args.dist_selftest
     # CPU baseline first, in its own process, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and wl.name in ("headline", "c1", "c2", "c3", "c4", "c5") and \
+    if rank == 0 and world == 1 and wl.name in ("headline", "headline_conv", "c1", "c2", "c3",
+                                                 "c4", "c5") and \
             not args.no_cpu_baseline:
         cpu = run_cpu_baseline(args)
 

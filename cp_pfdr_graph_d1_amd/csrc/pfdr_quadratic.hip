@@ -62,6 +62,24 @@ __global__ void k_edge_relabel(long E, const unsigned *__restrict__ eorig,
     emap[p] = (int)e;
 }
 
+// tile order: position p takes the edge now at perm[p]; its original id
+// (through eorig when the session was relabelled first) for the incidence
+// keys and the weights' permutation
+__global__ void k_edge_tile_order(long E, const unsigned *__restrict__ perm,
+                                  const unsigned *__restrict__ eorig, const int *__restrict__ Eu,
+                                  const int *__restrict__ Ev, int *__restrict__ nEu,
+                                  int *__restrict__ nEv, unsigned *__restrict__ eo,
+                                  int *__restrict__ emap) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const unsigned q = perm[p];
+    nEu[p] = Eu[q];
+    nEv[p] = Ev[q];
+    const unsigned e = eorig ? eorig[q] : q;
+    eo[p] = e;
+    emap[p] = (int)e;
+}
+
 template <typename real>
 class QuadSession final : public SessionBase {
   public:
@@ -154,6 +172,16 @@ class QuadSession final : public SessionBase {
     DevBuf<int> uptr_, blkok_;
     DevBuf<unsigned> mask_, oidx_;
     void build_split();
+    // tiled contributions (tile_sum in pfdr_quadratic_kernels.hpp): large
+    // single-GPU graphs keep their edges sorted by (u block, v block, edge);
+    // d2_ = CSR slot of every contribution address within its vertex block,
+    // ustart_ / tptr_, tstart_, tlen_ = the runs each block stages, tok_ =
+    // blocks whose lists fit the LDS (the others gather through the CSR)
+    bool tiled_ = false;
+    DevBuf<unsigned short> d2_;
+    DevBuf<unsigned char> lu_;  // u end mod 256 (k_edge_sweep_tl)
+    DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_;
+    void build_tiles();
     Ctrl<real> *hctrl_ = nullptr;  // pinned mirror
     int nbv_, nbe_, nbn_, rows_nb_, rows_cpb_;
     int it_ = 0;
@@ -358,12 +386,14 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     const size_t asz = mode_ == A_DIRECT ? (size_t)N_ * V : mode_ == A_ATA ? (size_t)Vglob_ * V
                      : mode_ == A_DIAG ? V : 0;
     copy_in(A_, p->A, asz, mem, s, pins_);
-    if (reordered_) {  // inputs into the internal labels (identity / diagonal A only)
+    if (emap_.p) {  // edge weights into the internal edge order
         permute(La_d1_, emap_.p, E, s);
+        emap_.release();
+    }
+    if (reordered_) {  // inputs into the internal labels (identity / diagonal A only)
         permute(La_l1_, order_.p, V, s);
         permute(Y_, order_.p, V, s);
         permute(A_, order_.p, V, s);
-        emap_.release();
         amp_orig_.alloc(V);
     }
     // scalar cap of the metric (ref :225-229), in `real` arithmetic like the reference
@@ -481,6 +511,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
+    acc(d2_.n * 2 + lu_.n + (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n) * 4);
     if (halo_) {
         plan_overlap();
     } else if (!tiny_) {
@@ -605,13 +636,78 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         std::swap(Ev_.p, nv.p);
         eg_ptr = eorig_.p;
     }
+    // tile order of large single-GPU graphs (see tile_sum): edges sorted by
+    // (u block, v block), stable in the current order; the incidence keys keep
+    // the original edge ids (summation order)
+    tiled_ = !halo_ && !tiny_ && E_ > 0 && (long)V_ > (long)kFuseBlocks * kBlock;
+    if (tiled_) {
+        const int nb = grid_for(V_);
+        int vbits = 1;
+        while (vbits < 31 && (1L << vbits) < (long)nb) vbits++;
+        DevBuf<unsigned long long> k(E), ks(E);
+        DevBuf<unsigned> v(E), perm(E);
+        k_tile_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, vbits, k.p, v.p);
+        PFDR_HIP(hipGetLastError());
+        radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, perm.p, (long)E, 2 * vbits, s);
+        DevBuf<int> nu(E), nv(E);
+        DevBuf<unsigned> eo(E);
+        emap_.alloc(E);
+        k_edge_tile_order<<<grid_for(E), kBlock, 0, s>>>(E_, perm.p, eorig_.p, Eu_.p, Ev_.p, nu.p,
+                                                         nv.p, eo.p, emap_.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipStreamSynchronize(s));
+        std::swap(Eu_.p, nu.p);
+        std::swap(Ev_.p, nv.p);
+        std::swap(eorig_.p, eo.p);
+        std::swap(eorig_.n, eo.n);
+        eg_ptr = eorig_.p;
+    }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
     wz_.alloc(2 * E_ + R ? 2 * E_ + R : 1);
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
-    if (!tiny_) build_split();
+    if (tiled_) build_tiles();
+    else if (!tiny_) build_split();
+}
+
+// the runs of every vertex block of a tile-ordered graph and the slots of
+// its contributions (see tile_sum)
+template <typename real>
+void QuadSession<real>::build_tiles() {
+    hipStream_t s = stream;
+    const int nb = grid_for(V_);
+    d2_.alloc(2 * (size_t)E_);
+    k_tile_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, d2_.p);
+    lu_.alloc((size_t)E_);
+    k_tile_lu<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, lu_.p);
+    ustart_.alloc((size_t)nb + 1);
+    k_tile_ustart<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, nb, Eu_.p, ustart_.p);
+    DevBuf<int> cnt(nb), fill(nb);
+    PFDR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * nb, s));
+    PFDR_HIP(hipMemsetAsync(fill.p, 0, sizeof(int) * nb, s));
+    k_tile_runs_count<<<grid_for(E_), kBlock, 0, s>>>(E_, Ev_.p, cnt.p);
+    PFDR_HIP(hipGetLastError());
+    std::vector<int> h(nb), tp((size_t)nb + 1, 0);
+    PFDR_HIP(hipMemcpyAsync(h.data(), cnt.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < nb; b++) tp[b + 1] = tp[b] + h[b];
+    const int R = tp[nb];
+    tptr_.alloc((size_t)nb + 1);
+    PFDR_HIP(hipMemcpyAsync(tptr_.p, tp.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice, s));
+    tstart_.alloc(R ? R : 1);
+    tlen_.alloc(R ? R : 1);
+    k_tile_runs_fill<<<grid_for(E_), kBlock, 0, s>>>(E_, Ev_.p, tptr_.p, fill.p, tstart_.p,
+                                                     tlen_.p);
+    tok_.alloc(nb);
+    k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, tok_.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipMemcpyAsync(h.data(), tok_.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    long n = 0;
+    for (int x : h) n += x;
+    tiled_blocks = n;
 }
 
 // Split incidence for the vertex sweep (split_sum): when the edges are
@@ -964,6 +1060,12 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
                                                      la_it(), la0_, rho_, c, nb, xm, f, pad_out());
         return;
     }
+    if (tiled_ && !fuse_ && rg.nb0 == nb && ebeg == 0 && eend == E_) {
+        k_edge_sweep_tl<real><<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, lu_.p, ustart_.p, Ev_.p, xp_.p,
+                                                   Z2_.p, A1_.p, cw_, gi_.p, la_it(), la0_, wz_.p,
+                                                   rho_, c, nb, xm);
+        return;
+    }
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
@@ -999,6 +1101,11 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.fwd = mode_ == A_IDENT ? 1 : (mode_ == A_DIAG ? 2 : 0);
     a.track = track_ ? 1 : 0; a.part = vpart_.p; a.ctrl = c;
     a.late = fuse_ ? 1 : 0;
+    a.E = E_;
+    if (tiled_) {
+        a.d2 = d2_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
+        a.tlen = tlen_.p; a.tok = tok_.p;
+    }
     a.terms = seqdif_ ? terms_.p : nullptr;
     a.tmap = (seqdif_ && reordered_) ? order_.p : nullptr;
     a.tstride = tstride_;

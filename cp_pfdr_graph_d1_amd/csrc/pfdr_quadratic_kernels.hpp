@@ -205,6 +205,172 @@ __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__res
     return s;
 }
 
+// ---------------------------------------------- tiled DR contributions --
+// Large single-GPU graphs store their edges in TILE order: sorted by
+// (u block, v block, edge), 256-vertex blocks (the vertex sweep's).  The
+// edge sweep then writes both contributions W*Z at the edge's position
+// (wz[p] u end, wz[E + p] v end) as plain streams, and every vertex block
+// finds ALL of its contributions in a few contiguous runs: the u ends of
+// its own block's edges (wz[ustart[b] .. ustart[b+1]), one run) and the
+// v ends of the (u block, b) tiles (runs of wz[E + p] listed in tptr /
+// tstart / tlen).  Each run is read once, coalesced, by exactly one
+// workgroup; every entry carries its slot in the block's CSR-ordered list
+// (d2, 16 bits, the CSR position of (edge, side) minus the block's first),
+// so staging puts each contribution where the reference's (e, side) order
+// wants it, and each lane then adds its vertex's slots in order -- the sums
+// of gather_sum / split_sum bit for bit, without a single gathered load.
+constexpr int kTileCap = 4096;  // staged entries per vertex block (LDS: GatherCap)
+constexpr int kTileRuns = 128;  // v-end runs per vertex block
+
+template <typename real, int GB>
+__device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
+                                         const int *__restrict__ ptr,
+                                         const unsigned short *__restrict__ d2,
+                                         const int *__restrict__ ustart,
+                                         const int *__restrict__ tptr,
+                                         const int *__restrict__ tstart,
+                                         const int *__restrict__ tlen,
+                                         const real *__restrict__ wz, real *lds, int *runs) {
+    const int tid = threadIdx.x;
+    const int v0 = blk * kBlock, vend = min(v0 + kBlock, V);
+    const int p0 = ptr[v0];
+    const int my0 = (v < V ? ptr[v] : ptr[vend]) - p0;
+    const int my1 = (v < V ? ptr[v + 1] : ptr[vend]) - p0;
+    const int us = ustart[blk], nu = ustart[blk + 1] - us;
+    const int t0 = tptr[blk], nt = tptr[blk + 1] - t0;
+    // run table: starts, then inclusive prefix of the lengths (wave 0)
+    int *rs = runs, *rp = runs + kTileRuns;
+    if (tid < kWave) {
+        int acc = 0;
+        for (int c = 0; c < nt; c += kWave) {
+            const int i = c + tid;
+            int len = 0;
+            if (i < nt) {
+                rs[i] = tstart[t0 + i];
+                len = tlen[t0 + i];
+            }
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int y = __shfl_up(len, o, kWave);
+                if (tid >= o) len += y;
+            }
+            if (i < nt) rp[i] = acc + len;
+            acc += __shfl(len, kWave - 1, kWave);
+        }
+    }
+    // u ends: one contiguous run, GB slots then GB values in flight per lane
+    for (int b = 0; b < nu; b += kBlock * GB) {
+        unsigned short d[GB];
+        real w[GB];
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            const int j = b + u * kBlock + tid;
+            const long a = us + (long)min(j, nu - 1);
+            d[u] = d2[a];
+            w[u] = wz[a];
+        }
+#pragma unroll
+        for (int u = 0; u < GB; u++)
+            if (b + u * kBlock + tid < nu) lds[d[u]] = w[u];
+    }
+    __syncthreads();  // run table
+    const int nv = nt ? rp[nt - 1] : 0;
+    for (int b = 0; b < nv; b += kBlock * GB) {
+        unsigned short d[GB];
+        real w[GB];
+        long ad[GB];
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            const int k = min(b + u * kBlock + tid, nv - 1);
+            int lo = 0, hi = nt - 1;  // first run whose inclusive prefix exceeds k
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (rp[mid] > k) hi = mid;
+                else lo = mid + 1;
+            }
+            ad[u] = E + rs[lo] + (k - (lo ? rp[lo - 1] : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < GB; u++) {
+            d[u] = d2[ad[u]];
+            w[u] = wz[ad[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < GB; u++)
+            if (b + u * kBlock + tid < nv) lds[d[u]] = w[u];
+    }
+    __syncthreads();
+    real s = real(0);
+    for (int j = my0; j < my1; j++) s += lds[j];
+    return s;
+}
+
+// tile-order keys: (u block, v block) in the high bits, edge position the value
+static __global__ void k_tile_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                   int vbits, unsigned long long *__restrict__ keys,
+                                   unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    keys[e] = ((unsigned long long)(Eu[e] / kBlock) << vbits) | (unsigned)(Ev[e] / kBlock);
+    vals[e] = (unsigned)e;
+}
+
+// d2[address] = CSR slot of the (edge, side) at that address, relative to the
+// first slot of its vertex block; one lane per vertex
+static __global__ void k_tile_slots(int V, const int *__restrict__ ptr,
+                                    const unsigned *__restrict__ idx,
+                                    unsigned short *__restrict__ d2) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int base = ptr[v - v % kBlock];
+    for (int j = ptr[v]; j < ptr[v + 1]; j++) d2[idx[j]] = (unsigned short)(j - base);
+}
+
+// ustart[b] = first position whose u end is in block >= b (tile order sorts by
+// u block), ustart[nb] = E
+static __global__ void k_tile_ustart(long E, int nb, const int *__restrict__ Eu,
+                                     int *__restrict__ ustart) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > E) return;
+    const int lo = p == 0 ? 0 : Eu[p - 1] / kBlock + 1;
+    const int hi = p == E ? nb : Eu[p] / kBlock;
+    for (int b = lo; b <= hi; b++) ustart[b] = (int)p;
+}
+
+// runs of equal v block in tile order: a run starts at p when p = 0 or the v
+// block changes; cnt[vb] counts the runs of every v block
+static __global__ void k_tile_runs_count(long E, const int *__restrict__ Ev, int *__restrict__ cnt) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const int vb = Ev[p] / kBlock;
+    if (p == 0 || Ev[p - 1] / kBlock != vb) atomicAdd(cnt + vb, 1);
+}
+
+// each run at its v block's next slot (the order of a block's runs does not
+// matter: every entry carries its slot), with its length
+static __global__ void k_tile_runs_fill(long E, const int *__restrict__ Ev,
+                                        const int *__restrict__ tptr, int *__restrict__ fill,
+                                        int *__restrict__ tstart, int *__restrict__ tlen) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const int vb = Ev[p] / kBlock;
+    if (p != 0 && Ev[p - 1] / kBlock == vb) return;
+    long q = p + 1;
+    while (q < E && Ev[q] / kBlock == vb) q++;
+    const int i = tptr[vb] + atomicAdd(fill + vb, 1);
+    tstart[i] = (int)p;
+    tlen[i] = (int)(q - p);
+}
+
+// tok[b] = 1 when block b's entries fit the LDS list and its runs the table
+static __global__ void k_tile_ok(int V, int nb, const int *__restrict__ ptr,
+                                 const int *__restrict__ tptr, int *__restrict__ tok) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int v0 = b * kBlock, v1 = min(v0 + kBlock, V);
+    tok[b] = (ptr[v1] - ptr[v0] <= kTileCap && tptr[b + 1] - tptr[b] <= kTileRuns) ? 1 : 0;
+}
+
 // ------------------------------------------------ split incidence setup --
 // counts edges out of u order or with a u end outside [0, V)
 static __global__ void k_u_order_check(long E, int V, const int *__restrict__ Eu,
@@ -1204,6 +1370,118 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
     edge_lane<real>(e0, eend, E, Eu, Ev, xp, Z2, A1, cw, gi, La_d1, la0, wz, rho, pd);
 }
 
+// Edge sweep of a tile-ordered graph (see tile_sum): sorted by u block, so
+// the u ends of a block's edges lie in a few consecutive u blocks.  The
+// block stages those blocks' (X, P) and (Ga, invAux) in LDS and each edge
+// names its u end by one byte (lu = u mod 256), its u block by its position
+// against the staged blocks' first positions (ustart): no Eu stream, no
+// u-end gather.  A block spanning more than TlBlocks u blocks reads Eu.
+// The v ends are gathered -- inside a (u block, v block) tile every v end
+// lies in one 256-vertex block, so the gathers of a run share their lines.
+// u blocks staged: 16 KB of LDS either way (f64 blocks cover 512 edges)
+template <typename real> struct TlBlocks { static constexpr int v = 16384 / (2 * 256 * sizeof(R2<real>)) ; };
+template <typename real>
+__global__ __launch_bounds__(256) void k_edge_sweep_tl(
+    long E, int V, const int *__restrict__ Eu, const unsigned char *__restrict__ lu,
+    const int *__restrict__ ustart, const int *__restrict__ Ev, const R2<real> *__restrict__ xp,
+    real *__restrict__ Z2, const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
+    const real *__restrict__ La_d1, real la0, real *__restrict__ wz, real rho,
+    const Ctrl<real> *ctrl, int nb, int xcd) {
+    if (ctrl && ctrl->halt) return;
+    constexpr int EPT = Vec<real>::kPer16B;
+    constexpr int NUB = TlBlocks<real>::v, SPAN = NUB * kBlock;
+    __shared__ R2<real> s_xp[SPAN];
+    __shared__ R2<real> s_gi[SPAN];
+    __shared__ int s_us[NUB + 1];
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;  // whole block
+    const int tid = threadIdx.x;
+    const long eb = (long)blk * kBlock * EPT;
+    const long el = min(eb + (long)kBlock * EPT, E) - 1;  // block's last edge
+    const int ub0 = Eu[eb] / kBlock, ub1 = Eu[el] / kBlock;
+    const int nub = ub1 - ub0 + 1;
+    const bool staged = nub <= NUB;  // block-uniform
+    const long e0 = eb + (long)tid * EPT;
+    const bool full = e0 + EPT <= E;
+    // streams and v-end gathers first: their latency hides under the staging
+    Pk<int, EPT> iv{};
+    Pk<unsigned char, EPT> il{};
+    Pk<real, 2 * EPT> z{};
+    Pk<real, EPT> la{}, a{};
+    R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
+    if (full) {
+        iv = ldv<int, EPT>(Ev + e0);
+        il = ldv<unsigned char, EPT>(lu + e0);
+        z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
+        la = la_vec<real, EPT>(e0, La_d1, la0);
+        if (A1) a = ldv<real, EPT>(A1 + e0);
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            pv[j] = xp[iv.v[j]];
+            gv[j] = gi[iv.v[j]];
+        }
+    }
+    if (staged) {
+        const int v0 = ub0 * kBlock, n = min(nub * kBlock, V - v0);
+        for (int i = tid; i < n; i += kBlock) {
+            s_xp[i] = xp[v0 + i];
+            s_gi[i] = gi[v0 + i];
+        }
+        if (tid <= nub) s_us[tid] = ustart[ub0 + tid];
+    }
+    __syncthreads();
+    if (e0 >= E) return;
+    if (full) {
+        if (staged) {
+            int k = 0;
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                while (k + 1 < nub && (long)s_us[k + 1] <= e0 + j) k++;
+                const int i = k * kBlock + il.v[j];
+                pu[j] = s_xp[i];
+                gu[j] = s_gi[i];
+            }
+        } else {
+            const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                pu[j] = xp[iu.v[j]];
+                gu[j] = gi[iu.v[j]];
+            }
+        }
+        if (!A1) {
+#pragma unroll
+            for (int j = 0; j < EPT; j++) a.v[j] = cw * la.v[j];
+        }
+        Pk<real, EPT> ou, ov;
+#pragma unroll
+        for (int j = 0; j < EPT; j++)
+            edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
+                            z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
+        stv<real, EPT>(wz + e0, ou);
+        stv<real, EPT>(wz + E + e0, ov);
+    } else {
+        for (long e = e0; e < E; e++) {
+            const int u = Eu[e], v = Ev[e];
+            real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            const real l = la_at(e, La_d1, la0);
+            edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou, ov,
+                            rho);
+            Z2[2 * e] = zu;
+            Z2[2 * e + 1] = zv;
+            wz[e] = ou;
+            wz[E + e] = ov;
+        }
+    }
+}
+
+// lu[p] = Eu[p] mod 256 (the u end within its block)
+static __global__ void k_tile_lu(long E, const int *__restrict__ Eu, unsigned char *__restrict__ lu) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < E) lu[p] = (unsigned char)(Eu[p] % kBlock);
+}
+
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
 // edge of each u, see k_uptr).  The u ends of a block's edges are a short
 // vertex range [ua, ub]: the block stages their edge offsets, (X, P) and
@@ -1364,6 +1642,10 @@ struct VArgs {
     real *part;     // 2 per block
     const Ctrl<real> *ctrl;
     int late;       // halt of ctrl tested after the sum, before the stores (small launches)
+    // tiled contributions (null d2: off; see tile_sum)
+    long E;
+    const unsigned short *d2;
+    const int *ustart, *tptr, *tstart, *tlen, *tok;
     // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
     // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
     // caller's order (tmap[v] for a relabelled session, else v), summed
@@ -1462,7 +1744,10 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
     real x;
-    if (a.blkok && a.blkok[blk])  // block-uniform
+    if (a.d2 && a.tok[blk])  // block-uniform
+        x = tile_sum<real, GB>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart, a.tlen,
+                               a.wz, lds, scan);
+    else if (a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
         x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
@@ -1491,7 +1776,7 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     }
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[kBlock / kWave];
+    __shared__ int scan[2 * kTileRuns];  // block scan (split_sum) / run table (tile_sum)
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;

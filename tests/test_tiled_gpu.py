@@ -1,0 +1,121 @@
+"""GPU: tile-ordered contributions (tile_sum, csrc/pfdr_quadratic_kernels.hpp).
+
+Large single-GPU graphs (past the fused small-graph range) keep their edges
+sorted by (u block, v block, edge): the edge sweep writes both contributions
+as streams and every vertex block stages its own contributions from a few
+contiguous runs, each entry carrying its slot in the block's CSR order, so
+the per-vertex sums run in the reference's (e, side) order without a
+gathered load.  Blocks whose lists exceed the LDS list (hubs) keep the CSR
+gather.  Every case must equal the restatement of the reference (oracle)
+bit for bit: 3-D 6-neighbour grids (3 edges per vertex), jittered k-NN
+lists (6 per vertex, mirrored duplicates), randomly labelled and shuffled
+edges (relabelled internally first), hub vertices, f32 and f64, fixed k and
+converged with reconditioning (sequential evolution sums: the reference's
+decisions)."""
+import numpy as np
+import pytest
+
+from cp_pfdr_graph_d1_amd import pfdr
+from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, uniform
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(V, Eu, Ev, Y, dt, itMax, difTol=0.0, difRcd=0.0, La=None, reorder=pfdr.REORDER_AUTO):
+    La = np.full(Eu.size, 0.1, dt) if La is None else La
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, np.zeros(V, dt), Y,
+                     La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=difTol,
+                     difRcd=difRcd, itMax=itMax, record_dif=True, reorder=reorder)
+    try:
+        q = {k: s.query(k) for k in ("tiled_blocks", "split_blocks", "reordered", "la_uniform")}
+        s.run(itMax)
+        X, it, _, Dif = s.result()
+    finally:
+        s.close()
+    return X, it, Dif, q
+
+
+def _oracle(oracle_port, V, Eu, Ev, Y, dt, itMax, difTol=0.0, difRcd=0.0, La=None):
+    La = np.full(Eu.size, 0.1, dt) if La is None else La
+    return oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev, La,
+                                       np.full(V, 0.01, dt), 0, 0, None, 1.5, 1e-3, difRcd,
+                                       difTol, itMax, dif=True)
+
+
+def _grid(shape, conn, seed):
+    Eu, Ev = grid_graph(shape, conn)
+    V = int(np.prod(shape))
+    return V, Eu.astype(np.int32), Ev.astype(np.int32)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_tiled_grid_matches_oracle(gpu_lib, oracle_port, dt):
+    shape = (72, 64, 64)
+    V, Eu, Ev = _grid(shape, 6, 1)
+    Y = piecewise_observation(shape, 3, dt)
+    X, it, D, q = _run(V, Eu, Ev, Y, dt, 25)
+    Xo, ito, _, Do = _oracle(oracle_port, V, Eu, Ev, Y, dt, 25)
+    nb = (V + 255) // 256
+    print(q)
+    assert q["tiled_blocks"] == nb and q["split_blocks"] == 0
+    assert it == ito == 25
+    assert np.array_equal(X, Xo)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_tiled_knn_converged_matches_oracle(gpu_lib, oracle_port, dt):
+    """6 nearest of 26 per vertex (mirrored duplicates), non-uniform La_d1,
+    reconditioning and a tolerance: iterates, iteration count and Dif"""
+    shape = (60, 60, 80)
+    Eu, Ev = pfdr.gen_knn_jitter_grid(shape, 6, 6, 0.25)
+    V = int(np.prod(shape))
+    Y = pfdr.gen_piecewise(shape[0], V, 2, dt, 0.2)
+    La = (0.05 + 0.1 * uniform(3, np.arange(Eu.size))).astype(dt)
+    kw = dict(difTol=1e-4 if dt == np.float32 else 1e-5, difRcd=1e-2, La=La)
+    X, it, D, q = _run(V, Eu, Ev, Y, dt, 2000, **kw)
+    Xo, ito, _, Do = _oracle(oracle_port, V, Eu, Ev, Y, dt, 2000, **kw)
+    print(q, it, ito)
+    assert q["tiled_blocks"] > 0 and q["la_uniform"] == 0
+    assert it == ito
+    assert np.array_equal(D[:it], Do[:ito])
+    assert np.array_equal(X, Xo)
+
+
+def test_tiled_after_relabelling_matches_oracle(gpu_lib, oracle_port):
+    """random vertex labels and shuffled edges (V >= 2^20: relabelled
+    internally, then tile-ordered)"""
+    shape = (128, 96, 96)
+    V, Eu, Ev = _grid(shape, 6, 1)
+    new_of = np.empty(V, np.int64)
+    new_of[np.argsort(uniform(17, np.arange(V)), kind="stable")] = np.arange(V)
+    ep = np.argsort(uniform(19, np.arange(Eu.size)), kind="stable")
+    Eu, Ev = new_of[Eu[ep]].astype(np.int32), new_of[Ev[ep]].astype(np.int32)
+    Y0 = piecewise_observation(shape, 5, np.float32)
+    Y = np.empty_like(Y0)
+    Y[new_of] = Y0
+    X, it, _, q = _run(V, Eu, Ev, Y, np.float32, 12)
+    Xo, ito, _, _ = _oracle(oracle_port, V, Eu, Ev, Y, np.float32, 12)
+    print(q)
+    assert q["reordered"] == 1 and q["tiled_blocks"] > 0
+    assert np.array_equal(X, Xo)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_tiled_hubs_fall_back_to_the_gather(gpu_lib, oracle_port, dt):
+    """hubs of 5,000 incident edges: their blocks exceed the LDS list and
+    gather through the CSR; the others stage runs; bit-exact"""
+    shape = (64, 64, 72)
+    V, Eu, Ev = _grid(shape, 6, 1)
+    hubs = np.array([5, 100000, 200001], np.int64)
+    u = np.repeat(hubs, 5000)
+    v = (uniform(23, np.arange(u.size)) * V).astype(np.int64)
+    v[v == u] = (v[v == u] + 1) % V
+    Eu = np.concatenate([Eu, u]).astype(np.int32)
+    Ev = np.concatenate([Ev, v]).astype(np.int32)
+    Y = piecewise_observation(shape, 7, dt)
+    X, it, _, q = _run(V, Eu, Ev, Y, dt, 15)
+    Xo, ito, _, _ = _oracle(oracle_port, V, Eu, Ev, Y, dt, 15)
+    nb = (V + 255) // 256
+    print(q)
+    assert 0 < q["tiled_blocks"] < nb
+    assert np.array_equal(X, Xo)

@@ -109,6 +109,23 @@ class Headline(Workload):
                     graph="%dx%dx%d" % g)
 
 
+class HeadlineConv(Headline):
+    """The headline solved to difTol 1e-5 (the parity run):
+    time to tolerance and the converged iteration count; the evolution sums
+    round as the reference's (PFDR_EVOLUTION_AUTO -> sequential at this size),
+    so the count is the reference's (248, tests/golden/fullsize/headline_conv)."""
+    name = "headline_conv"
+    partitionable = False
+    steps = 10000
+
+    def inputs(self, rank, world, strong=True):
+        d = Headline.inputs(self, 0, 1)
+        d["kw"].update(difTol=1e-5, record_dif=True)
+        d["converge"] = True
+        d["desc"] += ", solved to difTol 1e-5"
+        return d
+
+
 class HeadlineSlab8(Headline):
     """Rehearsal of one rank of the 8-GPU strong split on one GPU: the
     250x200x25 graph (1.25M vertices, 7.5M edges) every rank owns at N = 8,
@@ -408,5 +425,6 @@ class C3AtA(Workload):
         return 4 * V * (V + 1) // 2 + self.edge_bytes * E + self.vertex_bytes * V
 
 
-WORKLOADS = {w.name: w for w in (Headline(), HeadlineSlab8(), HeadlineShuffled(), C1(), C2(), C3(),
+WORKLOADS = {w.name: w for w in (Headline(), HeadlineConv(), HeadlineSlab8(), HeadlineShuffled(),
+                                  C1(), C2(), C3(),
                                   C3AtA(), C4(), C5())}
