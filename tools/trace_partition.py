@@ -94,8 +94,9 @@ def analyse(d, K):
         if len(launches) < 4 * K:
             continue
         # the window of the timed iterations: the last 4K+ launches of the thread
-        lo = launches[-4 * K][0]
-        win = [e for e in ev if e[0] >= lo]
+        # (up to the last launch: the session's teardown frees are not per iteration)
+        lo, hi = launches[-4 * K][0], launches[-1][1]
+        win = [e for e in ev if lo <= e[0] <= hi]
         api = sum(e[1] - e[0] for e in win)
         fn = defaultdict(float)
         for e in win:
