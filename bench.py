@@ -255,7 +255,11 @@ def main():
         strong = False
         parallelism = "independent replicas x%d" % world
     warm = 0 if converge else args.warmup
-    itMax = steps if converge else warm + steps
+    # N > 1: the timed steps run unprofiled, so RCCL partitions replay their
+    # captured chunks (pull, sweeps, push in one hipGraph launch per chunk);
+    # the kernel means come from a second, profiled pass of the same length
+    post_events = dist_on and not converge and not args.no_kernel_events
+    itMax = steps if converge else warm + steps + (steps if post_events else 0)
     t = time.perf_counter()
     sess = pfdr.Session(wl.kind, wl.dtype, V, E, itMax=itMax, **kw, **dist_kw)
     setup_s = time.perf_counter() - t
@@ -272,7 +276,8 @@ def main():
     timed = sorted({wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep",
                     "sx_vertex_sweep", "gemv_cols", "gemv_rows"})
     period = 4 if world == 1 else 8
-    sess.profile(not converge and not args.no_kernel_events, period=period, only=timed)
+    sess.profile(not converge and not args.no_kernel_events and not post_events, period=period,
+                 only=timed)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -289,6 +294,11 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         el_max, E_all = float(tmax[0]), int(tsum[0])
+    if post_events:
+        sess.profile(True, period=period, only=timed)
+        sess.run(steps)
+        torch.cuda.synchronize()
+        barrier()
     if converge:
         res_timed = sess.result()
         sess.close()
@@ -313,6 +323,13 @@ def main():
     knames = {f: ["k_" + f] for f in FAMILIES}
     if quad and sess.query("ustaged"):  # u ends staged in LDS for u-sorted edges
         knames["edge_sweep"] = ["k_edge_sweep_us"]
+    if quad and sess.query("tiled_blocks"):  # tile-ordered edges (large single-GPU graphs)
+        knames["edge_sweep"] = ["k_edge_sweep_tl"]
+    try:  # f32 16-byte tile staging (a library built before it has no such query)
+        if quad and sess.query("tile_vec_blocks"):
+            knames["vertex_sweep"] = ["k_vertex_sweep_tv"]
+    except pfdr.PFDRError:
+        pass
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
     sess.close()
@@ -384,8 +401,10 @@ def main():
             "traffic": dom.get("pmc_bytes"),
             **({"traffic_note": pmc_note} if pmc_note else {}),
             "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes"),
-            "timed_launches": "every %d-th launch of %s" % (period, ", ".join(
-                k for k in timed if stats.get(k, (0,))[0])),
+            "timed_launches": "every %d-th launch of %s%s" % (period, ", ".join(
+                k for k in timed if stats.get(k, (0,))[0]),
+                ", in a profiled pass of the same length after the unprofiled timed steps"
+                if post_events else ", inside the timed steps"),
             "launches": stats[wl.dominant][0],
             "mean_ms": dom.get("mean_ms"),
             "kernels": kernels,

@@ -181,6 +181,7 @@ class RcclTransport final : public Transport {
     // operations fail too instead of waiting on this rank (recorded, so the
     // owner's pfdr_comm_destroy skips the freed handle)
     void on_timeout() override { comm_abort(comm_); }
+    bool capturable() const override { return true; }
     void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
                   hipStream_t s) override {

@@ -43,6 +43,10 @@ class Transport {
     // wait for stream s (instead of hipStreamSynchronize) under the watchdog
     virtual void wait(hipStream_t s);
     virtual void on_timeout() {}
+    // the transport's per-iteration operations can be captured in a hipGraph
+    // (RCCL: yes, captured sends / receives / all-reduces replay on the
+    // communicator; loopback: no, its exchanges rendezvous on the host)
+    virtual bool capturable() const { return false; }
     // point-to-point exchange with every peer (entries for this rank and
     // zero sizes are skipped); enqueued on s
     virtual void exchange(const std::vector<const void *> &send,

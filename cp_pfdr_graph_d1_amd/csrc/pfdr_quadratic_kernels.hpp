@@ -305,6 +305,152 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
     return s;
 }
 
+// ------------------------------------ vectorised tile staging (f32) --
+// tile_sum issues one 2-byte and one 4-byte load per contribution and finds
+// the v-end runs through a run table loaded after the block's pointers: three
+// dependent round trips and ~100 load instructions per wave.  The f32 plan
+// (tdesc, one per vertex block, built at setup) lists the block's segments of
+// wz -- its u run, then its v runs in start order -- each widened to whole
+// 16-byte vectors (a few spare entries at the ends), with the running count
+// of vectors.  The block copies those vectors to LDS (lv) together with its
+// range of the inverse map (inv[slot] = LDS position of the contribution
+// whose CSR slot -- summation position -- is slot), both with 16-byte loads
+// whose addresses depend only on the plan and the CSR pointers (loaded with
+// the per-vertex operands): one dependent round trip, four contributions or
+// eight slots per load.  Each lane then adds lv[li[j]] over its own slots in
+// order: the sums of gather_sum bit for bit.  A block whose plan has more than
+// kSeg segments or more than kTvCap staged entries keeps tile_sum / the CSR
+// gather.
+constexpr int kSeg = 16;             // segments per block: the u run + 15 v runs
+constexpr int kDesc = 2 + 2 * kSeg;  // plan: nseg, nvec, starts[kSeg], vector prefix[kSeg]
+constexpr int kTvCap = 3328;         // staged floats (and slots) per block: 20 KB of LDS
+constexpr int kTvNV = 5;             // 16-byte vectors per lane in flight: (3328/4 + 3344/8) / 256
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float tile_vec_sum(int V, int blk, int v, const int *__restrict__ ptr,
+                                              const int *__restrict__ d,
+                                              const unsigned short *__restrict__ inv,
+                                              const float *__restrict__ wz, float *lv,
+                                              unsigned short *li) {
+    const int tid = threadIdx.x;
+    const int v0 = blk * kBlock, vend = min(v0 + kBlock, V);
+    const int p0 = ptr[v0], p1 = ptr[vend];
+    const int my0 = (v < V ? ptr[v] : p1) - p0;
+    const int my1 = (v < V ? ptr[v + 1] : p1) - p0;
+    const int ns = d[0], nvec = d[1];
+    const int ia0 = p0 & ~7;
+    const int ntot = nvec + ((((p1 + 7) & ~7) - ia0) >> 3);
+    for (int c = 0; c < ntot; c += kBlock * kTvNV) {
+        u32x4 x[kTvNV];
+#pragma unroll
+        for (int u = 0; u < kTvNV; u++) {
+            const int t = c + u * kBlock + tid;
+            x[u] = u32x4{0u, 0u, 0u, 0u};
+            if (t < nvec) {
+                int a = d[2], pre = 0;
+#pragma unroll
+                for (int s = 1; s < kSeg; s++) {
+                    const int q = d[2 + kSeg + s - 1];
+                    if (s < ns && t >= q) {
+                        a = d[2 + s];
+                        pre = q;
+                    }
+                }
+                x[u] = *reinterpret_cast<const u32x4 *>(wz + a + 4 * (t - pre));
+            } else if (t < ntot) {
+                x[u] = *reinterpret_cast<const u32x4 *>(inv + ia0 + 8 * (t - nvec));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kTvNV; u++) {
+            const int t = c + u * kBlock + tid;
+            if (t < nvec) *reinterpret_cast<u32x4 *>(lv + 4 * t) = x[u];
+            else if (t < ntot) *reinterpret_cast<u32x4 *>(li + 8 * (t - nvec)) = x[u];
+        }
+    }
+    __syncthreads();
+    const unsigned short *l = li + (p0 - ia0);
+    float s = 0.f;
+    int j = my0;
+    for (; j + 4 <= my1; j += 4) {  // 4 slot reads, then 4 value reads, then the adds in order
+        const int i0 = l[j], i1 = l[j + 1], i2 = l[j + 2], i3 = l[j + 3];
+        const float w0 = lv[i0], w1 = lv[i1], w2 = lv[i2], w3 = lv[i3];
+        s += w0;
+        s += w1;
+        s += w2;
+        s += w3;
+    }
+    for (; j < my1; j++) s += lv[l[j]];
+    return s;
+}
+
+// the plan of every vertex block (one lane per block); d[0] = 0: no plan
+template <int VW>
+static __global__ void k_tile_vdesc(int nb, long E, const int *__restrict__ ustart,
+                                    const int *__restrict__ tptr, const int *__restrict__ tstart,
+                                    const int *__restrict__ tlen, int cap, int *__restrict__ desc) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    int *d = desc + (long)b * kDesc;
+    d[0] = 0;
+    d[1] = 0;
+    const int t0 = tptr[b], nt = tptr[b + 1] - t0;
+    const int us = ustart[b], ue = ustart[b + 1];
+    const int nu = ue > us ? 1 : 0;
+    if (nu + nt > kSeg || nu + nt == 0) return;
+    long g0[kSeg], g1[kSeg];
+    if (nu) {
+        g0[0] = us;
+        g1[0] = ue;
+    }
+    for (int i = 0; i < nt; i++) {  // v runs in start order (a deterministic plan)
+        const long a = E + tstart[t0 + i], z = a + tlen[t0 + i];
+        int k = nu + i;
+        while (k > nu && g0[k - 1] > a) {
+            g0[k] = g0[k - 1];
+            g1[k] = g1[k - 1];
+            k--;
+        }
+        g0[k] = a;
+        g1[k] = z;
+    }
+    int nvec = 0;
+    for (int s = 0; s < nu + nt; s++) {
+        const long a0 = g0[s] & ~(long)(VW - 1), a1 = (g1[s] + VW - 1) & ~(long)(VW - 1);
+        nvec += (int)((a1 - a0) / VW);
+        d[2 + s] = (int)a0;
+        d[2 + kSeg + s] = nvec;
+    }
+    if ((long)nvec * VW > cap) return;
+    d[1] = nvec;
+    d[0] = nu + nt;
+}
+
+// inv[slot] = LDS position of the contribution at that CSR slot in its
+// block's plan (one lane per vertex)
+template <int VW>
+static __global__ void k_tile_inv(int V, const int *__restrict__ ptr,
+                                  const unsigned *__restrict__ idx, const int *__restrict__ desc,
+                                  unsigned short *__restrict__ inv) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int *d = desc + (long)(v / kBlock) * kDesc;
+    const int ns = d[0];
+    if (!ns) return;
+    for (int j = ptr[v]; j < ptr[v + 1]; j++) {
+        const long g = idx[j];
+        int pre = 0;
+        for (int s = 0; s < ns; s++) {
+            const int q = d[2 + kSeg + s];
+            if (g >= d[2 + s] && g < d[2 + s] + (long)VW * (q - pre)) {
+                inv[j] = (unsigned short)(VW * pre + (g - d[2 + s]));
+                break;
+            }
+            pre = q;
+        }
+    }
+}
+
 // tile-order keys: (u block, v block) in the high bits, edge position the value
 static __global__ void k_tile_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                                    int vbits, unsigned long long *__restrict__ keys,
@@ -364,11 +510,11 @@ static __global__ void k_tile_runs_fill(long E, const int *__restrict__ Ev,
 
 // tok[b] = 1 when block b's entries fit the LDS list and its runs the table
 static __global__ void k_tile_ok(int V, int nb, const int *__restrict__ ptr,
-                                 const int *__restrict__ tptr, int *__restrict__ tok) {
+                                 const int *__restrict__ tptr, int cap, int *__restrict__ tok) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const int v0 = b * kBlock, v1 = min(v0 + kBlock, V);
-    tok[b] = (ptr[v1] - ptr[v0] <= kTileCap && tptr[b + 1] - tptr[b] <= kTileRuns) ? 1 : 0;
+    tok[b] = (ptr[v1] - ptr[v0] <= cap && tptr[b + 1] - tptr[b] <= kTileRuns) ? 1 : 0;
 }
 
 // ------------------------------------------------ split incidence setup --
@@ -1371,22 +1517,27 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 }
 
 // Edge sweep of a tile-ordered graph (see tile_sum): sorted by u block, so
-// the u ends of a block's edges lie in a few consecutive u blocks.  The
-// block stages those blocks' (X, P) and (Ga, invAux) in LDS and each edge
-// names its u end by one byte (lu = u mod 256), its u block by its position
-// against the staged blocks' first positions (ustart): no Eu stream, no
-// u-end gather.  A block spanning more than TlBlocks u blocks reads Eu.
-// The v ends are gathered -- inside a (u block, v block) tile every v end
-// lies in one 256-vertex block, so the gathers of a run share their lines.
+// the u ends of a block's edges lie in a few consecutive u blocks, and
+// inside a (u block, v block) tile every v end lies in one 256-vertex block.
+// Each workgroup reads a 128-byte record of its edges (erec, built at
+// setup): the first u block and how many it spans, and the runs of equal v
+// block (start, v block base) -- at most kEbRuns.  Every edge names both
+// ends by one byte each (luv: u mod 256 | v mod 256 << 8), so neither Eu nor
+// Ev is streamed: the u ends come from the staged u blocks' (X, P) and
+// (Ga, invAux) in LDS, the v ends are gathered (a run's gathers share their
+// lines) at v block base + byte.  A block with more runs reads Ev, one
+// spanning more than TlBlocks u blocks reads Eu.
 // u blocks staged: 16 KB of LDS either way (f64 blocks cover 512 edges)
 template <typename real> struct TlBlocks { static constexpr int v = 16384 / (2 * 256 * sizeof(R2<real>)) ; };
+constexpr int kEbRuns = 14;             // v-block runs in an edge block's record
+constexpr int kErec = 4 + 2 * kEbRuns;  // record: ub0, nub, nruns, -, (start, v base)[kEbRuns]
 template <typename real>
 __global__ __launch_bounds__(256) void k_edge_sweep_tl(
-    long E, int V, const int *__restrict__ Eu, const unsigned char *__restrict__ lu,
-    const int *__restrict__ ustart, const int *__restrict__ Ev, const R2<real> *__restrict__ xp,
-    real *__restrict__ Z2, const real *__restrict__ A1, real cw, const R2<real> *__restrict__ gi,
-    const real *__restrict__ La_d1, real la0, real *__restrict__ wz, real rho,
-    const Ctrl<real> *ctrl, int nb, int xcd) {
+    long E, int V, const int *__restrict__ Eu, const unsigned short *__restrict__ luv,
+    const int *__restrict__ erec, const int *__restrict__ ustart, const int *__restrict__ Ev,
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
+    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
     if (ctrl && ctrl->halt) return;
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int NUB = TlBlocks<real>::v, SPAN = NUB * kBlock;
@@ -1396,29 +1547,40 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     const int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
     const int tid = threadIdx.x;
-    const long eb = (long)blk * kBlock * EPT;
-    const long el = min(eb + (long)kBlock * EPT, E) - 1;  // block's last edge
-    const int ub0 = Eu[eb] / kBlock, ub1 = Eu[el] / kBlock;
-    const int nub = ub1 - ub0 + 1;
+    const int *rec = erec + (long)blk * kErec;  // block-uniform (scalar loads)
+    const int ub0 = rec[0], nub = rec[1], nr = rec[2];
     const bool staged = nub <= NUB;  // block-uniform
-    const long e0 = eb + (long)tid * EPT;
+    const long e0 = (long)blk * kBlock * EPT + (long)tid * EPT;
     const bool full = e0 + EPT <= E;
     // streams and v-end gathers first: their latency hides under the staging
-    Pk<int, EPT> iv{};
-    Pk<unsigned char, EPT> il{};
+    Pk<unsigned short, EPT> ib{};
     Pk<real, 2 * EPT> z{};
     Pk<real, EPT> la{}, a{};
     R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
     if (full) {
-        iv = ldv<int, EPT>(Ev + e0);
-        il = ldv<unsigned char, EPT>(lu + e0);
+        ib = ldv<unsigned short, EPT>(luv + e0);
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
         la = la_vec<real, EPT>(e0, La_d1, la0);
         if (A1) a = ldv<real, EPT>(A1 + e0);
+        int iv[EPT];
+        if (nr) {  // block-uniform: v ends from the record's runs
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                int vb = rec[5];
+#pragma unroll
+                for (int r = 1; r < kEbRuns; r++)
+                    if (r < nr && e0 + j >= rec[4 + 2 * r]) vb = rec[5 + 2 * r];
+                iv[j] = vb + (ib.v[j] >> 8);
+            }
+        } else {
+            const Pk<int, EPT> x = ldv<int, EPT>(Ev + e0);
+#pragma unroll
+            for (int j = 0; j < EPT; j++) iv[j] = x.v[j];
+        }
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
-            pv[j] = xp[iv.v[j]];
-            gv[j] = gi[iv.v[j]];
+            pv[j] = xp[iv[j]];
+            gv[j] = gi[iv[j]];
         }
     }
     if (staged) {
@@ -1437,7 +1599,7 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
 #pragma unroll
             for (int j = 0; j < EPT; j++) {
                 while (k + 1 < nub && (long)s_us[k + 1] <= e0 + j) k++;
-                const int i = k * kBlock + il.v[j];
+                const int i = k * kBlock + (ib.v[j] & 0xff);
                 pu[j] = s_xp[i];
                 gu[j] = s_gi[i];
             }
@@ -1476,10 +1638,46 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     }
 }
 
-// lu[p] = Eu[p] mod 256 (the u end within its block)
-static __global__ void k_tile_lu(long E, const int *__restrict__ Eu, unsigned char *__restrict__ lu) {
+// luv[p] = (Eu[p] mod 256) | (Ev[p] mod 256) << 8: both ends within their blocks
+static __global__ void k_tile_luv(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                  unsigned short *__restrict__ luv) {
     const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < E) lu[p] = (unsigned char)(Eu[p] % kBlock);
+    if (p < E) luv[p] = (unsigned short)((Eu[p] % kBlock) | ((Ev[p] % kBlock) << 8));
+}
+
+// the record of every edge block of k_edge_sweep_tl (EB edges; one wave per
+// block): first u block and span, then the runs of equal v block in edge
+// order (nruns = 0 when there are more than kEbRuns: the block reads Ev)
+static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restrict__ Eu,
+                                   const int *__restrict__ Ev, int *__restrict__ erec) {
+    const int blk = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (blk >= nblk) return;  // whole wave
+    const long eb = (long)blk * EB, ee = min(eb + EB, E);
+    int *r = erec + (long)blk * kErec;
+    int count = 0;
+    for (long c = eb; c < ee; c += kWave) {
+        const long p = c + lane;
+        bool st = false;
+        int vb = 0;
+        if (p < ee) {
+            vb = Ev[p] / kBlock;
+            st = p == eb || Ev[p - 1] / kBlock != vb;
+        }
+        const unsigned long long m = __ballot(st);
+        const int k = count + __popcll(m & ((1ull << lane) - 1));
+        if (st && k < kEbRuns) {
+            r[4 + 2 * k] = (int)p;
+            r[5 + 2 * k] = vb * kBlock;
+        }
+        count += __popcll(m);
+    }
+    if (lane == 0) {
+        r[0] = Eu[eb] / kBlock;
+        r[1] = Eu[ee - 1] / kBlock - r[0] + 1;
+        r[2] = count <= kEbRuns ? count : 0;
+        r[3] = 0;
+    }
 }
 
 // Edge sweep of a graph whose edges are sorted by their u end (uptr: first
@@ -1646,6 +1844,9 @@ struct VArgs {
     long E;
     const unsigned short *d2;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
+    // f32 plans of the vectorised staging (null: off; see tile_vec_sum)
+    const int *tdesc;
+    const unsigned short *inv;
     // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
     // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
     // caller's order (tmap[v] for a relabelled session, else v), summed
@@ -1735,22 +1936,27 @@ __device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, r
     return q;
 }
 
-// one vertex block `blk` (all 256 lanes of the calling block take part)
-template <typename real, int GB>
+// one vertex block `blk` (all 256 lanes of the calling block take part);
+// CAP = LDS entries of `lds`, li = the inverse-map staging (tile_vec_sum)
+template <typename real, int GB, int CAP = GatherCap<real>::v>
 __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
                                              real (*red)[kBlock / kWave], int *scan,
-                                             int halt = 0) {
+                                             int halt = 0, unsigned short *li = nullptr) {
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
-    real x;
-    if (a.d2 && a.tok[blk])  // block-uniform
+    real x = real(0);
+    const int *plan = a.tdesc ? a.tdesc + (long)blk * kDesc : nullptr;  // f32 sessions only
+    if (plan && plan[0]) {  // block-uniform
+        if constexpr (std::is_same<real, float>::value)
+            x = tile_vec_sum(a.V, blk, v, a.ptr, plan, a.inv, a.wz, lds, li);
+    } else if (a.d2 && a.tok[blk])  // block-uniform
         x = tile_sum<real, GB>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart, a.tlen,
                                a.wz, lds, scan);
     else if (a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
-        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+        x = gather_sum<real, CAP, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
     if (halt) return;  // block-uniform (a.late)
     real num, den;
     vertex_finish(a, v, x, o, num, den);
@@ -1781,6 +1987,29 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan, halt);
+}
+
+// Vertex sweep of a tile-ordered f32 graph: the planned blocks stage with
+// tile_vec_sum; LDS 20 KB (staged values, then the inverse map -- the run
+// table of tile_sum and the gather's chunks reuse the same space) for 8
+// blocks per CU
+template <int GB>
+__global__ __launch_bounds__(256, 8) void k_vertex_sweep_tv(VArgs<float> a) {
+    int halt = 0;
+    if (a.ctrl) {
+        if (!a.late) {
+            if (a.ctrl->halt) return;
+        } else {
+            halt = a.ctrl->halt;
+        }
+    }
+    __shared__ __attribute__((aligned(16))) float lv[kTvCap];
+    __shared__ __attribute__((aligned(16))) unsigned short li[kTvCap + 16];
+    __shared__ float red[2][kBlock / kWave];
+    int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (lb >= a.nb) return;
+    if (lb >= a.bsplit) lb += a.bjump;
+    vertex_block<float, GB, 2048>(a, a.bbeg + lb, lv, red, reinterpret_cast<int *>(li), halt, li);
 }
 
 // Vertex sweep of a small graph (the fused-decision range) whose edge sweep

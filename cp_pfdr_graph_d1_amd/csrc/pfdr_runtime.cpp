@@ -490,6 +490,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     if (!strcmp(what, "reordered")) *value = s->impl->reordered;
     else if (!strcmp(what, "split_blocks")) *value = s->impl->split_blocks;
     else if (!strcmp(what, "tiled_blocks")) *value = s->impl->tiled_blocks;
+    else if (!strcmp(what, "tile_vec_blocks")) *value = s->impl->tile_vec_blocks;
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;
@@ -498,6 +499,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "seqdif")) *value = s->impl->seqdif;
     else if (!strcmp(what, "la_uniform")) *value = s->impl->la_uniform;
     else if (!strcmp(what, "ghosts")) *value = s->impl->ghosts;
+    else if (!strcmp(what, "graphs")) *value = s->impl->graphs;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;

@@ -61,6 +61,7 @@ class SessionBase {
     int64_t reordered = 0;  // internal locality relabelling applied
     int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
     int64_t tiled_blocks = 0;  // vertex blocks staging tile-ordered contributions
+    int64_t tile_vec_blocks = 0;  // of which with a 16-byte staging plan (f32)
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
     int64_t symv = 0;          // A^tA products from the block upper triangle
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch
@@ -70,6 +71,7 @@ class SessionBase {
     int64_t la_uniform = 0;    // one La_d1 value for every edge: the array is not streamed
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
     int64_t ghosts = 0;        // partitioned: ghost (halo) vertices of this rank
+    int64_t graphs = 0;        // chunks of iterations replayed as hipGraphs
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;

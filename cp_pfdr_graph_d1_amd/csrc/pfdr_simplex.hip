@@ -1303,7 +1303,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     PFDR_HIP(hipStreamSynchronize(s));
     pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
-    graphs_ok_ = !halo_ && !rec_obj_ && itMax_ >= 2 * chunk_;
+    // (RCCL partitions replay captured chunks too; loopback ranks rendezvous on the host)
+    graphs_ok_ = (!halo_ || halo_->tr->capturable()) && !rec_obj_ && itMax_ >= 2 * chunk_;
     {
         const char *t = getenv("PFDR_SX_TINY");
         const long maxEK = t ? atol(t) : kSxTinyEK;
@@ -1322,7 +1323,16 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         red_.alloc(2);
         seqdif = 1;
     }
-    if (graphs_ok_) (void)chunk_graph();  // instantiated with the setup
+    if (graphs_ok_) {  // instantiated with the setup
+        try {
+            (void)chunk_graph();
+        } catch (const std::exception &) {
+            if (!halo_) throw;
+            graphs_ok_ = false;  // this transport would not capture: launch directly
+            (void)hipGetLastError();
+        }
+    }
+    graphs = graphs_ok_ ? 1 : 0;
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,

@@ -112,6 +112,61 @@ def test_rccl_transport_single_rank(gpu_lib):
     assert it == G.FIXED_K and np.array_equal(X, g["fixk_X"])
 
 
+@pytest.mark.parametrize("kind", ["l1", "simplex"])
+def test_rccl_single_rank_graph_replay(gpu_lib, kind):
+    """RCCL partitioned sessions replay their chunks of iterations as
+    hipGraphs (the pull / push exchanges and the all-reduces captured with
+    the sweeps), re-captured after every reconditioning: on a 1-rank
+    communicator the iterates, iteration count and Dif equal the single-GPU
+    session's with the same (tree) evolution sums, bit for bit"""
+    import ctypes as C
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, simplex_observation
+    lib = pfdr.load()
+    idb = (C.c_char * 128)()
+    assert lib.pfdr_comm_unique_id(idb) == 0
+    comm = C.c_void_p()
+    assert lib.pfdr_comm_init(C.byref(comm), 1, 0, idb) == 0, lib.pfdr_last_error()
+    dt = np.float32
+    shape = (128, 96)
+    V = int(np.prod(shape))
+    if kind == "l1":
+        Eu, Ev = grid_graph(shape, 4)
+        args = (pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                np.zeros(V, dt), piecewise_observation(shape, 3, dt))
+        kw = dict(La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=1e-5, difRcd=1e-2)
+    else:
+        Eu, Ev = grid_graph(shape, 8)
+        v = np.arange(V)
+        Q = simplex_observation(V, 4, 4, (v * 4) // V, dt)
+        args = (pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.05, dt),
+                Q.copy(), Q)
+        kw = dict(K=4, al=0.1, rho=1.0, condMin=0.1, difTol=1e-5, difRcd=1e-2)
+    kw.update(itMax=1000, record_dif=True, evolution=pfdr.EVOLUTION_TREE)
+    try:
+        out = []
+        for part in (False, True):
+            extra = dict(nranks=1, rank=0, comm=comm.value, comm_kind=P.COMM_RCCL, vtx_begin=0,
+                         V_global=V) if part else {}
+            s = pfdr.Session(*args, **kw, **extra)
+            try:
+                if part:
+                    assert s.query("graphs") == 1
+                for n in (50, 950):  # a partial chunk launched, whole ones replayed
+                    s.run(n)
+                out.append(s.result())
+            finally:
+                s.close()
+    finally:
+        lib.pfdr_comm_destroy(comm)
+    (X0, it0, _, D0), (X1, it1, _, D1) = out
+    print("%s: it %d / %d" % (kind, it0, it1))
+    assert 0 < it0 < 1000 and it1 == it0
+    assert np.array_equal(X1, X0)
+    assert np.array_equal(D1[:it1], D0[:it0])
+
+
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 def test_partitioned_simplex_grid_matches_single(gpu_lib, dt):
     """C4's shape at a small size: K = 6 labels, KL loss, 8-neighbour grid,
