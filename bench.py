@@ -325,11 +325,6 @@ def main():
         knames["edge_sweep"] = ["k_edge_sweep_us"]
     if quad and sess.query("tiled_blocks"):  # tile-ordered edges (large single-GPU graphs)
         knames["edge_sweep"] = ["k_edge_sweep_tl"]
-    try:  # f32 16-byte tile staging (a library built before it has no such query)
-        if quad and sess.query("tile_vec_blocks"):
-            knames["vertex_sweep"] = ["k_vertex_sweep_tv"]
-    except pfdr.PFDRError:
-        pass
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
     sess.close()

@@ -182,10 +182,6 @@ class QuadSession final : public SessionBase {
     DevBuf<unsigned short> luv_;  // both ends mod 256 (k_edge_sweep_tl)
     DevBuf<int> erec_;            // per edge block: u blocks and v runs (k_edge_sweep_tl)
     DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_;
-    // f32: per-block plans of the 16-byte staging and the inverse map
-    // (tile_vec_sum); empty: off
-    DevBuf<int> tdesc_;
-    DevBuf<unsigned short> inv_;
     void build_tiles();
     Ctrl<real> *hctrl_ = nullptr;  // pinned mirror
     int nbv_, nbe_, nbn_, rows_nb_, rows_cpb_;
@@ -516,8 +512,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
-    acc(d2_.n * 2 + inv_.n * 2 + luv_.n * 2 +
-        (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + tdesc_.n + erec_.n) * 4);
+    acc(d2_.n * 2 + luv_.n * 2 +
+        (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
     if (halo_) {
         plan_overlap();
         // RCCL partitions replay captured chunks too (pull, sweeps, push and
@@ -684,7 +680,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
-    wz_.alloc(2 * E_ + R + 8);  // + the spare entries of the 16-byte staging (tile_vec_sum)
+    wz_.alloc(2 * E_ + R ? 2 * E_ + R : 1);
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
@@ -728,37 +724,14 @@ void QuadSession<real>::build_tiles() {
     tlen_.alloc(R ? R : 1);
     k_tile_runs_fill<<<grid_for(E_), kBlock, 0, s>>>(E_, Ev_.p, tptr_.p, fill.p, tstart_.p,
                                                      tlen_.p);
-    // f32: the vertex sweep's LDS holds kTvCap entries (k_vertex_sweep_tv)
-    constexpr bool vec = std::is_same<real, float>::value;
-    const int cap = vec ? kTvCap : kTileCap;
     tok_.alloc(nb);
-    k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, cap, tok_.p);
+    k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, kTileCap, tok_.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipMemcpyAsync(h.data(), tok_.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
     PFDR_HIP(hipStreamSynchronize(s));
     long n = 0;
     for (int x : h) n += x;
     tiled_blocks = n;
-    // 16-byte staging plans: wz indices as int, 16-byte aligned wz
-    if (vec && 2 * E_ + 8 < (long)INT32_MAX && (uintptr_t)wz_.p % 16 == 0) {
-        constexpr int VW = Vec<real>::kPer16B;
-        tdesc_.alloc((size_t)nb * kDesc);
-        k_tile_vdesc<VW><<<grid_for(nb), kBlock, 0, s>>>(nb, E_, ustart_.p, tptr_.p, tstart_.p,
-                                                          tlen_.p, kTvCap, tdesc_.p);
-        PFDR_HIP(hipGetLastError());
-        inv_.alloc(inc_.n + 16);
-        PFDR_HIP(hipMemsetAsync(inv_.p, 0, sizeof(unsigned short) * (inc_.n + 16), s));
-        k_tile_inv<VW><<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, tdesc_.p,
-                                                        inv_.p);
-        PFDR_HIP(hipGetLastError());
-        std::vector<int> pl((size_t)nb * kDesc);
-        PFDR_HIP(hipMemcpyAsync(pl.data(), tdesc_.p, sizeof(int) * pl.size(),
-                                hipMemcpyDeviceToHost, s));
-        PFDR_HIP(hipStreamSynchronize(s));
-        long m = 0;
-        for (int b = 0; b < nb; b++) m += pl[(size_t)b * kDesc] ? 1 : 0;
-        tile_vec_blocks = m;
-    }
 }
 
 // Split incidence for the vertex sweep (split_sum): when the edges are
@@ -1157,7 +1130,6 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     if (tiled_) {
         a.d2 = d2_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
-        a.tdesc = tdesc_.p; a.inv = inv_.p;
     }
     a.terms = seqdif_ ? terms_.p : nullptr;
     a.tmap = (seqdif_ && reordered_) ? order_.p : nullptr;
@@ -1185,12 +1157,6 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
         k_vertex_sweep_pad<real><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(
             a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
         return;
-    }
-    if constexpr (std::is_same<real, float>::value) {
-        if (a.tdesc) {
-            k_vertex_sweep_tv<8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
-            return;
-        }
     }
     k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }

@@ -305,152 +305,6 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
     return s;
 }
 
-// ------------------------------------ vectorised tile staging (f32) --
-// tile_sum issues one 2-byte and one 4-byte load per contribution and finds
-// the v-end runs through a run table loaded after the block's pointers: three
-// dependent round trips and ~100 load instructions per wave.  The f32 plan
-// (tdesc, one per vertex block, built at setup) lists the block's segments of
-// wz -- its u run, then its v runs in start order -- each widened to whole
-// 16-byte vectors (a few spare entries at the ends), with the running count
-// of vectors.  The block copies those vectors to LDS (lv) together with its
-// range of the inverse map (inv[slot] = LDS position of the contribution
-// whose CSR slot -- summation position -- is slot), both with 16-byte loads
-// whose addresses depend only on the plan and the CSR pointers (loaded with
-// the per-vertex operands): one dependent round trip, four contributions or
-// eight slots per load.  Each lane then adds lv[li[j]] over its own slots in
-// order: the sums of gather_sum bit for bit.  A block whose plan has more than
-// kSeg segments or more than kTvCap staged entries keeps tile_sum / the CSR
-// gather.
-constexpr int kSeg = 16;             // segments per block: the u run + 15 v runs
-constexpr int kDesc = 2 + 2 * kSeg;  // plan: nseg, nvec, starts[kSeg], vector prefix[kSeg]
-constexpr int kTvCap = 3328;         // staged floats (and slots) per block: 20 KB of LDS
-constexpr int kTvNV = 5;             // 16-byte vectors per lane in flight: (3328/4 + 3344/8) / 256
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float tile_vec_sum(int V, int blk, int v, const int *__restrict__ ptr,
-                                              const int *__restrict__ d,
-                                              const unsigned short *__restrict__ inv,
-                                              const float *__restrict__ wz, float *lv,
-                                              unsigned short *li) {
-    const int tid = threadIdx.x;
-    const int v0 = blk * kBlock, vend = min(v0 + kBlock, V);
-    const int p0 = ptr[v0], p1 = ptr[vend];
-    const int my0 = (v < V ? ptr[v] : p1) - p0;
-    const int my1 = (v < V ? ptr[v + 1] : p1) - p0;
-    const int ns = d[0], nvec = d[1];
-    const int ia0 = p0 & ~7;
-    const int ntot = nvec + ((((p1 + 7) & ~7) - ia0) >> 3);
-    for (int c = 0; c < ntot; c += kBlock * kTvNV) {
-        u32x4 x[kTvNV];
-#pragma unroll
-        for (int u = 0; u < kTvNV; u++) {
-            const int t = c + u * kBlock + tid;
-            x[u] = u32x4{0u, 0u, 0u, 0u};
-            if (t < nvec) {
-                int a = d[2], pre = 0;
-#pragma unroll
-                for (int s = 1; s < kSeg; s++) {
-                    const int q = d[2 + kSeg + s - 1];
-                    if (s < ns && t >= q) {
-                        a = d[2 + s];
-                        pre = q;
-                    }
-                }
-                x[u] = *reinterpret_cast<const u32x4 *>(wz + a + 4 * (t - pre));
-            } else if (t < ntot) {
-                x[u] = *reinterpret_cast<const u32x4 *>(inv + ia0 + 8 * (t - nvec));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kTvNV; u++) {
-            const int t = c + u * kBlock + tid;
-            if (t < nvec) *reinterpret_cast<u32x4 *>(lv + 4 * t) = x[u];
-            else if (t < ntot) *reinterpret_cast<u32x4 *>(li + 8 * (t - nvec)) = x[u];
-        }
-    }
-    __syncthreads();
-    const unsigned short *l = li + (p0 - ia0);
-    float s = 0.f;
-    int j = my0;
-    for (; j + 4 <= my1; j += 4) {  // 4 slot reads, then 4 value reads, then the adds in order
-        const int i0 = l[j], i1 = l[j + 1], i2 = l[j + 2], i3 = l[j + 3];
-        const float w0 = lv[i0], w1 = lv[i1], w2 = lv[i2], w3 = lv[i3];
-        s += w0;
-        s += w1;
-        s += w2;
-        s += w3;
-    }
-    for (; j < my1; j++) s += lv[l[j]];
-    return s;
-}
-
-// the plan of every vertex block (one lane per block); d[0] = 0: no plan
-template <int VW>
-static __global__ void k_tile_vdesc(int nb, long E, const int *__restrict__ ustart,
-                                    const int *__restrict__ tptr, const int *__restrict__ tstart,
-                                    const int *__restrict__ tlen, int cap, int *__restrict__ desc) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    int *d = desc + (long)b * kDesc;
-    d[0] = 0;
-    d[1] = 0;
-    const int t0 = tptr[b], nt = tptr[b + 1] - t0;
-    const int us = ustart[b], ue = ustart[b + 1];
-    const int nu = ue > us ? 1 : 0;
-    if (nu + nt > kSeg || nu + nt == 0) return;
-    long g0[kSeg], g1[kSeg];
-    if (nu) {
-        g0[0] = us;
-        g1[0] = ue;
-    }
-    for (int i = 0; i < nt; i++) {  // v runs in start order (a deterministic plan)
-        const long a = E + tstart[t0 + i], z = a + tlen[t0 + i];
-        int k = nu + i;
-        while (k > nu && g0[k - 1] > a) {
-            g0[k] = g0[k - 1];
-            g1[k] = g1[k - 1];
-            k--;
-        }
-        g0[k] = a;
-        g1[k] = z;
-    }
-    int nvec = 0;
-    for (int s = 0; s < nu + nt; s++) {
-        const long a0 = g0[s] & ~(long)(VW - 1), a1 = (g1[s] + VW - 1) & ~(long)(VW - 1);
-        nvec += (int)((a1 - a0) / VW);
-        d[2 + s] = (int)a0;
-        d[2 + kSeg + s] = nvec;
-    }
-    if ((long)nvec * VW > cap) return;
-    d[1] = nvec;
-    d[0] = nu + nt;
-}
-
-// inv[slot] = LDS position of the contribution at that CSR slot in its
-// block's plan (one lane per vertex)
-template <int VW>
-static __global__ void k_tile_inv(int V, const int *__restrict__ ptr,
-                                  const unsigned *__restrict__ idx, const int *__restrict__ desc,
-                                  unsigned short *__restrict__ inv) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= V) return;
-    const int *d = desc + (long)(v / kBlock) * kDesc;
-    const int ns = d[0];
-    if (!ns) return;
-    for (int j = ptr[v]; j < ptr[v + 1]; j++) {
-        const long g = idx[j];
-        int pre = 0;
-        for (int s = 0; s < ns; s++) {
-            const int q = d[2 + kSeg + s];
-            if (g >= d[2 + s] && g < d[2 + s] + (long)VW * (q - pre)) {
-                inv[j] = (unsigned short)(VW * pre + (g - d[2 + s]));
-                break;
-            }
-            pre = q;
-        }
-    }
-}
-
 // tile-order keys: (u block, v block) in the high bits, edge position the value
 static __global__ void k_tile_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                                    int vbits, unsigned long long *__restrict__ keys,
@@ -1844,9 +1698,6 @@ struct VArgs {
     long E;
     const unsigned short *d2;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
-    // f32 plans of the vectorised staging (null: off; see tile_vec_sum)
-    const int *tdesc;
-    const unsigned short *inv;
     // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
     // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
     // caller's order (tmap[v] for a relabelled session, else v), summed
@@ -1936,27 +1787,22 @@ __device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, r
     return q;
 }
 
-// one vertex block `blk` (all 256 lanes of the calling block take part);
-// CAP = LDS entries of `lds`, li = the inverse-map staging (tile_vec_sum)
-template <typename real, int GB, int CAP = GatherCap<real>::v>
+// one vertex block `blk` (all 256 lanes of the calling block take part)
+template <typename real, int GB>
 __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
                                              real (*red)[kBlock / kWave], int *scan,
-                                             int halt = 0, unsigned short *li = nullptr) {
+                                             int halt = 0) {
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
-    real x = real(0);
-    const int *plan = a.tdesc ? a.tdesc + (long)blk * kDesc : nullptr;  // f32 sessions only
-    if (plan && plan[0]) {  // block-uniform
-        if constexpr (std::is_same<real, float>::value)
-            x = tile_vec_sum(a.V, blk, v, a.ptr, plan, a.inv, a.wz, lds, li);
-    } else if (a.d2 && a.tok[blk])  // block-uniform
+    real x;
+    if (a.d2 && a.tok[blk])  // block-uniform
         x = tile_sum<real, GB>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart, a.tlen,
                                a.wz, lds, scan);
     else if (a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
-        x = gather_sum<real, CAP, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
     if (halt) return;  // block-uniform (a.late)
     real num, den;
     vertex_finish(a, v, x, o, num, den);
@@ -1987,29 +1833,6 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan, halt);
-}
-
-// Vertex sweep of a tile-ordered f32 graph: the planned blocks stage with
-// tile_vec_sum; LDS 20 KB (staged values, then the inverse map -- the run
-// table of tile_sum and the gather's chunks reuse the same space) for 8
-// blocks per CU
-template <int GB>
-__global__ __launch_bounds__(256, 8) void k_vertex_sweep_tv(VArgs<float> a) {
-    int halt = 0;
-    if (a.ctrl) {
-        if (!a.late) {
-            if (a.ctrl->halt) return;
-        } else {
-            halt = a.ctrl->halt;
-        }
-    }
-    __shared__ __attribute__((aligned(16))) float lv[kTvCap];
-    __shared__ __attribute__((aligned(16))) unsigned short li[kTvCap + 16];
-    __shared__ float red[2][kBlock / kWave];
-    int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
-    if (lb >= a.nb) return;
-    if (lb >= a.bsplit) lb += a.bjump;
-    vertex_block<float, GB, 2048>(a, a.bbeg + lb, lv, red, reinterpret_cast<int *>(li), halt, li);
 }
 
 // Vertex sweep of a small graph (the fused-decision range) whose edge sweep

@@ -61,7 +61,6 @@ class SessionBase {
     int64_t reordered = 0;  // internal locality relabelling applied
     int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
     int64_t tiled_blocks = 0;  // vertex blocks staging tile-ordered contributions
-    int64_t tile_vec_blocks = 0;  // of which with a 16-byte staging plan (f32)
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
     int64_t symv = 0;          // A^tA products from the block upper triangle
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch

@@ -6,9 +6,7 @@ as streams and every vertex block stages its own contributions from a few
 contiguous runs, each entry carrying its slot in the block's CSR order, so
 the per-vertex sums run in the reference's (e, side) order without a
 gathered load.  Blocks whose lists exceed the LDS list (hubs) keep the CSR
-gather.  In f32 a block whose runs form at most 16 segments stages them with 16-byte
-loads and an inverse slot map instead (tile_vec_sum).
-Every case must equal the restatement of the reference (oracle)
+gather.  Every case must equal the restatement of the reference (oracle)
 bit for bit: 3-D 6-neighbour grids (3 edges per vertex), jittered k-NN
 lists (6 per vertex, mirrored duplicates), randomly labelled and shuffled
 edges (relabelled internally first), hub vertices, f32 and f64, fixed k and
@@ -29,8 +27,7 @@ def _run(V, Eu, Ev, Y, dt, itMax, difTol=0.0, difRcd=0.0, La=None, reorder=pfdr.
                      La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=difTol,
                      difRcd=difRcd, itMax=itMax, record_dif=True, reorder=reorder)
     try:
-        q = {k: s.query(k) for k in ("tiled_blocks", "tile_vec_blocks", "split_blocks", "reordered",
-                                     "la_uniform")}
+        q = {k: s.query(k) for k in ("tiled_blocks", "split_blocks", "reordered", "la_uniform")}
         s.run(itMax)
         X, it, _, Dif = s.result()
     finally:
@@ -61,8 +58,6 @@ def test_tiled_grid_matches_oracle(gpu_lib, oracle_port, dt):
     nb = (V + 255) // 256
     print(q)
     assert q["tiled_blocks"] == nb and q["split_blocks"] == 0
-    # f32: every block stages with 16-byte loads (tile_vec_sum); f64: run table
-    assert q["tile_vec_blocks"] == (nb if dt == np.float32 else 0)
     assert it == ito == 25
     assert np.array_equal(X, Xo)
 
@@ -123,17 +118,14 @@ def test_tiled_hubs_fall_back_to_the_gather(gpu_lib, oracle_port, dt):
     nb = (V + 255) // 256
     print(q)
     assert 0 < q["tiled_blocks"] < nb
-    if dt == np.float32:
-        assert 0 < q["tile_vec_blocks"] <= q["tiled_blocks"]
     assert np.array_equal(X, Xo)
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
-def test_tiled_scattered_sources_take_the_run_table(gpu_lib, oracle_port, dt):
-    """random long-range edges (about 11 per vertex block): many vertex blocks
-    then receive v ends from more u blocks than a 16-segment staging plan
-    holds, so they stage through the run table (tile_sum) while the rest keep
-    the 16-byte plan; bit-exact either way"""
+def test_tiled_scattered_sources(gpu_lib, oracle_port, dt):
+    """random long-range edges (about 11 per vertex block): vertex blocks
+    stage v ends from many short runs (up to ~30) and edge-sweep blocks see
+    more v-block runs than their record holds (they read Ev); bit-exact"""
     shape = (64, 64, 72)
     V, Eu, Ev = _grid(shape, 6, 1)
     n = V // 24
@@ -148,6 +140,4 @@ def test_tiled_scattered_sources_take_the_run_table(gpu_lib, oracle_port, dt):
     nb = (V + 255) // 256
     print(q)
     assert q["tiled_blocks"] == nb
-    if dt == np.float32:
-        assert 0 < q["tile_vec_blocks"] < nb
     assert np.array_equal(X, Xo)
