@@ -1085,10 +1085,9 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
         return;
     }
     if (tiled_ && !fuse_ && rg.nb0 == nb && ebeg == 0 && eend == E_) {
-        k_edge_sweep_tl<real><<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, ustart_.p,
-                                                   Ev_.p, xp_.p,
-                                                   Z2_.p, A1_.p, cw_, gi_.p, la_it(), la0_, wz_.p,
-                                                   rho_, c, nb, xm);
+        auto k = (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true> : k_edge_sweep_tl<real, false>;
+        k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_,
+                               gi_.p, la_it(), la0_, wz_.p, rho_, c, nb, xm);
         return;
     }
     if (us_ && uptr_.p) {

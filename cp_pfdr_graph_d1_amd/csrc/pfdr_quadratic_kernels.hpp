@@ -275,20 +275,21 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
     }
     __syncthreads();  // run table
     const int nv = nt ? rp[nt - 1] : 0;
+    int lo = 0, end = nt ? rp[0] : 0, beg = 0;  // run of the lane's entry k, its bounds
     for (int b = 0; b < nv; b += kBlock * GB) {
         unsigned short d[GB];
         real w[GB];
         long ad[GB];
 #pragma unroll
         for (int u = 0; u < GB; u++) {
+            // the lane's entries grow by 256: its run only advances (about
+            // one run per step on the BASELINE grids), no search
             const int k = min(b + u * kBlock + tid, nv - 1);
-            int lo = 0, hi = nt - 1;  // first run whose inclusive prefix exceeds k
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (rp[mid] > k) hi = mid;
-                else lo = mid + 1;
+            while (end <= k) {
+                beg = end;
+                end = rp[++lo];
             }
-            ad[u] = E + rs[lo] + (k - (lo ? rp[lo - 1] : 0));
+            ad[u] = E + rs[lo] + (k - beg);
         }
 #pragma unroll
         for (int u = 0; u < GB; u++) {
@@ -1373,9 +1374,12 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 // Edge sweep of a tile-ordered graph (see tile_sum): sorted by u block, so
 // the u ends of a block's edges lie in a few consecutive u blocks, and
 // inside a (u block, v block) tile every v end lies in one 256-vertex block.
-// Each workgroup reads a 128-byte record of its edges (erec, built at
-// setup): the first u block and how many it spans, and the runs of equal v
-// block (start, v block base) -- at most kEbRuns.  Every edge names both
+// Each workgroup reads a 192-byte record of its edges (erec, built at
+// setup, scalar loads): the first u block, how many it spans and where in
+// the block each further u block starts, and the runs of equal v block
+// (start, v block base) -- at most kEbRuns; positions are relative to the
+// block's first edge, so every lookup is a 32-bit compare against a scalar
+// in a loop as long as the block's own run count.  Every edge names both
 // ends by one byte each (luv: u mod 256 | v mod 256 << 8), so neither Eu nor
 // Ev is streamed: the u ends come from the staged u blocks' (X, P) and
 // (Ga, invAux) in LDS, the v ends are gathered (a run's gathers share their
@@ -1383,30 +1387,36 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 // spanning more than TlBlocks u blocks reads Eu.
 // u blocks staged: 16 KB of LDS either way (f64 blocks cover 512 edges)
 template <typename real> struct TlBlocks { static constexpr int v = 16384 / (2 * 256 * sizeof(R2<real>)) ; };
-constexpr int kEbRuns = 14;             // v-block runs in an edge block's record
-constexpr int kErec = 4 + 2 * kEbRuns;  // record: ub0, nub, nruns, -, (start, v base)[kEbRuns]
-template <typename real>
-__global__ __launch_bounds__(256) void k_edge_sweep_tl(
+constexpr int kEbRuns = 20;  // v-block runs in an edge block's record
+constexpr int kErecU = 4;    // rec[4]: staged span; rec[4 + q]: start of u block ub0 + q
+                             // (q = 1..3; INT_MAX if q >= nub)
+constexpr int kErecS = 8;    // rec[kErecS + 2r]: start of run r (INT_MAX if r >= nruns), + 1: its v base
+// rec[0..3]: ub0, nub, nruns (0: read Ev), uoff (smallest u end - ub0 * 256);
+// the staged u range is [ub0 * 256 + uoff, + span), span = largest - smallest + 1
+constexpr int kErec = kErecS + 2 * kEbRuns;
+// UNI: one weight La_d1 for every edge (la0) and no A1 (before any
+// reconditioning): a_e = cw * la0 is one value, computed once per lane
+template <typename real, bool UNI>
+__device__ __forceinline__ void tl_gather(
     long E, int V, const int *__restrict__ Eu, const unsigned short *__restrict__ luv,
-    const int *__restrict__ erec, const int *__restrict__ ustart, const int *__restrict__ Ev,
+    const int *__restrict__ rec, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
-    if (ctrl && ctrl->halt) return;
+    real *__restrict__ wz, real rho, int blk, R2<real> *s_xp, R2<real> *s_gi) {
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int NUB = TlBlocks<real>::v, SPAN = NUB * kBlock;
-    __shared__ R2<real> s_xp[SPAN];
-    __shared__ R2<real> s_gi[SPAN];
-    __shared__ int s_us[NUB + 1];
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
-    if (blk >= nb) return;  // whole block
     const int tid = threadIdx.x;
-    const int *rec = erec + (long)blk * kErec;  // block-uniform (scalar loads)
     const int ub0 = rec[0], nub = rec[1], nr = rec[2];
-    const bool staged = nub <= NUB;  // block-uniform
-    const long e0 = (long)blk * kBlock * EPT + (long)tid * EPT;
+    const int uoff = rec[3], span = rec[kErecU];  // staged u range: ub0 * 256 + uoff, span
+    const bool staged = nub <= NUB && span <= SPAN;  // block-uniform
+    const int rel = tid * EPT;       // first edge of the lane, relative to the block's
+    const long e0 = (long)blk * kBlock * EPT + rel;
     const bool full = e0 + EPT <= E;
-    // streams and v-end gathers first: their latency hides under the staging
+    // streams first, then the staging loads of the block's u range (the
+    // first NS0 per lane issued unconditionally, clamped into the range, so
+    // the load counts stay static), then the v-end gathers once the end
+    // bytes are in: the three round trips overlap
+    constexpr int NS0 = SPAN / kBlock / 2;
     Pk<unsigned short, EPT> ib{};
     Pk<real, 2 * EPT> z{};
     Pk<real, EPT> la{}, a{};
@@ -1414,18 +1424,42 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     if (full) {
         ib = ldv<unsigned short, EPT>(luv + e0);
         z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
-        la = la_vec<real, EPT>(e0, La_d1, la0);
-        if (A1) a = ldv<real, EPT>(A1 + e0);
+        if (!UNI) {
+            la = la_vec<real, EPT>(e0, La_d1, la0);
+            if (A1) a = ldv<real, EPT>(A1 + e0);
+        }
+    }
+    const int su = ub0 * kBlock + uoff;  // first staged vertex
+    R2<real> sx[NS0], sg[NS0];
+    if (staged) {
+#pragma unroll
+        for (int q = 0; q < NS0; q++) {
+            const int i = su + min(q * kBlock + tid, span - 1);
+            sx[q] = xp[i];
+            sg[q] = gi[i];
+        }
+    }
+    if (full) {
         int iv[EPT];
         if (nr) {  // block-uniform: v ends from the record's runs
+            int vb[EPT];
 #pragma unroll
-            for (int j = 0; j < EPT; j++) {
-                int vb = rec[5];
+            for (int j = 0; j < EPT; j++) vb[j] = rec[kErecS + 1];
+            // runs in groups of four (one 32-byte scalar load each; starts
+            // past the block's last run are padded, never reached)
 #pragma unroll
-                for (int r = 1; r < kEbRuns; r++)
-                    if (r < nr && e0 + j >= rec[4 + 2 * r]) vb = rec[5 + 2 * r];
-                iv[j] = vb + (ib.v[j] >> 8);
+            for (int g = 1; g < kEbRuns; g += 4) {
+                if (g < nr) {  // block-uniform
+#pragma unroll
+                    for (int r = g; r < g + 4 && r < kEbRuns; r++) {
+                        const int st = rec[kErecS + 2 * r], bs = rec[kErecS + 2 * r + 1];
+#pragma unroll
+                        for (int j = 0; j < EPT; j++) vb[j] = rel + j >= st ? bs : vb[j];
+                    }
+                }
             }
+#pragma unroll
+            for (int j = 0; j < EPT; j++) iv[j] = vb[j] + (ib.v[j] >> 8);
         } else {
             const Pk<int, EPT> x = ldv<int, EPT>(Ev + e0);
 #pragma unroll
@@ -1438,24 +1472,38 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
         }
     }
     if (staged) {
-        const int v0 = ub0 * kBlock, n = min(nub * kBlock, V - v0);
-        for (int i = tid; i < n; i += kBlock) {
-            s_xp[i] = xp[v0 + i];
-            s_gi[i] = gi[v0 + i];
+#pragma unroll
+        for (int q = 0; q < NS0; q++) {
+            const int i = q * kBlock + tid;
+            if (i < span) {
+                s_xp[i] = sx[q];
+                s_gi[i] = sg[q];
+            }
         }
-        if (tid <= nub) s_us[tid] = ustart[ub0 + tid];
+        for (int i = NS0 * kBlock + tid; i < span; i += kBlock) {  // wide ranges
+            s_xp[i] = xp[su + i];
+            s_gi[i] = gi[su + i];
+        }
     }
     __syncthreads();
     if (e0 >= E) return;
     if (full) {
         if (staged) {
-            int k = 0;
+            int ku[EPT];  // staged u block of each edge, then its LDS slot
+#pragma unroll
+            for (int j = 0; j < EPT; j++) ku[j] = (ib.v[j] & 0xff) - uoff;
+            if (nub > 1) {  // block-uniform; starts of absent blocks padded
+#pragma unroll
+                for (int q = 1; q < NUB; q++) {
+                    const int st = rec[kErecU + q];
+#pragma unroll
+                    for (int j = 0; j < EPT; j++) ku[j] += rel + j >= st ? kBlock : 0;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < EPT; j++) {
-                while (k + 1 < nub && (long)s_us[k + 1] <= e0 + j) k++;
-                const int i = k * kBlock + (ib.v[j] & 0xff);
-                pu[j] = s_xp[i];
-                gu[j] = s_gi[i];
+                pu[j] = s_xp[ku[j]];
+                gu[j] = s_gi[ku[j]];
             }
         } else {
             const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
@@ -1465,7 +1513,14 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
                 gu[j] = gi[iu.v[j]];
             }
         }
-        if (!A1) {
+        if (UNI) {
+            const real a0 = cw * la0;
+#pragma unroll
+            for (int j = 0; j < EPT; j++) {
+                a.v[j] = a0;
+                la.v[j] = la0;
+            }
+        } else if (!A1) {
 #pragma unroll
             for (int j = 0; j < EPT; j++) a.v[j] = cw * la.v[j];
         }
@@ -1492,6 +1547,24 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     }
 }
 
+
+template <typename real, bool UNI>
+__global__ __launch_bounds__(256) void k_edge_sweep_tl(
+    long E, int V, const int *__restrict__ Eu, const unsigned short *__restrict__ luv,
+    const int *__restrict__ erec, const int *__restrict__ Ev,
+    const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
+    const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
+    if (ctrl && ctrl->halt) return;
+    constexpr int SPAN = TlBlocks<real>::v * kBlock;
+    __shared__ R2<real> s_xp[SPAN];
+    __shared__ R2<real> s_gi[SPAN];
+    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    if (blk >= nb) return;  // whole block
+    tl_gather<real, UNI>(E, V, Eu, luv, erec + (long)blk * kErec, Ev, xp, Z2, A1, cw, gi, La_d1,
+                         la0, wz, rho, blk, s_xp, s_gi);
+}
+
 // luv[p] = (Eu[p] mod 256) | (Ev[p] mod 256) << 8: both ends within their blocks
 static __global__ void k_tile_luv(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                                   unsigned short *__restrict__ luv) {
@@ -1500,8 +1573,10 @@ static __global__ void k_tile_luv(long E, const int *__restrict__ Eu, const int 
 }
 
 // the record of every edge block of k_edge_sweep_tl (EB edges; one wave per
-// block): first u block and span, then the runs of equal v block in edge
-// order (nruns = 0 when there are more than kEbRuns: the block reads Ev)
+// block): first u block, span and the smallest / largest u end, where each
+// further u block starts, then the runs of equal v block in edge order
+// (nruns = 0 when there are more than kEbRuns: the block reads Ev); starts
+// relative to the block's first edge, padded past the last run
 static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restrict__ Eu,
                                    const int *__restrict__ Ev, int *__restrict__ erec) {
     const int blk = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
@@ -1509,7 +1584,8 @@ static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restri
     if (blk >= nblk) return;  // whole wave
     const long eb = (long)blk * EB, ee = min(eb + EB, E);
     int *r = erec + (long)blk * kErec;
-    int count = 0;
+    const int ub0 = Eu[eb] / kBlock;
+    int count = 0, umin = 0x7fffffff, umax = -1;
     for (long c = eb; c < ee; c += kWave) {
         const long p = c + lane;
         bool st = false;
@@ -1517,20 +1593,39 @@ static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restri
         if (p < ee) {
             vb = Ev[p] / kBlock;
             st = p == eb || Ev[p - 1] / kBlock != vb;
+            const int u = Eu[p];
+            umin = min(umin, u);
+            umax = max(umax, u);
+            // u blocks ub0 + q starting here (edges sorted by u block)
+            const int q1 = u / kBlock - ub0;
+            const int q0 = p == eb ? q1 : Eu[p - 1] / kBlock - ub0;
+            for (int q = q0 + 1; q <= q1 && q < kErecS - kErecU; q++) r[kErecU + q] = (int)(p - eb);
         }
         const unsigned long long m = __ballot(st);
         const int k = count + __popcll(m & ((1ull << lane) - 1));
         if (st && k < kEbRuns) {
-            r[4 + 2 * k] = (int)p;
-            r[5 + 2 * k] = vb * kBlock;
+            r[kErecS + 2 * k] = (int)(p - eb);
+            r[kErecS + 2 * k + 1] = vb * kBlock;
         }
         count += __popcll(m);
     }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        umin = min(umin, __shfl_xor(umin, o, kWave));
+        umax = max(umax, __shfl_xor(umax, o, kWave));
+    }
+    const int nub = Eu[ee - 1] / kBlock - ub0 + 1;
+    for (int k = count + lane; k < kEbRuns; k += kWave) {  // padding: never reached
+        r[kErecS + 2 * k] = 0x7fffffff;
+        r[kErecS + 2 * k + 1] = 0;
+    }
     if (lane == 0) {
-        r[0] = Eu[eb] / kBlock;
-        r[1] = Eu[ee - 1] / kBlock - r[0] + 1;
+        r[0] = ub0;
+        r[1] = nub;
         r[2] = count <= kEbRuns ? count : 0;
-        r[3] = 0;
+        r[3] = umin - ub0 * kBlock;
+        r[kErecU] = umax - umin + 1;
+        for (int q = max(nub, 1); q < kErecS - kErecU; q++) r[kErecU + q] = 0x7fffffff;
     }
 }
 

@@ -141,3 +141,21 @@ def test_tiled_scattered_sources(gpu_lib, oracle_port, dt):
     print(q)
     assert q["tiled_blocks"] == nb
     assert np.array_equal(X, Xo)
+
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_tiled_sparse_rows(gpu_lib, oracle_port, dt):
+    """a 2-D grid whose upper half keeps one right-hand edge in three: the
+    edge-sweep blocks there span more u blocks than they stage (they read
+    Eu), the dense half stages its u ends; bit-exact"""
+    nx, ny = 1000, 700
+    V, Eu, Ev = _grid((ny, nx), 4, 1)
+    keep = (Eu < V // 2) | ((Ev == Eu + 1) & (Eu % 3 == 0))  # sparse upper rows
+    Eu, Ev = Eu[keep], Ev[keep]
+    Y = pfdr.gen_piecewise(nx, V, 13, dt, 0.2)
+    X, it, _, q = _run(V, Eu, Ev, Y, dt, 15)
+    Xo, ito, _, _ = _oracle(oracle_port, V, Eu, Ev, Y, dt, 15)
+    print(q)
+    assert q["tiled_blocks"] > 0
+    assert np.array_equal(X, Xo)
