@@ -80,6 +80,34 @@ __global__ void k_edge_tile_order(long E, const unsigned *__restrict__ perm,
     emap[p] = (int)e;
 }
 
+// the same for a partitioned rank: eo = the global edge id (incidence
+// keys), emap = the rank-local position (the caller's per-edge arrays)
+__global__ void k_edge_tile_order_halo(long E, const unsigned *__restrict__ perm,
+                                       const unsigned *__restrict__ eg, long e_offset,
+                                       const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                       int *__restrict__ nEu, int *__restrict__ nEv,
+                                       unsigned *__restrict__ eo, int *__restrict__ emap,
+                                       unsigned *__restrict__ inv) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const unsigned q = perm[p];
+    nEu[p] = Eu[q];
+    nEv[p] = Ev[q];
+    eo[p] = eg ? eg[q] : (unsigned)(e_offset + q);
+    emap[p] = (int)q;
+    inv[q] = (unsigned)p;
+}
+
+// the halo's push addresses (side E + e) into the tile order
+__global__ void k_remap_push(long n, long E, const unsigned *__restrict__ inv,
+                             unsigned *__restrict__ addr) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned a = addr[i];
+    const unsigned side = a >= (unsigned)E ? 1u : 0u;
+    addr[i] = side * (unsigned)E + inv[a - side * (unsigned)E];
+}
+
 template <typename real>
 class QuadSession final : public SessionBase {
   public:
@@ -223,6 +251,7 @@ class QuadSession final : public SessionBase {
     hipStream_t comm_ = nullptr;
     hipEvent_t ev_[4] = {};  // xp ready, pulled, boundary W*Z ready, pushed
     long elo_ = 0, ehi_ = 0;
+    long Eint_ = 0;  // tiled partitioned rank: edges [0, Eint_) have no ghost end
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
@@ -652,26 +681,46 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         std::swap(Ev_.p, nv.p);
         eg_ptr = eorig_.p;
     }
-    // tile order of large single-GPU graphs (see tile_sum): edges sorted by
-    // (u block, v block), stable in the current order; the incidence keys keep
-    // the original edge ids (summation order)
-    tiled_ = !halo_ && !tiny_ && E_ > 0 && (long)V_ > (long)kFuseBlocks * kBlock;
+    // tile order of large graphs (see tile_sum): edges sorted by (u block,
+    // v block), stable in the current order; the incidence keys keep the
+    // original edge ids (summation order).  A partitioned rank puts the
+    // edges with a ghost end after the others (the interior ones overlap
+    // the halo pull) and renumbers its push addresses.
+    tiled_ = !tiny_ && E_ > 0 && (long)V_ > (long)kFuseBlocks * kBlock;
     if (tiled_) {
-        const int nb = grid_for(V_);
+        const int nb = grid_for(Vg_);
         int vbits = 1;
         while (vbits < 31 && (1L << vbits) < (long)nb) vbits++;
-        DevBuf<unsigned long long> k(E), ks(E);
+        DevBuf<unsigned long long> k(E), ks(E), nint(1);
         DevBuf<unsigned> v(E), perm(E);
-        k_tile_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, vbits, k.p, v.p);
+        if (halo_) PFDR_HIP(hipMemsetAsync(nint.p, 0, sizeof(unsigned long long), s));
+        k_tile_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, vbits, k.p, v.p, V_,
+                                                   halo_ ? nint.p : nullptr);
         PFDR_HIP(hipGetLastError());
-        radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, perm.p, (long)E, 2 * vbits, s);
+        radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, perm.p, (long)E,
+                                                    2 * vbits + (halo_ ? 1 : 0), s);
         DevBuf<int> nu(E), nv(E);
         DevBuf<unsigned> eo(E);
         emap_.alloc(E);
-        k_edge_tile_order<<<grid_for(E), kBlock, 0, s>>>(E_, perm.p, eorig_.p, Eu_.p, Ev_.p, nu.p,
-                                                         nv.p, eo.p, emap_.p);
-        PFDR_HIP(hipGetLastError());
-        PFDR_HIP(hipStreamSynchronize(s));
+        if (halo_) {
+            DevBuf<unsigned> inv(E);
+            k_edge_tile_order_halo<<<grid_for(E), kBlock, 0, s>>>(
+                E_, perm.p, eg.p, e_offset, Eu_.p, Ev_.p, nu.p, nv.p, eo.p, emap_.p, inv.p);
+            const long np = halo_->push_send_off.back();
+            if (np) k_remap_push<<<grid_for(np), kBlock, 0, s>>>(np, E_, inv.p, halo_->push_addr.p);
+            PFDR_HIP(hipGetLastError());
+            unsigned long long ni = 0;
+            PFDR_HIP(hipMemcpyAsync(&ni, nint.p, sizeof(ni), hipMemcpyDeviceToHost, s));
+            PFDR_HIP(hipStreamSynchronize(s));
+            Eint_ = (long)ni;
+            e_offset = 0;
+        } else {
+            k_edge_tile_order<<<grid_for(E), kBlock, 0, s>>>(E_, perm.p, eorig_.p, Eu_.p, Ev_.p,
+                                                             nu.p, nv.p, eo.p, emap_.p);
+            PFDR_HIP(hipGetLastError());
+            PFDR_HIP(hipStreamSynchronize(s));
+            Eint_ = E_;
+        }
         std::swap(Eu_.p, nu.p);
         std::swap(Ev_.p, nv.p);
         std::swap(eorig_.p, eo.p);
@@ -694,7 +743,8 @@ template <typename real>
 void QuadSession<real>::build_tiles() {
     hipStream_t s = stream;
     const int nb = grid_for(V_);
-    d2_.alloc(2 * (size_t)E_);
+    const long R = halo_ ? halo_->R : 0;
+    d2_.alloc(2 * (size_t)E_ + R);
     k_tile_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, d2_.p);
     luv_.alloc((size_t)E_);
     k_tile_luv<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, luv_.p);
@@ -707,23 +757,33 @@ void QuadSession<real>::build_tiles() {
         PFDR_HIP(hipGetLastError());
     }
     ustart_.alloc((size_t)nb + 1);
-    k_tile_ustart<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, nb, Eu_.p, ustart_.p);
+    // u runs: the interior edges (sorted by u block); a partitioned rank's
+    // boundary edges [Eint_, E) add their owned u ends as runs, its received
+    // contributions theirs (k_tile_runs_count)
+    k_tile_ustart<<<grid_for(Eint_ + 1), kBlock, 0, s>>>(Eint_, nb, Eu_.p, ustart_.p);
     DevBuf<int> cnt(nb), fill(nb);
     PFDR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * nb, s));
     PFDR_HIP(hipMemsetAsync(fill.p, 0, sizeof(int) * nb, s));
-    k_tile_runs_count<<<grid_for(E_), kBlock, 0, s>>>(E_, Ev_.p, cnt.p);
+    struct Src { long n; const int *a; const unsigned long long *keys; long rs; };
+    const Src src[3] = {{E_, Ev_.p, nullptr, 0},
+                        {E_ - Eint_, Eu_.p + Eint_, nullptr, Eint_ - E_},
+                        {R, nullptr, halo_ ? halo_->recv_keys.p : nullptr, E_}};
+    for (const Src &q : src)
+        if (q.n > 0) k_tile_runs_count<<<grid_for(q.n), kBlock, 0, s>>>(q.n, q.a, q.keys, V_, cnt.p);
     PFDR_HIP(hipGetLastError());
     std::vector<int> h(nb), tp((size_t)nb + 1, 0);
     PFDR_HIP(hipMemcpyAsync(h.data(), cnt.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
     PFDR_HIP(hipStreamSynchronize(s));
     for (int b = 0; b < nb; b++) tp[b + 1] = tp[b] + h[b];
-    const int R = tp[nb];
+    const int nruns = tp[nb];
     tptr_.alloc((size_t)nb + 1);
     PFDR_HIP(hipMemcpyAsync(tptr_.p, tp.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice, s));
-    tstart_.alloc(R ? R : 1);
-    tlen_.alloc(R ? R : 1);
-    k_tile_runs_fill<<<grid_for(E_), kBlock, 0, s>>>(E_, Ev_.p, tptr_.p, fill.p, tstart_.p,
-                                                     tlen_.p);
+    tstart_.alloc(nruns ? nruns : 1);
+    tlen_.alloc(nruns ? nruns : 1);
+    for (const Src &q : src)
+        if (q.n > 0)
+            k_tile_runs_fill<<<grid_for(q.n), kBlock, 0, s>>>(q.n, q.a, q.keys, V_, q.rs, tptr_.p,
+                                                              fill.p, tstart_.p, tlen_.p);
     tok_.alloc(nb);
     k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, kTileCap, tok_.p);
     PFDR_HIP(hipGetLastError());
@@ -1084,12 +1144,16 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
                                                      la_it(), la0_, rho_, c, nb, xm, f, pad_out());
         return;
     }
-    if (tiled_ && !fuse_ && rg.nb0 == nb && ebeg == 0 && eend == E_) {
+    constexpr long EB = kBlock * EPT;  // edges per tiled edge-sweep block
+    if (tiled_ && !fuse_ && rg.nb0 == nb && ebeg % EB == 0 && (eend % EB == 0 || eend == E_)) {
+        // edge blocks [ebeg / EB, ...) of the tile order (a partitioned rank
+        // sweeps its interior blocks and the rest in two launches)
         auto k = (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true> : k_edge_sweep_tl<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_,
-                               gi_.p, la_it(), la0_, wz_.p, rho_, c, nb, xm);
+                               gi_.p, la_it(), la0_, wz_.p, rho_, c, (int)(ebeg / EB), nb, xm);
         return;
     }
+    if (tiled_) throw std::logic_error("tiled edge sweep: range not on edge blocks");
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
@@ -1262,6 +1326,11 @@ void QuadSession<real>::plan_overlap() {
     // both cuts on the lane width: every launch starts vector-aligned
     elo_ = ((best0 + EPT - 1) / EPT) * EPT;
     ehi_ = std::max(elo_, (best1 / EPT) * EPT);
+    if (tiled_) {  // tile order: the interior edges come first, cut on whole edge blocks
+        constexpr long EB = kBlock * EPT;
+        elo_ = 0;
+        ehi_ = (Eint_ / EB) * EB;
+    }
     // vertex blocks: any CSR entry from the received tail
     std::vector<int> ptr(V_ + 1);
     std::vector<unsigned> idx(inc_.n);

@@ -264,6 +264,7 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         real w[GB];
 #pragma unroll
         for (int u = 0; u < GB; u++) {
+            if (b + u * kBlock >= nu) break;  // block-uniform: no load past the run
             const int j = b + u * kBlock + tid;
             const long a = us + (long)min(j, nu - 1);
             d[u] = d2[a];
@@ -282,6 +283,7 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         long ad[GB];
 #pragma unroll
         for (int u = 0; u < GB; u++) {
+            if (b + u * kBlock >= nv) break;  // block-uniform
             // the lane's entries grow by 256: its run only advances (about
             // one run per step on the BASELINE grids), no search
             const int k = min(b + u * kBlock + tid, nv - 1);
@@ -293,6 +295,7 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         }
 #pragma unroll
         for (int u = 0; u < GB; u++) {
+            if (b + u * kBlock >= nv) break;
             d[u] = d2[ad[u]];
             w[u] = wz[ad[u]];
         }
@@ -301,19 +304,40 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
             if (b + u * kBlock + tid < nv) lds[d[u]] = w[u];
     }
     __syncthreads();
+    // the vertex's slots in order; four reads in flight ahead of the adds
     real s = real(0);
-    for (int j = my0; j < my1; j++) s += lds[j];
+    int j = my0;
+    for (; j + 4 <= my1; j += 4) {
+        const real a0 = lds[j], a1 = lds[j + 1], a2 = lds[j + 2], a3 = lds[j + 3];
+        s += a0;
+        s += a1;
+        s += a2;
+        s += a3;
+    }
+    for (; j < my1; j++) s += lds[j];
     return s;
 }
 
-// tile-order keys: (u block, v block) in the high bits, edge position the value
+// tile-order keys: (u block, v block) in the high bits, edge position the
+// value; a partitioned rank (split) puts the edges with a ghost end after
+// all the others (bit 2 vbits) and counts the interior ones
 static __global__ void k_tile_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                                    int vbits, unsigned long long *__restrict__ keys,
-                                   unsigned *__restrict__ vals) {
+                                   unsigned *__restrict__ vals, int V = 0,
+                                   unsigned long long *__restrict__ ninterior = nullptr) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    keys[e] = ((unsigned long long)(Eu[e] / kBlock) << vbits) | (unsigned)(Ev[e] / kBlock);
-    vals[e] = (unsigned)e;
+    bool inner = false;
+    if (e < E) {
+        const int u = Eu[e], v = Ev[e];
+        inner = u < V && v < V;
+        const unsigned long long g = ninterior && !inner ? 1ull << (2 * vbits) : 0ull;
+        keys[e] = g | ((unsigned long long)(u / kBlock) << vbits) | (unsigned)(v / kBlock);
+        vals[e] = (unsigned)e;
+    }
+    if (ninterior) {
+        const unsigned long long m = __ballot(inner);
+        if ((threadIdx.x & (kWave - 1)) == 0 && m) atomicAdd(ninterior, (unsigned long long)__popcll(m));
+    }
 }
 
 // d2[address] = CSR slot of the (edge, side) at that address, relative to the
@@ -338,29 +362,45 @@ static __global__ void k_tile_ustart(long E, int nb, const int *__restrict__ Eu,
     for (int b = lo; b <= hi; b++) ustart[b] = (int)p;
 }
 
-// runs of equal v block in tile order: a run starts at p when p = 0 or the v
-// block changes; cnt[vb] counts the runs of every v block
-static __global__ void k_tile_runs_count(long E, const int *__restrict__ Ev, int *__restrict__ cnt) {
-    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= E) return;
-    const int vb = Ev[p] / kBlock;
-    if (p == 0 || Ev[p - 1] / kBlock != vb) atomicAdd(cnt + vb, 1);
+// Runs of a vertex block's contributions outside its u run, each a maximal
+// stretch of entries i of one source whose vertex lies in that block:
+//   v ends (a = Ev over [0, E), rs = 0): wz[E + i];
+//   u ends of a partitioned rank's boundary edges (a = Eu + Eint, rs = Eint - E):
+//     wz[Eint + i];
+//   received contributions (keys = the halo's recv_keys, rs = E): wz[2E + i];
+// vertices >= V (ghosts) belong to no block.  A run is stored as its start
+// relative to E (tstart = rs + i: the vertex sweep reads wz[E + tstart + k])
+// and its length.
+__device__ __forceinline__ int run_block(long i, const int *__restrict__ a,
+                                         const unsigned long long *__restrict__ keys, int V) {
+    const int x = keys ? (int)(keys[i] >> 32) : a[i];
+    return x < V ? x / kBlock : -1;
+}
+static __global__ void k_tile_runs_count(long n, const int *__restrict__ a,
+                                         const unsigned long long *__restrict__ keys, int V,
+                                         int *__restrict__ cnt) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = run_block(i, a, keys, V);
+    if (b >= 0 && (i == 0 || run_block(i - 1, a, keys, V) != b)) atomicAdd(cnt + b, 1);
 }
 
-// each run at its v block's next slot (the order of a block's runs does not
+// each run at its block's next slot (the order of a block's runs does not
 // matter: every entry carries its slot), with its length
-static __global__ void k_tile_runs_fill(long E, const int *__restrict__ Ev,
-                                        const int *__restrict__ tptr, int *__restrict__ fill,
-                                        int *__restrict__ tstart, int *__restrict__ tlen) {
-    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= E) return;
-    const int vb = Ev[p] / kBlock;
-    if (p != 0 && Ev[p - 1] / kBlock == vb) return;
-    long q = p + 1;
-    while (q < E && Ev[q] / kBlock == vb) q++;
-    const int i = tptr[vb] + atomicAdd(fill + vb, 1);
-    tstart[i] = (int)p;
-    tlen[i] = (int)(q - p);
+static __global__ void k_tile_runs_fill(long n, const int *__restrict__ a,
+                                        const unsigned long long *__restrict__ keys, int V,
+                                        long rs, const int *__restrict__ tptr,
+                                        int *__restrict__ fill, int *__restrict__ tstart,
+                                        int *__restrict__ tlen) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = run_block(i, a, keys, V);
+    if (b < 0 || (i != 0 && run_block(i - 1, a, keys, V) == b)) return;
+    long q = i + 1;
+    while (q < n && run_block(q, a, keys, V) == b) q++;
+    const int j = tptr[b] + atomicAdd(fill + b, 1);
+    tstart[j] = (int)(rs + i);
+    tlen[j] = (int)(q - i);
 }
 
 // tok[b] = 1 when block b's entries fit the LDS list and its runs the table
@@ -1554,13 +1594,14 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     const int *__restrict__ erec, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int nb, int xcd) {
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int b0, int nb, int xcd) {
     if (ctrl && ctrl->halt) return;
     constexpr int SPAN = TlBlocks<real>::v * kBlock;
     __shared__ R2<real> s_xp[SPAN];
     __shared__ R2<real> s_gi[SPAN];
-    const int blk = xcd_block(blockIdx.x, nb, xcd);
+    int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
+    blk += b0;  // edge blocks [b0, b0 + nb) of this launch
     tl_gather<real, UNI>(E, V, Eu, luv, erec + (long)blk * kErec, Ev, xp, Z2, A1, cw, gi, La_d1,
                          la0, wz, rho, blk, s_xp, s_gi);
 }

@@ -202,7 +202,7 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              vtx_label=None if order is None else order[v0:v1])
             queries[r] = {"ghosts": s.query("ghosts")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
-                queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged")})
+                queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks")})
             s.run(itMax)
             results[r] = s.result()
             s.close()
