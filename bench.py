@@ -114,7 +114,9 @@ def cpu_baseline_child(args):
         Eu, Ev = kw["Eu"], kw["Ev"]
     Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
     if name != "headline":  # bounded sample: about 10 s of host work
-        args.cpu_k0, args.cpu_k1 = 1, (2 if name == "c3" else 3)
+        # (C5: 6 iterations apart -- at 2 the difference of two whole calls
+        # was within the setup's run-to-run noise)
+        args.cpu_k0, args.cpu_k1 = {"c3": (1, 2), "c5": (2, 8)}.get(name, (1, 3))
     times = {}
     for k in (args.cpu_k0, args.cpu_k1):
         t = time.perf_counter()
@@ -134,6 +136,8 @@ def cpu_baseline_child(args):
                                 kw["La_l1"], 0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
         times[k] = time.perf_counter() - t
     per_it = (times[args.cpu_k1] - times[args.cpu_k0]) / (args.cpu_k1 - args.cpu_k0)
+    if per_it <= 0:
+        raise RuntimeError("CPU sample too short: T(%d) <= T(%d)" % (args.cpu_k1, args.cpu_k0))
     print(json.dumps({
         "value": Eu.size / per_it / 1e6, "unit": "Medge-updates/s",
         "cores": len(cores) if kind == "reference" else 1, "kind": kind,
