@@ -693,12 +693,12 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
         while (vbits < 31 && (1L << vbits) < (long)nb) vbits++;
         DevBuf<unsigned long long> k(E), ks(E), nint(1);
         DevBuf<unsigned> v(E), perm(E);
-        if (halo_) PFDR_HIP(hipMemsetAsync(nint.p, 0, sizeof(unsigned long long), s));
         k_tile_keys<<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, vbits, k.p, v.p, V_,
-                                                   halo_ ? nint.p : nullptr);
+                                                   halo_ != nullptr);
         PFDR_HIP(hipGetLastError());
         radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, perm.p, (long)E,
                                                     2 * vbits + (halo_ ? 1 : 0), s);
+        if (halo_) k_count_below<<<1, 1, 0, s>>>(E_, ks.p, 1ull << (2 * vbits), nint.p);
         DevBuf<int> nu(E), nv(E);
         DevBuf<unsigned> eo(E);
         emap_.alloc(E);

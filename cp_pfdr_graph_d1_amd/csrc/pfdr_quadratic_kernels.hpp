@@ -264,7 +264,6 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         real w[GB];
 #pragma unroll
         for (int u = 0; u < GB; u++) {
-            if (b + u * kBlock >= nu) break;  // block-uniform: no load past the run
             const int j = b + u * kBlock + tid;
             const long a = us + (long)min(j, nu - 1);
             d[u] = d2[a];
@@ -283,7 +282,6 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         long ad[GB];
 #pragma unroll
         for (int u = 0; u < GB; u++) {
-            if (b + u * kBlock >= nv) break;  // block-uniform
             // the lane's entries grow by 256: its run only advances (about
             // one run per step on the BASELINE grids), no search
             const int k = min(b + u * kBlock + tid, nv - 1);
@@ -295,7 +293,6 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         }
 #pragma unroll
         for (int u = 0; u < GB; u++) {
-            if (b + u * kBlock >= nv) break;
             d[u] = d2[ad[u]];
             w[u] = wz[ad[u]];
         }
@@ -320,24 +317,28 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
 
 // tile-order keys: (u block, v block) in the high bits, edge position the
 // value; a partitioned rank (split) puts the edges with a ghost end after
-// all the others (bit 2 vbits) and counts the interior ones
+// all the others (bit 2 vbits)
 static __global__ void k_tile_keys(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                                    int vbits, unsigned long long *__restrict__ keys,
-                                   unsigned *__restrict__ vals, int V = 0,
-                                   unsigned long long *__restrict__ ninterior = nullptr) {
+                                   unsigned *__restrict__ vals, int V = 0, bool split = false) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    bool inner = false;
-    if (e < E) {
-        const int u = Eu[e], v = Ev[e];
-        inner = u < V && v < V;
-        const unsigned long long g = ninterior && !inner ? 1ull << (2 * vbits) : 0ull;
-        keys[e] = g | ((unsigned long long)(u / kBlock) << vbits) | (unsigned)(v / kBlock);
-        vals[e] = (unsigned)e;
+    if (e >= E) return;
+    const int u = Eu[e], v = Ev[e];
+    const unsigned long long g = split && (u >= V || v >= V) ? 1ull << (2 * vbits) : 0ull;
+    keys[e] = g | ((unsigned long long)(u / kBlock) << vbits) | (unsigned)(v / kBlock);
+    vals[e] = (unsigned)e;
+}
+
+// *out = the number of sorted keys below `bound` (one lane, binary search)
+static __global__ void k_count_below(long n, const unsigned long long *__restrict__ keys,
+                                     unsigned long long bound, unsigned long long *out) {
+    long lo = 0, hi = n;
+    while (lo < hi) {
+        const long mid = (lo + hi) >> 1;
+        if (keys[mid] < bound) lo = mid + 1;
+        else hi = mid;
     }
-    if (ninterior) {
-        const unsigned long long m = __ballot(inner);
-        if ((threadIdx.x & (kWave - 1)) == 0 && m) atomicAdd(ninterior, (unsigned long long)__popcll(m));
-    }
+    *out = (unsigned long long)lo;
 }
 
 // d2[address] = CSR slot of the (edge, side) at that address, relative to the
