@@ -252,6 +252,11 @@ class QuadSession final : public SessionBase {
     hipEvent_t ev_[4] = {};  // xp ready, pulled, boundary W*Z ready, pushed
     long elo_ = 0, ehi_ = 0;
     long Eint_ = 0;  // tiled partitioned rank: edges [0, Eint_) have no ghost end
+    long zs_ = 0;    // Z layout: 0 half-edge pairs, E side-major (tiled sessions)
+    // Z-direct: a tiled single-GPU session with one edge weight and no A1
+    // (before any reconditioning) skips the W * Z stores of the edge sweep;
+    // the vertex sweep reads Z and forms each term with its own weight
+    bool zdirect() const { return tiled_ && !halo_ && !la_it() && !A1_.p; }
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
@@ -506,7 +511,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     PFDR_HIP(hipMemsetAsync(ubad.p, 0, sizeof(int), s));
     if (E_) k_uniform_check<real><<<grid_for(E), kBlock, 0, s>>>(E_, La_d1_.p, ubad.p);
     // Z = X at both ends, first preconditioning, first forward step
-    if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p);
+    zs_ = tiled_ ? E_ : 0;
+    if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, zs_);
     precondition(true);
     if (mode_ == A_IDENT || mode_ == A_DIAG) {
         grad_.alloc(V);
@@ -1071,7 +1077,7 @@ void QuadSession<real>::precondition(bool init) {
         k_d1_weights<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, La_d1_.p, ctrl_.p, init ? 1 : 0,
                                                    condMin_, xp_.p, first_recond ? nullptr : A1_.p,
                                                    cw_, invAux_.p, A1_.p, wz_.p, Ga_.p, grad_.p,
-                                                   Z2_.p);
+                                                   Z2_.p, zs_);
         PFDR_HIP(hipGetLastError());
     }
     if (halo_) halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), s);
@@ -1084,7 +1090,7 @@ void QuadSession<real>::precondition(bool init) {
     pull(invAux_.p, sizeof(real));
     if (E_ && !init) {
         k_recond_edge<real><<<nbe_, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, A1_.p, invAux_.p, Ga_.p,
-                                                    xp_.p, grad_.p, Z2_.p);
+                                                    xp_.p, grad_.p, Z2_.p, zs_);
     }
     k_gi_pack<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, Ga_.p, invAux_.p, gi_.p);
     PFDR_HIP(hipGetLastError());
@@ -1150,7 +1156,8 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
         // sweeps its interior blocks and the rest in two launches)
         auto k = (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true> : k_edge_sweep_tl<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_,
-                               gi_.p, la_it(), la0_, wz_.p, rho_, c, (int)(ebeg / EB), nb, xm);
+                               gi_.p, la_it(), la0_, zdirect() ? nullptr : wz_.p, rho_, c,
+                               (int)(ebeg / EB), nb, xm);
         return;
     }
     if (tiled_) throw std::logic_error("tiled edge sweep: range not on edge blocks");
@@ -1193,6 +1200,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     if (tiled_) {
         a.d2 = d2_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
+        a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
     }
     a.terms = seqdif_ ? terms_.p : nullptr;
     a.tmap = (seqdif_ && reordered_) ? order_.p : nullptr;
@@ -1221,7 +1229,10 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
             a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
         return;
     }
-    k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
+    if (zdirect())
+        k_vertex_sweep<real, 8, true><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
+    else
+        k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }
 
 template <typename real>

@@ -75,12 +75,15 @@ __device__ __forceinline__ bool gated(const Ctrl<real> *c, int gate) {
 // degrees, coalesced index reads, GB index loads then GB value gathers in
 // flight per lane — into LDS chunks; then each lane adds its own vertex's
 // entries in CSR order, i.e. in the reference's order (e, side).
-template <typename real, int CAP, int GB = 16>
+// ZD: the list holds the edge variables Z and each term is w * z, w the
+// vertex's own splitting weight (the contribution the edge sweep did not
+// form, see k_edge_sweep_tl), computed as the edge sweep would
+template <typename real, int CAP, int GB = 16, bool ZD = false>
 __device__ __forceinline__ real gather_sum(int V, int v0,
                                            const int *__restrict__ ptr,
                                            const unsigned *__restrict__ idx,
                                            const real *__restrict__ wz,
-                                           real *lds) {
+                                           real *lds, real wv = real(1)) {
     static_assert(CAP % (kBlock * GB) == 0, "chunk must be a whole batch");
     const int tid = threadIdx.x;
     const int v = v0 + tid;
@@ -112,7 +115,7 @@ __device__ __forceinline__ real gather_sum(int V, int v0,
         }
         __syncthreads();
         const long a = max(my0, c0), e = min(my1, c0 + (long)n);
-        for (long j = a; j < e; j++) s += lds[j - c0];
+        for (long j = a; j < e; j++) s += ZD ? wv * lds[j - c0] : lds[j - c0];
         __syncthreads();
     }
     return s;
@@ -222,7 +225,7 @@ __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__res
 constexpr int kTileCap = 4096;  // staged entries per vertex block (LDS: GatherCap)
 constexpr int kTileRuns = 128;  // v-end runs per vertex block
 
-template <typename real, int GB>
+template <typename real, int GB, bool ZD = false>
 __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const int *__restrict__ ptr,
                                          const unsigned short *__restrict__ d2,
@@ -230,7 +233,8 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const int *__restrict__ tptr,
                                          const int *__restrict__ tstart,
                                          const int *__restrict__ tlen,
-                                         const real *__restrict__ wz, real *lds, int *runs) {
+                                         const real *__restrict__ wz, real *lds, int *runs,
+                                         real wv = real(1)) {
     const int tid = threadIdx.x;
     const int v0 = blk * kBlock, vend = min(v0 + kBlock, V);
     const int p0 = ptr[v0];
@@ -306,12 +310,12 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
     int j = my0;
     for (; j + 4 <= my1; j += 4) {
         const real a0 = lds[j], a1 = lds[j + 1], a2 = lds[j + 2], a3 = lds[j + 3];
-        s += a0;
-        s += a1;
-        s += a2;
-        s += a3;
+        s += ZD ? wv * a0 : a0;
+        s += ZD ? wv * a1 : a1;
+        s += ZD ? wv * a2 : a2;
+        s += ZD ? wv * a3 : a3;
     }
-    for (; j < my1; j++) s += lds[j];
+    for (; j < my1; j++) s += ZD ? wv * lds[j] : lds[j];
     return s;
 }
 
@@ -520,16 +524,22 @@ __global__ void k_scatter(long n, const T *__restrict__ src, const int *__restri
     if (i < n) dst[map[i]] = src[i];
 }
 
-// Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324); half-edge layout Z2[2e + side]
+// edge variable (e, side): half-edge layout Z2[2e + side] (zs = 0), or
+// side-major Z[side * zs + e] (zs = E: tile-ordered sessions)
+__device__ __forceinline__ long zat(long e, int side, long zs) {
+    return zs ? side * zs + e : 2 * e + side;
+}
+
+// Z_u = X[Eu], Z_v = X[Ev]   (ref :320-324)
 template <typename real>
 __global__ void k_z_init(long E, const int *__restrict__ Eu,
                          const int *__restrict__ Ev,
                          const R2<real> *__restrict__ xp,
-                         real *__restrict__ Z2) {
+                         real *__restrict__ Z2, long zs) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
-    Z2[2 * e] = xp[Eu[e]].x;
-    Z2[2 * e + 1] = xp[Ev[e]].x;
+    Z2[zat(e, 0, zs)] = xp[Eu[e]].x;
+    Z2[zat(e, 1, zs)] = xp[Ev[e]].x;
 }
 
 // diagonal of A^t A for the identity / diagonal / A^tA modes (ref :101-122)
@@ -1010,7 +1020,7 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
                              real *A1, real *__restrict__ wz,
                              const real *__restrict__ Ga,
                              const real *__restrict__ grad,
-                             real *__restrict__ Z2) {
+                             real *__restrict__ Z2, long zs) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const real c = ctrl->c;
@@ -1023,8 +1033,9 @@ __global__ void k_d1_weights(long E, const int *__restrict__ Eu,
         const real gu = Ga[u], gv = Ga[v];
         const real a0 = edge_a(e, A1old, La_d1, cw);
         const real wu = a0 * invAux[u], wv = a0 * invAux[v];
-        Z2[2 * e] = (wu / gu) * (xu - gu * grad[u] - Z2[2 * e]);
-        Z2[2 * e + 1] = (wv / gv) * (xv - gv * grad[v] - Z2[2 * e + 1]);
+        const long iu = zat(e, 0, zs), iv = zat(e, 1, zs);
+        Z2[iu] = (wu / gu) * (xu - gu * grad[u] - Z2[iu]);
+        Z2[iv] = (wv / gv) * (xv - gv * grad[v] - Z2[iv]);
         real a = xu, b = xv, d = a - b;
         if (a < real(0)) a = -a;
         if (b < real(0)) b = -b;
@@ -1088,15 +1099,16 @@ template <typename real>
 __global__ void k_recond_edge(long E, const int *__restrict__ Eu, const int *__restrict__ Ev,
                               const real *__restrict__ A1, const real *__restrict__ invAux,
                               const real *__restrict__ Ga, const R2<real> *__restrict__ xp,
-                              const real *__restrict__ grad, real *__restrict__ Z2) {
+                              const real *__restrict__ grad, real *__restrict__ Z2, long zs) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const int u = Eu[e], v = Ev[e];
     const real wu = A1[e] * invAux[u];
     const real wv = A1[e] * invAux[v];
     const real gu = Ga[u], gv = Ga[v];
-    Z2[2 * e] = xp[u].x - gu * (grad[u] + Z2[2 * e] / wu);
-    Z2[2 * e + 1] = xp[v].x - gv * (grad[v] + Z2[2 * e + 1] / wv);
+    const long iu = zat(e, 0, zs), iv = zat(e, 1, zs);
+    Z2[iu] = xp[u].x - gu * (grad[u] + Z2[iu] / wu);
+    Z2[iv] = xp[v].x - gv * (grad[v] + Z2[iv] / wv);
 }
 
 // (Ga, invAux) pairs of owned and ghost vertices: one 8/16-byte gather per
@@ -1462,9 +1474,14 @@ __device__ __forceinline__ void tl_gather(
     Pk<real, 2 * EPT> z{};
     Pk<real, EPT> la{}, a{};
     R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
-    if (full) {
+    if (full) {  // Z side-major (tiled sessions): zu at e, zv at E + e
         ib = ldv<unsigned short, EPT>(luv + e0);
-        z = ldv<real, 2 * EPT>(Z2 + 2 * e0);
+        const Pk<real, EPT> zu = ldv<real, EPT>(Z2 + e0), zv = ldv<real, EPT>(Z2 + E + e0);
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            z.v[2 * j] = zu.v[j];
+            z.v[2 * j + 1] = zv.v[j];
+        }
         if (!UNI) {
             la = la_vec<real, EPT>(e0, La_d1, la0);
             if (A1) a = ldv<real, EPT>(A1 + e0);
@@ -1570,20 +1587,31 @@ __device__ __forceinline__ void tl_gather(
         for (int j = 0; j < EPT; j++)
             edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
                             z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
-        stv<real, 2 * EPT>(Z2 + 2 * e0, z);
-        stv<real, EPT>(wz + e0, ou);
-        stv<real, EPT>(wz + E + e0, ov);
+        Pk<real, EPT> zu, zv;
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            zu.v[j] = z.v[2 * j];
+            zv.v[j] = z.v[2 * j + 1];
+        }
+        stv<real, EPT>(Z2 + e0, zu);
+        stv<real, EPT>(Z2 + E + e0, zv);
+        if (wz) {  // block-uniform; null: the vertex sweep forms W * Z itself
+            stv<real, EPT>(wz + e0, ou);
+            stv<real, EPT>(wz + E + e0, ov);
+        }
     } else {
         for (long e = e0; e < E; e++) {
             const int u = Eu[e], v = Ev[e];
-            real zu = Z2[2 * e], zv = Z2[2 * e + 1], ou, ov;
+            real zu = Z2[e], zv = Z2[E + e], ou, ov;
             const real l = la_at(e, La_d1, la0);
             edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou, ov,
                             rho);
-            Z2[2 * e] = zu;
-            Z2[2 * e + 1] = zv;
-            wz[e] = ou;
-            wz[E + e] = ov;
+            Z2[e] = zu;
+            Z2[E + e] = zv;
+            if (wz) {
+                wz[e] = ou;
+                wz[E + e] = ov;
+            }
         }
     }
 }
@@ -1835,6 +1863,11 @@ struct VArgs {
     long E;
     const unsigned short *d2;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
+    // Z-direct (tiled single-GPU sessions with one edge weight, no A1): the
+    // lists hold Z (side-major, zs) and each term is (a0 * invAux[v]) * z
+    const real *zs;
+    const real *invAux;
+    real a0;
     // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
     // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
     // caller's order (tmap[v] for a relabelled session, else v), summed
@@ -1925,21 +1958,24 @@ __device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, r
 }
 
 // one vertex block `blk` (all 256 lanes of the calling block take part)
-template <typename real, int GB>
+template <typename real, int GB, bool ZD = false>
 __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real *lds,
                                              real (*red)[kBlock / kWave], int *scan,
                                              int halt = 0) {
     const int v0 = blk * kBlock;
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
+    // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
+    const real wv = ZD && v < a.V ? a.a0 * a.invAux[v] : real(1);
     real x;
     if (a.d2 && a.tok[blk])  // block-uniform
-        x = tile_sum<real, GB>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart, a.tlen,
-                               a.wz, lds, scan);
-    else if (a.blkok && a.blkok[blk])
+        x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart,
+                                   a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
+    else if (!ZD && a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
     else
-        x = gather_sum<real, GatherCap<real>::v, GB>(a.V, v0, a.ptr, a.idx, a.wz, lds);
+        x = gather_sum<real, GatherCap<real>::v, GB, ZD>(a.V, v0, a.ptr, a.idx,
+                                                         ZD ? a.zs : a.wz, lds, wv);
     if (halt) return;  // block-uniform (a.late)
     real num, den;
     vertex_finish(a, v, x, o, num, den);
@@ -1953,7 +1989,7 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     }
 }
 
-template <typename real, int GB>
+template <typename real, int GB, bool ZD = false>
 __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs<real> a) {
     int halt = 0;
     if (a.ctrl) {
@@ -1969,7 +2005,7 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;
-    vertex_block<real, GB>(a, a.bbeg + lb, lds, red, scan, halt);
+    vertex_block<real, GB, ZD>(a, a.bbeg + lb, lds, red, scan, halt);
 }
 
 // Vertex sweep of a small graph (the fused-decision range) whose edge sweep
