@@ -256,7 +256,11 @@ class QuadSession final : public SessionBase {
     // Z-direct: a tiled single-GPU session with one edge weight and no A1
     // (before any reconditioning) skips the W * Z stores of the edge sweep;
     // the vertex sweep reads Z and forms each term with its own weight
-    bool zdirect() const { return tiled_ && !halo_ && !la_it() && !A1_.p; }
+    // (a partitioned session only when every rank qualifies with the same
+    // weight, zd_ranks_: the ranks then push Z, and each owner forms the
+    // received terms with its own weight like the local ones)
+    bool zd_ranks_ = false;
+    bool zdirect() const { return tiled_ && !A1_.p && (halo_ ? zd_ranks_ : !la_it()); }
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
@@ -455,7 +459,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     }  // X0 goes back to the device cache (reused once the stream is idle)
     // edge state and per-vertex metric
     const size_t En = E ? E : 1;
-    Z2_.alloc(2 * En);
+    // (tiled partitioned ranks: Z's received tail after the 2E local entries,
+    // for the Z-direct iteration)
+    Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0));
     gi_.alloc(Vg);
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
     if (flavour_ == 0 && p->La_l1) Th_l1_.alloc(V);
@@ -533,6 +539,23 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         PFDR_HIP(hipMemcpy(&la0_, La_d1_.p, sizeof(real), hipMemcpyDeviceToHost));
         la_uniform_ = bad == 0;
         la_uniform = la_uniform_ ? 1 : 0;
+    }
+    if (halo_) {  // Z-direct on every rank or on none (see zdirect)
+        Transport &tr = *halo_->tr;
+        DevBuf<real> l0(1);
+        DevBuf<int64_t> nbad(1);
+        PFDR_HIP(hipMemcpyAsync(l0.p, &la0_, sizeof(real), hipMemcpyHostToDevice, s));
+        tr.broadcast(l0.p, sizeof(real), 0, s);
+        real la0r0 = real(0);
+        PFDR_HIP(hipMemcpyAsync(&la0r0, l0.p, sizeof(real), hipMemcpyDeviceToHost, s));
+        tr.wait(s);
+        const int64_t mine = (tiled_ && la_uniform_ && la0_ == la0r0) ? 0 : 1;
+        PFDR_HIP(hipMemcpyAsync(nbad.p, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
+        tr.allreduce_sum(nbad.p, 1, 2, s);
+        int64_t all = 1;
+        PFDR_HIP(hipMemcpyAsync(&all, nbad.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        tr.wait(s);
+        zd_ranks_ = all == 0;
     }
     pins_.release();
     stopped_ = (itMax_ <= 0);
@@ -1277,7 +1300,8 @@ void QuadSession<real>::body(int i, int n) {
         PFDR_HIP(hipStreamWaitEvent(comm_, ev_[2], 0));
         {
             ProfScope ps(prof, "halo_push", comm_);
-            halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), comm_);
+            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
+            halo_->push(src, src + 2 * E_, sizeof(real), comm_);
         }
         PFDR_HIP(hipEventRecord(ev_[3], comm_));
         vertex_sweep(blo_, bhi_, c, "vertex_sweep");
@@ -1291,7 +1315,8 @@ void QuadSession<real>::body(int i, int n) {
         edge_sweep(0, E_, c, "edge_sweep");
         if (halo_) {
             ProfScope ps(prof, "halo_push", s);
-            halo_->push(wz_.p, wz_.p + 2 * E_, sizeof(real), s);
+            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
+            halo_->push(src, src + 2 * E_, sizeof(real), s);
         }
         vertex_sweep(0, nbv_, c, "vertex_sweep");
     }

@@ -1431,14 +1431,16 @@ __global__ __launch_bounds__(256) void k_edge_sweep(
 // setup, scalar loads): the first u block, how many it spans and where in
 // the block each further u block starts, and the runs of equal v block
 // (start, v block base) -- at most kEbRuns; positions are relative to the
-// block's first edge, so every lookup is a 32-bit compare against a scalar
-// in a loop as long as the block's own run count.  Every edge names both
-// ends by one byte each (luv: u mod 256 | v mod 256 << 8), so neither Eu nor
-// Ev is streamed: the u ends come from the staged u blocks' (X, P) and
-// (Ga, invAux) in LDS, the v ends are gathered (a run's gathers share their
-// lines) at v block base + byte.  A block with more runs reads Ev, one
-// spanning more than TlBlocks u blocks reads Eu.
-// u blocks staged: 16 KB of LDS either way (f64 blocks cover 512 edges)
+// block's first edge, so every lookup is a 32-bit compare against scalars
+// in groups of four runs.  Every edge names both ends by one byte each
+// (luv: u mod 256 | v mod 256 << 8), so neither Eu nor Ev is streamed: the
+// u ends come from the block's staged u range of (X, P) and (Ga, invAux) in
+// LDS, the v ends are gathered (a run's gathers share their lines) at v
+// block base + byte.  A block with more runs reads Ev, one spanning more
+// than TlBlocks u blocks reads Eu.  Z is side-major (Z[e], Z[E + e]); wz
+// null (Z-direct, see tile_sum's ZD) leaves the W * Z products to the
+// vertex sweep.
+// u range staged: at most 16 KB of LDS (f64 blocks cover 512 edges)
 template <typename real> struct TlBlocks { static constexpr int v = 16384 / (2 * 256 * sizeof(R2<real>)) ; };
 constexpr int kEbRuns = 20;  // v-block runs in an edge block's record
 constexpr int kErecU = 4;    // rec[4]: staged span; rec[4 + q]: start of u block ub0 + q
