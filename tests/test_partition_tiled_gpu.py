@@ -13,7 +13,12 @@ on a one-rank RCCL communicator (hipGraph-replayed chunks)."""
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [
+    pytest.mark.gpu,
+    # kTiledPartitions (csrc/pfdr_quadratic.hip) is off: a full-size 2-rank
+    # split differed intermittently; these cases passed with it on
+    pytest.mark.skip(reason="tiled partitioned ranks disabled pending a full-size race"),
+]
 
 
 def _single(args, kw):
