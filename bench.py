@@ -359,6 +359,9 @@ def main():
             row["pmc_bytes"] = int(t)
             row["pmc_over_algorithmic"] = round(t / alg_b, 3)
             row["pmc_GBps"] = round(t / (ms * 1e-3) / 1e9, 1)
+            # the bytes the kernel moves: below SURVEY's figure where the layout
+            # needs less (Z-direct: no W*Z stores), so frac can pass 1 and this not
+            row["pmc_frac"] = round(row["pmc_GBps"] / HBM_PEAK_GBS, 4)
         kernels[fam] = row
     dom = kernels.get(wl.dominant, {})
     it_bytes = wl.iteration_bytes(V, E)
@@ -400,6 +403,7 @@ def main():
             "unit": "GB/s",
             "frac": dom.get("frac"),
             "traffic": dom.get("pmc_bytes"),
+            "traffic_frac": dom.get("pmc_frac"),
             **({"traffic_note": pmc_note} if pmc_note else {}),
             "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes"),
             "timed_launches": "every %d-th launch of %s%s" % (period, ", ".join(

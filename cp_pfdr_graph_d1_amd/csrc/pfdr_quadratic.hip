@@ -113,7 +113,11 @@ __global__ void k_remap_push(long n, long E, const unsigned *__restrict__ inv,
 // of the 10M-vertex headline differed from the single GPU in about one run
 // of three (rank 1's top planes, nondeterministic) and the root cause is
 // not found yet; partitioned ranks keep the u-sorted layout until it is.
-constexpr bool kTiledPartitions = false;
+// (-DPFDR_TILED_PARTITIONS=1 builds it on, for tools/variant.sh diagnostics)
+#ifndef PFDR_TILED_PARTITIONS
+#define PFDR_TILED_PARTITIONS 0
+#endif
+constexpr bool kTiledPartitions = PFDR_TILED_PARTITIONS != 0;
 
 template <typename real>
 class QuadSession final : public SessionBase {
@@ -580,7 +584,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     acc(d2_.n * 2 + luv_.n * 2 +
         (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
     if (halo_) {
+#ifndef PFDR_NO_OVERLAP  // diagnostics (tools/variant.sh): exchanges in line on the stream
         plan_overlap();
+#endif
         // RCCL partitions replay captured chunks too (pull, sweeps, push and
         // the all-reduces of a chunk of iterations in one hipGraph launch:
         // the host's ~30 API calls per iteration otherwise approach a rank's
