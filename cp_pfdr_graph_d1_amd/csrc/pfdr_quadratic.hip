@@ -560,7 +560,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         real la0r0 = real(0);
         PFDR_HIP(hipMemcpyAsync(&la0r0, l0.p, sizeof(real), hipMemcpyDeviceToHost, s));
         tr.wait(s);
+#ifdef PFDR_NO_ZD  // diagnostics (tools/variant.sh): partitioned ranks push W * Z
+        const int64_t mine = 1;
+#else
         const int64_t mine = (tiled_ && la_uniform_ && la0_ == la0r0) ? 0 : 1;
+#endif
         PFDR_HIP(hipMemcpyAsync(nbad.p, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
         tr.allreduce_sum(nbad.p, 1, 2, s);
         int64_t all = 1;
