@@ -29,6 +29,7 @@ static void copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStre
 template <typename real>
 static int dtype_of() { return sizeof(real) == 4 ? PFDR_F32 : PFDR_F64; }
 
+
 // d <- d[map] (map[i] = source index of element i)
 template <typename T>
 static void permute(DevBuf<T> &d, const int *map, size_t n, hipStream_t s) {
@@ -108,16 +109,6 @@ __global__ void k_remap_push(long n, long E, const unsigned *__restrict__ inv,
     addr[i] = side * (unsigned)E + inv[a - side * (unsigned)E];
 }
 
-// Tile order on partitioned ranks (round 3): built and bit-exact
-// in every loopback test up to 819,200 vertices, but a 2-rank loopback split
-// of the 10M-vertex headline differed from the single GPU in about one run
-// of three (rank 1's top planes, nondeterministic) and the root cause is
-// not found yet; partitioned ranks keep the u-sorted layout until it is.
-// (-DPFDR_TILED_PARTITIONS=1 builds it on, for tools/variant.sh diagnostics)
-#ifndef PFDR_TILED_PARTITIONS
-#define PFDR_TILED_PARTITIONS 0
-#endif
-constexpr bool kTiledPartitions = PFDR_TILED_PARTITIONS != 0;
 
 template <typename real>
 class QuadSession final : public SessionBase {
@@ -174,6 +165,13 @@ class QuadSession final : public SessionBase {
     long tstride_ = 0;
     DevBuf<real> terms_;
     DevBuf<char> dws_;
+    // partitioned sessions: the terms of the ranks in rank order are summed
+    // rank to rank (ChainSum); a relabelled partition (lab_) writes its terms
+    // at the caller's labels of a V_global-long array, all-reduced (one
+    // writer per position) into tall_ and summed whole on every rank
+    ChainSum<real> chain_;
+    DevBuf<real> tall_;
+    void seq_evolution();
     static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
@@ -365,9 +363,6 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     evo_ = p->evolution;
     if (evo_ < PFDR_EVOLUTION_AUTO || evo_ > PFDR_EVOLUTION_TREE)
         throw std::runtime_error("evolution must be PFDR_EVOLUTION_AUTO, _SEQUENTIAL or _TREE");
-    if (evo_ == PFDR_EVOLUTION_SEQUENTIAL && (p->nranks > 1 || p->comm))
-        throw std::runtime_error("PFDR_EVOLUTION_SEQUENTIAL needs a single GPU (a partitioned "
-                                 "session sums the evolution statistic in a tree)");
     const bool want_seq = track_ && evo_ == PFDR_EVOLUTION_SEQUENTIAL;
     Ldiag_ = (p->Ltype == PFDR_LIPSCHITZ_DIAG) && p->L;
     us_ = E_ >= 4L * V_ || E_ < (1L << 22);
@@ -419,6 +414,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         }
         lab_.alloc(V_);
         PFDR_HIP(hipMemcpy(lab_.p, h32.data(), sizeof(int) * V_, hipMemcpyHostToDevice));
+        check_permutation(lab_.p, V_, Vglob_, *halo_->tr, s);
     }
     if (mode_ == A_ATA && -(long)N_ != Vglob_)
         throw std::runtime_error("N < 0 requires A = A^tA (columns of the owned vertices, "
@@ -560,11 +556,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         real la0r0 = real(0);
         PFDR_HIP(hipMemcpyAsync(&la0r0, l0.p, sizeof(real), hipMemcpyDeviceToHost, s));
         tr.wait(s);
-#ifdef PFDR_NO_ZD  // diagnostics (tools/variant.sh): partitioned ranks push W * Z
-        const int64_t mine = 1;
-#else
         const int64_t mine = (tiled_ && la_uniform_ && la0_ == la0r0) ? 0 : 1;
-#endif
         PFDR_HIP(hipMemcpyAsync(nbad.p, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
         tr.allreduce_sum(nbad.p, 1, 2, s);
         int64_t all = 1;
@@ -588,9 +580,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     acc(d2_.n * 2 + luv_.n * 2 +
         (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
     if (halo_) {
-#ifndef PFDR_NO_OVERLAP  // diagnostics (tools/variant.sh): exchanges in line on the stream
         plan_overlap();
-#endif
         // RCCL partitions replay captured chunks too (pull, sweeps, push and
         // the all-reduces of a chunk of iterations in one hipGraph launch:
         // the host's ~30 API calls per iteration otherwise approach a rank's
@@ -605,17 +595,27 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         fused = fuse_ ? 1 : 0;
         if (fuse_) plan_pad();
     }
-    // sequential evolution statistic: the plain multi-launch loop on one GPU
-    seqdif_ = track_ && !halo_ && !tiny_ && !fuse_ &&
-              (want_seq || (evo_ == PFDR_EVOLUTION_AUTO && (long)V_ >= kSeqDifMin));
+    // sequential evolution statistic: the plain multi-launch loop on one GPU;
+    // a partition sums in the caller's order across the ranks (seq_evolution)
+    seqdif_ = track_ && !tiny_ && !fuse_ &&
+              (want_seq || (evo_ == PFDR_EVOLUTION_AUTO && Vglob_ >= kSeqDifMin));
     if (seqdif_) {
-        tstride_ = ((long)V_ + 3) / 4 * 4;  // 16-byte aligned second array
+        const long nt = halo_ && lab_.p ? Vglob_ : (long)V_;  // terms per sum
+        tstride_ = (nt + 3) / 4 * 4;  // 16-byte aligned second array
         terms_.alloc(2 * (size_t)tstride_);
-        dws_.alloc(mono_ws_bytes<real>(V_, 2));
+        if (!halo_ || lab_.p) dws_.alloc(mono_ws_bytes<real>(nt, 2));
+        if (halo_ && lab_.p) {
+            if (2 * tstride_ > 0x7fffffffL) throw std::runtime_error("V_global too large");
+            PFDR_HIP(hipMemsetAsync(terms_.p, 0, sizeof(real) * terms_.n, s));
+            tall_.alloc(terms_.n);
+        } else if (halo_) {
+            chain_.init(V_, 2, *halo_->tr);
+        }
         seqdif = 1;
     }
     if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
     acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
+    acc(tall_.n * sizeof(real) + chain_.ws.n + ampg_.n * sizeof(real));
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
     // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
     // which a small solve timed to tolerance would otherwise pay in its loop)
@@ -732,8 +732,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     // original edge ids (summation order).  A partitioned rank puts the
     // edges with a ghost end after the others (the interior ones overlap
     // the halo pull) and renumbers its push addresses.
-    tiled_ = !tiny_ && E_ > 0 && (long)V_ > (long)kFuseBlocks * kBlock &&
-             (!halo_ || kTiledPartitions);
+    tiled_ = !tiny_ && E_ > 0 && (long)V_ > (long)kFuseBlocks * kBlock;
     if (tiled_) {
         const int nb = grid_for(Vg_);
         int vbits = 1;
@@ -800,7 +799,7 @@ void QuadSession<real>::build_tiles() {
         const int neb = (int)((E_ + EB - 1) / EB);
         erec_.alloc((size_t)neb * kErec);
         k_tile_erec<<<(neb + kBlock / kWave - 1) / (kBlock / kWave), kBlock, 0, s>>>(
-            E_, EB, neb, Eu_.p, Ev_.p, erec_.p);
+            E_, EB, 0, neb, Eu_.p, Ev_.p, erec_.p);
         PFDR_HIP(hipGetLastError());
     }
     ustart_.alloc((size_t)nb + 1);
@@ -1244,7 +1243,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
     }
     a.terms = seqdif_ ? terms_.p : nullptr;
-    a.tmap = (seqdif_ && reordered_) ? order_.p : nullptr;
+    a.tmap = !seqdif_ ? nullptr : reordered_ ? order_.p : halo_ ? lab_.p : nullptr;
     a.tstride = tstride_;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
     a.bsplit = a.nb; a.bjump = 0;
@@ -1341,8 +1340,7 @@ void QuadSession<real>::body(int i, int n) {
     if (seqdif_) {
         // the reference's two sequential sums (ref :518-526), then its decision
         ProfScope ps(prof, "seq_evolution", s);
-        mono_sum<real>(V_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
-                       &ctrl_.p->halt);
+        seq_evolution();
         k_decide<real><<<1, 64, 0, s>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     } else if (gated && !halo_) {
         k_reduce_decide<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, ctrl_.p,
@@ -1357,6 +1355,26 @@ void QuadSession<real>::body(int i, int n) {
     PFDR_HIP(hipGetLastError());
     if (mode_ == A_DIRECT || mode_ == A_ATA) forward_dense(gated ? GATE_ACTIVE : GATE_NONE);
     if (rec_obj_) objective();
+}
+
+// red_[0..2) = the sums of (X_ - X)^2 and X^2 over every vertex in the
+// caller's order, rounded as the reference's one-thread loop
+template <typename real>
+void QuadSession<real>::seq_evolution() {
+    hipStream_t s = stream;
+    const int *halt = &ctrl_.p->halt;
+    if (!halo_) {
+        mono_sum<real>(V_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
+                       halt);
+    } else if (!lab_.p) {
+        chain_.run(*halo_->tr, terms_.p, tstride_, red_.p, halt, s);
+    } else {
+        PFDR_HIP(hipMemcpyAsync(tall_.p, terms_.p, sizeof(real) * terms_.n,
+                                hipMemcpyDeviceToDevice, s));
+        halo_->tr->allreduce_sum(tall_.p, (int)tall_.n, dtype_of<real>(), s);
+        mono_sum<real>(Vglob_, tall_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2,
+                       tstride_, halt);
+    }
 }
 
 // interior edge range and vertex-block range of a partitioned session (the
@@ -1618,4 +1636,49 @@ extern "C" int pfdr_quadratic_d1_bounds_f64(int V, int E, int N, double *X,
     return quadratic_host<double>("pfdr_quadratic_d1_bounds_f64", PFDR_KIND_BOUNDS, V, E, N, X, Y,
                                   A, Eu, Ev, La_d1, nullptr, 0, min, max, Ltype, L, rho, condMin,
                                   difRcd, difTol, itMax, it, Obj, Dif, verbose);
+}
+
+// Test hook (pfdr_mi355x.h, "debug"): the edge-block records of
+// k_edge_sweep_tl for host arrays; only blocks [blk_begin, blk_begin +
+// blk_count) are built, every other record keeps the caller's contents.
+extern "C" int pfdr_debug_tile_erec(int64_t E, int dtype, const int *Eu, const int *Ev,
+                                    int blk_begin, int blk_count, int *rec, int64_t rec_ints) {
+    using namespace pfdr;
+    const char *fn = "pfdr_debug_tile_erec";
+    try {
+        if (E <= 0 || !Eu || !Ev || !rec || (dtype != PFDR_F32 && dtype != PFDR_F64))
+            return report_error(fn, "invalid argument");
+        const int EB = kBlock * (dtype == PFDR_F32 ? Vec<float>::kPer16B : Vec<double>::kPer16B);
+        const long neb = (E + EB - 1) / EB;
+        if (rec_ints != neb * kErec || blk_begin < 0 || blk_count < 0 || blk_begin + blk_count > neb)
+            return report_error(fn, "record array or block range does not match E");
+        hipStream_t s = lib_stream();
+        DevBuf<int> dEu(E), dEv(E), dr(rec_ints);
+        PFDR_HIP(hipMemcpyAsync(dEu.p, Eu, E * 4, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemcpyAsync(dEv.p, Ev, E * 4, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemcpyAsync(dr.p, rec, rec_ints * 4, hipMemcpyHostToDevice, s));
+        if (blk_count) {
+            const int wpb = kBlock / kWave;
+            k_tile_erec<<<(blk_count + wpb - 1) / wpb, kBlock, 0, s>>>(E, EB, blk_begin,
+                                                                     blk_begin + blk_count, dEu.p,
+                                                                     dEv.p, dr.p);
+            PFDR_HIP(hipGetLastError());
+        }
+        PFDR_HIP(hipMemcpyAsync(rec, dr.p, rec_ints * 4, hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    } catch (const HipError &h) {
+        return report_error(fn, h);
+    } catch (const std::exception &ex) {
+        return report_error(fn, ex.what());
+    }
+    return PFDR_OK;
+}
+
+// the record layout the hook writes: ints per record, v runs per record,
+// nub of an unstaged (u-block drop) block
+extern "C" int pfdr_debug_erec_layout(int *ints, int *runs, int *nostage) {
+    if (ints) *ints = pfdr::kErec;
+    if (runs) *runs = pfdr::kEbRuns;
+    if (nostage) *nostage = pfdr::kErecNoStage;
+    return PFDR_OK;
 }

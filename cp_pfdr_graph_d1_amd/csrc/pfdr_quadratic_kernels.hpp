@@ -1644,19 +1644,33 @@ static __global__ void k_tile_luv(long E, const int *__restrict__ Eu, const int 
     if (p < E) luv[p] = (unsigned short)((Eu[p] % kBlock) | ((Ev[p] % kBlock) << 8));
 }
 
+// nub of a block whose u blocks are not nondecreasing: never staged
+constexpr int kErecNoStage = 1 << 30;
+
 // the record of every edge block of k_edge_sweep_tl (EB edges; one wave per
 // block): first u block, span and the smallest / largest u end, where each
 // further u block starts, then the runs of equal v block in edge order
 // (nruns = 0 when there are more than kEbRuns: the block reads Ev); starts
-// relative to the block's first edge, padded past the last run
-static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restrict__ Eu,
+// relative to the block's first edge, padded past the last run.  Blocks
+// [b0, nblk).  Only the block's own record is written.
+//
+// A partitioned rank's edge block that straddles its interior / boundary cut
+// (the edges with a ghost end are sorted after the interior ones, each part
+// by u block) sees the u block DROP inside the block.  Its u ends are not a
+// few consecutive blocks from ub0 on, so the block is marked unstaged (nub =
+// kErecNoStage: k_edge_sweep_tl reads Eu) and no u-block start is recorded
+// -- u blocks below ub0 would otherwise index before the record.
+static __global__ void k_tile_erec(long E, int EB, int b0, int nblk, const int *__restrict__ Eu,
                                    const int *__restrict__ Ev, int *__restrict__ erec) {
-    const int blk = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int blk = b0 + blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
     const int lane = threadIdx.x & (kWave - 1);
     if (blk >= nblk) return;  // whole wave
     const long eb = (long)blk * EB, ee = min(eb + EB, E);
     int *r = erec + (long)blk * kErec;
     const int ub0 = Eu[eb] / kBlock;
+    bool drop = false;
+    for (long p = eb + 1 + lane; p < ee; p += kWave) drop |= Eu[p] / kBlock < Eu[p - 1] / kBlock;
+    drop = __ballot(drop) != 0;  // wave-uniform
     int count = 0, umin = 0x7fffffff, umax = -1;
     for (long c = eb; c < ee; c += kWave) {
         const long p = c + lane;
@@ -1668,10 +1682,12 @@ static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restri
             const int u = Eu[p];
             umin = min(umin, u);
             umax = max(umax, u);
-            // u blocks ub0 + q starting here (edges sorted by u block)
+            // u blocks ub0 + q starting here (edges sorted by u block: q1 >= q0 >= 0)
             const int q1 = u / kBlock - ub0;
             const int q0 = p == eb ? q1 : Eu[p - 1] / kBlock - ub0;
-            for (int q = q0 + 1; q <= q1 && q < kErecS - kErecU; q++) r[kErecU + q] = (int)(p - eb);
+            if (!drop)
+                for (int q = q0 + 1; q <= q1 && q < kErecS - kErecU; q++)
+                    r[kErecU + q] = (int)(p - eb);
         }
         const unsigned long long m = __ballot(st);
         const int k = count + __popcll(m & ((1ull << lane) - 1));
@@ -1686,7 +1702,7 @@ static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restri
         umin = min(umin, __shfl_xor(umin, o, kWave));
         umax = max(umax, __shfl_xor(umax, o, kWave));
     }
-    const int nub = Eu[ee - 1] / kBlock - ub0 + 1;
+    const int nub = drop ? kErecNoStage : Eu[ee - 1] / kBlock - ub0 + 1;
     for (int k = count + lane; k < kEbRuns; k += kWave) {  // padding: never reached
         r[kErecS + 2 * k] = 0x7fffffff;
         r[kErecS + 2 * k + 1] = 0;
@@ -1697,7 +1713,7 @@ static __global__ void k_tile_erec(long E, int EB, int nblk, const int *__restri
         r[2] = count <= kEbRuns ? count : 0;
         r[3] = umin - ub0 * kBlock;
         r[kErecU] = umax - umin + 1;
-        for (int q = max(nub, 1); q < kErecS - kErecU; q++) r[kErecU + q] = 0x7fffffff;
+        for (int q = drop ? 1 : max(nub, 1); q < kErecS - kErecU; q++) r[kErecU + q] = 0x7fffffff;
     }
 }
 

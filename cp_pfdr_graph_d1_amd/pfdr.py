@@ -60,6 +60,7 @@ EXPORTED = (
     "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create", "pfdr_loopback_abort",
     "pfdr_loopback_destroy", "pfdr_plan_create", "pfdr_plan_get",
     "pfdr_plan_set_incoming", "pfdr_plan_finish", "pfdr_plan_destroy",
+    "pfdr_debug_tile_erec", "pfdr_debug_erec_layout",
     "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
     "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
     "pfdr_gen_uniform_f32", "pfdr_gen_uniform_f64", "pfdr_gen_matvec_f32",

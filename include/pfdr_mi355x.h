@@ -457,6 +457,17 @@ int pfdr_plan_set_incoming(pfdr_plan *plan, int peer, int what, int64_t n,
 int pfdr_plan_finish(pfdr_plan *plan);
 void pfdr_plan_destroy(pfdr_plan *plan);
 
+/* ---------------------------------------------------------- test hooks -- */
+/* The per-edge-block records of the tiled edge sweep (k_edge_sweep_tl), built
+ * on the device from host endpoint arrays already in tile order: blocks
+ * [blk_begin, blk_begin + blk_count) of 1,024 (f32) / 512 (f64) edges are
+ * written, every other record of rec (rec_ints = blocks * ints per record)
+ * keeps what the caller put there -- so a test can check that building one
+ * block's record touches nothing else.  Layout: pfdr_debug_erec_layout. */
+int pfdr_debug_tile_erec(int64_t E, int dtype, const int *Eu, const int *Ev,
+    int blk_begin, int blk_count, int *rec, int64_t rec_ints);
+int pfdr_debug_erec_layout(int *ints, int *runs, int *nostage);
+
 /* -------------------------------------------------- synthetic inputs -- */
 /* Host-side deterministic generators (no device needed), identical laws to
  * cp_pfdr_graph_d1_amd/graphs.py.  Edges are written for emitters

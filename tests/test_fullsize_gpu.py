@@ -55,10 +55,10 @@ def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
     for k in (2, 4):
         Xk, info = _partitioned(WORKLOADS["headline"], inp, k, info=True)
         assert np.array_equal(Xk, X1), "partitioned (%d ranks) differs" % k
-        # every rank's slab keeps the fast paths of u-sorted edges (the
-        # scaling bench runs exactly these sessions over RCCL)
+        # every rank's slab runs the tile order (the scaling bench runs
+        # exactly these sessions over RCCL)
         for q in info["queries"]:
-            assert q["ustaged"] == 1 and q["split_blocks"] > 0, q
+            assert q["tiled_blocks"] > 0, q
     _, Xr, rel = _single("headline", reorder=pfdr.REORDER_ON)
     assert rel == 1
     assert np.array_equal(Xr, X1)
