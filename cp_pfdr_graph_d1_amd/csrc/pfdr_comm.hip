@@ -57,6 +57,11 @@ extern "C" int pfdr_comm_init(void **comm_out, int nranks, int rank, const void 
     ncclComm_t comm;
     ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
     if (r != ncclSuccess) return pfdr::report_rccl("pfdr_comm_init", r);
+    {   // a new communicator at the address of one the watchdog aborted (and
+        // the caller never destroyed): the old entry is stale
+        std::lock_guard<std::mutex> l(pfdr::g_aborted_m);
+        pfdr::g_aborted.erase(comm);
+    }
     *comm_out = comm;
     return PFDR_OK;
 }

@@ -721,6 +721,36 @@ void contribution_incidence(const int *Eu, const int *Ev, long E, int V, const u
     build_incidence_keyed(keys.p, vals.p, n, V, inc, s);
 }
 
+static __global__ void k_label_count(int n, const int *__restrict__ lab,
+                                     unsigned long long *__restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[lab[i]], 1ull);
+}
+static __global__ void k_count_not_one(long n, const unsigned long long *__restrict__ cnt,
+                                       unsigned long long *__restrict__ bad) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && cnt[i] != 1ull) atomicAdd(bad, 1ull);
+}
+
+// the labels of all ranks (vtx_label) must be a permutation of [0, V_global):
+// the relabelled amplitude and evolution sums all-reduce arrays with one
+// writer per position (collective, once at setup)
+void check_permutation(const int *lab, int V, long Vglob, Transport &tr, hipStream_t s) {
+    DevBuf<unsigned long long> cnt(Vglob), bad(1);
+    PFDR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * Vglob, s));
+    PFDR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
+    if (V) k_label_count<<<grid_for(V), kBlock, 0, s>>>(V, lab, cnt.p);
+    PFDR_HIP(hipGetLastError());
+    if (Vglob > 0x7fffffffL) throw std::runtime_error("V_global too large");
+    tr.allreduce_sum(cnt.p, (int)Vglob, 2, s);
+    k_count_not_one<<<grid_for(Vglob), kBlock, 0, s>>>(Vglob, cnt.p, bad.p);
+    PFDR_HIP(hipGetLastError());
+    unsigned long long nb = 0;
+    PFDR_HIP(hipMemcpyAsync(&nb, bad.p, sizeof(nb), hipMemcpyDeviceToHost, s));
+    tr.wait(s);
+    if (nb) throw std::runtime_error("vtx_label of the ranks is not a permutation of [0, V_global)");
+}
+
 }  // namespace pfdr
 
 extern "C" int pfdr_loopback_create(void **hub_out, int nranks) {

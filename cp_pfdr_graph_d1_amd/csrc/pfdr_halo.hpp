@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "pfdr_graph.hpp"
+#include "pfdr_monosum.hpp"
 
 namespace pfdr {
 
@@ -153,11 +154,69 @@ void partition_setup(const pfdr_problem *p, int V, long E, std::unique_ptr<Halo>
                      DevBuf<int> &Eu, DevBuf<int> &Ev, DevBuf<unsigned> &eg, long *e_offset,
                      hipStream_t s);
 
+// Collective check (setup): the caller's labels of every rank's owned
+// vertices (vtx_label, device, V per rank) form a permutation of
+// [0, V_global); throws otherwise.
+void check_permutation(const int *lab, int V, long Vglob, Transport &tr, hipStream_t s);
+
 // Contribution CSR of both solvers: the 2E local slots (address e = u end,
 // E + e = v end) keyed by (local vertex, 2 e_global + side) — the
 // reference's summation order — then the halo's received tail (addresses
 // 2E + j, keys from the plan).  eg: global edge ids or NULL (e_offset + e).
 void contribution_incidence(const int *Eu, const int *Ev, long E, int V, const unsigned *eg,
                             long e_offset, const Halo *halo, Incidence &inc, hipStream_t s);
+
+// Iterate-evolution sums of a partition with the reference's sequential
+// rounding (src/PFDR_graph_quadratic_d1_l1.cpp:514-529, simplex
+// src/PFDR_graph_loss_d1_simplex.cpp:653-691): nsum sums whose terms lie on
+// the ranks in rank order (rank r holds its n terms of sum y at a + y *
+// astride, the caller's order continuing rank to rank).  The binade scan of
+// pfdr_monosum.hpp splits cleanly at the ranks: each rank summarises its
+// tiles in parallel on binades predicted from the f64 totals of the ranks
+// before it (one all-reduce of nranks * nsum doubles), then the exact
+// running sum is carried rank to rank through the walks (chain_recv ->
+// k_mono_walk -> chain_send) and the last rank broadcasts it -- every rank
+// gets the single-GPU value bit for bit.  The rank-to-rank part is one
+// walk per rank (~1/N of the single-GPU walk) plus N point-to-point hops.
+template <typename real>
+struct ChainSum {
+    long n = 0;
+    int nsum = 1, nranks = 1, rank = 0;
+    DevBuf<char> ws;
+    DevBuf<double> tot;
+    DevBuf<real> seed;
+    void init(long n_, int nsum_, const Transport &tr) {
+        n = n_; nsum = nsum_; nranks = tr.nranks; rank = tr.rank;
+        ws.alloc(mono_ws_bytes<real>(n, nsum));
+        tot.alloc((size_t)nranks * nsum);
+        seed.alloc(nsum);
+    }
+    bool ready() const { return ws.p != nullptr; }
+    // out[0 .. nsum): the whole sums, on every rank (device); halt as mono_sum
+    void run(Transport &tr, const real *a, long astride, real *out, const int *halt,
+             hipStream_t s) {
+        constexpr long TILE = MonoTile<real>::TILE;
+        const long nt = (n + TILE - 1) / TILE;
+        long long *summ = static_cast<long long *>((void *)ws.p);
+        double *tsum = reinterpret_cast<double *>(summ + 2 * kMonoCand * nt * nsum);
+        int *ebase = reinterpret_cast<int *>(tsum + nt * nsum);
+        const dim3 gt((unsigned)nt, (unsigned)nsum), g1(1, (unsigned)nsum);
+        k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, tsum, halt);
+        PFDR_HIP(hipMemsetAsync(tot.p, 0, sizeof(double) * nranks * nsum, s));
+        k_mono_total<<<g1, 256, 0, s>>>((int)nt, tsum, tot.p + (size_t)rank * nsum, halt);
+        PFDR_HIP(hipGetLastError());
+        tr.allreduce_sum(tot.p, nranks * nsum, PFDR_F64, s);
+        k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, nullptr, 0, ebase, halt, tot.p, rank);
+        k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, summ, halt);
+        PFDR_HIP(hipGetLastError());
+        tr.chain_recv(seed.p, sizeof(real) * nsum, s);
+        k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ,
+                                                      rank > 0 ? seed.p : nullptr, 1, 0, nullptr,
+                                                      out, nullptr, halt);
+        PFDR_HIP(hipGetLastError());
+        tr.chain_send(out, sizeof(real) * nsum, s);
+        tr.broadcast(out, sizeof(real) * nsum, nranks - 1, s);
+    }
+};
 
 }  // namespace pfdr

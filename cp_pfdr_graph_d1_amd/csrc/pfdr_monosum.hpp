@@ -322,19 +322,30 @@ __global__ __launch_bounds__(256) void k_mono_tile_sums(long n, const real *__re
     if (threadIdx.x == 0) tsum[blockIdx.x] = z;
 }
 
-// 2. exclusive prefix -> predicted grid exponent at each tile start
+// 2. exclusive prefix -> predicted grid exponent at each tile start.  The
+//    running sum starts at seed[y * sstride] (nullptr: 0) or, for the part of
+//    a sum held by rank `prank` of a partition (chain_mono_sum), at the f64
+//    totals of the ranks before it, dpre[q * nsum + y] for q < prank.
 template <typename real>
 __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double *__restrict__ tsum,
-                                                       const real *__restrict__ seed,
+                                                       const real *__restrict__ seed, int sstride,
                                                        int *__restrict__ ebase,
-                                                       const int *__restrict__ halt) {
+                                                       const int *__restrict__ halt,
+                                                       const double *__restrict__ dpre = nullptr,
+                                                       int prank = 0) {
     __shared__ double wsum[1024 / kWave];
     __shared__ double carry;
     if (halt && *halt) return;
-    tsum += (long)blockIdx.y * ntiles;
-    ebase += (long)blockIdx.y * ntiles;
+    const int y = blockIdx.y;
+    tsum += (long)y * ntiles;
+    ebase += (long)y * ntiles;
     const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-    if (t == 0) carry = seed ? (double)*seed : 0.0;
+    if (t == 0) {
+        double c = seed ? (double)seed[y * sstride] : 0.0;
+        if (dpre)
+            for (int q = 0; q < prank; q++) c += dpre[q * gridDim.y + y];
+        carry = c;
+    }
     __syncthreads();
     for (int c0 = 0; c0 < ntiles; c0 += 1024) {
         const int j = c0 + t;
@@ -353,6 +364,20 @@ __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double 
         if (t == 1023) carry = pre + inc;
         __syncthreads();
     }
+}
+
+// f64 total of each sum's tiles (fixed order) at tot[y] (rank totals of a
+// partitioned sum, see chain_mono_sum)
+static __global__ __launch_bounds__(256) void k_mono_total(int ntiles, const double *__restrict__ tsum,
+                                                    double *__restrict__ tot,
+                                                    const int *__restrict__ halt) {
+    __shared__ double red[kBlock / kWave];
+    if (halt && *halt) return;
+    tsum += (long)blockIdx.y * ntiles;
+    double z = 0.0;
+    for (int j = threadIdx.x; j < ntiles; j += 256) z += tsum[j];
+    z = block_sum(z, red);
+    if (threadIdx.x == 0) tot[blockIdx.y] = z;
 }
 
 // 3. summaries (d0, d1) of tile blockIdx.x on the grids 2^(ebase - 1 + c),
@@ -408,7 +433,7 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *
                                                             const int *__restrict__ ebase,
                                                             const long long *__restrict__ summ,
                                                             const real *__restrict__ seed,
-                                                            int nparts,
+                                                            int sstride, int nparts,
                                                             const int *__restrict__ cnt_part,
                                                             real *__restrict__ sum_out,
                                                             long long *__restrict__ cnt_out,
@@ -425,7 +450,7 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *
     if (cnt_out && blockIdx.y == 0) mono_count<real>(nparts, cnt_part, cnt_out, sh);
     if (t == 0) sh.exit_at = INT_MAX;
     __syncthreads();
-    real s = seed ? *seed : real(0);
+    real s = seed ? seed[blockIdx.y * sstride] : real(0);
     int j = 0;
     while (j < ntiles && s < Lim<real>::huge) {
         const int ue = grid_exp(s);
@@ -490,9 +515,9 @@ void mono_sum(long n, const real *a, const real *seed, int nparts, const int *cn
     int *ebase = reinterpret_cast<int *>(tsum + nt * nsum);
     const dim3 gt((unsigned)nt, (unsigned)nsum), g1(1, (unsigned)nsum);
     k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, tsum, halt);
-    k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, seed, ebase, halt);
+    k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, seed, 0, ebase, halt);
     k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, summ, halt);
-    k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ, seed,
+    k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ, seed, 0,
                                                   nparts, cnt_part, out, cnt_out, halt);
 }
 

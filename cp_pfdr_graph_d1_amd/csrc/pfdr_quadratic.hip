@@ -1578,6 +1578,15 @@ static int quadratic_host(const char *fn, int kind, int V, int E, int N, real *X
     try {
         CallTrace tr(fn);
         if (verbose) { printf("Initializing constants and variables... "); fflush(stdout); }
+        const std::vector<int> devs = multidev_devices(&p);
+        if (!devs.empty()) {  // partitioned across the configured devices
+            if (verbose) { printf("done (%d devices).\n", (int)devs.size()); fflush(stdout); }
+            int its = 0;
+            multidev_solve(&p, devs, &its, Obj, Dif);
+            if (it) *it = its;
+            tr.finish(V, E, N, 1, its);
+            return PFDR_OK;
+        }
         std::unique_ptr<QuadSession<real>> s(new QuadSession<real>(&p));
         if (verbose) { printf("done.\nPreconditioned forward-Douglas-Rachford algorithm\n"); fflush(stdout); }
         tr.setup_done();

@@ -89,6 +89,13 @@ struct CallTrace {
     void finish(long V, long E, long N, int K, int it);
 };
 
+// Several GPUs behind one drop-in call (pfdr_multidev.hip): the devices a
+// host-pointer problem is partitioned across (empty: the one-GPU session),
+// and the synchronous partitioned solve over them.
+std::vector<int> multidev_devices(const pfdr_problem *p);
+void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it, void *Obj,
+                    void *Dif);
+
 }  // namespace pfdr
 
 struct pfdr_session {

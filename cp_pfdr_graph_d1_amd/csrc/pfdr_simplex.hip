@@ -598,6 +598,7 @@ struct SxProjArgs {
     real *part;
     const Ctrl<real> *ctrl;
     real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
+    const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
 };
 
 // projection + evolution + next explicit step, one thread per vertex
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
                 real d = a.P[b + k] - x[k];
                 if (d < real(0)) d = -d;
                 dif += d;
-                if (a.terms) a.terms[b + k] = d;
+                if (a.terms) a.terms[(a.tmap ? (long)a.tmap[v] * K : b) + k] = d;
             }
         } else if (a.track == 2) {
             real mx = x[0];
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
             for (int k = 1; k < K; k++) if (x[k] > mx) { mx = x[k]; l = k; }
             const real fl = (real)l;
             if (fl != a.lab[v]) { dif = real(1); a.lab[v] = fl; }
-            if (a.terms) a.terms[v] = dif;
+            if (a.terms) a.terms[a.tmap ? a.tmap[v] : v] = dif;
         }
         for (int k = 0; k < K; k++) {
             const real p = x[k];
@@ -670,6 +671,7 @@ struct SxVArgs {
     real *part;
     const Ctrl<real> *ctrl;
     real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
+    const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
 };
 
 // One block of the fused vertex sweep: NT lanes (t = the lane within
@@ -742,7 +744,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             for (int d = 1; d < K; d++) if (x[d] > mx) { mx = x[d]; l = d; }
             const real fl = (real)l;
             if (fl != a.lab[v0 + t]) { dif = real(1); a.lab[v0 + t] = fl; }
-            if (a.terms) a.terms[v0 + t] = dif;
+            if (a.terms) a.terms[a.tmap ? a.tmap[v0 + t] : v0 + t] = dif;
         }
     }
     __syncthreads();
@@ -752,7 +754,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             real d = a.P[i] - p;
             if (d < real(0)) d = -d;
             dif += d;
-            if (a.terms) a.terms[i] = d;
+            if (a.terms) a.terms[a.tmap ? (long)a.tmap[v] * K + k : i] = d;
         }
         a.P[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
@@ -1116,6 +1118,15 @@ class SimplexSession final : public SessionBase {
     DevBuf<real> terms_;
     DevBuf<char> dws_;
     static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
+    // partitions: the ranks' terms summed rank to rank in the caller's order
+    // (ChainSum); a relabelled partition (vtx_label) writes them at its
+    // caller labels (tlab_) of a V_global * K array, all-reduced into tall_
+    // and summed whole on every rank.  Label counts (track 2) add 0 / 1:
+    // exact in any order, so partitions keep the tree for them.
+    ChainSum<real> chain_;
+    DevBuf<int> tlab_;
+    DevBuf<real> tall_;
+    void seq_evolution();
     DevBuf<int> Eu_, Ev_;
     DevBuf<real> La_d1_, La_f_, Q_, P_, Pavg_, Ga_, GaQ_, invAux_, lab_;
     // (P, explicit step) pairs per (v, k), ghosts included: written with P
@@ -1218,9 +1229,6 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     const int evo = p->evolution;
     if (evo < PFDR_EVOLUTION_AUTO || evo > PFDR_EVOLUTION_TREE)
         throw std::runtime_error("evolution must be PFDR_EVOLUTION_AUTO, _SEQUENTIAL or _TREE");
-    if (evo == PFDR_EVOLUTION_SEQUENTIAL && (p->nranks > 1 || p->comm))
-        throw std::runtime_error("PFDR_EVOLUTION_SEQUENTIAL needs a single GPU (a partitioned "
-                                 "session sums the evolution statistic in a tree)");
     nterms_ = track_ == 2 ? (long)V_ : (long)V_ * K_;
 
     const int mem = p->mem;
@@ -1314,13 +1322,35 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         tiny = tiny_ ? 1 : 0;
         if (tiny_) graphs_ok_ = false;
     }
-    seqdif_ = track_ && !halo_ && !tiny_ &&
+    const long nglob = track_ == 2 ? Vglob_ : Vglob_ * K_;  // terms over all ranks
+    seqdif_ = track_ && !tiny_ && !(halo_ && track_ == 2) &&
               (evo == PFDR_EVOLUTION_SEQUENTIAL ||
-               (evo == PFDR_EVOLUTION_AUTO && nterms_ >= kSeqDifMin));
+               (evo == PFDR_EVOLUTION_AUTO && nglob >= kSeqDifMin));
     if (seqdif_) {
-        terms_.alloc((size_t)nterms_);
-        dws_.alloc(mono_ws_bytes<real>(nterms_, 1));
+        const bool gathered = halo_ && p->vtx_label;
+        const long n = gathered ? nglob : nterms_;
+        terms_.alloc((size_t)n);
+        if (!halo_ || gathered) dws_.alloc(mono_ws_bytes<real>(n, 1));
         red_.alloc(2);
+        if (gathered) {
+            if (n > 0x7fffffffL) throw std::runtime_error("V_global * K too large");
+            std::vector<int64_t> h64(V_);
+            PFDR_HIP(hipMemcpy(h64.data(), p->vtx_label, sizeof(int64_t) * V_,
+                               mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+            std::vector<int> h32(V_);
+            for (int v = 0; v < V_; v++) {
+                if (h64[v] < 0 || h64[v] >= Vglob_)
+                    throw std::runtime_error("vtx_label outside [0, V_global)");
+                h32[v] = (int)h64[v];
+            }
+            tlab_.alloc(V_);
+            PFDR_HIP(hipMemcpy(tlab_.p, h32.data(), sizeof(int) * V_, hipMemcpyHostToDevice));
+            check_permutation(tlab_.p, V_, Vglob_, *halo_->tr, s);
+            PFDR_HIP(hipMemsetAsync(terms_.p, 0, sizeof(real) * n, s));
+            tall_.alloc((size_t)n);
+        } else if (halo_) {
+            chain_.init(nterms_, 1, *halo_->tr);
+        }
         seqdif = 1;
     }
     if (graphs_ok_) {  // instantiated with the setup
@@ -1336,7 +1366,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
-                            &Dif_, &terms_})
+                            &Dif_, &terms_, &tall_})
         device_bytes += (int64_t)(b->n * sizeof(real));
     device_bytes += (int64_t)((GI_.n + PF_.n) * sizeof(SxR2<real>));
 }
@@ -1426,6 +1456,7 @@ void SimplexSession<real>::body() {
         a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
         a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         a.terms = seqdif_ ? terms_.p : nullptr;
+        a.tmap = tlab_.p;
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
@@ -1441,6 +1472,7 @@ void SimplexSession<real>::body() {
         a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
         a.P = P_.p; a.PF = PF_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
         a.terms = seqdif_ ? terms_.p : nullptr;
+        a.tmap = tlab_.p;
         ProfScope ps(prof, "sx_project", s);
         launch_project(a);
     }
@@ -1450,18 +1482,17 @@ void SimplexSession<real>::body() {
         pullPF();
     }
     const int nparts = vb_ ? nbs_ : nbv_;
-    if (gated && halo_) {
+    if (seqdif_) {
+        // the reference's sequential sum (ref :655-689), then its decision
+        ProfScope ps(prof, "seq_evolution", s);
+        seq_evolution();
+        k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
+                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
+    } else if (gated && halo_) {
         if (track_) {
             k_sx_partsum<real><<<1, kBlock, 0, s>>>(nparts, part_.p, ctrl_.p, red_.p);
             halo_->tr->allreduce_sum(red_.p, 1, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
         }
-        k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
-                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
-    } else if (seqdif_) {
-        // the reference's sequential sum (ref :655-689), then its decision
-        ProfScope ps(prof, "seq_evolution", s);
-        mono_sum<real>(nterms_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
-                       &ctrl_.p->halt);
         k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
                                                  rec_dif_ ? Dif_.p : nullptr, red_.p);
     } else if (gated) {
@@ -1470,6 +1501,26 @@ void SimplexSession<real>::body() {
     }
     PFDR_HIP(hipGetLastError());
     if (rec_obj_) objective();
+}
+
+// red_[0] = the evolution sum over every (vertex, label) in the caller's
+// order, rounded as the reference's one-thread loop
+template <typename real>
+void SimplexSession<real>::seq_evolution() {
+    hipStream_t s = stream;
+    const int *halt = &ctrl_.p->halt;
+    if (!halo_) {
+        mono_sum<real>(nterms_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
+                       halt);
+    } else if (!tlab_.p) {
+        chain_.run(*halo_->tr, terms_.p, 0, red_.p, halt, s);
+    } else {
+        PFDR_HIP(hipMemcpyAsync(tall_.p, terms_.p, sizeof(real) * terms_.n,
+                                hipMemcpyDeviceToDevice, s));
+        halo_->tr->allreduce_sum(tall_.p, (int)tall_.n, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
+        mono_sum<real>((long)tall_.n, tall_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1,
+                       0, halt);
+    }
 }
 
 // K-wide DR contributions of ghost-vertex ends to their owners
@@ -1646,6 +1697,15 @@ static int simplex_host(const char *fn, int K, int V, int E, real al, const real
     try {
         CallTrace tr(fn);
         if (verbose) { printf("Initializing constants and variables... "); fflush(stdout); }
+        const std::vector<int> devs = multidev_devices(&p);
+        if (!devs.empty()) {  // partitioned across the configured devices
+            if (verbose) { printf("done (%d devices).\n", (int)devs.size()); fflush(stdout); }
+            int its = 0;
+            multidev_solve(&p, devs, &its, Obj, Dif);
+            if (it) *it = its;
+            tr.finish(V, E, 0, K, its);
+            return PFDR_OK;
+        }
         std::unique_ptr<SimplexSession<real>> s(new SimplexSession<real>(&p));
         if (verbose) { printf("done.\nPreconditioned forward-Douglas-Rachford algorithm\n"); fflush(stdout); }
         tr.setup_done();

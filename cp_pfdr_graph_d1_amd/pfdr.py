@@ -60,7 +60,7 @@ EXPORTED = (
     "pfdr_comm_allreduce_max_f64", "pfdr_loopback_create", "pfdr_loopback_abort",
     "pfdr_loopback_destroy", "pfdr_plan_create", "pfdr_plan_get",
     "pfdr_plan_set_incoming", "pfdr_plan_finish", "pfdr_plan_destroy",
-    "pfdr_debug_tile_erec", "pfdr_debug_erec_layout",
+    "pfdr_set_devices", "pfdr_debug_tile_erec", "pfdr_debug_erec_layout",
     "pfdr_gen_knn_jitter_grid", "pfdr_gen_grid_edges",
     "pfdr_gen_piecewise_f32", "pfdr_gen_piecewise_f64",
     "pfdr_gen_uniform_f32", "pfdr_gen_uniform_f64", "pfdr_gen_matvec_f32",
@@ -587,6 +587,21 @@ class Session:
             self.close()
         except Exception:
             pass
+
+
+# ------------------------------------------------------ device group ----
+def set_devices(devices, min_vertices=-1):
+    """Partition this process's drop-in calls (Lib, and any CP / C++ caller of
+    the library) across `devices` (a list of device ids; [] = one GPU): one
+    host thread per device, RCCL over xGMI, bit-identical to one GPU.  Calls
+    below min_vertices vertices (< 0: 2^20) stay on one GPU.  A list repeating
+    one device runs the ranks as threads on it (loopback; tests)."""
+    devs = [int(d) for d in devices]
+    arr = (C.c_int * max(len(devs), 1))(*devs)
+    lib = load()
+    lib.pfdr_set_devices.argtypes = [C.c_int, C.c_void_p, C.c_int64]
+    _check(lib.pfdr_set_devices(len(devs), arr if devs else None, int(min_vertices)),
+           "pfdr_set_devices")
 
 
 # ------------------------------------------------------- native inputs ----

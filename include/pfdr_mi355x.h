@@ -427,6 +427,16 @@ int pfdr_loopback_destroy(void *hub);
  * <op, peers, bytes>" to stderr, aborts the communicator (RCCL) or the hub
  * (loopback) and fails the call with that message (no retry). */
 
+/* Several GPUs behind the drop-in entry points (one synchronous call, one
+ * host thread per device, RCCL communicators from ncclCommInitAll, created
+ * once and cached across calls): the drop-in calls of this process with at
+ * least min_vertices vertices (< 0: the default 2^20) are vertex-range
+ * partitioned across devices[0 .. n) -- bit-identical to the one-GPU solve.
+ * n = 0 returns to one GPU.  A list that repeats one device runs the ranks
+ * as threads on it (loopback transport; for tests).  Without this call the
+ * PFDR_DEVICES environment variable (N or "all") selects devices 0 .. N-1. */
+int pfdr_set_devices(int n, const int *devices, int64_t min_vertices);
+
 /* Host-only partition planner (what the partitioned session runs at setup;
  * exposed so the partition logic can be driven by any transport, e.g. the
  * CPU tests).  Rank `rank` owns global vertices [offsets[rank],

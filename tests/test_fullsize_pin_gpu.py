@@ -100,3 +100,35 @@ def test_fullsize_matches_reference(gpu_lib, name):
         print("  converged: it %d, first Dif below tolerance at %s" % (
             it, below[0] if below.size else None))
         assert below.size and below[0] == it - 1
+
+
+@pytest.mark.parametrize("name,k", [("headline_conv", 2), ("c4_conv", 2), ("headline_conv", 3)])
+def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
+    """The converged full-size solves split over k ranks (loopback threads on
+    one GPU: the RCCL session code with device-copy exchanges): the iterate
+    evolution is summed rank to rank with the reference's sequential rounding
+    (ChainSum, pfdr_halo.hpp), so the stopping iteration, every Dif and X's
+    sha256 equal the reference's (src/PFDR_graph_quadratic_d1_l1.cpp:429,
+    514-529; simplex src/PFDR_graph_loss_d1_simplex.cpp:653-691)."""
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    g = _gold(name)
+    case = F.build(name)
+    assert F.input_digest(case) == str(g["in_sha256"])
+    a = case["args"]
+    if case["solver"] == "simplex":
+        X, it, _, Dif, info = P.solve_loopback(
+            k, pfdr.PFDR_KIND_SIMPLEX, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["P0"], a["Q"],
+            La_l1=a["La_f"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, K=a["K"], al=a["al"])
+    else:
+        X, it, _, Dif, info = P.solve_loopback(
+            k, pfdr.PFDR_KIND_L1, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
+            La_l1=a["La_l1"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True)
+    d = F.digest(X, it, Dif[:it], case["sample_m"])
+    print("%s k=%d: it %d/%d sha256 equal %s" % (name, k, it, int(g["it"]),
+                                                  str(d["sha256"]) == str(g["sha256"])))
+    assert it == int(g["it"])
+    assert np.array_equal(Dif[:it], g["Dif"][:it]), "partitioned Dif differs from the reference"
+    assert str(d["sha256"]) == str(g["sha256"])

@@ -15,7 +15,7 @@ CASES = ["l1_grid2d_f64", "l1_grid2d_f32", "l1_knn_shuffled_f32", "l1_l22_f64",
          "bounds_upper_recond_f32", "l1_chain_kat_f64"] + G.names("simplex_")
 
 
-def _solve(c, k, fixed):
+def _solve(c, k, fixed, evolution=0):
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
     a = dict(c)
@@ -27,7 +27,8 @@ def _solve(c, k, fixed):
             k, pfdr.PFDR_KIND_SIMPLEX, P0.dtype, a["Eu"], a["Ev"], a["La_d1"], P0, a["Q"],
             La_l1=a["La_f"], rho=float(a["rho"]), condMin=float(a["condMin"]),
             difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
-            record_obj=True, record_dif=True, K=int(a["K"]), al=float(a["al"]))
+            record_obj=True, record_dif=True, K=int(a["K"]), al=float(a["al"]),
+            evolution=evolution)
     kind = pfdr.PFDR_KIND_L1 if str(a["solver"]) == "l1" else pfdr.PFDR_KIND_BOUNDS
     X0 = a["X0"]
     return P.solve_loopback(
@@ -36,7 +37,7 @@ def _solve(c, k, fixed):
         lo=float(a.get("lo", -np.inf)), hi=float(a.get("hi", np.inf)), Ltype=int(a["Ltype"]),
         L=a["L"], rho=float(a["rho"]), condMin=float(a["condMin"]),
         difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
-        record_obj=True, record_dif=True)
+        record_obj=True, record_dif=True, evolution=evolution)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -61,6 +62,26 @@ def test_partitioned_equals_reference(gpu_lib, name, k, fixed):
         assert np.allclose(Obj[: n + 1], go, rtol=rtol, atol=1e-6 * np.abs(go).max())
 
 
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("k", [2, 3])
+def test_partitioned_sequential_evolution_equals_reference(gpu_lib, name, k):
+    """converged golden cases with the evolution summed rank to rank in the
+    reference's sequential rounding (ChainSum; forced, as these graphs are
+    below AUTO's 2^17 vertices): the stopping iteration and EVERY Dif equal
+    the reference's bit for bit (src/PFDR_graph_quadratic_d1_l1.cpp:514-529,
+    simplex src/PFDR_graph_loss_d1_simplex.cpp:653-691)"""
+    from cp_pfdr_graph_d1_amd import pfdr
+    c, g = G.load(name)
+    V = c["X0"].size if "X0" in c else c["P0"].size // int(c["K"])
+    if V < 4 * k:
+        pytest.skip("graph too small for %d ranks" % k)
+    X, it, Obj, Dif, info = _solve(c, k, False, pfdr.EVOLUTION_SEQUENTIAL)
+    print("%s k=%d it=%d/%d" % (name, k, it, int(g["conv_it"])))
+    assert it == int(g["conv_it"])
+    assert np.array_equal(X, g["conv_X"])
+    assert np.array_equal(Dif[:it], g["conv_Dif"][:it])
+
+
 def test_partitioned_headline_slab_matches_single(gpu_lib):
     """weak-scaling geometry of bench.py at a small size: slabs of a jittered
     6-NN grid, 4 ranks, against the single-GPU session"""
@@ -81,6 +102,17 @@ def test_partitioned_headline_slab_matches_single(gpu_lib):
     X, it, _, Dif, _ = P.solve_loopback(4, pfdr.PFDR_KIND_L1, np.float32, Eu, Ev, La, X0, Y,
                                         La_l1=L1, difTol=1e-5, itMax=300, record_dif=True)
     assert it == its
+    assert np.array_equal(X, Xs)
+    # the evolution summed rank to rank like the single GPU (both sequential)
+    kw = dict(La_l1=L1, difTol=1e-5, itMax=300, record_dif=True,
+              evolution=pfdr.EVOLUTION_SEQUENTIAL)
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, Eu.size, Eu, Ev, La, X0, Y, **kw)
+    s.run(300)
+    Xs, its, _, Difs = s.result()
+    s.close()
+    X, it, _, Dif, _ = P.solve_loopback(4, pfdr.PFDR_KIND_L1, np.float32, Eu, Ev, La, X0, Y, **kw)
+    assert it == its
+    assert np.array_equal(Dif[:it], Difs[:its])
     assert np.array_equal(X, Xs)
 
 
@@ -274,3 +306,16 @@ def test_relabelled_partition_random_labels(gpu_lib, k, kind):
     assert np.array_equal(Xr, X1)
     assert np.array_equal(Xp, X1)
     assert g_rel * 5 < g_raw
+    # tracked, converged: the relabelled ranks gather their evolution terms at
+    # the caller's labels and sum them in that order (sequential rounding)
+    kw.update(itMax=2000, difTol=1e-4 if kind == "simplex" else 1e-5, record_dif=True,
+              evolution=pfdr.EVOLUTION_SEQUENTIAL)
+    s = pfdr.Session(args[1], dt, V, Eu.size, *args[3:], **kw)
+    s.run(kw["itMax"])
+    X1, it1, _, D1 = s.result()
+    s.close()
+    Xr, itr, _, Dr, _ = P.solve_loopback(*args, relabel=True, **kw)
+    print("%s k=%d converged: it %d / %d" % (kind, k, it1, itr))
+    assert 0 < it1 < kw["itMax"] and itr == it1
+    assert np.array_equal(Dr[:itr], D1[:it1])
+    assert np.array_equal(Xr, X1)

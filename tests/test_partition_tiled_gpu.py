@@ -7,23 +7,21 @@ runs the interior edge blocks while the halo pull is in flight and the rest
 after it; the vertex sweep finds the u ends of those boundary edges and the
 received contributions as extra runs of its blocks, each entry with its slot
 in the reference's (e, side) order.  Expected bit-exact against the
-single-GPU session with tree evolution sums (iterates and iteration count;
-Dif to rounding, its partial sums regroup across ranks), with k ranks as k threads on one GPU (loopback transport) and
-on a one-rank RCCL communicator (hipGraph-replayed chunks)."""
+single-GPU session: iterates, iteration count and Dif (the evolution is
+summed rank to rank with the reference's sequential rounding), with k ranks
+as k threads on one GPU (loopback transport) and on a one-rank RCCL
+communicator (hipGraph-replayed chunks).  The edge block that straddles a
+rank's interior / boundary cut is covered deterministically by
+tests/test_erec_gpu.py."""
 import numpy as np
 import pytest
 
-pytestmark = [
-    pytest.mark.gpu,
-    # kTiledPartitions (csrc/pfdr_quadratic.hip) is off: a full-size 2-rank
-    # split differed intermittently (DESIGN §10); these cases passed with it on
-    pytest.mark.skip(reason="tiled partitioned ranks disabled pending a full-size race"),
-]
+pytestmark = pytest.mark.gpu
 
 
 def _single(args, kw):
     from cp_pfdr_graph_d1_amd import pfdr
-    s = pfdr.Session(*args, **kw, evolution=pfdr.EVOLUTION_TREE)
+    s = pfdr.Session(*args, **kw)
     try:
         s.run(kw["itMax"])
         return s.result()
@@ -56,8 +54,41 @@ def test_tiled_partition_matches_single(gpu_lib, k, dt, conv):
     print(k, dt.__name__, "it", it, its, q)
     assert all(r["tiled_blocks"] > 0 and r["ghosts"] > 0 for r in q)
     assert it == its and (conv or it == 20)
-    # the evolution's partial sums meet in a different tree across ranks
-    assert np.allclose(D[:it], Ds[:its], rtol=1e-4, atol=0)
+    assert np.array_equal(D[:it], Ds[:its])
+    assert np.array_equal(X, Xs)
+
+
+@pytest.mark.parametrize("k,width,dup", [(2, 420, True), (3, 420, True), (2, 640, False)],
+                         ids=["k2-w420-mirrored", "k3-w420-mirrored", "k2-w640"])
+def test_tiled_partition_narrow_grid(gpu_lib, k, width, dup):
+    """a narrow 2-D grid (bandwidth 420 / 640 vertices, 1-3 u blocks): every
+    rank past 1,024 vertex blocks, its boundary edges starting one or two u
+    blocks below the interior edges they follow, so the edge block that
+    straddles the cut drops its u block by less than the LDS stage spans --
+    the case where a staged lookup would read the wrong u end (k_tile_erec
+    marks such a block unstaged).  Mirrored duplicates give every rank
+    ghost edges."""
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation
+    shape = (width, 1400 * k // 2 + 300)
+    V = int(np.prod(shape))
+    Eu, Ev = grid_graph(shape, 4)
+    if dup:
+        Eu, Ev = np.concatenate([Eu, Ev]), np.concatenate([Ev, Eu])
+    dt = np.float32
+    Y = piecewise_observation(shape, 3, dt)
+    La = np.full(Eu.size, 0.1, dt)
+    kw = dict(La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=0.0, difRcd=0.0,
+              itMax=30, record_dif=True)
+    X0 = np.zeros(V, dt)
+    Xs, its, _, _ = _single((pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, X0, Y), kw)
+    X, it, _, _, info = P.solve_loopback(k, pfdr.PFDR_KIND_L1, dt, Eu, Ev, La, X0, Y, **kw)
+    q = info["queries"]
+    print(k, width, q)
+    assert all(r["tiled_blocks"] > 0 for r in q)
+    assert all(r["ghosts"] > 0 for r in q) or not dup
+    assert it == its == 30
     assert np.array_equal(X, Xs)
 
 

@@ -11,8 +11,9 @@ i=0
 for sel in "$@"; do
     i=$((i + 1))
     t0=$(date +%s)
-    timeout -k 10 "${LIMIT:-900}" python -u -m pytest $sel -m gpu -x -v -rf -s --timeout "${TLIMIT:-600}" \
-        --timeout-method thread > "$OUT/pytest_$i.log" 2>&1
+    # (eval: a selection may quote a -k expression, e.g. 'tests/x.py -k "a or b"')
+    eval timeout -k 10 "${LIMIT:-900}" python -u -m pytest $sel -m gpu -x -v -rf -s \
+        --timeout "${TLIMIT:-600}" --timeout-method thread > "$OUT/pytest_$i.log" 2>&1
     rc=$?
     echo "[pytest_$i: $sel] rc=$rc $(( $(date +%s) - t0 ))s"
     tail -n 4 "$OUT/pytest_$i.log"
