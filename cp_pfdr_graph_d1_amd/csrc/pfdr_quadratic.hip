@@ -120,7 +120,13 @@ class QuadSession final : public SessionBase {
             pinned_small_put(hctrl_);
         }
         for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : evv_) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : evd_) if (e) (void)hipEventDestroy(e);
         if (comm_) (void)hipStreamDestroy(comm_);
+        if (evs_) {
+            (void)hipStreamSynchronize(evs_);
+            (void)hipStreamDestroy(evs_);
+        }
         drop_graphs();
     }
     int run(int iters) override;
@@ -155,6 +161,10 @@ class QuadSession final : public SessionBase {
     // the one value la0_ instead of streaming the array (4 B per edge)
     bool la_uniform_ = false;
     real la0_ = real(0);
+    // uniform La_l1 (the headline's 0.01): the vertex sweep forms Th_l1 =
+    // Ga * l1u instead of reading it (4 B per vertex)
+    bool l1_uniform_ = false;
+    real l1u_ = real(0);
     const real *la_it() const { return la_uniform_ ? nullptr : La_d1_.p; }
     // iterate evolution with the reference's sequential rounding
     // (PFDR_EVOLUTION_*, include/pfdr_mi355x.h): the vertex sweep stores the
@@ -171,7 +181,24 @@ class QuadSession final : public SessionBase {
     // writer per position) into tall_ and summed whole on every rank
     ChainSum<real> chain_;
     DevBuf<real> tall_;
-    void seq_evolution();
+    void seq_evolution(real *terms, hipStream_t s);
+    // Speculative iteration (single GPU, sequential evolution, no
+    // reconditioning (difRcd = 0), no objective record, identity / diagonal
+    // A): the evolution sums and the decision on iteration t run on a second
+    // stream (evs_) while iteration t + 1 sweeps; iteration t + 2 waits for
+    // that decision.  X is ping-ponged (iteration t reads xpb(t - 1), writes
+    // xpb(t)) and the terms are double-buffered, so when the decision on t
+    // stops the loop, X_t is intact in xpb(t) and the speculative t + 1 (its
+    // Z, its X in the other buffer) is simply discarded: the iterate,
+    // iteration count and Dif are the sequential loop's, bit for bit.
+    bool spec_ = false;
+    int it0_ = 0;  // completed iterations when the captured / launched bodies start
+    DevBuf<R2<real>> xp2_;
+    R2<real> *xpb(int t) { return spec_ && (t & 1) ? xp2_.p : xp_.p; }
+    R2<real> *xr_ = nullptr, *xw_ = nullptr;  // the sweeps' read / write (X, P)
+    hipStream_t evs_ = nullptr;
+    hipEvent_t evv_[2] = {}, evd_[2] = {};
+    void body_spec(int i, int n);
     static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
     // internal relabelling (pfdr_order.hpp): order_[new] = old, where_[old] = new,
@@ -232,9 +259,13 @@ class QuadSession final : public SessionBase {
     // an iteration of a small graph.  Re-captured after a reconditioning
     // (new kernel arguments).
     bool graphs_ok_ = false;
+    bool capturable_ = false;  // prepare(): graphs of any run length on request
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
-    hipGraphExec_t chunk_graph();
+    hipGraphExec_t chunk_graph(int n);
+  public:
+    void prepare(int iters) override;
+  private:
     void drop_graphs() {
         for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
         graphs_.clear();
@@ -519,10 +550,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         k_diag<real><<<grid_for(V), kBlock, 0, s>>>(V_, mode_, A_.p, Vglob_, v0_, diag_.p);
     }
     PFDR_HIP(hipGetLastError());
-    // uniform La_d1? (read back with c below)
-    DevBuf<int> ubad(1);
-    PFDR_HIP(hipMemsetAsync(ubad.p, 0, sizeof(int), s));
+    // uniform La_d1 / La_l1? (read back with c below)
+    DevBuf<int> ubad(2);
+    PFDR_HIP(hipMemsetAsync(ubad.p, 0, 2 * sizeof(int), s));
     if (E_) k_uniform_check<real><<<grid_for(E), kBlock, 0, s>>>(E_, La_d1_.p, ubad.p);
+    if (La_l1_.p) k_uniform_check<real><<<grid_for(V), kBlock, 0, s>>>(V_, La_l1_.p, ubad.p + 1);
     // Z = X at both ends, first preconditioning, first forward step
     zs_ = tiled_ ? E_ : 0;
     if (E_) k_z_init<real><<<grid_for(E), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, zs_);
@@ -546,6 +578,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         PFDR_HIP(hipMemcpy(&la0_, La_d1_.p, sizeof(real), hipMemcpyDeviceToHost));
         la_uniform_ = bad == 0;
         la_uniform = la_uniform_ ? 1 : 0;
+    }
+    if (La_l1_.p) {
+        int bad = 1;
+        PFDR_HIP(hipMemcpy(&bad, ubad.p + 1, sizeof(int), hipMemcpyDeviceToHost));
+        PFDR_HIP(hipMemcpy(&l1u_, La_l1_.p, sizeof(real), hipMemcpyDeviceToHost));
+        l1_uniform_ = bad == 0;
     }
     if (halo_) {  // Z-direct on every rank or on none (see zdirect)
         Transport &tr = *halo_->tr;
@@ -585,8 +623,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         // the all-reduces of a chunk of iterations in one hipGraph launch:
         // the host's ~30 API calls per iteration otherwise approach a rank's
         // GPU time at N = 8); the loopback transport rendezvous on the host
-        graphs_ok_ = itMax_ >= 2 * chunk_ && halo_->tr->capturable() && !rec_obj_;
+        capturable_ = halo_->tr->capturable() && !rec_obj_;
+        graphs_ok_ = itMax_ >= 2 * chunk_ && capturable_;
     } else if (!tiny_) {
+        capturable_ = true;
         graphs_ok_ = itMax_ >= 2 * chunk_;
         // (an edgeless graph has no edge sweep to carry the decision)
         fuse_ = track_ && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
@@ -612,19 +652,37 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             chain_.init(V_, 2, *halo_->tr);
         }
         seqdif = 1;
+        spec_ = !halo_ && difRcd2_ == real(0) && !rec_obj_ &&
+                (mode_ == A_IDENT || mode_ == A_DIAG);
+        if (spec_) {
+            DevBuf<real> t2(4 * (size_t)tstride_);  // terms of both parities
+            std::swap(terms_.p, t2.p);
+            std::swap(terms_.n, t2.n);
+            xp2_.alloc(Vg_);
+            PFDR_HIP(hipMemcpyAsync(xp2_.p, xp_.p, sizeof(R2<real>) * Vg_,
+                                    hipMemcpyDeviceToDevice, s));
+            PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
+            for (int k = 0; k < 2; k++) {
+                PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
+                PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
+            }
+            speculative = 1;
+        }
     }
+    xr_ = xw_ = xp_.p;
     if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
     acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
-    acc(tall_.n * sizeof(real) + chain_.ws.n + ampg_.n * sizeof(real));
+    acc(tall_.n * sizeof(real) + chain_.ws.n + ampg_.n * sizeof(real) +
+        xp2_.n * sizeof(R2<real>));
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
     // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
     // which a small solve timed to tolerance would otherwise pay in its loop)
     if (graphs_ok_) {
         try {
-            (void)chunk_graph();
+            (void)chunk_graph(chunk_);
         } catch (const std::exception &) {
             if (!halo_) throw;
-            graphs_ok_ = false;  // this transport would not capture: launch directly
+            graphs_ok_ = capturable_ = false;  // this transport would not capture: launch directly
             (void)hipGetLastError();
         }
     }
@@ -1195,7 +1253,7 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
         // edge blocks [ebeg / EB, ...) of the tile order (a partitioned rank
         // sweeps its interior blocks and the rest in two launches)
         auto k = (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true> : k_edge_sweep_tl<real, false>;
-        k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_,
+        k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xr_, Z2_.p, A1_.p, cw_,
                                gi_.p, la_it(), la0_, zdirect() ? nullptr : wz_.p, rho_, c,
                                (int)(ebeg / EB), nb, xm);
         return;
@@ -1203,11 +1261,11 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     if (tiled_) throw std::logic_error("tiled edge sweep: range not on edge blocks");
     if (us_ && uptr_.p) {
         auto k = fuse_ ? k_edge_sweep_us<real, true> : k_edge_sweep_us<real, false>;
-        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p,
+        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, uptr_.p, xr_, Z2_.p, A1_.p, cw_, gi_.p,
                                la_it(), la0_, wz_.p, rho_, c, nb, xm, rg, f, pad_out());
     } else {
         auto k = fuse_ ? k_edge_sweep<real, true> : k_edge_sweep<real, false>;
-        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xp_.p, Z2_.p, A1_.p, cw_, gi_.p, la_it(), la0_,
+        k<<<g, kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, xr_, Z2_.p, A1_.p, cw_, gi_.p, la_it(), la0_,
                                wz_.p, rho_, c, nb, xm, rg, f, pad_out());
     }
 }
@@ -1229,7 +1287,8 @@ void QuadSession<real>::tiny_chunk(int n) {
 template <typename real>
 VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     VArgs<real> a{};
-    a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xp_.p; a.wz = wz_.p;
+    a.V = V_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p; a.xp = xr_; a.wz = wz_.p;
+    a.xpo = xw_ == xr_ ? nullptr : xw_;
     a.uptr = uptr_.p; a.mask = mask_.p; a.oidx = oidx_.p; a.blkok = blkok_.p;
     a.Y = Y_.p; a.A = A_.p; a.Ga = Ga_.p; a.Th_l1 = Th_l1_.p;
     a.prox = prox_; a.positivity = positivity_; a.lo = lo_; a.hi = hi_;
@@ -1241,7 +1300,10 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
         a.d2 = d2_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
+        a.gi = gi_.p;  // (Ga, 1/Aux) in one load
     }
+    a.l1uni = l1_uniform_ ? 1 : 0;
+    a.l1u = l1u_;
     a.terms = seqdif_ ? terms_.p : nullptr;
     a.tmap = !seqdif_ ? nullptr : reordered_ ? order_.p : halo_ ? lab_.p : nullptr;
     a.tstride = tstride_;
@@ -1275,9 +1337,35 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
         k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }
 
+// iteration t = it0_ + 1 + i of a speculative session (see spec_)
+template <typename real>
+void QuadSession<real>::body_spec(int i, int n) {
+    hipStream_t s = stream;
+    const int t = it0_ + 1 + i;
+    const Ctrl<real> *c = ctrl_.p;
+    if (i >= 2) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // the decision on t - 2
+    xr_ = xpb(t - 1);
+    xw_ = xpb(t);
+    real *terms = terms_.p + (t & 1) * 2 * tstride_;
+    real *const keep = terms_.p;
+    terms_.p = terms;  // vargs() hands the sweep this iteration's terms
+    edge_sweep(0, E_, c, "edge_sweep");
+    vertex_sweep(0, nbv_, c, "vertex_sweep");
+    terms_.p = keep;
+    xr_ = xw_ = xp_.p;
+    PFDR_HIP(hipEventRecord(evv_[t & 1], s));
+    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[t & 1], 0));
+    seq_evolution(terms, evs_);  // overlaps the sweeps of t + 1
+    k_decide<real><<<1, 64, 0, evs_>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipEventRecord(evd_[t & 1], evs_));
+    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // join: the chunk's last
+}
+
 template <typename real>
 void QuadSession<real>::body(int i, int n) {
     hipStream_t s = stream;
+    if (spec_) { body_spec(i, n); return; }
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     if (fuse_) {
@@ -1340,7 +1428,7 @@ void QuadSession<real>::body(int i, int n) {
     if (seqdif_) {
         // the reference's two sequential sums (ref :518-526), then its decision
         ProfScope ps(prof, "seq_evolution", s);
-        seq_evolution();
+        seq_evolution(terms_.p, s);
         k_decide<real><<<1, 64, 0, s>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     } else if (gated && !halo_) {
         k_reduce_decide<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, ctrl_.p,
@@ -1360,11 +1448,10 @@ void QuadSession<real>::body(int i, int n) {
 // red_[0..2) = the sums of (X_ - X)^2 and X^2 over every vertex in the
 // caller's order, rounded as the reference's one-thread loop
 template <typename real>
-void QuadSession<real>::seq_evolution() {
-    hipStream_t s = stream;
+void QuadSession<real>::seq_evolution(real *terms, hipStream_t s) {
     const int *halt = &ctrl_.p->halt;
     if (!halo_) {
-        mono_sum<real>(V_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
+        mono_sum<real>(V_, terms, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
                        halt);
     } else if (!lab_.p) {
         chain_.run(*halo_->tr, terms_.p, tstride_, red_.p, halt, s);
@@ -1431,17 +1518,19 @@ void QuadSession<real>::plan_overlap() {
     (void)s;
 }
 
-// the captured graph of a whole chunk (chunk_ bodies), instantiated once --
-// at the end of the setup, and again after a reconditioning dropped it
+// the captured graph of n bodies (a whole chunk, or a run's tail after
+// prepare()), instantiated once -- at the end of the setup for chunk_, and
+// again after a reconditioning dropped them
 template <typename real>
-hipGraphExec_t QuadSession<real>::chunk_graph() {
-    auto it = graphs_.find(chunk_);
+hipGraphExec_t QuadSession<real>::chunk_graph(int n) {
+    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);  // speculative: X buffers by parity
+    auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-        for (int i = 0; i < chunk_; i++) body(i, chunk_);
+        for (int i = 0; i < n; i++) body(i, n);
     } catch (...) {
         (void)hipStreamEndCapture(stream, &g);
         if (g) (void)hipGraphDestroy(g);
@@ -1451,19 +1540,37 @@ hipGraphExec_t QuadSession<real>::chunk_graph() {
     const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     PFDR_HIP(e);
-    graphs_.emplace(chunk_, ge);
+    graphs_.emplace(key, ge);
     return ge;
 }
 
 // whole chunks replay the captured graph; a partial chunk (the tail of a
-// run) is launched directly rather than captured for one use
+// run) replays one only if prepare() built it, else it is launched directly
+// rather than captured for one use
 template <typename real>
 void QuadSession<real>::run_bodies(int n) {
+    it0_ = it_;
+    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);
+    if (!prof.on && capturable_ && graphs_.count(key)) {
+        PFDR_HIP(hipGraphLaunch(graphs_[key], stream));
+        return;
+    }
     if (!graphs_ok_ || prof.on || n != chunk_) {
         for (int i = 0; i < n; i++) body(i, n);
         return;
     }
-    PFDR_HIP(hipGraphLaunch(chunk_graph(), stream));
+    PFDR_HIP(hipGraphLaunch(chunk_graph(chunk_), stream));
+}
+
+// the graphs a run of `iters` iterations will replay (chunks of chunk_ and
+// the tail), built now so that the run itself launches no capture
+template <typename real>
+void QuadSession<real>::prepare(int iters) {
+    if (!capturable_ || iters <= 0) return;
+    it0_ = it_;  // (the run starts here: its parity)
+    if (iters >= chunk_) (void)chunk_graph(chunk_);
+    if (iters % chunk_) (void)chunk_graph(iters % chunk_);
+    PFDR_HIP(hipStreamSynchronize(stream));
 }
 
 template <typename real>
@@ -1523,9 +1630,10 @@ template <typename real>
 void *QuadSession<real>::device_x() {
     if (xout_.n < (size_t)V_) xout_.alloc(V_);
     if (reordered_)
-        k_x_extract_perm<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xp_.p, where_.p, xout_.p);
+        k_x_extract_perm<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xpb(it_), where_.p,
+                                                                    xout_.p);
     else
-        k_x_extract<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xp_.p, xout_.p);
+        k_x_extract<real><<<grid_for(V_), kBlock, 0, stream>>>(V_, xpb(it_), xout_.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipStreamSynchronize(stream));
     return xout_.p;

@@ -1869,6 +1869,7 @@ struct VArgs {
     const int *blkok;       // per block: 1 = split path
     const real *wz;         // contributions (local side-major, then received)
     R2<real> *xp;
+    R2<real> *xpo;          // where the new (X, P) go (null: xp, in place)
     const real *Y, *A, *Ga, *Th_l1;
     int prox, positivity;
     real lo, hi;
@@ -1886,6 +1887,12 @@ struct VArgs {
     const real *zs;
     const real *invAux;
     real a0;
+    // per-vertex constants: gi = (Ga, invAux) pairs (null: the separate
+    // arrays); l1uni: La_l1 is one value l1u, so Th_l1 = Ga * l1u (the
+    // preconditioner's own product, k_precond_vertex) is not read
+    const R2<real> *gi;
+    int l1uni;
+    real l1u;
     // sequential evolution statistic (null: off): the terms (X_ - X)^2 at
     // terms[i] and X^2 at terms[tstride + i], i = the vertex's label in the
     // caller's order (tmap[v] for a relabelled session, else v), summed
@@ -1908,15 +1915,26 @@ template <> struct VSweep<double> { static constexpr int waves = 4; };
 template <typename real>
 struct VOps {
     R2<real> q{};
-    real th = real(0), yv = real(0), gv = real(0), av = real(0);
+    real th = real(0), yv = real(0), gv = real(0), av = real(0), ia = real(0);
 };
+// The old iterate (X_, P_) is read only where it is used: the evolution
+// terms (tracked) or the dense modes (P kept until their forward step); an
+// untracked identity / diagonal-A sweep overwrites both (8 B per vertex).
 template <typename real>
 __device__ __forceinline__ VOps<real> vertex_ops(const VArgs<real> &a, int v) {
     VOps<real> o;
     if (v < a.V) {
-        o.q = a.xp[v];
-        if (a.prox == PROX_L1) o.th = a.Th_l1[v];
-        if (a.fwd) { o.yv = a.Y[v]; o.gv = a.Ga[v]; }
+        if (a.track || !a.fwd) o.q = a.xp[v];
+        real g = real(0);
+        if (a.gi) {
+            const R2<real> p = a.gi[v];
+            g = p.x;
+            o.ia = p.y;
+        } else if (a.fwd || a.l1uni) {
+            g = a.Ga[v];
+        }
+        if (a.prox == PROX_L1) o.th = a.l1uni ? g * a.l1u : a.Th_l1[v];
+        if (a.fwd) { o.yv = a.Y[v]; o.gv = g; }
         if (a.fwd == 2) o.av = a.A[v];
     }
     return o;
@@ -1970,7 +1988,7 @@ __device__ __forceinline__ R2<real> vertex_finish(const VArgs<real> &a, int v, r
             p -= yv;
             q.y = real(2) * x - gv * p;
         }
-        a.xp[v] = q;
+        (a.xpo ? a.xpo : a.xp)[v] = q;
     }
     return q;
 }
@@ -1984,7 +2002,7 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     const int v = v0 + threadIdx.x;
     const VOps<real> o = vertex_ops(a, v);
     // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
-    const real wv = ZD && v < a.V ? a.a0 * a.invAux[v] : real(1);
+    const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
     if (a.d2 && a.tok[blk])  // block-uniform
         x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart,

@@ -410,6 +410,15 @@ extern "C" int pfdr_session_run(pfdr_session *s, int iters, int *it_total) {
     return PFDR_OK;
 }
 
+extern "C" int pfdr_session_prepare(pfdr_session *s, int iters) {
+    if (!s) return report_error("pfdr_session_prepare", "null session");
+    PFDR_GUARD("pfdr_session_prepare", {
+        StreamScope sc(s->impl->stream, s->impl->device);
+        s->impl->prepare(iters);
+    });
+    return PFDR_OK;
+}
+
 extern "C" int pfdr_session_result(pfdr_session *s, void *X, int *it,
                                    void *Obj, void *Dif) {
     if (!s) return report_error("pfdr_session_result", "null session");
@@ -499,6 +508,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "la_uniform")) *value = s->impl->la_uniform;
     else if (!strcmp(what, "ghosts")) *value = s->impl->ghosts;
     else if (!strcmp(what, "graphs")) *value = s->impl->graphs;
+    else if (!strcmp(what, "speculative")) *value = s->impl->speculative;
     else if (!strcmp(what, "dense_exact")) *value = s->impl->dense_exact;
     else if (!strcmp(what, "interior_edges")) *value = s->impl->interior_edges;
     else if (!strcmp(what, "device_bytes")) *value = s->impl->device_bytes;

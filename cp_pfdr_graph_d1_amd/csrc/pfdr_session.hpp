@@ -57,6 +57,8 @@ class SessionBase {
     virtual void result(void *X_host, int *it, void *Obj_host,
                         void *Dif_host) = 0;
     virtual void *device_x() = 0;
+    // capture (once) the graphs a later run(iters) replays; no iteration runs
+    virtual void prepare(int iters) { (void)iters; }
     int64_t device_bytes = 0;
     int64_t reordered = 0;  // internal locality relabelling applied
     int64_t split_blocks = 0;  // vertex blocks on the split-incidence path
@@ -71,6 +73,7 @@ class SessionBase {
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
     int64_t ghosts = 0;        // partitioned: ghost (halo) vertices of this rank
     int64_t graphs = 0;        // chunks of iterations replayed as hipGraphs
+    int64_t speculative = 0;   // evolution decision overlapped with the next iteration
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;

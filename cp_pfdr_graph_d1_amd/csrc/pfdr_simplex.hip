@@ -1163,11 +1163,15 @@ class SimplexSession final : public SessionBase {
     bool graphs_ok_ = false;
     std::map<int, hipGraphExec_t> graphs_;
     void run_bodies(int n);
+    bool capturable_ = false;  // prepare(): graphs of any run length on request
+  public:
+    void prepare(int iters) override;
+  private:
     // small single-GPU problems: a chunk of iterations in one workgroup
     // (k_sx_tiny_iterate; PFDR_SX_TINY = most (edge, label) entries, 0 off)
     bool tiny_ = false;
     void tiny_chunk(int n);
-    hipGraphExec_t chunk_graph();
+    hipGraphExec_t chunk_graph(int n);
     void drop_graphs() {
         for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
         graphs_.clear();
@@ -1312,7 +1316,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     pins_.release();  // the stream was synchronised above
     stopped_ = itMax_ <= 0;
     // (RCCL partitions replay captured chunks too; loopback ranks rendezvous on the host)
-    graphs_ok_ = (!halo_ || halo_->tr->capturable()) && !rec_obj_ && itMax_ >= 2 * chunk_;
+    capturable_ = (!halo_ || halo_->tr->capturable()) && !rec_obj_;
+    graphs_ok_ = capturable_ && itMax_ >= 2 * chunk_;
     {
         const char *t = getenv("PFDR_SX_TINY");
         const long maxEK = t ? atol(t) : kSxTinyEK;
@@ -1320,7 +1325,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
                 EK_ > 0 && EK_ <= maxEK && nbs_ <= (t ? kSxTinyMaxBlocks : SxTinyBlocks<real>::v) &&
                 !(track_ && evo == PFDR_EVOLUTION_SEQUENTIAL);
         tiny = tiny_ ? 1 : 0;
-        if (tiny_) graphs_ok_ = false;
+        if (tiny_) graphs_ok_ = capturable_ = false;
     }
     const long nglob = track_ == 2 ? Vglob_ : Vglob_ * K_;  // terms over all ranks
     seqdif_ = track_ && !tiny_ && !(halo_ && track_ == 2) &&
@@ -1355,10 +1360,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     }
     if (graphs_ok_) {  // instantiated with the setup
         try {
-            (void)chunk_graph();
+            (void)chunk_graph(chunk_);
         } catch (const std::exception &) {
             if (!halo_) throw;
-            graphs_ok_ = false;  // this transport would not capture: launch directly
+            graphs_ok_ = capturable_ = false;  // this transport would not capture: launch directly
             (void)hipGetLastError();
         }
     }
@@ -1569,14 +1574,14 @@ void SimplexSession<real>::tiny_chunk(int n) {
 // the captured graph of a whole chunk (chunk_ bodies), instantiated once --
 // at the end of the setup, and again after a reconditioning dropped it
 template <typename real>
-hipGraphExec_t SimplexSession<real>::chunk_graph() {
-    auto it = graphs_.find(chunk_);
+hipGraphExec_t SimplexSession<real>::chunk_graph(int n) {
+    auto it = graphs_.find(n);
     if (it != graphs_.end()) return it->second;
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-        for (int i = 0; i < chunk_; i++) body();
+        for (int i = 0; i < n; i++) body();
     } catch (...) {
         (void)hipStreamEndCapture(stream, &g);
         if (g) (void)hipGraphDestroy(g);
@@ -1586,19 +1591,30 @@ hipGraphExec_t SimplexSession<real>::chunk_graph() {
     const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     PFDR_HIP(e);
-    graphs_.emplace(chunk_, ge);
+    graphs_.emplace(n, ge);
     return ge;
 }
 
-// whole chunks replay the captured graph; a partial chunk (the tail of a
-// run) is launched directly rather than captured for one use
 template <typename real>
 void SimplexSession<real>::run_bodies(int n) {
+    if (!prof.on && capturable_ && graphs_.count(n)) {  // prepared (or whole) chunk
+        PFDR_HIP(hipGraphLaunch(graphs_[n], stream));
+        return;
+    }
     if (!graphs_ok_ || prof.on || n != chunk_) {
         for (int i = 0; i < n; i++) body();
         return;
     }
-    PFDR_HIP(hipGraphLaunch(chunk_graph(), stream));
+    PFDR_HIP(hipGraphLaunch(chunk_graph(chunk_), stream));
+}
+
+// the graphs a run of `iters` iterations will replay, built now
+template <typename real>
+void SimplexSession<real>::prepare(int iters) {
+    if (!capturable_ || iters <= 0) return;
+    if (iters >= chunk_) (void)chunk_graph(chunk_);
+    if (iters % chunk_) (void)chunk_graph(iters % chunk_);
+    PFDR_HIP(hipStreamSynchronize(stream));
 }
 
 template <typename real>

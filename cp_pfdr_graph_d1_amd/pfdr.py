@@ -52,7 +52,7 @@ EXPORTED = (
     "pfdr_cpgraph_simplex_capacities", "pfdr_cpgraph_simplex_expand",
     "pfdr_cpgraph_simplex_activate", "pfdr_cpgraph_simplex_merge", "pfdr_cpgraph_simplex_labels",
     "pfdr_cpgraph_capacities_duplex", "pfdr_cpgraph_activate_duplex",
-    "pfdr_session_create", "pfdr_session_run", "pfdr_session_result",
+    "pfdr_session_create", "pfdr_session_run", "pfdr_session_prepare", "pfdr_session_result",
     "pfdr_session_device_x", "pfdr_session_set_profiling", "pfdr_session_profile_filter",
     "pfdr_session_kernel_stats", "pfdr_session_sync",
     "pfdr_session_device_bytes", "pfdr_session_query", "pfdr_session_destroy",
@@ -540,6 +540,10 @@ class Session:
 
     def sync(self):
         _check(self.lib.pfdr_session_sync(self.h), "pfdr_session_sync")
+
+    def prepare(self, iters):
+        """capture the hipGraphs run(iters) will replay (no iteration runs)"""
+        _check(self.lib.pfdr_session_prepare(self.h, C.c_int(int(iters))), "pfdr_session_prepare")
 
     def profile(self, on=True, period=1, only=None):
         """time kernels with HIP events: every `period`-th launch, of the

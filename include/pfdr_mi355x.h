@@ -206,6 +206,12 @@ int pfdr_session_create(pfdr_session **out, const pfdr_problem *p);
 /* Run up to `iters` more iterations (stopping early on difTol / itMax as the
  * reference does).  *it_total receives the total iteration count so far. */
 int pfdr_session_run(pfdr_session *s, int iters, int *it_total);
+/* Capture now the hipGraphs that a later pfdr_session_run(s, iters) replays
+ * (chunks of 32 iterations and the run's tail), so that the run itself
+ * instantiates nothing; no iteration runs.  A no-op where the session
+ * launches directly (small one-workgroup graphs, objective record, loopback
+ * partitions). */
+int pfdr_session_prepare(pfdr_session *s, int iters);
 /* Copy X (or P) back to host memory, and the iteration count; Obj/Dif copy
  * it+1 / it values when recorded (may be NULL). */
 int pfdr_session_result(pfdr_session *s, void *X_host, int *it, void *Obj_host,

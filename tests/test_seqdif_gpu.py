@@ -129,7 +129,42 @@ def test_auto_sequential_simplex_matches_restatement(gpu_lib):
         assert np.array_equal(P, Po)
 
 
-def test_relabelled_session_sums_in_caller_order(gpu_lib):
+@pytest.mark.parametrize("pieces", [(3000,), (7, 50, 3000), (31, 1, 32, 3000)],
+                         ids=["one-run", "runs-7-50", "runs-31-1-32"])
+def test_speculative_decision_matches_restatement(gpu_lib, pieces):
+    """difRcd = 0 at size: the evolution sums and the decision on iteration t
+    run beside the sweeps of t + 1 (speculative session, X ping-ponged); the
+    stopping iteration, every Dif and X equal the restatement's whatever the
+    run lengths (chunks of 32 replayed, partial chunks launched, prepared
+    tails replayed) and wherever in a chunk the stop falls"""
+    import oracle
+    from cp_pfdr_graph_d1_amd import pfdr
+    dt = np.float32
+    V, Eu, Ev, Y = _grid_problem(512, dt, seed=4)
+    La = np.full(Eu.size, 0.1, dt)
+    L1 = np.full(V, 0.01, dt)
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, np.zeros(V, dt), Y,
+                     La_l1=L1, rho=1.5, condMin=1e-3, difRcd=0.0, difTol=1e-4, itMax=3000,
+                     record_dif=True)
+    try:
+        assert s.query("speculative") == 1 and s.query("seqdif") == 1
+        for n in pieces:
+            s.prepare(n)
+            s.run(n)
+        X, it, _, Dif = s.result()
+    finally:
+        s.close()
+    Xo, ito, _, Difo = oracle.Oracle("port").quadratic_d1_l1(
+        np.zeros(V, dt), Y, None, 0, Eu, Ev, La, L1, 0, pfdr.SCAL, None, 1.5, 1e-3, 0.0, 1e-4,
+        3000, dif=True)
+    print("pieces %s: it %d / %d" % (pieces, it, ito))
+    assert it == ito < 3000
+    assert np.array_equal(Dif[:it], Difo[:ito])
+    assert np.array_equal(X, Xo)
+
+
+@pytest.mark.parametrize("difRcd", [1e-2, 0.0], ids=["recond", "speculative"])
+def test_relabelled_session_sums_in_caller_order(gpu_lib, difRcd):
     """random vertex labels, relabelling forced on: the terms are stored at
     the caller's labels, so Dif equals the plain (unrelabelled) session's
     and the restatement's, bit for bit"""
@@ -145,11 +180,11 @@ def test_relabelled_session_sums_in_caller_order(gpu_lib):
     La = np.full(Eu.size, 0.1, dt)
     c = dict(solver="l1", X0=np.zeros(V, dt), Y=Yp, A=None, N=0, Eu=Eu, Ev=Ev, La_d1=La,
              La_l1=np.full(V, 0.01, dt), positivity=0, Ltype=pfdr.SCAL, L=None, rho=1.5,
-             condMin=1e-3, difRcd=1e-2, difTol=1e-4, itMax=2000)
+             condMin=1e-3, difRcd=difRcd, difTol=1e-4, itMax=2000)
     X1, it1, D1, s1 = _session_replay(c, False, pfdr.EVOLUTION_SEQUENTIAL, pfdr.REORDER_ON)
     X0, it0, D0, s0 = _session_replay(c, False, pfdr.EVOLUTION_SEQUENTIAL, pfdr.REORDER_OFF)
     Xo, ito, _, Do = oracle.Oracle("port").quadratic_d1_l1(
-        c["X0"], Yp, None, 0, Eu, Ev, La, c["La_l1"], 0, pfdr.SCAL, None, 1.5, 1e-3, 1e-2,
+        c["X0"], Yp, None, 0, Eu, Ev, La, c["La_l1"], 0, pfdr.SCAL, None, 1.5, 1e-3, difRcd,
         1e-4, 2000, dif=True)
     print("it %d / %d / %d" % (it1, it0, ito))
     assert s1 == s0 == 1
