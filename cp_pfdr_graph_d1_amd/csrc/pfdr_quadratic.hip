@@ -243,6 +243,7 @@ class QuadSession final : public SessionBase {
     // blocks whose lists fit the LDS (the others gather through the CSR)
     bool tiled_ = false;
     DevBuf<unsigned short> d2_;
+    DevBuf<unsigned char> deg8_;  // CSR entries per vertex (tile_sum)
     DevBuf<unsigned short> luv_;  // both ends mod 256 (k_edge_sweep_tl)
     DevBuf<int> erec_;            // per edge block: u blocks and v runs (k_edge_sweep_tl)
     DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_;
@@ -615,7 +616,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
-    acc(d2_.n * 2 + luv_.n * 2 +
+    acc(d2_.n * 2 + luv_.n * 2 + deg8_.n +
         (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
     if (halo_) {
         plan_overlap();
@@ -890,6 +891,8 @@ void QuadSession<real>::build_tiles() {
                                                               fill.p, tstart_.p, tlen_.p);
     tok_.alloc(nb);
     k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, kTileCap, tok_.p);
+    deg8_.alloc(V_);
+    k_tile_deg<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, deg8_.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipMemcpyAsync(h.data(), tok_.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
     PFDR_HIP(hipStreamSynchronize(s));
@@ -1297,7 +1300,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.late = fuse_ ? 1 : 0;
     a.E = E_;
     if (tiled_) {
-        a.d2 = d2_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
+        a.d2 = d2_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
         a.gi = gi_.p;  // (Ga, 1/Aux) in one load

@@ -225,9 +225,12 @@ __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__res
 constexpr int kTileCap = 4096;  // staged entries per vertex block (LDS: GatherCap)
 constexpr int kTileRuns = 128;  // v-end runs per vertex block
 
+// Each vertex's slots [my0, my0 + deg) in the block's list come from its
+// degree (deg8: one byte per vertex, < 256 in every tiled block -- k_tile_ok)
+// by a block scan, instead of two CSR pointers (1 B per vertex, not 4).
 template <typename real, int GB, bool ZD = false>
 __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
-                                         const int *__restrict__ ptr,
+                                         const unsigned char *__restrict__ deg8,
                                          const unsigned short *__restrict__ d2,
                                          const int *__restrict__ ustart,
                                          const int *__restrict__ tptr,
@@ -235,15 +238,20 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const int *__restrict__ tlen,
                                          const real *__restrict__ wz, real *lds, int *runs,
                                          real wv = real(1)) {
-    const int tid = threadIdx.x;
-    const int v0 = blk * kBlock, vend = min(v0 + kBlock, V);
-    const int p0 = ptr[v0];
-    const int my0 = (v < V ? ptr[v] : ptr[vend]) - p0;
-    const int my1 = (v < V ? ptr[v + 1] : ptr[vend]) - p0;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int dg = v < V ? deg8[v] : 0;
     const int us = ustart[blk], nu = ustart[blk + 1] - us;
     const int t0 = tptr[blk], nt = tptr[blk + 1] - t0;
-    // run table: starts, then inclusive prefix of the lengths (wave 0)
-    int *rs = runs, *rp = runs + kTileRuns;
+    // run table: starts, then inclusive prefix of the lengths (wave 0);
+    // the degrees' wave totals after it (read after the barriers below)
+    int *rs = runs, *rp = runs + kTileRuns, *wt = runs + 2 * kTileRuns;
+    int dinc = dg;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(dinc, o, kWave);
+        if (lane >= o) dinc += y;
+    }
+    if (lane == kWave - 1) wt[w] = dinc;
     if (tid < kWave) {
         int acc = 0;
         for (int c = 0; c < nt; c += kWave) {
@@ -305,6 +313,9 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
             if (b + u * kBlock + tid < nv) lds[d[u]] = w[u];
     }
     __syncthreads();
+    int my0 = dinc - dg;
+    for (int q = 0; q < w; q++) my0 += wt[q];
+    const int my1 = my0 + dg;
     // the vertex's slots in order; four reads in flight ahead of the adds
     real s = real(0);
     int j = my0;
@@ -409,12 +420,24 @@ static __global__ void k_tile_runs_fill(long n, const int *__restrict__ a,
 }
 
 // tok[b] = 1 when block b's entries fit the LDS list and its runs the table
+// tok[b] = 1: block b's list fits the LDS (cap entries), its runs the run
+// table, and every degree a byte (deg8, tile_sum)
 static __global__ void k_tile_ok(int V, int nb, const int *__restrict__ ptr,
                                  const int *__restrict__ tptr, int cap, int *__restrict__ tok) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const int v0 = b * kBlock, v1 = min(v0 + kBlock, V);
-    tok[b] = (ptr[v1] - ptr[v0] <= cap && tptr[b + 1] - tptr[b] <= kTileRuns) ? 1 : 0;
+    bool ok = ptr[v1] - ptr[v0] <= cap && tptr[b + 1] - tptr[b] <= kTileRuns;
+    for (int v = v0; ok && v < v1; v++) ok = ptr[v + 1] - ptr[v] < 256;
+    tok[b] = ok ? 1 : 0;
+}
+
+// deg8[v] = the vertex's CSR entries (clamped; blocks with a larger one are
+// not tiled)
+static __global__ void k_tile_deg(int V, const int *__restrict__ ptr,
+                                  unsigned char *__restrict__ deg8) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) deg8[v] = (unsigned char)min(ptr[v + 1] - ptr[v], 255);
 }
 
 // ------------------------------------------------ split incidence setup --
@@ -1881,6 +1904,7 @@ struct VArgs {
     // tiled contributions (null d2: off; see tile_sum)
     long E;
     const unsigned short *d2;
+    const unsigned char *deg8;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
     // Z-direct (tiled single-GPU sessions with one edge weight, no A1): the
     // lists hold Z (side-major, zs) and each term is (a0 * invAux[v]) * z
@@ -2005,7 +2029,7 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
     if (a.d2 && a.tok[blk])  // block-uniform
-        x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.ptr, a.d2, a.ustart, a.tptr, a.tstart,
+        x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.d2, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
     else if (!ZD && a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
@@ -2037,7 +2061,8 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     }
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[2 * kTileRuns];  // block scan (split_sum) / run table (tile_sum)
+    __shared__ int scan[2 * kTileRuns + kBlock / kWave];  // block scan (split_sum) / run table
+                                                         // and degree totals (tile_sum)
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
     if (lb >= a.bsplit) lb += a.bjump;

@@ -140,7 +140,7 @@ def test_speculative_decision_matches_restatement(gpu_lib, pieces):
     import oracle
     from cp_pfdr_graph_d1_amd import pfdr
     dt = np.float32
-    V, Eu, Ev, Y = _grid_problem(512, dt, seed=4)
+    V, Eu, Ev, Y = _grid_problem(600, dt, seed=4)  # 1,407 blocks: past the fused range
     La = np.full(Eu.size, 0.1, dt)
     L1 = np.full(V, 0.01, dt)
     s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, np.zeros(V, dt), Y,

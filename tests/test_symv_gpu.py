@@ -68,3 +68,26 @@ def test_dense_ata_matches_oracle(gpu_lib, oracle_port, V, nx, dt, asym, symv):
     assert got[1] == ref[1] == 20
     assert e <= _tol(dt, True)
     assert np.allclose(got[2], ref[2], rtol=(1e-4 if dt == np.float32 else 1e-10))
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_dense_ata_symv_converged_matches_oracle(gpu_lib, oracle_port, dt):
+    """the upper-triangle products run to the tolerance (reconditioning on
+    the way): the stopping iteration within 2 of the restatement's and the
+    converged iterate within the converged dense tolerance (the full-size
+    A^tA pin, c3_ata_k3 at V = 32,768 against the reference's f64 run, is
+    tests/test_fullsize_pin_gpu.py)"""
+    V = 8320
+    A, Y, Eu, Ev, L = _problem(V, dt, 17, 64)
+    La = np.full(Eu.size, 0.05, dt)
+    L1 = np.full(V, 0.01, dt)
+    X0 = np.zeros(V, dt)
+    Af = A.ravel(order="F")
+    kw = dict(La_l1=L1, positivity=0, Ltype=0, L=L, rho=1.5, condMin=1e-3, difRcd=1e-2,
+              difTol=1e-4 if dt == np.float32 else 1e-6, itMax=1000, dif=True)
+    ref = oracle_port.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
+    got = gpu_lib.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
+    e = G.rel_l2(got[0], ref[0])
+    print("V=%d %s converged: it %d / %d, rel_l2 %.3e" % (V, np.dtype(dt).name, got[1], ref[1], e))
+    assert 0 < ref[1] < 1000 and abs(got[1] - ref[1]) <= 2
+    assert e <= _tol(dt, False)
