@@ -599,6 +599,8 @@ struct SxProjArgs {
     const Ctrl<real> *ctrl;
     real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
     const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
+    real *Po;          // where the new P and (P, step) go (null: P, PF in place)
+    SxR2<real> *PFo;
 };
 
 // projection + evolution + next explicit step, one thread per vertex
@@ -630,11 +632,11 @@ __global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
         }
         for (int k = 0; k < K; k++) {
             const real p = x[k];
-            a.P[b + k] = p;
+            (a.Po ? a.Po : a.P)[b + k] = p;
             SxR2<real> q;
             q.x = p;
             q.y = sx_explicit(a.c, p, a.GaQ[b + k], a.Q[b + k]);
-            a.PF[b + k] = q;
+            (a.PFo ? a.PFo : a.PF)[b + k] = q;
         }
     }
     if (a.track) {
@@ -672,6 +674,8 @@ struct SxVArgs {
     const Ctrl<real> *ctrl;
     real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
     const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
+    real *Po;          // where the new P and (P, step) go (null: P, PF in place)
+    SxR2<real> *PFo;
 };
 
 // One block of the fused vertex sweep: NT lanes (t = the lane within
@@ -756,12 +760,12 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             dif += d;
             if (a.terms) a.terms[a.tmap ? (long)a.tmap[v] * K + k : i] = d;
         }
-        a.P[i] = p;
+        (a.Po ? a.Po : a.P)[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
         SxR2<real> q;
         q.x = p;
         q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
-        a.PF[i] = q;
+        (a.PFo ? a.PFo : a.PF)[i] = q;
     }
     if (a.track) {
         dif = wave_sum(dif);
@@ -1092,10 +1096,16 @@ class SimplexSession final : public SessionBase {
             pinned_small_put(hctrl_);
         }
         drop_graphs();
+        for (hipEvent_t e : evv_) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : evd_) if (e) (void)hipEventDestroy(e);
+        if (evs_) {
+            (void)hipStreamSynchronize(evs_);
+            (void)hipStreamDestroy(evs_);
+        }
     }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
-    void *device_x() override { return P_.p; }
+    void *device_x() override { return Pb(it_); }
 
   private:
     SxConst<real> c_;
@@ -1126,7 +1136,23 @@ class SimplexSession final : public SessionBase {
     ChainSum<real> chain_;
     DevBuf<int> tlab_;
     DevBuf<real> tall_;
-    void seq_evolution();
+    void seq_evolution(real *terms, hipStream_t s);
+    // Speculative iteration (one GPU, sequential evolution, difRcd = 0, no
+    // objective record), as the quadratic session's spec_: the sum and the
+    // decision on iteration t run on evs_ beside the sweeps of t + 1, P and
+    // (P, step) are ping-ponged (iteration t reads Pb(t - 1), writes Pb(t)),
+    // the terms double-buffered; a stop at t leaves P_t in Pb(t) and the
+    // speculative t + 1 is discarded.
+    bool spec_ = false;
+    int it0_ = 0;
+    DevBuf<real> P2_;
+    DevBuf<SxR2<real>> PF2_;
+    real *Pb(int t) { return spec_ && (t & 1) ? P2_.p : P_.p; }
+    SxR2<real> *PFb(int t) { return spec_ && (t & 1) ? PF2_.p : PF_.p; }
+    hipStream_t evs_ = nullptr;
+    hipEvent_t evv_[2] = {}, evd_[2] = {};
+    void body_spec(int i, int n);
+    void sweeps(const Ctrl<real> *c, int t);  // edge + vertex pass of iteration t
     DevBuf<int> Eu_, Ev_;
     DevBuf<real> La_d1_, La_f_, Q_, P_, Pavg_, Ga_, GaQ_, invAux_, lab_;
     // (P, explicit step) pairs per (v, k), ghosts included: written with P
@@ -1357,6 +1383,20 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
             chain_.init(nterms_, 1, *halo_->tr);
         }
         seqdif = 1;
+        spec_ = !halo_ && difRcd_ == real(0) && !rec_obj_;
+        if (spec_) {
+            DevBuf<real> t2(2 * (size_t)n);  // terms of both parities
+            std::swap(terms_.p, t2.p);
+            std::swap(terms_.n, t2.n);
+            P2_.alloc((size_t)Vg_ * K_);
+            PF2_.alloc((size_t)Vg_ * K_);
+            PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
+            for (int k = 0; k < 2; k++) {
+                PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
+                PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
+            }
+            speculative = 1;
+        }
     }
     if (graphs_ok_) {  // instantiated with the setup
         try {
@@ -1371,9 +1411,9 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
-                            &Dif_, &terms_, &tall_})
+                            &Dif_, &terms_, &tall_, &P2_})
         device_bytes += (int64_t)(b->n * sizeof(real));
-    device_bytes += (int64_t)((GI_.n + PF_.n) * sizeof(SxR2<real>));
+    device_bytes += (int64_t)((GI_.n + PF_.n + PF2_.n) * sizeof(SxR2<real>));
 }
 
 // ref :64-370
@@ -1428,69 +1468,38 @@ void SimplexSession<real>::objective() {
     PFDR_HIP(hipGetLastError());
 }
 
+// iteration t = it0_ + 1 + i of a speculative session (see spec_)
+template <typename real>
+void SimplexSession<real>::body_spec(int i, int n) {
+    hipStream_t s = stream;
+    const int t = it0_ + 1 + i;
+    if (i >= 2) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // the decision on t - 2
+    real *terms = terms_.p + (t & 1) * (terms_.n / 2);
+    real *const keep = terms_.p;
+    terms_.p = terms;
+    sweeps(ctrl_.p, t);
+    terms_.p = keep;
+    PFDR_HIP(hipEventRecord(evv_[t & 1], s));
+    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[t & 1], 0));
+    seq_evolution(terms, evs_);  // overlaps the sweeps of t + 1
+    k_sx_finalize<real><<<1, kBlock, 0, evs_>>>(0, nullptr, Vglob_, track_, ctrl_.p,
+                                                rec_dif_ ? Dif_.p : nullptr, red_.p);
+    PFDR_HIP(hipGetLastError());
+    PFDR_HIP(hipEventRecord(evd_[t & 1], evs_));
+    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // join: the chunk's last
+}
+
 template <typename real>
 void SimplexSession<real>::body() {
     hipStream_t s = stream;
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
-    if (EK_) {
-        ProfScope ps(prof, "sx_edge_sweep", s);
-        const int pair = K_ % 2 == 0 ? 2 : 1;  // see k_sx_edge_sweep
-        const int nb = grid_for(EK_ / pair);
-        const int xm = xcd_fit(nb, sx_xcd_e_);
-        if (pair == 2)
-            k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
-                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
-                                                               Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               vb_ ? nullptr : wz_.p,
-                                                               rho_, c, nb, xm);
-        else
-            k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PF_.p,
-                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
-                                                               Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               vb_ ? nullptr : wz_.p,
-                                                               rho_, c, nb, xm);
-    }
-    if (halo_) {
-        ProfScope ps(prof, "halo_push", s);
-        push_wz();
-    }
-    if (vb_) {
-        SxVArgs<real> a{};
-        a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
-        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
-        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
-        a.terms = seqdif_ ? terms_.p : nullptr;
-        a.tmap = tlab_.p;
-        ProfScope ps(prof, "sx_vertex_sweep", s);
-        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
-        a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
-        const int g = xcd_grid(nbs_, a.xcd);
-        k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
-    } else {
-        {
-            ProfScope ps(prof, "sx_average", s);
-            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, inc_.ptr.p,
-                                                                inc_.idx.p, wz_.p, Pavg_.p, c);
-        }
-        SxProjArgs<real> a{};
-        a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
-        a.P = P_.p; a.PF = PF_.p; a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
-        a.terms = seqdif_ ? terms_.p : nullptr;
-        a.tmap = tlab_.p;
-        ProfScope ps(prof, "sx_project", s);
-        launch_project(a);
-    }
-    if (halo_) {
-        ProfScope ps(prof, "halo_pull", s);
-        pullK(P_);
-        pullPF();
-    }
+    sweeps(c, 0);
     const int nparts = vb_ ? nbs_ : nbv_;
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
-        seq_evolution();
+        seq_evolution(terms_.p, s);
         k_sx_finalize<real><<<1, kBlock, 0, s>>>(0, nullptr, Vglob_, track_, ctrl_.p,
                                                  rec_dif_ ? Dif_.p : nullptr, red_.p);
     } else if (gated && halo_) {
@@ -1508,17 +1517,83 @@ void SimplexSession<real>::body() {
     if (rec_obj_) objective();
 }
 
+// the edge and vertex passes of one iteration (t: its number in a
+// speculative session, whose P buffers alternate; else 0, in place)
+template <typename real>
+void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
+    hipStream_t s = stream;
+    SxR2<real> *PFin = spec_ ? PFb(t - 1) : PF_.p;
+    real *Pin = spec_ ? Pb(t - 1) : P_.p;
+    real *Po = spec_ ? Pb(t) : nullptr;
+    SxR2<real> *PFo = spec_ ? PFb(t) : nullptr;
+    if (EK_) {
+        ProfScope ps(prof, "sx_edge_sweep", s);
+        const int pair = K_ % 2 == 0 ? 2 : 1;  // see k_sx_edge_sweep
+        const int nb = grid_for(EK_ / pair);
+        const int xm = xcd_fit(nb, sx_xcd_e_);
+        if (pair == 2)
+            k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
+                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Wd1u_.p, Wd1v_.p, Th_.p,
+                                                               vb_ ? nullptr : wz_.p,
+                                                               rho_, c, nb, xm);
+        else
+            k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
+                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Wd1u_.p, Wd1v_.p, Th_.p,
+                                                               vb_ ? nullptr : wz_.p,
+                                                               rho_, c, nb, xm);
+    }
+    if (halo_) {
+        ProfScope ps(prof, "halo_push", s);
+        push_wz();
+    }
+    if (vb_) {
+        SxVArgs<real> a{};
+        a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
+        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = Pin; a.PF = PFin;
+        a.Po = Po; a.PFo = PFo;
+        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        a.terms = seqdif_ ? terms_.p : nullptr;
+        a.tmap = tlab_.p;
+        ProfScope ps(prof, "sx_vertex_sweep", s);
+        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
+        a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
+        const int g = xcd_grid(nbs_, a.xcd);
+        k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
+    } else {
+        {
+            ProfScope ps(prof, "sx_average", s);
+            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, inc_.ptr.p,
+                                                                inc_.idx.p, wz_.p, Pavg_.p, c);
+        }
+        SxProjArgs<real> a{};
+        a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
+        a.P = Pin; a.PF = PFin; a.Po = Po; a.PFo = PFo;
+        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+        a.terms = seqdif_ ? terms_.p : nullptr;
+        a.tmap = tlab_.p;
+        ProfScope ps(prof, "sx_project", s);
+        launch_project(a);
+    }
+    if (halo_) {
+        ProfScope ps(prof, "halo_pull", s);
+        pullK(P_);
+        pullPF();
+    }
+    PFDR_HIP(hipGetLastError());
+}
+
 // red_[0] = the evolution sum over every (vertex, label) in the caller's
 // order, rounded as the reference's one-thread loop
 template <typename real>
-void SimplexSession<real>::seq_evolution() {
-    hipStream_t s = stream;
+void SimplexSession<real>::seq_evolution(real *terms, hipStream_t s) {
     const int *halt = &ctrl_.p->halt;
     if (!halo_) {
-        mono_sum<real>(nterms_, terms_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
+        mono_sum<real>(nterms_, terms, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
                        halt);
     } else if (!tlab_.p) {
-        chain_.run(*halo_->tr, terms_.p, 0, red_.p, halt, s);
+        chain_.run(*halo_->tr, terms, 0, red_.p, halt, s);
     } else {
         PFDR_HIP(hipMemcpyAsync(tall_.p, terms_.p, sizeof(real) * terms_.n,
                                 hipMemcpyDeviceToDevice, s));
@@ -1575,13 +1650,14 @@ void SimplexSession<real>::tiny_chunk(int n) {
 // at the end of the setup, and again after a reconditioning dropped it
 template <typename real>
 hipGraphExec_t SimplexSession<real>::chunk_graph(int n) {
-    auto it = graphs_.find(n);
+    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);  // speculative: P buffers by parity
+    auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     PFDR_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-        for (int i = 0; i < n; i++) body();
+        for (int i = 0; i < n; i++) spec_ ? body_spec(i, n) : body();
     } catch (...) {
         (void)hipStreamEndCapture(stream, &g);
         if (g) (void)hipGraphDestroy(g);
@@ -1591,18 +1667,20 @@ hipGraphExec_t SimplexSession<real>::chunk_graph(int n) {
     const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     PFDR_HIP(e);
-    graphs_.emplace(n, ge);
+    graphs_.emplace(key, ge);
     return ge;
 }
 
 template <typename real>
 void SimplexSession<real>::run_bodies(int n) {
-    if (!prof.on && capturable_ && graphs_.count(n)) {  // prepared (or whole) chunk
-        PFDR_HIP(hipGraphLaunch(graphs_[n], stream));
+    it0_ = it_;
+    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);
+    if (!prof.on && capturable_ && graphs_.count(key)) {  // prepared (or whole) chunk
+        PFDR_HIP(hipGraphLaunch(graphs_[key], stream));
         return;
     }
     if (!graphs_ok_ || prof.on || n != chunk_) {
-        for (int i = 0; i < n; i++) body();
+        for (int i = 0; i < n; i++) spec_ ? body_spec(i, n) : body();
         return;
     }
     PFDR_HIP(hipGraphLaunch(chunk_graph(chunk_), stream));
@@ -1612,6 +1690,7 @@ void SimplexSession<real>::run_bodies(int n) {
 template <typename real>
 void SimplexSession<real>::prepare(int iters) {
     if (!capturable_ || iters <= 0) return;
+    it0_ = it_;
     if (iters >= chunk_) (void)chunk_graph(chunk_);
     if (iters % chunk_) (void)chunk_graph(iters % chunk_);
     PFDR_HIP(hipStreamSynchronize(stream));
@@ -1679,7 +1758,7 @@ template <typename real>
 void SimplexSession<real>::result(void *X_host, int *it, void *Obj_host, void *Dif_host) {
     hipStream_t s = stream;
     HostPins hp(s);
-    if (X_host) hp.copy(X_host, P_.p, sizeof(real) * VK_, hipMemcpyDeviceToHost);
+    if (X_host) hp.copy(X_host, Pb(it_), sizeof(real) * VK_, hipMemcpyDeviceToHost);
     if (it) *it = it_;
     if (Obj_host && rec_obj_)
         hp.copy(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost);

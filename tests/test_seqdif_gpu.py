@@ -163,6 +163,40 @@ def test_speculative_decision_matches_restatement(gpu_lib, pieces):
     assert np.array_equal(X, Xo)
 
 
+@pytest.mark.parametrize("difTol", [1e-3, 1.0], ids=["l1", "labels"])
+def test_speculative_simplex_matches_restatement(gpu_lib, difTol):
+    """the simplex session's speculative decision (P and (P, step)
+    ping-ponged), run in pieces: it, Dif and P equal the restatement's"""
+    import oracle
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, simplex_observation
+    n, K = 256, 5
+    Eu, Ev = grid_graph((n, n), 8)
+    V = n * n
+    v = np.arange(V)
+    lab = ((v % n) * 3 // n) + 3 * ((v // n) * 2 // n)
+    Q = simplex_observation(V, K, 4, lab, np.float32)
+    La = np.full(Eu.size, 0.05, np.float32)
+    Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
+    s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, np.float32, V, Eu.size, Eu, Ev, La, Q.copy(), Q,
+                     K=K, al=0.1, rho=1.0, condMin=0.1, difRcd=0.0, difTol=difTol, itMax=400,
+                     record_dif=True)
+    try:
+        assert s.query("speculative") == 1
+        for m in (5, 33, 400):
+            s.prepare(m)
+            s.run(m)
+        P, it, _, Dif = s.result()
+    finally:
+        s.close()
+    Po, ito, _, Difo = oracle.Oracle("port").loss_d1_simplex(
+        Q.copy(), Q, K, Eu, Ev, La, 0.1, None, 1.0, 0.1, 0.0, difTol, 400, dif=True)
+    print("difTol %g: it %d / %d" % (difTol, it, ito))
+    assert it == ito
+    assert np.array_equal(Dif[:it], Difo[:ito])
+    assert np.array_equal(P, Po)
+
+
 @pytest.mark.parametrize("difRcd", [1e-2, 0.0], ids=["recond", "speculative"])
 def test_relabelled_session_sums_in_caller_order(gpu_lib, difRcd):
     """random vertex labels, relabelling forced on: the terms are stored at
