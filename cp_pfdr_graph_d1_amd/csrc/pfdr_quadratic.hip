@@ -490,8 +490,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         DevBuf<real> X0;
         copy_in(X0, p->X, V, mem, s, pins_);
         if (reordered_) permute(X0, order_.p, V, s);
-        xp_.alloc(Vg);
-        PFDR_HIP(hipMemsetAsync(xp_.p, 0, Vg * sizeof(R2<real>), s));
+        xp_.alloc(Vg + 2);  // (+2: the tiled edge sweep stages vertex pairs, k_edge_sweep_tl)
+        PFDR_HIP(hipMemsetAsync(xp_.p, 0, (Vg + 2) * sizeof(R2<real>), s));
         k_xp_init<real><<<grid_for(V), kBlock, 0, s>>>(V_, X0.p, xp_.p);
         PFDR_HIP(hipGetLastError());
         pull(xp_.p, sizeof(R2<real>));
@@ -501,7 +501,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     // (tiled partitioned ranks: Z's received tail after the 2E local entries,
     // for the Z-direct iteration)
     Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0));
-    gi_.alloc(Vg);
+    gi_.alloc(Vg + 2);
+    PFDR_HIP(hipMemsetAsync(gi_.p, 0, (Vg + 2) * sizeof(R2<real>), s));
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
     if (flavour_ == 0 && p->La_l1) Th_l1_.alloc(V);
     nbv_ = grid_for(V);
@@ -659,8 +660,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             DevBuf<real> t2(4 * (size_t)tstride_);  // terms of both parities
             std::swap(terms_.p, t2.p);
             std::swap(terms_.n, t2.n);
-            xp2_.alloc(Vg_);
-            PFDR_HIP(hipMemcpyAsync(xp2_.p, xp_.p, sizeof(R2<real>) * Vg_,
+            xp2_.alloc(Vg_ + 2);  // (+2 as xp_)
+            PFDR_HIP(hipMemcpyAsync(xp2_.p, xp_.p, sizeof(R2<real>) * (Vg_ + 2),
                                     hipMemcpyDeviceToDevice, s));
             PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
             for (int k = 0; k < 2; k++) {

@@ -1513,13 +1513,27 @@ __device__ __forceinline__ void tl_gather(
         }
     }
     const int su = ub0 * kBlock + uoff;  // first staged vertex
+    // f32: the staged (X, P) and (Ga, invAux) pairs are loaded two vertices
+    // per 16-byte access from the even vertex at or below su (one load per
+    // array and lane covers 512 vertices: the headline's u range is ~170) --
+    // the texture addresser, not HBM, bounds this sweep, so its load
+    // instructions are what counts.  f64 pairs are 16 bytes already.
+    constexpr bool PAIRS = sizeof(real) == 4;
+    const int sb = su & ~1, so = su - sb;  // PAIRS: entries counted from sb
     R2<real> sx[NS0], sg[NS0];
+    Pk<real, 4> px{}, pg{};
     if (staged) {
+        if (PAIRS) {
+            const int j = min(tid, (span + so - 1) >> 1);  // (the arrays carry 2 spare vertices)
+            px = ldv<real, 4>(reinterpret_cast<const real *>(xp + sb) + 4 * j);
+            pg = ldv<real, 4>(reinterpret_cast<const real *>(gi + sb) + 4 * j);
+        } else {
 #pragma unroll
-        for (int q = 0; q < NS0; q++) {
-            const int i = su + min(q * kBlock + tid, span - 1);
-            sx[q] = xp[i];
-            sg[q] = gi[i];
+            for (int q = 0; q < NS0; q++) {
+                const int i = su + min(q * kBlock + tid, span - 1);
+                sx[q] = xp[i];
+                sg[q] = gi[i];
+            }
         }
     }
     if (full) {
@@ -1555,17 +1569,35 @@ __device__ __forceinline__ void tl_gather(
         }
     }
     if (staged) {
-#pragma unroll
-        for (int q = 0; q < NS0; q++) {
-            const int i = q * kBlock + tid;
-            if (i < span) {
-                s_xp[i] = sx[q];
-                s_gi[i] = sg[q];
+        if (PAIRS) {
+            const int i0 = 2 * tid - so;  // LDS slot of the pair's first vertex
+            if (2 * tid < span + so) {       // the pair starts inside the staged range
+                if (i0 >= 0) {
+                    s_xp[i0].x = px.v[0]; s_xp[i0].y = px.v[1];
+                    s_gi[i0].x = pg.v[0]; s_gi[i0].y = pg.v[1];
+                }
+                if (i0 + 1 < span) {
+                    s_xp[i0 + 1].x = px.v[2]; s_xp[i0 + 1].y = px.v[3];
+                    s_gi[i0 + 1].x = pg.v[2]; s_gi[i0 + 1].y = pg.v[3];
+                }
             }
-        }
-        for (int i = NS0 * kBlock + tid; i < span; i += kBlock) {  // wide ranges
-            s_xp[i] = xp[su + i];
-            s_gi[i] = gi[su + i];
+            for (int i = 2 * kBlock - so + tid; i < span; i += kBlock) {  // wide ranges
+                s_xp[i] = xp[su + i];
+                s_gi[i] = gi[su + i];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NS0; q++) {
+                const int i = q * kBlock + tid;
+                if (i < span) {
+                    s_xp[i] = sx[q];
+                    s_gi[i] = sg[q];
+                }
+            }
+            for (int i = NS0 * kBlock + tid; i < span; i += kBlock) {  // wide ranges
+                s_xp[i] = xp[su + i];
+                s_gi[i] = gi[su + i];
+            }
         }
     }
     __syncthreads();

@@ -102,10 +102,12 @@ def test_fullsize_matches_reference(gpu_lib, name):
         assert below.size and below[0] == it - 1
 
 
-@pytest.mark.parametrize("name,k", [("headline_conv", 2), ("c4_conv", 2), ("headline_conv", 3)])
+@pytest.mark.parametrize("name,k", [("headline_conv", 2), ("c4_conv", 2), ("headline_conv", 3),
+                                    ("c2_conv", 4), ("c5_k1", 8)])
 def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
     """The converged full-size solves split over k ranks (loopback threads on
-    one GPU: the RCCL session code with device-copy exchanges): the iterate
+    one GPU: the RCCL session code with device-copy exchanges), and C5 (640^3,
+    262M vertices, the 8-GPU configuration) split over 8 ranks: the iterate
     evolution is summed rank to rank with the reference's sequential rounding
     (ChainSum, pfdr_halo.hpp), so the stopping iteration, every Dif and X's
     sha256 equal the reference's (src/PFDR_graph_quadratic_d1_l1.cpp:429,
@@ -121,6 +123,11 @@ def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
             k, pfdr.PFDR_KIND_SIMPLEX, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["P0"], a["Q"],
             La_l1=a["La_f"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
             difTol=a["difTol"], itMax=a["itMax"], record_dif=True, K=a["K"], al=a["al"])
+    elif case["solver"] == "bounds":  # C5: 640^3, the 8-GPU configuration, as 8 ranks
+        X, it, _, Dif, info = P.solve_loopback(
+            k, pfdr.PFDR_KIND_BOUNDS, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
+            lo=a["lo"], hi=a["hi"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True)
     else:
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_L1, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],

@@ -166,11 +166,12 @@ def test_speculative_decision_matches_restatement(gpu_lib, pieces):
 @pytest.mark.parametrize("difTol", [1e-3, 1.0], ids=["l1", "labels"])
 def test_speculative_simplex_matches_restatement(gpu_lib, difTol):
     """the simplex session's speculative decision (P and (P, step)
-    ping-ponged), run in pieces: it, Dif and P equal the restatement's"""
+    ping-ponged), run in pieces: it, Dif and P equal the restatement's
+    (384^2 vertices: AUTO's 2^17 terms for the label count too)"""
     import oracle
     from cp_pfdr_graph_d1_amd import pfdr
     from cp_pfdr_graph_d1_amd.graphs import grid_graph, simplex_observation
-    n, K = 256, 5
+    n, K = 384, 5
     Eu, Ev = grid_graph((n, n), 8)
     V = n * n
     v = np.arange(V)
