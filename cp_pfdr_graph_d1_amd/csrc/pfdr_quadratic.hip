@@ -500,7 +500,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     const size_t En = E ? E : 1;
     // (tiled partitioned ranks: Z's received tail after the 2E local entries,
     // for the Z-direct iteration)
-    Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0));
+    // (+4: the tiled vertex sweep reads whole 16-byte vectors of a run's tail, tile_sum)
+    Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0) + 4);
     gi_.alloc(Vg + 2);
     PFDR_HIP(hipMemsetAsync(gi_.p, 0, (Vg + 2) * sizeof(R2<real>), s));
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
@@ -835,7 +836,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
-    wz_.alloc(2 * E_ + R ? 2 * E_ + R : 1);
+    wz_.alloc(2 * E_ + R + 4);  // (+4: tile_sum's whole vectors)
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
@@ -850,7 +851,7 @@ void QuadSession<real>::build_tiles() {
     hipStream_t s = stream;
     const int nb = grid_for(V_);
     const long R = halo_ ? halo_->R : 0;
-    d2_.alloc(2 * (size_t)E_ + R);
+    d2_.alloc(2 * (size_t)E_ + R + 4);  // (+4: tile_sum's whole vectors)
     k_tile_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, d2_.p);
     luv_.alloc((size_t)E_);
     k_tile_luv<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, luv_.p);

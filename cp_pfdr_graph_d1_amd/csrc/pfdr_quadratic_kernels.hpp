@@ -223,11 +223,20 @@ __device__ __forceinline__ real split_sum(int V, int v0, int v, const int *__res
 // wants it, and each lane then adds its vertex's slots in order -- the sums
 // of gather_sum / split_sum bit for bit, without a single gathered load.
 constexpr int kTileCap = 4096;  // staged entries per vertex block (LDS: GatherCap)
-constexpr int kTileRuns = 128;  // v-end runs per vertex block
 
 // Each vertex's slots [my0, my0 + deg) in the block's list come from its
 // degree (deg8: one byte per vertex, < 256 in every tiled block -- k_tile_ok)
 // by a block scan, instead of two CSR pointers (1 B per vertex, not 4).
+// The runs are staged with 16-byte loads (4 f32 / 2 f64 contributions and
+// their 16-bit slots per access, from the aligned vector at or below each
+// run's start; elements outside the run are dropped): a quarter of the
+// load instructions of one contribution per access, which is what the
+// texture addresser prices.  The contribution and slot arrays carry one
+// spare vector at their end for the last run's tail.
+constexpr int kTileRuns = 128;  // v-end runs per vertex block
+template <typename real>
+struct TileVec { static constexpr int n = Vec<real>::kPer16B; };  // entries per staged vector
+
 template <typename real, int GB, bool ZD = false>
 __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const unsigned char *__restrict__ deg8,
@@ -238,13 +247,16 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const int *__restrict__ tlen,
                                          const real *__restrict__ wz, real *lds, int *runs,
                                          real wv = real(1)) {
+    constexpr int VE = TileVec<real>::n, GV = GB / VE > 0 ? GB / VE : 1;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const int dg = v < V ? deg8[v] : 0;
     const int us = ustart[blk], nu = ustart[blk + 1] - us;
     const int t0 = tptr[blk], nt = tptr[blk + 1] - t0;
-    // run table: starts, then inclusive prefix of the lengths (wave 0);
-    // the degrees' wave totals after it (read after the barriers below)
-    int *rs = runs, *rp = runs + kTileRuns, *wt = runs + 2 * kTileRuns;
+    // run table (wave 0): starts, lengths, inclusive prefix of the runs'
+    // vector counts; the degrees' wave totals after it (read after the
+    // barriers below)
+    int *rs = runs, *rl = runs + kTileRuns, *rp = runs + 2 * kTileRuns;
+    int *wt = runs + 3 * kTileRuns;
     int dinc = dg;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -256,61 +268,82 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         int acc = 0;
         for (int c = 0; c < nt; c += kWave) {
             const int i = c + tid;
-            int len = 0;
+            int nvec = 0;
             if (i < nt) {
-                rs[i] = tstart[t0 + i];
-                len = tlen[t0 + i];
+                const int st = tstart[t0 + i], len = tlen[t0 + i];
+                rs[i] = st;
+                rl[i] = len;
+                const long A = E + st;
+                nvec = len > 0 ? (int)((A + len - 1) / VE - A / VE + 1) : 0;
             }
 #pragma unroll
             for (int o = 1; o < kWave; o <<= 1) {
-                const int y = __shfl_up(len, o, kWave);
-                if (tid >= o) len += y;
+                const int y = __shfl_up(nvec, o, kWave);
+                if (tid >= o) nvec += y;
             }
-            if (i < nt) rp[i] = acc + len;
-            acc += __shfl(len, kWave - 1, kWave);
+            if (i < nt) rp[i] = acc + nvec;
+            acc += __shfl(nvec, kWave - 1, kWave);
         }
     }
-    // u ends: one contiguous run, GB slots then GB values in flight per lane
-    for (int b = 0; b < nu; b += kBlock * GB) {
-        unsigned short d[GB];
-        real w[GB];
+    // u ends: one contiguous run [us, us + nu), GV vectors in flight per lane
+    {
+        const long fu = us / VE;
+        const int nvu = nu > 0 ? (int)((us + nu - 1) / VE - fu + 1) : 0;
+        for (int b = 0; b < nvu; b += kBlock * GV) {
+            Pk<unsigned short, VE> d[GV];
+            Pk<real, VE> x[GV];
 #pragma unroll
-        for (int u = 0; u < GB; u++) {
-            const int j = b + u * kBlock + tid;
-            const long a = us + (long)min(j, nu - 1);
-            d[u] = d2[a];
-            w[u] = wz[a];
+            for (int u = 0; u < GV; u++) {
+                const long base = (fu + min(b + u * kBlock + tid, nvu - 1)) * VE;
+                d[u] = ldv<unsigned short, VE>(d2 + base);
+                x[u] = ldv<real, VE>(wz + base);
+            }
+#pragma unroll
+            for (int u = 0; u < GV; u++) {
+                const int k = b + u * kBlock + tid;
+                if (k < nvu) {
+                    const long base = (fu + k) * VE;
+#pragma unroll
+                    for (int q = 0; q < VE; q++)
+                        if (base + q >= us && base + q < (long)us + nu) lds[d[u].v[q]] = x[u].v[q];
+                }
+            }
         }
-#pragma unroll
-        for (int u = 0; u < GB; u++)
-            if (b + u * kBlock + tid < nu) lds[d[u]] = w[u];
     }
     __syncthreads();  // run table
-    const int nv = nt ? rp[nt - 1] : 0;
-    int lo = 0, end = nt ? rp[0] : 0, beg = 0;  // run of the lane's entry k, its bounds
-    for (int b = 0; b < nv; b += kBlock * GB) {
-        unsigned short d[GB];
-        real w[GB];
-        long ad[GB];
+    const int nvv = nt ? rp[nt - 1] : 0;
+    // run of the lane's vector k and its bounds in the vector list
+    int lo = 0, end = nt ? rp[0] : 0, beg = 0;
+    for (int b = 0; b < nvv; b += kBlock * GV) {
+        Pk<unsigned short, VE> d[GV];
+        Pk<real, VE> x[GV];
+        long base[GV], A[GV];
+        int L[GV];
 #pragma unroll
-        for (int u = 0; u < GB; u++) {
-            // the lane's entries grow by 256: its run only advances (about
-            // one run per step on the BASELINE grids), no search
-            const int k = min(b + u * kBlock + tid, nv - 1);
+        for (int u = 0; u < GV; u++) {
+            // the lane's vectors grow by 256: its run only advances, no search
+            const int k = min(b + u * kBlock + tid, nvv - 1);
             while (end <= k) {
                 beg = end;
                 end = rp[++lo];
             }
-            ad[u] = E + rs[lo] + (k - beg);
+            A[u] = E + rs[lo];
+            L[u] = rl[lo];
+            base[u] = (A[u] / VE + (k - beg)) * VE;
         }
 #pragma unroll
-        for (int u = 0; u < GB; u++) {
-            d[u] = d2[ad[u]];
-            w[u] = wz[ad[u]];
+        for (int u = 0; u < GV; u++) {
+            d[u] = ldv<unsigned short, VE>(d2 + base[u]);
+            x[u] = ldv<real, VE>(wz + base[u]);
         }
 #pragma unroll
-        for (int u = 0; u < GB; u++)
-            if (b + u * kBlock + tid < nv) lds[d[u]] = w[u];
+        for (int u = 0; u < GV; u++)
+            if (b + u * kBlock + tid < nvv) {
+#pragma unroll
+                for (int q = 0; q < VE; q++)
+                    if (base[u] + q >= A[u] && base[u] + q < A[u] + L[u])
+                        lds[d[u].v[q]] = x[u].v[q];
+            }
     }
     __syncthreads();
     int my0 = dinc - dg;
@@ -2093,7 +2126,7 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     }
     __shared__ real lds[GatherCap<real>::v];
     __shared__ real red[2][kBlock / kWave];
-    __shared__ int scan[2 * kTileRuns + kBlock / kWave];  // block scan (split_sum) / run table
+    __shared__ int scan[3 * kTileRuns + kBlock / kWave];  // block scan (split_sum) / run table
                                                          // and degree totals (tile_sum)
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;

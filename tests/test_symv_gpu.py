@@ -84,10 +84,22 @@ def test_dense_ata_symv_converged_matches_oracle(gpu_lib, oracle_port, dt):
     X0 = np.zeros(V, dt)
     Af = A.ravel(order="F")
     kw = dict(La_l1=L1, positivity=0, Ltype=0, L=L, rho=1.5, condMin=1e-3, difRcd=1e-2,
-              difTol=1e-4 if dt == np.float32 else 1e-6, itMax=1000, dif=True)
+              difTol=2e-3 if dt == np.float32 else 1e-5, itMax=2000, dif=True)
     ref = oracle_port.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
     got = gpu_lib.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
     e = G.rel_l2(got[0], ref[0])
     print("V=%d %s converged: it %d / %d, rel_l2 %.3e" % (V, np.dtype(dt).name, got[1], ref[1], e))
-    assert 0 < ref[1] < 1000 and abs(got[1] - ref[1]) <= 2
-    assert e <= _tol(dt, False)
+    assert 0 < ref[1] < 2000 and abs(got[1] - ref[1]) <= 2
+    if dt == np.float64:
+        assert e <= _tol(dt, False)
+        return
+    # f32 over ~200 iterations: both runs regroup / accumulate rounding in
+    # their own dot products; the yardstick is the f64 solve of the same
+    # (exactly widened) problem, as for the full-size dense pins: the GPU
+    # iterate at least as close to it as the restatement's f32 run
+    w = lambda a: None if a is None else np.asarray(a, np.float64)
+    kw64 = dict(kw, La_l1=w(L1), L=w(L))
+    r64 = oracle_port.quadratic_d1_l1(w(X0), w(Y), w(Af), -V, Eu, Ev, w(La), **kw64)
+    e_gpu, e_ref = G.rel_l2(got[0], r64[0]), G.rel_l2(ref[0], r64[0])
+    print("  vs f64: GPU %.3e, restatement f32 %.3e (it %d)" % (e_gpu, e_ref, r64[1]))
+    assert e_gpu <= 1.5 * e_ref + 1e-6
