@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -43,6 +45,64 @@ namespace {
 // below this many vertices a call stays on one GPU: CP's reduced problems
 // are latency-bound, and a split only adds exchanges to them
 constexpr long kMultiMinVertices = 1L << 20;
+
+// Persistent host threads, one per rank slot: a thread keeps its library
+// stream (lib_stream is per thread and device) and its device's cached
+// blocks across calls, instead of a fresh thread -- and a fresh stream --
+// for every drop-in call.  Never destroyed (like the device cache).
+class RankPool {
+  public:
+    // run f(r) for r in [0, n) on n pool threads; returns when all are done
+    void run(int n, const std::function<void(int)> &f) {
+        std::unique_lock<std::mutex> lk(m_);
+        while ((int)slots_.size() < n) {
+            slots_.emplace_back(new Slot());
+            Slot *sl = slots_.back().get();
+            const int r = (int)slots_.size() - 1;
+            std::thread([this, sl, r] { loop(sl, r); }).detach();
+        }
+        fn_ = &f;
+        pending_ = n;
+        for (int r = 0; r < n; r++) { slots_[r]->go = true; slots_[r]->cv.notify_one(); }
+        done_.wait(lk, [&] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    struct Slot {
+        std::condition_variable cv;
+        bool go = false;
+    };
+    void loop(Slot *sl, int r) {
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            sl->cv.wait(lk, [&] { return sl->go; });
+            sl->go = false;
+            const std::function<void(int)> *f = fn_;
+            lk.unlock();
+            (*f)(r);  // never throws (rank_main catches)
+            lk.lock();
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable done_;
+    std::vector<std::unique_ptr<Slot>> slots_;
+    const std::function<void(int)> *fn_ = nullptr;
+    int pending_ = 0;
+};
+
+RankPool &rank_pool() {
+    static RankPool *p = new RankPool();
+    return *p;
+}
+
+// one drop-in multi-device call at a time (the pool and the communicators
+// serve one partitioned solve)
+std::mutex &multidev_call_mutex() {
+    static std::mutex *m = new std::mutex();
+    return *m;
+}
 
 struct DeviceConfig {
     std::mutex m;
@@ -246,15 +306,18 @@ void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it
         } catch (const std::exception &ex) {
             err[r] = "rank " + std::to_string(r) + " (device " + std::to_string(devs[r]) + "): " +
                      ex.what();
+        } catch (...) {
+            err[r] = "rank " + std::to_string(r) + ": unknown exception";
         }
         if (!err[r].empty()) {  // wake the other ranks: their collectives fail too
             if (loop) pfdr_loopback_abort(hub, err[r].c_str());
             else for (ncclComm_t cm : comms) comm_abort(cm);
         }
     };
-    std::vector<std::thread> th;
-    for (int r = 0; r < n; r++) th.emplace_back(rank_main, r);
-    for (auto &t : th) t.join();
+    {
+        std::lock_guard<std::mutex> call(multidev_call_mutex());
+        rank_pool().run(n, rank_main);
+    }
     if (hub) pfdr_loopback_destroy(hub);
     // the first failure is the cause, the others its consequence
     std::string first;
