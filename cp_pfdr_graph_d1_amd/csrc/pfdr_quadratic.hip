@@ -673,6 +673,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         }
     }
     xr_ = xw_ = xp_.p;
+    // a speculative session launches directly on its two streams: the
+    // decision's kernels must run BESIDE the next sweeps, and a replayed
+    // graph ran its branches one after the other (headline_conv 0.852
+    // ms/iter with the graph, r4h)
+    if (spec_) graphs_ok_ = capturable_ = false;
     if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
     acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
     acc(tall_.n * sizeof(real) + chain_.ws.n + ampg_.n * sizeof(real) +

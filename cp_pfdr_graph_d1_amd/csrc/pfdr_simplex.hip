@@ -1396,6 +1396,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
                 PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
             }
             speculative = 1;
+            graphs_ok_ = capturable_ = false;  // launched directly (see QuadSession)
         }
     }
     if (graphs_ok_) {  // instantiated with the setup

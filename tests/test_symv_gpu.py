@@ -84,7 +84,7 @@ def test_dense_ata_symv_converged_matches_oracle(gpu_lib, oracle_port, dt):
     X0 = np.zeros(V, dt)
     Af = A.ravel(order="F")
     kw = dict(La_l1=L1, positivity=0, Ltype=0, L=L, rho=1.5, condMin=1e-3, difRcd=1e-2,
-              difTol=2e-3 if dt == np.float32 else 1e-5, itMax=2000, dif=True)
+              difTol=2e-3, itMax=2000, dif=True)
     ref = oracle_port.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
     got = gpu_lib.quadratic_d1_l1(X0, Y, Af, -V, Eu, Ev, La, **kw)
     e = G.rel_l2(got[0], ref[0])
