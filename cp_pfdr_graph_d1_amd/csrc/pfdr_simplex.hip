@@ -684,7 +684,8 @@ struct SxVArgs {
 // no live lane); the block's evolution partial goes to *part_out (lane 0).
 // The body of k_sx_vertex_sweep, shared with the one-workgroup
 // k_sx_tiny_iterate (four blocks side by side).
-template <typename real, int NT>
+// SPLIT (speculative sessions): the new P and (P, step) go to Po / PFo
+template <typename real, int NT, bool SPLIT = false>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
                                                 real *ms, real *red, real *part_out) {
     const int K = a.c.K, vb = a.vb;
@@ -760,12 +761,12 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             dif += d;
             if (a.terms) a.terms[a.tmap ? (long)a.tmap[v] * K + k : i] = d;
         }
-        (a.Po ? a.Po : a.P)[i] = p;
+        (SPLIT ? a.Po : a.P)[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
         SxR2<real> q;
         q.x = p;
         q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
-        (a.PFo ? a.PFo : a.PF)[i] = q;
+        (SPLIT ? a.PFo : a.PF)[i] = q;
     }
     if (a.track) {
         dif = wave_sum(dif);
@@ -778,14 +779,14 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     }
 }
 
-template <typename real, int NT>
+template <typename real, int NT, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real xs[NT], ms[NT];
     __shared__ real red[NT / kWave];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
-    sx_vertex_block<real, NT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+    sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
 }
 
 // ------------------------------------------ small problems, one launch --
@@ -1561,7 +1562,8 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
         a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
-        k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
+        if (Po) k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
+        else k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
     } else {
         {
             ProfScope ps(prof, "sx_average", s);
