@@ -197,22 +197,24 @@ struct ChainSum {
              hipStream_t s) {
         constexpr long TILE = MonoTile<real>::TILE;
         const long nt = (n + TILE - 1) / TILE;
-        long long *summ = static_cast<long long *>((void *)ws.p);
-        double *tsum = reinterpret_cast<double *>(summ + 2 * kMonoCand * nt * nsum);
-        int *ebase = reinterpret_cast<int *>(tsum + nt * nsum);
+        const MonoWs<real> w(ws.p, nt, nsum);
+        double *tsum = w.tsum;
+        int *ebase = w.ebase;
         const dim3 gt((unsigned)nt, (unsigned)nsum), g1(1, (unsigned)nsum);
         k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, tsum, halt);
         PFDR_HIP(hipMemsetAsync(tot.p, 0, sizeof(double) * nranks * nsum, s));
         k_mono_total<<<g1, 256, 0, s>>>((int)nt, tsum, tot.p + (size_t)rank * nsum, halt);
         PFDR_HIP(hipGetLastError());
         tr.allreduce_sum(tot.p, nranks * nsum, PFDR_F64, s);
-        k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, nullptr, 0, ebase, halt, tot.p, rank);
-        k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, summ, halt);
+        k_mono_predict<real><<<g1, kPredThreads, 0, s>>>((int)nt, tsum, nullptr, 0, ebase, halt,
+                                                         tot.p, rank);
+        k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, w.summ, w.subs,
+                                                           halt);
         PFDR_HIP(hipGetLastError());
         tr.chain_recv(seed.p, sizeof(real) * nsum, s);
-        k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ,
-                                                      rank > 0 ? seed.p : nullptr, 1, 0, nullptr,
-                                                      out, nullptr, halt);
+        k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, w.summ,
+                                                      w.subs, rank > 0 ? seed.p : nullptr, 1, 0,
+                                                      nullptr, out, nullptr, halt);
         PFDR_HIP(hipGetLastError());
         tr.chain_send(out, sizeof(real) * nsum, s);
         tr.broadcast(out, sizeof(real) * nsum, nranks - 1, s);

@@ -20,9 +20,42 @@
 // Used for the amplitude sum of the preconditioner, whose order is the
 // reference's single-thread loop (src/PFDR_graph_quadratic_d1_l1.cpp:146-152).
 #pragma once
+#include <type_traits>
+
 #include "pfdr_dev.hpp"
 
 namespace pfdr {
+
+// Phase timers of the walk for tools/monoprof.hip (compiled out otherwise):
+// lane 0 of sum 0 charges the wall-clock time since the previous tick to
+// phase k and counts the phase.
+#ifdef PFDR_MONO_PROFILE
+__device__ unsigned long long g_mono_prof[32];
+struct MonoProf {
+    unsigned long long t[16], n[16], last;
+    __device__ MonoProf() : last(wall_clock64()) {
+        for (int k = 0; k < 16; k++) t[k] = n[k] = 0;
+    }
+    __device__ void tick(int k) {
+        const unsigned long long now = wall_clock64();
+        t[k] += now - last;
+        n[k]++;
+        last = now;
+    }
+    __device__ void out() const {
+        if (threadIdx.x == 0 && blockIdx.y == 0)
+            for (int k = 0; k < 16; k++) {
+                g_mono_prof[k] = t[k];
+                g_mono_prof[16 + k] = n[k];
+            }
+    }
+};
+#else
+struct MonoProf {
+    __device__ void tick(int) {}
+    __device__ void out() const {}
+};
+#endif
 
 template <typename real> struct FpGrid;
 template <> struct FpGrid<float> {
@@ -33,6 +66,11 @@ template <> struct FpGrid<double> {
     static constexpr int p = 53, emin = -1022;
     static constexpr double min_normal = 2.2250738585072013831e-308;
 };
+
+// integer counts on the grid of a binade: below 2^p + 1 per tile after
+// saturation, so 32 bits hold them for f32 (half the ALU work of 64)
+template <typename real>
+using mcnt = typename std::conditional<sizeof(real) == 4, int, long long>::type;
 
 // exponent of the spacing of the floats around s >= 0 (subnormals and 0 share
 // the spacing of the smallest normal binade)
@@ -45,7 +83,7 @@ __device__ __forceinline__ int grid_exp(real s) {
 // term a >= 0 on the grid 2^ue: floor(a / u) and how the remainder rounds
 // (0 down, 1 up, 2 exact half, 3 the term alone reaches 2^p u)
 template <typename real>
-__device__ __forceinline__ void grid_term(real a, int ue, long long &fl, int &cls) {
+__device__ __forceinline__ void grid_term(real a, int ue, mcnt<real> &fl, int &cls) {
     constexpr real top = real(1ll << FpGrid<real>::p);
     const real q = ldexp(a, -ue);  // exact (a scaled by a power of two), or
     if (!(q < top)) {              // underflowed far below one half
@@ -54,29 +92,30 @@ __device__ __forceinline__ void grid_term(real a, int ue, long long &fl, int &cl
         return;
     }
     const real f = floor(q), r = q - f;
-    fl = (long long)f;
+    fl = (mcnt<real>)f;
     cls = r < real(0.5) ? 0 : (r > real(0.5) ? 1 : 2);
 }
 
 template <typename real>
-__device__ __forceinline__ long long grid_inc(long long fl, int cls, long long parity) {
-    constexpr long long cap = (1ll << FpGrid<real>::p) + 1;
+__device__ __forceinline__ mcnt<real> grid_inc(mcnt<real> fl, int cls, mcnt<real> parity) {
+    constexpr mcnt<real> cap = (1ll << FpGrid<real>::p) + 1;
     return cls == 3 ? cap : fl + (cls == 2 ? ((parity + fl) & 1) : cls);
 }
 
 // (d0, d1) summaries; increments saturate at 2^p + 1 (past that point the
 // binade has been left and everything after the exit is discarded)
 template <typename real>
-__device__ __forceinline__ long long sat_add(long long a, long long b) {
-    constexpr long long cap = (1ll << FpGrid<real>::p) + 1;
-    const long long x = a + b;
+__device__ __forceinline__ mcnt<real> sat_add(mcnt<real> a, mcnt<real> b) {
+    constexpr mcnt<real> cap = (1ll << FpGrid<real>::p) + 1;
+    const mcnt<real> x = a + b;
     return x > cap ? cap : x;
 }
 template <typename real>
-__device__ __forceinline__ void compose(long long a0, long long a1, long long &b0, long long &b1) {
+__device__ __forceinline__ void compose(mcnt<real> a0, mcnt<real> a1, mcnt<real> &b0,
+                                        mcnt<real> &b1) {
     // (A then B) for start parity 0 and 1; result in (b0, b1)
-    const long long n0 = sat_add<real>(a0, (a0 & 1) ? b1 : b0);
-    const long long n1 = sat_add<real>(a1, ((1 + a1) & 1) ? b1 : b0);
+    const mcnt<real> n0 = sat_add<real>(a0, (a0 & 1) ? b1 : b0);
+    const mcnt<real> n1 = sat_add<real>(a1, ((1 + a1) & 1) ? b1 : b0);
     b0 = n0;
     b1 = n1;
 }
@@ -88,16 +127,29 @@ template <typename real>
 struct MonoTile {
     static constexpr int J = 64 / sizeof(real);             // terms per lane
     static constexpr long TILE = (long)kMonoThreads * J;     // terms per tile
+    static constexpr int SUB = kWave * J;                   // terms per sub-tile (a wave's)
+    static constexpr int NSUB = kMonoThreads / kWave;       // sub-tiles per tile
+    static constexpr int FJ = SUB / kMonoThreads;           // terms per lane in a fine scan
 };
 
-constexpr int kMonoSerial = 256;  // terms added by one lane after each exit
+constexpr int kMonoSerial = 256;     // terms added by one lane after each exit (mono_range)
+constexpr int kMonoSerialFine = kWave;  // the same in the walk (fine_scan, serial_wave)
 
-// Shared state of a workgroup walking terms one tile at a time.
+// Shared state of a workgroup walking terms one tile at a time.  The tile
+// held in registers is also kept in LDS: the terms after an exit are added
+// by one lane from there, and the scan resumes on the registers (one global
+// load per tile, however many exits it holds).
 struct MonoShared {
-    alignas(16) char ser[kMonoSerial * sizeof(double)];
-    long long w0[kMonoThreads / kWave], w1[kMonoThreads / kWave];
+    static constexpr int NW = kMonoThreads / kWave;
+    alignas(16) char tile[kMonoThreads * 64];
+    long long w0[NW], w1[NW];                // wave totals (mono_range)
+    long long fw0[2][NW], fw1[2][NW];        // wave totals of fine_scan, by parity
+    long long cw0[NW], cw1[NW], lastS[NW];   // the walk's chain steps
+    long long subs[2 * kMonoCand * NW];      // the staged tile's sub-tile summaries
+    long long cexl[2];                       // fine_scan: the count before its exit, by parity
+    int cnt[NW];
     int exit_at;
-    int k;
+    int fexit[2];                            // fine_scan's exit, by parity
     long long S;
     double sd;  // the running sum's bits travel as a double (exact for both reals)
 };
@@ -123,12 +175,12 @@ __device__ __forceinline__ void mono_load(real *x, const real *__restrict__ a, l
 }
 
 // lane summary (d0, d1) of J terms on the grid 2^ue
-template <typename real>
-__device__ __forceinline__ void mono_run(const real *x, int ue, long long &d0, long long &d1) {
+template <typename real, int N = MonoTile<real>::J>
+__device__ __forceinline__ void mono_run(const real *x, int ue, mcnt<real> &d0, mcnt<real> &d1) {
     d0 = d1 = 0;
 #pragma unroll
-    for (int j = 0; j < MonoTile<real>::J; j++) {
-        long long fl;
+    for (int j = 0; j < N; j++) {
+        mcnt<real> fl;
         int cls;
         grid_term(x[j], ue, fl, cls);
         d0 = sat_add<real>(d0, grid_inc<real>(fl, cls, d0));
@@ -136,14 +188,86 @@ __device__ __forceinline__ void mono_run(const real *x, int ue, long long &d0, l
     }
 }
 
-// inclusive scan of summaries over the wave (earlier lanes first)
-template <typename real>
-__device__ __forceinline__ void mono_wave_scan(long long &i0, long long &i1, int lane) {
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const long long p0 = __shfl_up(i0, o, kWave), p1 = __shfl_up(i1, o, kWave);
-        if (lane >= o) compose<real>(p0, p1, i0, i1);
+// DPP moves (gfx9 encodings; a lane whose source is outside the pattern
+// reads 0, the identity of compose): row_shr:n (lane i <- i - n within its
+// row of 16), row_bcast:15 / :31 (the previous row's last lane to the rows
+// of ROWS), wave_shr:1 (lane i <- i - 1)
+constexpr int kDppRowShr = 0x110, kDppWaveShr1 = 0x138, kDppBcast15 = 0x142, kDppBcast31 = 0x143;
+template <int CTRL, int ROWS, typename T>
+__device__ __forceinline__ T dpp_mov(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xf, false);
+    } else {
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffff), CTRL, ROWS, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, ROWS, 0xf, false);
+        return (T)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
     }
+}
+template <typename real, int CTRL, int ROWS>
+__device__ __forceinline__ void scan_step(mcnt<real> &i0, mcnt<real> &i1) {
+    mcnt<real> p0 = dpp_mov<CTRL, ROWS>(i0), p1 = dpp_mov<CTRL, ROWS>(i1);
+    compose<real>(p0, p1, i0, i1);
+}
+
+// inclusive scan of summaries over the wave (earlier lanes first): rows of
+// 16 by row_shr 1, 2, 4, 8, then the rows joined by the two broadcasts
+template <typename real>
+__device__ __forceinline__ void mono_wave_scan(mcnt<real> &i0, mcnt<real> &i1) {
+    scan_step<real, kDppRowShr + 1, 0xf>(i0, i1);
+    scan_step<real, kDppRowShr + 2, 0xf>(i0, i1);
+    scan_step<real, kDppRowShr + 4, 0xf>(i0, i1);
+    scan_step<real, kDppRowShr + 8, 0xf>(i0, i1);
+    scan_step<real, kDppBcast15, 0xa>(i0, i1);
+    scan_step<real, kDppBcast31, 0xc>(i0, i1);
+}
+// lane k's count (k uniform)
+template <typename T>
+__device__ __forceinline__ T read_lane(T v, int k) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_amdgcn_readlane(v, k);
+    } else {
+        const unsigned lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), k);
+        const unsigned hi = __builtin_amdgcn_readlane((int)(v >> 32), k);
+        return (T)(((unsigned long long)hi << 32) | lo);
+    }
+}
+// the summary of the lanes before this one (lane 0: the identity)
+template <typename real>
+__device__ __forceinline__ void mono_wave_excl(mcnt<real> i0, mcnt<real> i1, mcnt<real> &e0,
+                                               mcnt<real> &e1) {
+    e0 = dpp_mov<kDppWaveShr1, 0xf>(i0);
+    e1 = dpp_mov<kDppWaveShr1, 0xf>(i1);
+}
+
+// s + q[0] + ... + q[m-1] for m <= kWave, every lane of the wave alike: one
+// LDS read per lane, then the terms in order from the lanes (fully unrolled:
+// the zeros past m add nothing to a sum of nonnegative terms)
+template <typename real>
+__device__ __forceinline__ real serial_wave(real s, const real *q, int m) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const real v = lane < m ? q[lane] : real(0);
+#pragma unroll
+    for (int i = 0; i < kWave; i++) {
+        if constexpr (sizeof(real) == 4) {
+            s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+        } else {
+            const long long b = __double_as_longlong(v);
+            const unsigned lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), i);
+            const unsigned hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
+            s += __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        }
+    }
+    return s;
+}
+
+// s + q[0] + ... + q[m-1] by one lane from LDS (q of any alignment)
+template <typename real>
+__device__ __forceinline__ real serial_add(real s, const real *q, int m) {
+    while (m > 0 && (reinterpret_cast<uintptr_t>(q) & 15)) {
+        s += *q++;
+        m--;
+    }
+    return ordered_add(s, q, m);
 }
 
 // s + a[lo] + ... + a[hi-1] by the whole workgroup, term by term semantics:
@@ -151,49 +275,61 @@ __device__ __forceinline__ void mono_wave_scan(long long &i0, long long &i1, int
 // it with one floating-point addition, and resumes after that term.
 template <typename real>
 __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s, MonoShared &sh) {
-    constexpr int NT = kMonoThreads, J = MonoTile<real>::J;
+    constexpr int J = MonoTile<real>::J, W = Vec<real>::kPer16B;
     constexpr long TILE = MonoTile<real>::TILE;
-    constexpr long long TOP = 1ll << FpGrid<real>::p;
+    constexpr mcnt<real> TOP = 1ll << FpGrid<real>::p;
+    using P = Pk<real, W>;
     const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+    real *tb = reinterpret_cast<real *>(sh.tile);
     // tiles are aligned to TILE (16-byte loads); terms before `start` are
     // masked to zero, which adds nothing
-    long start = lo;
+    long start = lo, xb = -1;  // xb: the tile held in x and in sh.tile
     real x[J], nx[J];
-    bool have = false;  // nx holds the tile at `base`
+    bool have = false;  // nx holds the tile at xb + TILE
     while (start < hi && s < Lim<real>::huge) {
         const int ue = grid_exp(s);
-        long long S = (long long)ldexp(s, -ue);  // s / u, an integer below 2^p
+        mcnt<real> S = (mcnt<real>)ldexp(s, -ue);  // s / u, an integer below 2^p
         bool left = false;
         for (long base = start / TILE * TILE; base < hi; base += TILE) {
-            if (have) {
+            if (base != xb) {
+                if (have && base == xb + TILE) {
 #pragma unroll
-                for (int j = 0; j < J; j++) x[j] = nx[j];
-            } else {
-                mono_load(x, a, hi, base, t);
+                    for (int j = 0; j < J; j++) x[j] = nx[j];
+                } else {
+                    mono_load(x, a, hi, base, t);
+                }
+                const bool more = base + TILE < hi;
+                if (more) mono_load(nx, a, hi, base + TILE, t);  // in flight during the scan
+                have = more;
+                xb = base;
+#pragma unroll
+                for (int v = 0; v < J / W; v++) {
+                    P pk;
+#pragma unroll
+                    for (int k = 0; k < W; k++) pk.v[k] = x[v * W + k];
+                    *reinterpret_cast<P *>(tb + t * J + v * W) = pk;
+                }
             }
-            const bool more = base + TILE < hi;
-            if (more) mono_load(nx, a, hi, base + TILE, t);  // in flight during the scan
-            have = more;
             if (start > base) {
 #pragma unroll
                 for (int j = 0; j < J; j++)
                     if (base + (long)t * J + j < start) x[j] = real(0);
             }
-            long long r0, r1;
+            mcnt<real> r0, r1;
             mono_run(x, ue, r0, r1);
-            long long i0 = r0, i1 = r1;
-            mono_wave_scan<real>(i0, i1, lane);
+            mcnt<real> i0 = r0, i1 = r1;
+            mono_wave_scan<real>(i0, i1);
             if (lane == kWave - 1) {
                 sh.w0[w] = i0;
                 sh.w1[w] = i1;
             }
-            long long e0 = __shfl_up(i0, 1, kWave), e1 = __shfl_up(i1, 1, kWave);
-            if (lane == 0) e0 = e1 = 0;
+            mcnt<real> e0, e1;
+            mono_wave_excl<real>(i0, i1, e0, e1);
             __syncthreads();
             // prefix of the earlier waves (in order), then this lane's start
-            long long q0 = 0, q1 = 0;
+            mcnt<real> q0 = 0, q1 = 0;
             for (int k = 0; k < w; k++) {
-                long long b0 = sh.w0[k], b1 = sh.w1[k];
+                mcnt<real> b0 = sh.w0[k], b1 = sh.w1[k];
                 compose<real>(q0, q1, b0, b1);
                 q0 = b0;
                 q1 = b1;
@@ -201,17 +337,17 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
             compose<real>(q0, q1, e0, e1);
             // this lane's exact starting count; only a lane whose run ends
             // outside the binade walks its terms to find the exit
-            long long cur = sat_add<real>(S, (S & 1) ? e1 : e0), cex = 0;
-            const long long end = sat_add<real>(cur, (cur & 1) ? r1 : r0);
+            mcnt<real> cur = sat_add<real>(S, (S & 1) ? e1 : e0), cex = 0;
+            const mcnt<real> end = sat_add<real>(cur, (cur & 1) ? r1 : r0);
             int mine = INT_MAX;
             real xex = real(0);
-            if (end >= TOP) {
+            if (cur < TOP && end >= TOP) {  // the one lane that leaves the binade
 #pragma unroll
                 for (int j = 0; j < J; j++) {
-                    long long fl;
+                    mcnt<real> fl;
                     int cls;
                     grid_term(x[j], ue, fl, cls);  // recomputed: fewer live registers
-                    const long long inc = grid_inc<real>(fl, cls, cur);
+                    const mcnt<real> inc = grid_inc<real>(fl, cls, cur);
                     if (mine == INT_MAX && (cls == 3 || cur + inc >= TOP)) {
                         mine = t * J + j;
                         cex = cur;
@@ -225,31 +361,26 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
             __syncthreads();
             const int ex = sh.exit_at;
             if (ex == INT_MAX) {  // the whole tile stays in the binade
-                if (t == NT - 1) sh.S = cur;
+                if (t == kMonoThreads - 1) sh.S = cur;
                 __syncthreads();
                 S = sh.S;
                 __syncthreads();
                 continue;
             }
-            // the earliest exit term: one ordinary addition (s = cex * u exactly)
-            if (mine == ex) sh.sd = (double)(ldexp((real)cex, ue) + xex);
-            __syncthreads();
-            s = (real)sh.sd;
-            if (t == 0) sh.exit_at = INT_MAX;
-            // exits cluster where the sum is young (it doubles every few
-            // terms): the next kMonoSerial terms are added by one lane, from LDS
+            // the earliest exit term: one ordinary addition (s = cex * u
+            // exactly); exits cluster where the sum is young (it doubles
+            // every few terms): the next kMonoSerial terms of the tile are
+            // added by the same lane, from LDS
             start = base + ex + 1;
-            const int m = (int)min((long)kMonoSerial, hi - start);
-            real *buf = reinterpret_cast<real *>(sh.ser);
-            for (int i = t; i < m; i += NT) buf[i] = a[start + i];
-            __syncthreads();
-            if (t == 0) sh.sd = (double)ordered_add(s, buf, m);
+            if (mine == ex) {
+                const int m = (int)min((long)kMonoSerial, min(hi, base + TILE) - start);
+                sh.sd = (double)serial_add(ldexp((real)cex, ue) + xex, tb + ex + 1, m);
+            }
             __syncthreads();
             s = (real)sh.sd;
-            start += m;
-            have = false;
+            if (t == 0) sh.exit_at = INT_MAX;  // every lane has read it
+            start += (int)min((long)kMonoSerial, min(hi, base + TILE) - start);
             left = true;
-            __syncthreads();
             break;
         }
         if (!left) {
@@ -258,6 +389,112 @@ __device__ real mono_range(const real *__restrict__ a, long lo, long hi, real s,
         }
     }
     return s;
+}
+
+// lane t's J terms x into the LDS copy of the tile
+template <typename real>
+__device__ __forceinline__ void mono_stage(real *tb, const real *x, int t) {
+    constexpr int J = MonoTile<real>::J, W = Vec<real>::kPer16B;
+    using P = Pk<real, W>;
+#pragma unroll
+    for (int v = 0; v < J / W; v++) {
+        P pk;
+#pragma unroll
+        for (int k = 0; k < W; k++) pk.v[k] = x[v * W + k];
+        *reinterpret_cast<P *>(tb + t * J + v * W) = pk;
+    }
+}
+
+// One pass of the workgroup over sub-tile `sub` of the tile staged in LDS
+// (tb; positions relative to the tile, those before p masked, len terms in
+// the tile) on the grid 2^ue from the count S.  No exit: S <- the count at
+// the sub-tile's end, returns -1.  Otherwise the first term that leaves the
+// binade is added with one floating-point addition and the next
+// min(kMonoSerialFine, len - exit - 1) terms one by one (every lane alike,
+// from LDS): returns the exit position, the running sum after those terms
+// in s.  Every lane learns from the wave totals whether the sub-tile stays
+// in the binade (the counts never decrease), so a pass without an exit
+// costs one barrier; the LDS slots alternate with the parity `par` of the
+// pass, so no barrier is needed to release them.
+template <typename real>
+__device__ int fine_scan(const real *tb, int sub, int p, int len, int ue, mcnt<real> &S, real &s,
+                         MonoShared &sh, int &par, MonoProf &mp) {
+    constexpr int FJ = MonoTile<real>::FJ, SUB = MonoTile<real>::SUB, NW = MonoShared::NW;
+    constexpr mcnt<real> TOP = 1ll << FpGrid<real>::p;
+    const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave, pr = par;
+    par ^= 1;
+    const int i0 = sub * SUB + t * FJ;
+    real x[FJ];
+#pragma unroll
+    for (int j = 0; j < FJ; j++) x[j] = (i0 + j >= p) ? tb[i0 + j] : real(0);
+    mcnt<real> r0, r1;
+    mono_run<real, FJ>(x, ue, r0, r1);
+    mcnt<real> c0 = r0, c1 = r1, e0, e1;
+    mono_wave_scan<real>(c0, c1);
+    if (lane == kWave - 1) {
+        sh.fw0[pr][w] = c0;
+        sh.fw1[pr][w] = c1;
+    }
+    mono_wave_excl<real>(c0, c1, e0, e1);
+    mp.tick(5);
+    __syncthreads();
+    mp.tick(6);
+    // the earlier waves' prefix and the sub-tile's total
+    mcnt<real> v0[NW], v1[NW];
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        v0[k] = (mcnt<real>)sh.fw0[pr][k];
+        v1[k] = (mcnt<real>)sh.fw1[pr][k];
+    }
+    mcnt<real> q0 = 0, q1 = 0, f0 = 0, f1 = 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        if (k == w) {
+            f0 = q0;
+            f1 = q1;
+        }
+        mcnt<real> b0 = v0[k], b1 = v1[k];
+        compose<real>(q0, q1, b0, b1);
+        q0 = b0;
+        q1 = b1;
+    }
+    const mcnt<real> tot = sat_add<real>(S, (S & 1) ? q1 : q0);
+    mp.tick(7);
+    if (tot < TOP) {
+        S = tot;
+        return -1;
+    }
+    compose<real>(f0, f1, e0, e1);
+    mcnt<real> cur = sat_add<real>(S, (S & 1) ? e1 : e0);
+    const mcnt<real> end = sat_add<real>(cur, (cur & 1) ? r1 : r0);
+    // the counts never decrease: exactly one lane starts inside the binade
+    // and ends outside it, and the exit is among its terms
+    if (cur < TOP && end >= TOP) {
+        int mine = INT_MAX;
+        mcnt<real> cex = 0;
+#pragma unroll
+        for (int j = 0; j < FJ; j++) {
+            mcnt<real> fl;
+            int cls;
+            grid_term(x[j], ue, fl, cls);
+            const mcnt<real> inc = grid_inc<real>(fl, cls, cur);
+            if (mine == INT_MAX && (cls == 3 || cur + inc >= TOP)) {
+                mine = i0 + j;
+                cex = cur;
+            }
+            cur = sat_add<real>(cur, inc);
+        }
+        sh.fexit[pr] = mine;
+        sh.cexl[pr] = cex;
+    }
+    mp.tick(8);
+    __syncthreads();
+    mp.tick(9);
+    const int ex = sh.fexit[pr];
+    const real cex = (real)(mcnt<real>)sh.cexl[pr];
+    s = serial_wave(ldexp(cex, ue) + tb[ex], tb + ex + 1, min(kMonoSerialFine, len - ex - 1));
+    mp.tick(10);
+    return ex;
 }
 
 template <typename real>
@@ -325,15 +562,20 @@ __global__ __launch_bounds__(256) void k_mono_tile_sums(long n, const real *__re
 // 2. exclusive prefix -> predicted grid exponent at each tile start.  The
 //    running sum starts at seed[y * sstride] (nullptr: 0) or, for the part of
 //    a sum held by rank `prank` of a partition (chain_mono_sum), at the f64
-//    totals of the ranks before it, dpre[q * nsum + y] for q < prank.
+//    totals of the ranks before it, dpre[q * nsum + y] for q < prank.  With
+//    bpart, the tile sums are formed here from the block sums the producer
+//    of the terms already has (bpart[nsum * b + y], kBlock terms per block b;
+//    only a prediction, so their order and rounding do not matter) and step
+//    1 is skipped.  One workgroup of kPredThreads per sum: small enough to be
+//    dispatched between the sweeps' workgroups when it runs beside them.
+constexpr int kPredThreads = 256;
 template <typename real>
-__global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double *__restrict__ tsum,
-                                                       const real *__restrict__ seed, int sstride,
-                                                       int *__restrict__ ebase,
-                                                       const int *__restrict__ halt,
-                                                       const double *__restrict__ dpre = nullptr,
-                                                       int prank = 0) {
-    __shared__ double wsum[1024 / kWave];
+__global__ __launch_bounds__(kPredThreads) void k_mono_predict(
+    int ntiles, const double *__restrict__ tsum, const real *__restrict__ seed, int sstride,
+    int *__restrict__ ebase, const int *__restrict__ halt, const double *__restrict__ dpre = nullptr,
+    int prank = 0, const real *__restrict__ bpart = nullptr, int nbpart = 0) {
+    constexpr int BPT = MonoTile<real>::TILE / kBlock;
+    __shared__ double wsum[kPredThreads / kWave];
     __shared__ double carry;
     if (halt && *halt) return;
     const int y = blockIdx.y;
@@ -347,9 +589,16 @@ __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double 
         carry = c;
     }
     __syncthreads();
-    for (int c0 = 0; c0 < ntiles; c0 += 1024) {
+    for (int c0 = 0; c0 < ntiles; c0 += kPredThreads) {
         const int j = c0 + t;
-        double v = j < ntiles ? tsum[j] : 0.0, inc = v;
+        double v = 0.0;
+        if (j < ntiles && bpart) {
+            const int b1 = min(nbpart, (j + 1) * BPT);
+            for (int b = j * BPT; b < b1; b++) v += (double)bpart[(long)gridDim.y * b + y];
+        } else if (j < ntiles) {
+            v = tsum[j];
+        }
+        double inc = v;
 #pragma unroll
         for (int o = 1; o < kWave; o <<= 1) {
             const double p = __shfl_up(inc, o, kWave);
@@ -361,7 +610,7 @@ __global__ __launch_bounds__(1024) void k_mono_predict(int ntiles, const double 
         for (int k = 0; k < w; k++) pre += wsum[k];
         if (j < ntiles) ebase[j] = grid_exp((real)(pre + inc - v));
         __syncthreads();
-        if (t == 1023) carry = pre + inc;
+        if (t == kPredThreads - 1) carry = pre + inc;
         __syncthreads();
     }
 }
@@ -387,6 +636,7 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_summaries(long n, const r
                                                                  long astride,
                                                                  const int *__restrict__ ebase,
                                                                  long long *__restrict__ summ,
+                                                                 long long *__restrict__ subs,
                                                                  const int *__restrict__ halt) {
     constexpr int J = MonoTile<real>::J, NW = kMonoThreads / kWave;
     __shared__ long long w0[kMonoCand][NW], w1[kMonoCand][NW];
@@ -395,6 +645,7 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_summaries(long n, const r
     a += blockIdx.y * astride;
     ebase += (long)blockIdx.y * nt;
     summ += (long)blockIdx.y * nt * 2 * kMonoCand;
+    subs += (long)blockIdx.y * nt * 2 * kMonoCand * NW;
     const int tile = blockIdx.x;
     const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
     real x[J];
@@ -402,19 +653,21 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_summaries(long n, const r
     const int e0 = ebase[tile] - 1;
 #pragma unroll
     for (int c = 0; c < kMonoCand; c++) {
-        long long i0, i1;
+        mcnt<real> i0, i1;
         mono_run(x, e0 + c, i0, i1);
-        mono_wave_scan<real>(i0, i1, lane);
+        mono_wave_scan<real>(i0, i1);
         if (lane == kWave - 1) {
             w0[c][w] = i0;
             w1[c][w] = i1;
+            subs[2 * (((long)tile * kMonoCand + c) * NW + w)] = i0;  // sub-tile w
+            subs[2 * (((long)tile * kMonoCand + c) * NW + w) + 1] = i1;
         }
     }
     __syncthreads();
     if (t < kMonoCand) {
-        long long q0 = 0, q1 = 0;
+        mcnt<real> q0 = 0, q1 = 0;
         for (int k = 0; k < NW; k++) {
-            long long b0 = w0[t][k], b1 = w1[t][k];
+            mcnt<real> b0 = w0[t][k], b1 = w1[t][k];
             compose<real>(q0, q1, b0, b1);
             q0 = b0;
             q1 = b1;
@@ -424,14 +677,18 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_summaries(long n, const r
     }
 }
 
-// 4. one workgroup per sum: wave 0 chains the summaries of 64 tiles at a
-//    time on the current binade; the first tile that would leave it (or has
-//    no summary for it) is scanned term by term by the workgroup (mono_range).
+// 4. one workgroup per sum: chains the summaries of kMonoThreads tiles at a
+//    time on the current binade.  The first tile that would leave it (or has
+//    no summary for it) is staged in LDS; its sub-tiles are chained on their
+//    own summaries while the binade has one, and only the sub-tile that
+//    leaves it is scanned term by term (fine_scan), 1/NSUB of the tile per
+//    pass.
 template <typename real>
 __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *__restrict__ a,
                                                             long astride, int ntiles,
                                                             const int *__restrict__ ebase,
                                                             const long long *__restrict__ summ,
+                                                            const long long *__restrict__ subs,
                                                             const real *__restrict__ seed,
                                                             int sstride, int nparts,
                                                             const int *__restrict__ cnt_part,
@@ -439,55 +696,133 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *
                                                             long long *__restrict__ cnt_out,
                                                             const int *__restrict__ halt) {
     constexpr long TILE = MonoTile<real>::TILE;
-    constexpr long long TOP = 1ll << FpGrid<real>::p, CAP = TOP + 1;
+    constexpr int J = MonoTile<real>::J, SUB = MonoTile<real>::SUB, NSUB = MonoTile<real>::NSUB;
+    constexpr mcnt<real> TOP = 1ll << FpGrid<real>::p, CAP = TOP + 1;
     __shared__ MonoShared sh;
     if (halt && *halt) return;
     a += blockIdx.y * astride;
     ebase += (long)blockIdx.y * ntiles;
     summ += (long)blockIdx.y * ntiles * 2 * kMonoCand;
+    subs += (long)blockIdx.y * ntiles * 2 * kMonoCand * NSUB;
     sum_out += blockIdx.y;
-    const int t = threadIdx.x, lane = t & (kWave - 1);
+    real *tb = reinterpret_cast<real *>(sh.tile);
+    const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+    MonoProf mp;
     if (cnt_out && blockIdx.y == 0) mono_count<real>(nparts, cnt_part, cnt_out, sh);
-    if (t == 0) sh.exit_at = INT_MAX;
     __syncthreads();
     real s = seed ? seed[blockIdx.y * sstride] : real(0);
-    int j = 0;
+    int j = 0, par = 0;
+    // the next chain step's tile (j + t): its predicted binade and its
+    // summaries on every candidate, loaded ahead (during the previous
+    // crossing tile's scans)
+    int pe = 0;
+    long long sc[2 * kMonoCand];
+    auto fetch = [&](int base) {
+        const int jj = base + t;
+        if (jj < ntiles) {
+            pe = ebase[jj];
+#pragma unroll
+            for (int q = 0; q < 2 * kMonoCand; q++) sc[q] = summ[2 * (long)jj * kMonoCand + q];
+        }
+    };
+    fetch(0);
     while (j < ntiles && s < Lim<real>::huge) {
         const int ue = grid_exp(s);
-        long long S = (long long)ldexp(s, -ue);
-        for (;;) {  // whole tiles on this binade
-            if (t < kWave) {
-                const int jj = j + lane;
-                const int c = jj < ntiles ? ue - ebase[jj] + 1 : -1;
-                long long i0 = CAP, i1 = CAP;  // no summary: stops the chain here
-                if (c >= 0 && c < kMonoCand) {
-                    i0 = summ[2 * ((long)jj * kMonoCand + c)];
-                    i1 = summ[2 * ((long)jj * kMonoCand + c) + 1];
+        mcnt<real> S = (mcnt<real>)ldexp(s, -ue);
+        for (;;) {  // whole tiles on this binade, kMonoThreads at a time
+            const int c = j + t < ntiles ? ue - pe + 1 : -1;
+            mcnt<real> i0 = CAP, i1 = CAP;  // no summary: stops the chain here
+#pragma unroll
+            for (int q = 0; q < kMonoCand; q++)
+                if (c == q) {
+                    i0 = (mcnt<real>)sc[2 * q];
+                    i1 = (mcnt<real>)sc[2 * q + 1];
                 }
-                mono_wave_scan<real>(i0, i1, lane);
-                const long long after = sat_add<real>(S, (S & 1) ? i1 : i0);
-                const unsigned long long stop = __ballot(after >= TOP);
-                const int k = stop ? __ffsll(stop) - 1 : kWave;
-                if (lane == k - 1) sh.S = after;
-                if (t == 0) {
-                    sh.k = k;
-                    if (k == 0) sh.S = S;
-                }
+            mono_wave_scan<real>(i0, i1);
+            if (lane == kWave - 1) {
+                sh.cw0[w] = i0;
+                sh.cw1[w] = i1;
             }
             __syncthreads();
-            const int k = sh.k;
-            S = sh.S;
+            mcnt<real> q0 = 0, q1 = 0;
+#pragma unroll
+            for (int k = 0; k < MonoShared::NW; k++) {
+                mcnt<real> b0 = (mcnt<real>)sh.cw0[k], b1 = (mcnt<real>)sh.cw1[k];
+                if (k < w) {
+                    compose<real>(q0, q1, b0, b1);
+                    q0 = b0;
+                    q1 = b1;
+                }
+            }
+            compose<real>(q0, q1, i0, i1);
+            // the counts never decrease along the chain, so the tiles that
+            // stay in the binade are a prefix: count them, keep the last
+            const mcnt<real> after = sat_add<real>(S, (S & 1) ? i1 : i0);
+            const int ng = __popcll(__ballot(after < TOP));
+            if (lane == 0) sh.cnt[w] = ng;
+            if (ng > 0 && lane == ng - 1) sh.lastS[w] = after;
             __syncthreads();
+            int k = 0;
+#pragma unroll
+            for (int q = 0; q < MonoShared::NW; q++) k += sh.cnt[q];
+            if (k > 0) S = (mcnt<real>)sh.lastS[(k - 1) / kWave];
             j += k;
-            if (k < kWave || j >= ntiles) break;
+            fetch(k < kMonoThreads ? j + 1 : j);  // after the crossing tile / the next step
+            mp.tick(0);
+            if (k < kMonoThreads || j >= ntiles) break;
         }
         s = ldexp((real)S, ue);
         if (j >= ntiles) break;
-        // tile j leaves the binade (or was not predicted): term by term
-        s = mono_range(a, (long)j * TILE, min(n, (long)(j + 1) * TILE), s, sh);
+        // tile j leaves the binade (or was not predicted): staged in LDS with
+        // its sub-tile summaries on every candidate binade
+        {
+            real x[J];
+            mono_load(x, a, n, (long)j * TILE, t);
+            if (t < 2 * kMonoCand * NSUB) sh.subs[t] = subs[2 * (long)j * kMonoCand * NSUB + t];
+            mono_stage(tb, x, t);
+        }
+        const int len = (int)min(TILE, n - (long)j * TILE), eb = ebase[j];
+        __syncthreads();
+        mp.tick(1);
+        int p = 0;
+        while (p < len && s < Lim<real>::huge) {
+            const int u2 = grid_exp(s), c = u2 - eb + 1;
+            mcnt<real> S2 = (mcnt<real>)ldexp(s, -u2);
+            if (p % SUB == 0 && c >= 0 && c < kMonoCand) {
+                // whole sub-tiles on their summaries (every wave alike)
+                const int sb = p / SUB;
+                mcnt<real> i0 = CAP, i1 = CAP;
+                if (lane < NSUB - sb) {
+                    i0 = (mcnt<real>)sh.subs[2 * (c * NSUB + sb + lane)];
+                    i1 = (mcnt<real>)sh.subs[2 * (c * NSUB + sb + lane) + 1];
+                }
+                mono_wave_scan<real>(i0, i1);
+                const mcnt<real> after = sat_add<real>(S2, (S2 & 1) ? i1 : i0);
+                const int k = __popcll(__ballot(after < TOP));
+                mp.tick(2);
+                if (k > 0) {
+                    S2 = read_lane(after, k - 1);
+                    s = ldexp((real)S2, u2);
+                    p += k * SUB;
+                    if (p >= len) break;
+                }
+            }
+            real se = s;
+            const int ex = fine_scan<real>(tb, p / SUB, p, len, u2, S2, se, sh, par, mp);
+            mp.tick(3);
+            if (ex < 0) {
+                s = ldexp((real)S2, u2);
+                p = (p / SUB + 1) * SUB;
+            } else {
+                s = se;
+                p = ex + 1 + min(kMonoSerialFine, len - ex - 1);
+            }
+        }
         j++;
     }
     if (t == 0) *sum_out = s;
+    mp.tick(4);
+    mp.out();
 }
 
 // nsum sums of n terms each, sum y at a + y * astride (device), seed
@@ -497,28 +832,44 @@ __global__ __launch_bounds__(kMonoThreads) void k_mono_walk(long n, const real *
 template <typename real>
 inline size_t mono_ws_bytes(long n, int nsum = 1) {
     const long nt = (n + MonoTile<real>::TILE - 1) / MonoTile<real>::TILE;
-    return (size_t)nsum * nt * (sizeof(double) + sizeof(int) + 2 * kMonoCand * sizeof(long long)) +
+    return (size_t)nsum * nt *
+               (sizeof(double) + sizeof(int) +
+                2 * kMonoCand * (1 + MonoTile<real>::NSUB) * sizeof(long long)) +
            64;
 }
+// the scratch's parts: tile and sub-tile summaries, f64 tile sums, binades
+template <typename real>
+struct MonoWs {
+    long long *summ, *subs;
+    double *tsum;
+    int *ebase;
+    MonoWs(void *ws, long nt, int nsum) {
+        summ = static_cast<long long *>(ws);
+        subs = summ + 2 * kMonoCand * nt * nsum;
+        tsum = reinterpret_cast<double *>(subs + 2 * kMonoCand * MonoTile<real>::NSUB * nt * nsum);
+        ebase = reinterpret_cast<int *>(tsum + nt * nsum);
+    }
+};
+// bpart (may be nullptr): block sums of the terms, see k_mono_predict
 template <typename real>
 void mono_sum(long n, const real *a, const real *seed, int nparts, const int *cnt_part, real *out,
               long long *cnt_out, void *ws, hipStream_t s, int nsum = 1, long astride = 0,
-              const int *halt = nullptr) {
+              const int *halt = nullptr, const real *bpart = nullptr, int nbpart = 0) {
     constexpr long TILE = MonoTile<real>::TILE;
     const long nt = (n + TILE - 1) / TILE;
     if (nt <= 4 && nsum == 1 && !halt) {
         k_mono_sum<real><<<1, kMonoThreads, 0, s>>>(n, a, seed, nparts, cnt_part, out, cnt_out);
         return;
     }
-    long long *summ = static_cast<long long *>(ws);
-    double *tsum = reinterpret_cast<double *>(summ + 2 * kMonoCand * nt * nsum);
-    int *ebase = reinterpret_cast<int *>(tsum + nt * nsum);
+    const MonoWs<real> w(ws, nt, nsum);
     const dim3 gt((unsigned)nt, (unsigned)nsum), g1(1, (unsigned)nsum);
-    k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, tsum, halt);
-    k_mono_predict<real><<<g1, 1024, 0, s>>>((int)nt, tsum, seed, 0, ebase, halt);
-    k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, ebase, summ, halt);
-    k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, ebase, summ, seed, 0,
-                                                  nparts, cnt_part, out, cnt_out, halt);
+    if (!bpart) k_mono_tile_sums<real><<<gt, 256, 0, s>>>(n, a, astride, w.tsum, halt);
+    k_mono_predict<real><<<g1, kPredThreads, 0, s>>>((int)nt, w.tsum, seed, 0, w.ebase, halt,
+                                                     nullptr, 0, bpart, nbpart);
+    k_mono_summaries<real><<<gt, kMonoThreads, 0, s>>>(n, a, astride, w.ebase, w.summ, w.subs,
+                                                       halt);
+    k_mono_walk<real><<<g1, kMonoThreads, 0, s>>>(n, a, astride, (int)nt, w.ebase, w.summ, w.subs,
+                                                  seed, 0, nparts, cnt_part, out, cnt_out, halt);
 }
 
 // The same sum by one lane (PFDR_SEQSUM=lane, and the A/B tests): all lanes

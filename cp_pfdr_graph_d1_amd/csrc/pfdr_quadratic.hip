@@ -181,7 +181,7 @@ class QuadSession final : public SessionBase {
     // writer per position) into tall_ and summed whole on every rank
     ChainSum<real> chain_;
     DevBuf<real> tall_;
-    void seq_evolution(real *terms, hipStream_t s);
+    void seq_evolution(real *terms, const real *part, hipStream_t s);
     // Speculative iteration (single GPU, sequential evolution, no
     // reconditioning (difRcd = 0), no objective record, identity / diagonal
     // A): the evolution sums and the decision on iteration t run on a second
@@ -661,6 +661,9 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             DevBuf<real> t2(4 * (size_t)tstride_);  // terms of both parities
             std::swap(terms_.p, t2.p);
             std::swap(terms_.n, t2.n);
+            DevBuf<real> p2(4 * (size_t)nbv_);  // and their block sums
+            std::swap(vpart_.p, p2.p);
+            std::swap(vpart_.n, p2.n);
             xp2_.alloc(Vg_ + 2);  // (+2 as xp_)
             PFDR_HIP(hipMemcpyAsync(xp2_.p, xp_.p, sizeof(R2<real>) * (Vg_ + 2),
                                     hipMemcpyDeviceToDevice, s));
@@ -1356,16 +1359,18 @@ void QuadSession<real>::body_spec(int i, int n) {
     if (i >= 2) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // the decision on t - 2
     xr_ = xpb(t - 1);
     xw_ = xpb(t);
-    real *terms = terms_.p + (t & 1) * 2 * tstride_;
-    real *const keep = terms_.p;
+    real *terms = terms_.p + (t & 1) * 2 * tstride_, *part = vpart_.p + (t & 1) * 2 * nbv_;
+    real *const keep = terms_.p, *const keepp = vpart_.p;
     terms_.p = terms;  // vargs() hands the sweep this iteration's terms
+    vpart_.p = part;
     edge_sweep(0, E_, c, "edge_sweep");
     vertex_sweep(0, nbv_, c, "vertex_sweep");
     terms_.p = keep;
+    vpart_.p = keepp;
     xr_ = xw_ = xp_.p;
     PFDR_HIP(hipEventRecord(evv_[t & 1], s));
     PFDR_HIP(hipStreamWaitEvent(evs_, evv_[t & 1], 0));
-    seq_evolution(terms, evs_);  // overlaps the sweeps of t + 1
+    seq_evolution(terms, part, evs_);  // overlaps the sweeps of t + 1
     k_decide<real><<<1, 64, 0, evs_>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipEventRecord(evd_[t & 1], evs_));
@@ -1438,7 +1443,7 @@ void QuadSession<real>::body(int i, int n) {
     if (seqdif_) {
         // the reference's two sequential sums (ref :518-526), then its decision
         ProfScope ps(prof, "seq_evolution", s);
-        seq_evolution(terms_.p, s);
+        seq_evolution(terms_.p, vpart_.p, s);
         k_decide<real><<<1, 64, 0, s>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     } else if (gated && !halo_) {
         k_reduce_decide<real><<<1, kBlock, 0, s>>>(nbv_, vpart_.p, red_.p, ctrl_.p,
@@ -1456,13 +1461,15 @@ void QuadSession<real>::body(int i, int n) {
 }
 
 // red_[0..2) = the sums of (X_ - X)^2 and X^2 over every vertex in the
-// caller's order, rounded as the reference's one-thread loop
+// caller's order, rounded as the reference's one-thread loop.  part: the
+// vertex sweep's per-block sums of the same terms (their binades predicted
+// from them when the terms lie in vertex order)
 template <typename real>
-void QuadSession<real>::seq_evolution(real *terms, hipStream_t s) {
+void QuadSession<real>::seq_evolution(real *terms, const real *part, hipStream_t s) {
     const int *halt = &ctrl_.p->halt;
     if (!halo_) {
         mono_sum<real>(V_, terms, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
-                       halt);
+                       halt, reordered_ ? nullptr : part, nbv_);
     } else if (!lab_.p) {
         chain_.run(*halo_->tr, terms_.p, tstride_, red_.p, halt, s);
     } else {

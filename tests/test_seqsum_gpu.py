@@ -44,6 +44,11 @@ def _cases(dt):
                                     np.full(4, np.finfo(dt).max / 3, dt),
                                     rng.random(1000).astype(dt)]),
         "tile_edges": rng.random(8192 * 3 + 17).astype(dt) * f(2.0 ** 10),
+        # more tiles than one chain step of the walk holds (512), and a
+        # binade crossing in almost every tile (geometric growth)
+        "uniform_6M": rng.random(6_000_003).astype(dt),
+        "geometric": np.geomspace(1e-20, 1e10, 3_000_000).astype(dt),
+        "loguniform_wide": np.exp(rng.uniform(np.log(1e-30), 0.0, 2_000_000)).astype(dt),
     }
     if dt == np.float32:
         out["stall_2p24"] = np.ones(2 ** 24 + 1000, dt)
