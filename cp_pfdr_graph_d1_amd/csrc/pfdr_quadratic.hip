@@ -242,7 +242,7 @@ class QuadSession final : public SessionBase {
     // ustart_ / tptr_, tstart_, tlen_ = the runs each block stages, tok_ =
     // blocks whose lists fit the LDS (the others gather through the CSR)
     bool tiled_ = false;
-    DevBuf<unsigned short> d2_;
+    DevBuf<Slots12> slots_;
     DevBuf<unsigned char> deg8_;  // CSR entries per vertex (tile_sum)
     DevBuf<unsigned short> luv_;  // both ends mod 256 (k_edge_sweep_tl)
     DevBuf<int> erec_;            // per edge block: u blocks and v runs (k_edge_sweep_tl)
@@ -500,8 +500,8 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     const size_t En = E ? E : 1;
     // (tiled partitioned ranks: Z's received tail after the 2E local entries,
     // for the Z-direct iteration)
-    // (+4: the tiled vertex sweep reads whole 16-byte vectors of a run's tail, tile_sum)
-    Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0) + 4);
+    // (+kSlotGroup: the tiled vertex sweep reads whole groups of a run's tail, tile_sum)
+    Z2_.alloc(2 * En + (halo_ ? (size_t)halo_->R : 0) + kSlotGroup);
     gi_.alloc(Vg + 2);
     PFDR_HIP(hipMemsetAsync(gi_.p, 0, (Vg + 2) * sizeof(R2<real>), s));
     diag_.alloc(V); Ga_.alloc(Vg); invAux_.alloc(Vg); absval_.alloc(V);
@@ -618,7 +618,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         acc(b->n * sizeof(real));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
-    acc(d2_.n * 2 + luv_.n * 2 + deg8_.n +
+    acc(slots_.n * sizeof(Slots12) + luv_.n * 2 + deg8_.n +
         (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
     if (halo_) {
         plan_overlap();
@@ -844,7 +844,7 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
     }
     // contributions: local side-major [u ends | v ends] then the received tail
     const long R = halo_ ? halo_->R : 0;
-    wz_.alloc(2 * E_ + R + 4);  // (+4: tile_sum's whole vectors)
+    wz_.alloc(2 * E_ + R + kSlotGroup);  // (+kSlotGroup: tile_sum's whole groups)
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg_ptr ? eg_ptr : eg.p, e_offset, halo_.get(),
                            inc_, s);
     eorig_.release();
@@ -859,8 +859,14 @@ void QuadSession<real>::build_tiles() {
     hipStream_t s = stream;
     const int nb = grid_for(V_);
     const long R = halo_ ? halo_->R : 0;
-    d2_.alloc(2 * (size_t)E_ + R + 4);  // (+4: tile_sum's whole vectors)
-    k_tile_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, d2_.p);
+    {
+        const long n = 2 * E_ + R, ng = n / kSlotGroup + 1;  // (+1: tile_sum's whole groups)
+        DevBuf<unsigned short> d2(n);
+        k_tile_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, inc_.idx.p, d2.p);
+        slots_.alloc(ng);
+        k_pack_slots<<<grid_for(ng), kBlock, 0, s>>>(ng, n, d2.p, slots_.p);
+        PFDR_HIP(hipGetLastError());
+    }  // (d2's block is reused only once the stream is idle, dev_free)
     luv_.alloc((size_t)E_);
     k_tile_luv<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, luv_.p);
     {
@@ -1310,7 +1316,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.late = fuse_ ? 1 : 0;
     a.E = E_;
     if (tiled_) {
-        a.d2 = d2_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
+        a.slots = slots_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
         a.gi = gi_.p;  // (Ga, 1/Aux) in one load

@@ -227,33 +227,40 @@ constexpr int kTileCap = 4096;  // staged entries per vertex block (LDS: GatherC
 // Each vertex's slots [my0, my0 + deg) in the block's list come from its
 // degree (deg8: one byte per vertex, < 256 in every tiled block -- k_tile_ok)
 // by a block scan, instead of two CSR pointers (1 B per vertex, not 4).
-// The runs are staged with 16-byte loads (4 f32 / 2 f64 contributions and
-// their 16-bit slots per access, from the aligned vector at or below each
-// run's start; elements outside the run are dropped): a quarter of the
-// load instructions of one contribution per access, which is what the
-// texture addresser prices.  The contribution and slot arrays carry one
-// spare vector at their end for the last run's tail.
+// The slots are 12-bit (a tiled block lists at most kTileCap = 4096
+// contributions), packed eight to a 12-byte group (Slots12), and the runs
+// are staged a group at a time: one 12-byte slot load beside the group's
+// contributions (two 16-byte loads f32, four f64), from the aligned group
+// at or below each run's start, elements outside the run dropped.  The
+// contribution arrays carry one spare group at their end for the last
+// run's tail.
 constexpr int kTileRuns = 128;  // v-end runs per vertex block
-template <typename real>
-struct TileVec { static constexpr int n = Vec<real>::kPer16B; };  // entries per staged vector
+constexpr int kSlotGroup = 8;   // contributions per packed slot group
+struct alignas(4) Slots12 { unsigned w[3]; };  // 8 x 12 bits, little-endian
+__device__ __forceinline__ int slot12(const Slots12 &g, int i) {
+    const unsigned long long lo = g.w[0] | ((unsigned long long)g.w[1] << 32);  // bits 0..63
+    const unsigned long long hi = g.w[1] | ((unsigned long long)g.w[2] << 32);  // bits 32..95
+    return i < 5 ? (int)((lo >> (12 * i)) & 0xfff) : (int)((hi >> (12 * i - 32)) & 0xfff);
+}
 
 template <typename real, int GB, bool ZD = false>
 __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
                                          const unsigned char *__restrict__ deg8,
-                                         const unsigned short *__restrict__ d2,
+                                         const Slots12 *__restrict__ slots,
                                          const int *__restrict__ ustart,
                                          const int *__restrict__ tptr,
                                          const int *__restrict__ tstart,
                                          const int *__restrict__ tlen,
                                          const real *__restrict__ wz, real *lds, int *runs,
                                          real wv = real(1)) {
-    constexpr int VE = TileVec<real>::n, GV = GB / VE > 0 ? GB / VE : 1;
+    constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE;
+    constexpr int GG = GB / G > 0 ? GB / G : 1;  // groups in flight per lane
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const int dg = v < V ? deg8[v] : 0;
     const int us = ustart[blk], nu = ustart[blk + 1] - us;
     const int t0 = tptr[blk], nt = tptr[blk + 1] - t0;
     // run table (wave 0): starts, lengths, inclusive prefix of the runs'
-    // vector counts; the degrees' wave totals after it (read after the
+    // group counts; the degrees' wave totals after it (read after the
     // barriers below)
     int *rs = runs, *rl = runs + kTileRuns, *rp = runs + 2 * kTileRuns;
     int *wt = runs + 3 * kTileRuns;
@@ -268,81 +275,84 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
         int acc = 0;
         for (int c = 0; c < nt; c += kWave) {
             const int i = c + tid;
-            int nvec = 0;
+            int ng = 0;
             if (i < nt) {
                 const int st = tstart[t0 + i], len = tlen[t0 + i];
                 rs[i] = st;
                 rl[i] = len;
                 const long A = E + st;
-                nvec = len > 0 ? (int)((A + len - 1) / VE - A / VE + 1) : 0;
+                ng = len > 0 ? (int)((A + len - 1) / G - A / G + 1) : 0;
             }
 #pragma unroll
             for (int o = 1; o < kWave; o <<= 1) {
-                const int y = __shfl_up(nvec, o, kWave);
-                if (tid >= o) nvec += y;
+                const int y = __shfl_up(ng, o, kWave);
+                if (tid >= o) ng += y;
             }
-            if (i < nt) rp[i] = acc + nvec;
-            acc += __shfl(nvec, kWave - 1, kWave);
+            if (i < nt) rp[i] = acc + ng;
+            acc += __shfl(ng, kWave - 1, kWave);
         }
     }
-    // u ends: one contiguous run [us, us + nu), GV vectors in flight per lane
+    // u ends: one contiguous run [us, us + nu), GG groups in flight per lane
     {
-        const long fu = us / VE;
-        const int nvu = nu > 0 ? (int)((us + nu - 1) / VE - fu + 1) : 0;
-        for (int b = 0; b < nvu; b += kBlock * GV) {
-            Pk<unsigned short, VE> d[GV];
-            Pk<real, VE> x[GV];
+        const long fu = us / G;
+        const int ngu = nu > 0 ? (int)((us + nu - 1) / G - fu + 1) : 0;
+        for (int b = 0; b < ngu; b += kBlock * GG) {
+            Slots12 d[GG];
+            Pk<real, VE> x[GG][ZV];
 #pragma unroll
-            for (int u = 0; u < GV; u++) {
-                const long base = (fu + min(b + u * kBlock + tid, nvu - 1)) * VE;
-                d[u] = ldv<unsigned short, VE>(d2 + base);
-                x[u] = ldv<real, VE>(wz + base);
+            for (int u = 0; u < GG; u++) {
+                const long g = fu + min(b + u * kBlock + tid, ngu - 1);
+                d[u] = slots[g];
+#pragma unroll
+                for (int z = 0; z < ZV; z++) x[u][z] = ldv<real, VE>(wz + g * G + z * VE);
             }
 #pragma unroll
-            for (int u = 0; u < GV; u++) {
+            for (int u = 0; u < GG; u++) {
                 const int k = b + u * kBlock + tid;
-                if (k < nvu) {
-                    const long base = (fu + k) * VE;
+                if (k < ngu) {
+                    const long base = (fu + k) * G;
 #pragma unroll
-                    for (int q = 0; q < VE; q++)
-                        if (base + q >= us && base + q < (long)us + nu) lds[d[u].v[q]] = x[u].v[q];
+                    for (int q = 0; q < G; q++)
+                        if (base + q >= us && base + q < (long)us + nu)
+                            lds[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
                 }
             }
         }
     }
     __syncthreads();  // run table
-    const int nvv = nt ? rp[nt - 1] : 0;
-    // run of the lane's vector k and its bounds in the vector list
+    const int ngv = nt ? rp[nt - 1] : 0;
+    // run of the lane's group k and its bounds in the group list
     int lo = 0, end = nt ? rp[0] : 0, beg = 0;
-    for (int b = 0; b < nvv; b += kBlock * GV) {
-        Pk<unsigned short, VE> d[GV];
-        Pk<real, VE> x[GV];
-        long base[GV], A[GV];
-        int L[GV];
+    for (int b = 0; b < ngv; b += kBlock * GG) {
+        Slots12 d[GG];
+        Pk<real, VE> x[GG][ZV];
+        long base[GG], A[GG];
+        int L[GG];
 #pragma unroll
-        for (int u = 0; u < GV; u++) {
-            // the lane's vectors grow by 256: its run only advances, no search
-            const int k = min(b + u * kBlock + tid, nvv - 1);
+        for (int u = 0; u < GG; u++) {
+            // the lane's groups grow by 256: its run only advances, no search
+            const int k = min(b + u * kBlock + tid, ngv - 1);
             while (end <= k) {
                 beg = end;
                 end = rp[++lo];
             }
             A[u] = E + rs[lo];
             L[u] = rl[lo];
-            base[u] = (A[u] / VE + (k - beg)) * VE;
+            base[u] = (A[u] / G + (k - beg)) * G;
         }
 #pragma unroll
-        for (int u = 0; u < GV; u++) {
-            d[u] = ldv<unsigned short, VE>(d2 + base[u]);
-            x[u] = ldv<real, VE>(wz + base[u]);
+        for (int u = 0; u < GG; u++) {
+            d[u] = slots[base[u] / G];
+#pragma unroll
+            for (int z = 0; z < ZV; z++) x[u][z] = ldv<real, VE>(wz + base[u] + z * VE);
         }
 #pragma unroll
-        for (int u = 0; u < GV; u++)
-            if (b + u * kBlock + tid < nvv) {
+        for (int u = 0; u < GG; u++)
+            if (b + u * kBlock + tid < ngv) {
 #pragma unroll
-                for (int q = 0; q < VE; q++)
+                for (int q = 0; q < G; q++)
                     if (base[u] + q >= A[u] && base[u] + q < A[u] + L[u])
-                        lds[d[u].v[q]] = x[u].v[q];
+                        lds[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
             }
     }
     __syncthreads();
@@ -398,6 +408,34 @@ static __global__ void k_tile_slots(int V, const int *__restrict__ ptr,
     if (v >= V) return;
     const int base = ptr[v - v % kBlock];
     for (int j = ptr[v]; j < ptr[v + 1]; j++) d2[idx[j]] = (unsigned short)(j - base);
+}
+
+// the slots of addresses [8 g, 8 g + 8) packed into group g (12 bits each,
+// slot i at bits [12 i, 12 i + 12); a tiled block's slots are < kTileCap)
+static __global__ void k_pack_slots(long ngroups, long n, const unsigned short *__restrict__ d2,
+                                    Slots12 *__restrict__ out) {
+    const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ngroups) return;
+    unsigned long long lo = 0, hi = 0;  // bits 0..63, 64..95
+#pragma unroll
+    for (int q = 0; q < kSlotGroup; q++) {
+        const long p = g * kSlotGroup + q;
+        const unsigned long long x = p < n ? (d2[p] & 0xfffu) : 0u;
+        const int bit = 12 * q;
+        if (bit + 12 <= 64) {
+            lo |= x << bit;
+        } else if (bit >= 64) {
+            hi |= x << (bit - 64);
+        } else {
+            lo |= x << bit;
+            hi |= x >> (64 - bit);
+        }
+    }
+    Slots12 r;
+    r.w[0] = (unsigned)lo;
+    r.w[1] = (unsigned)(lo >> 32);
+    r.w[2] = (unsigned)hi;
+    out[g] = r;
 }
 
 // ustart[b] = first position whose u end is in block >= b (tile order sorts by
@@ -1968,7 +2006,7 @@ struct VArgs {
     int late;       // halt of ctrl tested after the sum, before the stores (small launches)
     // tiled contributions (null d2: off; see tile_sum)
     long E;
-    const unsigned short *d2;
+    const Slots12 *slots;
     const unsigned char *deg8;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
     // Z-direct (tiled single-GPU sessions with one edge weight, no A1): the
@@ -2093,8 +2131,8 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
     const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
-    if (a.d2 && a.tok[blk])  // block-uniform
-        x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.d2, a.ustart, a.tptr, a.tstart,
+    if (a.slots && a.tok[blk])  // block-uniform
+        x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
     else if (!ZD && a.blkok && a.blkok[blk])
         x = split_sum<real, GB>(a.V, v0, v, a.ptr, a.uptr, a.mask, a.oidx, a.wz, lds, scan);
