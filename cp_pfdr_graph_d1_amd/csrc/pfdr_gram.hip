@@ -176,14 +176,24 @@ __global__ __launch_bounds__(256) void k_gram(int P, long K, const real *__restr
 
 // The same tile with 16-byte operand loads and a register prefetch of the
 // next K slice while the matrix cores work on the current one (needs
-// ld % (16 / sizeof(real)) == 0 and a 16-byte aligned A).
-template <typename real, int LAYOUT>
-__global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__restrict__ A, long ld,
-                                              long kchunk, int nchunk, real *__restrict__ Gpart) {
+// ld % (16 / sizeof(real)) == 0 and a 16-byte aligned A).  WG waves per
+// block: 4 -> a 2x2 grid of MFMA tiles per wave; 2 -> 4x2 per wave (each
+// k step reads 4 + 2 operand fragments for 8 MFMAs instead of 2 + 2 for
+// 4, and a wave does twice the MFMAs per K slice and barrier).  Measured
+// (r4t, rocprofv3 MfmaUtil on C3's A A^t): 4x2 tiles need 324-352 VGPRs,
+// one wave per SIMD, 94 TF/s / MfmaUtil 63 % against 113 TF/s / 81 % for
+// 2x2 -- so 2x2 it is.
+constexpr int kGramWaves = 4;
+template <typename real, int LAYOUT, int WG = kGramWaves>
+__global__ __launch_bounds__(64 * WG) void k_gram_v(int P, long K, const real *__restrict__ A,
+                                                   long ld, long kchunk, int nchunk,
+                                                   real *__restrict__ Gpart) {
     using M = Mfma<real>;
-    constexpr int BT = M::BT, BK = M::BK, T = M::T, WT = BT / 2, NT = WT / T;
+    constexpr int NTH = 64 * WG, WI = WG == 4 ? 2 : 1;     // waves along i (2 along j)
+    constexpr int BT = M::BT, BK = M::BK, T = M::T, TI = BT / WI, TJ = BT / 2;
+    constexpr int NX = TI / T, NY = TJ / T;               // MFMA tiles per wave
     constexpr int VW = 16 / sizeof(real);                 // reals per 16-byte load
-    constexpr int NL = BT * BK / (256 * VW);               // vector loads per operand per lane
+    constexpr int NL = BT * BK / (NTH * VW);              // vector loads per operand per lane
     int bi, bj, z;
     if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
     const long k0 = (long)z * kchunk;
@@ -197,13 +207,13 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
     constexpr int PADC = (LAYOUT == GRAM_TN && sizeof(real) == 4) ? 1 : VW;
     __shared__ alignas(16) real Ls[BK][BT + PADC], Rs[BK][BT + PADC];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wi = w & 1, wj = w >> 1;
+    const int wi = w % WI, wj = w / WI;
     const long i0 = (long)bi * BT, j0 = (long)bj * BT;
-    typename M::acc_t acc[NT][NT];
+    typename M::acc_t acc[NX][NY];
 #pragma unroll
-    for (int a = 0; a < NT; a++)
+    for (int a = 0; a < NX; a++)
 #pragma unroll
-        for (int b = 0; b < NT; b++)
+        for (int b = 0; b < NY; b++)
 #pragma unroll
             for (int r = 0; r < M::NR; r++) acc[a][b][r] = real(0);
     // lane's vector slots: NT layout (i, k) = (4 consecutive i, one k);
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
     auto load = [&](long kb) {
 #pragma unroll
         for (int q = 0; q < NL; q++) {
-            const int f = t + 256 * q;
+            const int f = t + NTH * q;
             int i, k;
             if (LAYOUT == GRAM_NT) { k = f / (BT / VW); i = (f - k * (BT / VW)) * VW; }
             else { i = f / (BK / VW); k = (f - i * (BK / VW)) * VW; }
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
     auto store = [&]() {
 #pragma unroll
         for (int q = 0; q < NL; q++) {
-            const int f = t + 256 * q;
+            const int f = t + NTH * q;
             if (LAYOUT == GRAM_NT) {
                 const int k = f / (BT / VW), i = (f - k * (BT / VW)) * VW;
                 stv<real, VW>(&Ls[k][i], lr[q]);
@@ -260,16 +270,15 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
 #pragma unroll 4
         for (int ks = 0; ks < BK; ks += M::KS) {
             const int kr = ks + lane / T, c = lane % T;
-            real a[NT], b[NT];
+            real a[NX], b[NY];
 #pragma unroll
-            for (int q = 0; q < NT; q++) {
-                a[q] = Ls[kr][wi * WT + q * T + c];
-                b[q] = Rs[kr][wj * WT + q * T + c];
-            }
+            for (int q = 0; q < NX; q++) a[q] = Ls[kr][wi * TI + q * T + c];
 #pragma unroll
-            for (int x = 0; x < NT; x++)
+            for (int q = 0; q < NY; q++) b[q] = Rs[kr][wj * TJ + q * T + c];
 #pragma unroll
-                for (int y = 0; y < NT; y++) acc[x][y] = M::mma(a[x], b[y], acc[x][y]);
+            for (int x = 0; x < NX; x++)
+#pragma unroll
+                for (int y = 0; y < NY; y++) acc[x][y] = M::mma(a[x], b[y], acc[x][y]);
         }
         __syncthreads();
     }
@@ -278,15 +287,15 @@ __global__ __launch_bounds__(256) void k_gram_v(int P, long K, const real *__res
     // diagonal, the mirror tile the same way (the accumulator map puts
     // consecutive lanes on consecutive COLUMNS: storing it directly made one
     // of the two writes a stride-P scatter, which dominated for large P)
-    __shared__ real Os[4][T][T + 1];
+    __shared__ real Os[WG][T][T + 1];
     real(*O)[T + 1] = Os[w];
     constexpr int JS = 64 / T;
     const int li = lane % T, lj = lane / T;
 #pragma unroll
-    for (int x = 0; x < NT; x++)
+    for (int x = 0; x < NX; x++)
 #pragma unroll
-        for (int y = 0; y < NT; y++) {
-            const long ib = i0 + wi * WT + x * T, jb = j0 + wj * WT + y * T;
+        for (int y = 0; y < NY; y++) {
+            const long ib = i0 + wi * TI + x * T, jb = j0 + wj * TJ + y * T;
 #pragma unroll
             for (int r = 0; r < M::NR; r++) O[M::row(lane, r)][M::col(lane, r)] = acc[x][y][r];
             __syncthreads();
@@ -338,8 +347,12 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
     if (vec) {
-        if (which == 0) k_gram_v<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
-        else k_gram_v<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
+        if (which == 0)
+            k_gram_v<real, GRAM_TN><<<grid, 64 * kGramWaves, 0, s>>>(P, K, A, ld, kchunk,
+                                                                    (int)nchunk, out);
+        else
+            k_gram_v<real, GRAM_NT><<<grid, 64 * kGramWaves, 0, s>>>(P, K, A, ld, kchunk,
+                                                                    (int)nchunk, out);
     } else {
         if (which == 0) k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
         else k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
