@@ -377,6 +377,7 @@ def main():
     quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
     split_blocks = sess.query("split_blocks") if quad else 0
     tiled_blocks = sess.query("tiled_blocks") if quad else 0
+    record_blocks = sess.query("record_blocks") if quad else 0
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     seqdif = sess.query("seqdif")
     # kernel names behind each family (rocprof / PMC summaries)
@@ -453,6 +454,7 @@ def main():
             "relabelled": reordered,
             "split_incidence_blocks": split_blocks,
             "tiled_blocks": tiled_blocks,
+            "record_blocks": record_blocks,
             "sequential_evolution": bool(seqdif),
             **({"symv_upper_triangle": bool(symv)} if wl.dominant == "symv" else {}),
             "finite": finite,

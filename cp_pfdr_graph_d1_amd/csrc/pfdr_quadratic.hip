@@ -246,7 +246,7 @@ class QuadSession final : public SessionBase {
     DevBuf<unsigned char> deg8_;  // CSR entries per vertex (tile_sum)
     DevBuf<unsigned short> luv_;  // both ends mod 256 (k_edge_sweep_tl)
     DevBuf<int> erec_;            // per edge block: u blocks and v runs (k_edge_sweep_tl)
-    DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_;
+    DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_, trec_;
     void build_tiles();
     Ctrl<real> *hctrl_ = nullptr;  // pinned mirror
     int nbv_, nbe_, nbn_, rows_nb_, rows_cpb_;
@@ -619,7 +619,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
     acc(slots_.n * sizeof(Slots12) + luv_.n * 2 + deg8_.n +
-        (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + erec_.n) * 4);
+        (ustart_.n + tptr_.n + tstart_.n + tlen_.n + tok_.n + trec_.n + erec_.n) * 4);
     if (halo_) {
         plan_overlap();
         // RCCL partitions replay captured chunks too (pull, sweeps, push and
@@ -907,14 +907,21 @@ void QuadSession<real>::build_tiles() {
                                                               fill.p, tstart_.p, tlen_.p);
     tok_.alloc(nb);
     k_tile_ok<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tptr_.p, kTileCap, tok_.p);
+    trec_.alloc((size_t)nb * kTileRec);
+    k_tile_rec<<<grid_for(nb), kBlock, 0, s>>>(nb, ustart_.p, tptr_.p, tstart_.p, tlen_.p, tok_.p,
+                                               trec_.p);
     deg8_.alloc(V_);
     k_tile_deg<<<grid_for(V_), kBlock, 0, s>>>(V_, inc_.ptr.p, deg8_.p);
     PFDR_HIP(hipGetLastError());
     PFDR_HIP(hipMemcpyAsync(h.data(), tok_.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
     PFDR_HIP(hipStreamSynchronize(s));
-    long n = 0;
-    for (int x : h) n += x;
+    long n = 0, nr = 0;
+    for (int x : h) {
+        n += x != 0;
+        nr += x == 2;
+    }
     tiled_blocks = n;
+    record_blocks = nr;
 }
 
 // Split incidence for the vertex sweep (split_sum): when the edges are
@@ -1316,7 +1323,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.late = fuse_ ? 1 : 0;
     a.E = E_;
     if (tiled_) {
-        a.slots = slots_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
+        a.slots = slots_.p; a.trec = trec_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
         a.gi = gi_.p;  // (Ga, 1/Aux) in one load

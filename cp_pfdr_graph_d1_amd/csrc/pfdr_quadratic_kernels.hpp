@@ -373,6 +373,110 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
     return s;
 }
 
+// tile_sum from a per-block record (blocks with at most kRecRuns v-end runs,
+// tok = 2): [u start, u count, runs, (start, length) x runs] in 32 ints, so
+// the block's metadata is ONE load round (the run table otherwise costs two
+// dependent ones, tptr then tstart / tlen, and a barrier), every wave holds
+// the runs in its lanes, and the u-end and v-end groups are loaded in the
+// same round -- two groups in flight per lane -- before one barrier.
+constexpr int kRecRuns = 14, kTileRec = 32;
+template <typename real, bool ZD = false>
+__device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
+                                             const unsigned char *__restrict__ deg8,
+                                             const Slots12 *__restrict__ slots,
+                                             const int *__restrict__ trec,
+                                             const real *__restrict__ wz, real *lds, int *wt,
+                                             real wv = real(1)) {
+    constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int dg = v < V ? deg8[v] : 0;
+    const int rv = lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
+    int dinc = dg;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(dinc, o, kWave);
+        if (lane >= o) dinc += y;
+    }
+    if (lane == kWave - 1) wt[w] = dinc;
+    const int us = __builtin_amdgcn_readlane(rv, 0), nu = __builtin_amdgcn_readlane(rv, 1);
+    const int nt = __builtin_amdgcn_readlane(rv, 2);
+    // run r in lane r: start, length, groups, inclusive prefix of the groups
+    const int st = __shfl(rv, min(3 + 2 * lane, kWave - 1), kWave);
+    const int ln = __shfl(rv, min(4 + 2 * lane, kWave - 1), kWave);
+    int P = 0;
+    if (lane < nt && ln > 0) {
+        const long A = E + st;
+        P = (int)((A + ln - 1) / G - A / G + 1);
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(P, o, kWave);
+        if (lane >= o) P += y;
+    }
+    const int ngv = __builtin_amdgcn_readlane(P, kWave - 1);
+    const long fu = us / G;
+    const int ngu = nu > 0 ? (int)((us + nu - 1) / G - fu + 1) : 0;
+    const int tot = ngu + ngv;
+    for (int b = 0; b < tot; b += 2 * kBlock) {
+        Slots12 d[2];
+        Pk<real, VE> x[2][ZV];
+        long gb[2], lo[2], hi[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int k = min(b + u * kBlock + tid, tot - 1);
+            // the run of a v-end group (every lane takes part in the
+            // shuffles: a lane's run table entries must be read while it is
+            // active)
+            const int kv = k - ngu;
+            int r = 0;
+            for (int q = 0; q < nt; q++) r += __builtin_amdgcn_readlane(P, q) <= kv;
+            r = min(r, kWave - 1);
+            const int sr = __shfl(st, r, kWave), lr = __shfl(ln, r, kWave);
+            const int pb = __shfl(P, max(r - 1, 0), kWave);
+            if (k < ngu) {
+                gb[u] = fu + k;
+                lo[u] = us;
+                hi[u] = (long)us + nu;
+            } else {
+                const long A = E + sr;
+                gb[u] = A / G + (kv - (r > 0 ? pb : 0));
+                lo[u] = A;
+                hi[u] = A + lr;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            d[u] = slots[gb[u]];
+#pragma unroll
+            for (int z = 0; z < ZV; z++) x[u][z] = ldv<real, VE>(wz + gb[u] * G + z * VE);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (b + u * kBlock + tid < tot) {
+#pragma unroll
+                for (int q = 0; q < G; q++) {
+                    const long p = gb[u] * G + q;
+                    if (p >= lo[u] && p < hi[u]) lds[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
+                }
+            }
+    }
+    __syncthreads();
+    int my0 = dinc - dg;
+    for (int q = 0; q < w; q++) my0 += wt[q];
+    const int my1 = my0 + dg;
+    real s = real(0);
+    int j = my0;
+    for (; j + 4 <= my1; j += 4) {
+        const real a0 = lds[j], a1 = lds[j + 1], a2 = lds[j + 2], a3 = lds[j + 3];
+        s += ZD ? wv * a0 : a0;
+        s += ZD ? wv * a1 : a1;
+        s += ZD ? wv * a2 : a2;
+        s += ZD ? wv * a3 : a3;
+    }
+    for (; j < my1; j++) s += ZD ? wv * lds[j] : lds[j];
+    return s;
+}
+
 // tile-order keys: (u block, v block) in the high bits, edge position the
 // value; a partitioned rank (split) puts the edges with a ghost end after
 // all the others (bit 2 vbits)
@@ -501,6 +605,28 @@ static __global__ void k_tile_ok(int V, int nb, const int *__restrict__ ptr,
     bool ok = ptr[v1] - ptr[v0] <= cap && tptr[b + 1] - tptr[b] <= kTileRuns;
     for (int v = v0; ok && v < v1; v++) ok = ptr[v + 1] - ptr[v] < 256;
     tok[b] = ok ? 1 : 0;
+}
+
+// the per-block records of tile_sum_rec for tiled blocks with at most
+// kRecRuns v-end runs (tok 1 -> 2)
+static __global__ void k_tile_rec(int nb, const int *__restrict__ ustart,
+                                  const int *__restrict__ tptr, const int *__restrict__ tstart,
+                                  const int *__restrict__ tlen, int *__restrict__ tok,
+                                  int *__restrict__ rec) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int t0 = tptr[b], nt = tptr[b + 1] - t0;
+    int *r = rec + (long)b * kTileRec;
+    for (int q = 0; q < kTileRec; q++) r[q] = 0;
+    if (!tok[b] || nt > kRecRuns) return;
+    r[0] = ustart[b];
+    r[1] = ustart[b + 1] - ustart[b];
+    r[2] = nt;
+    for (int q = 0; q < nt; q++) {
+        r[3 + 2 * q] = tstart[t0 + q];
+        r[4 + 2 * q] = tlen[t0 + q];
+    }
+    tok[b] = 2;
 }
 
 // deg8[v] = the vertex's CSR entries (clamped; blocks with a larger one are
@@ -2007,6 +2133,7 @@ struct VArgs {
     // tiled contributions (null d2: off; see tile_sum)
     long E;
     const Slots12 *slots;
+    const int *trec;        // per-block records (tile_sum_rec; tok == 2)
     const unsigned char *deg8;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
     // Z-direct (tiled single-GPU sessions with one edge weight, no A1): the
@@ -2131,7 +2258,11 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
     const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
-    if (a.slots && a.tok[blk])  // block-uniform
+    const int tk = a.slots ? a.tok[blk] : 0;  // block-uniform
+    if (tk == 2)
+        x = tile_sum_rec<real, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
+                                   lds, scan + 3 * kTileRuns, wv);
+    else if (tk)
         x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
     else if (!ZD && a.blkok && a.blkok[blk])

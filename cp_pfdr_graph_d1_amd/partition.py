@@ -204,7 +204,8 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              evolution=evolution)
             queries[r] = {"ghosts": s.query("ghosts")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
-                queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks")})
+                queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks",
+                                                            "record_blocks")})
             s.run(itMax)
             results[r] = s.result()
             s.close()

@@ -240,7 +240,10 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
  * (1: such a graph's contributions are stored in per-vertex-block lists, so
  * its vertex sweep stages them without dependent address loads),
  * "dense_exact" (1: the dense products run in the reference's sequential
- * order, bit-exact; small single-GPU problems). */
+ * order, bit-exact; small single-GPU problems), "tiled_blocks" (vertex
+ * blocks staging tile-ordered contributions) and "record_blocks" (of those,
+ * the blocks whose runs fit one per-block record), "speculative" (1: the
+ * evolution sums run beside the next iteration's sweeps). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 

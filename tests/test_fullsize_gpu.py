@@ -33,6 +33,7 @@ def _single(wl_name, **extra):
     s.run(ITS)
     X = s.result()[0]
     rel = s.query("reordered")
+    _single.blocks = (s.query("tiled_blocks"), s.query("record_blocks"))
     s.close()
     return inp, X, rel
 
@@ -52,6 +53,11 @@ def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
     from cp_pfdr_graph_d1_amd import pfdr
     inp, X1, _ = _single("headline")
     assert np.all(np.isfinite(X1))
+    # tiled blocks with at most kRecRuns v-end runs read one record each
+    # (tile_sum_rec), the others the run table (tile_sum)
+    nt, nr = _single.blocks
+    print("headline: %d tiled blocks, %d through records" % (nt, nr))
+    assert 0 < nr <= nt
     for k in (2, 4):
         Xk, info = _partitioned(WORKLOADS["headline"], inp, k, info=True)
         assert np.array_equal(Xk, X1), "partitioned (%d ranks) differs" % k
@@ -59,6 +65,8 @@ def test_headline_partitioned_and_relabelled_equal_single(gpu_lib):
         # exactly these sessions over RCCL)
         for q in info["queries"]:
             assert q["tiled_blocks"] > 0, q
+        print("%d ranks: tiled / record blocks %s" % (
+            k, [(q["tiled_blocks"], q["record_blocks"]) for q in info["queries"]]))
     _, Xr, rel = _single("headline", reorder=pfdr.REORDER_ON)
     assert rel == 1
     assert np.array_equal(Xr, X1)
