@@ -15,8 +15,8 @@
  * Arithmetic is written so that each floating point operation happens in the
  * same order and with the same operands as in the reference, which makes the
  * restatement bit-exact against the reference compiled without OpenMP and
- * with -ffp-contract=off (pinned by tests/test_oracle_vs_ref.py and the
- * golden fixtures in tests/golden/).
+ * with -ffp-contract=off (pinned by test_oracle_vs_reference_random in
+ * tests/test_oracle.py and by the golden fixtures in tests/golden/).
  *
  * Parity pinning:  tests/golden/*.npz were produced by the REAL reference
  * (oracle/_ref, compiled from /root/reference/src by oracle/Makefile) via
