@@ -119,6 +119,8 @@ class QuadSession final : public SessionBase {
             (void)hipStreamSynchronize(stream);  // no control-block copy in flight
             pinned_small_put(hctrl_);
         }
+        for (Ctrl<real> *c : snap_) if (c) pinned_small_put(c);
+        for (hipEvent_t e : snapev_) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : evv_) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : evd_) if (e) (void)hipEventDestroy(e);
@@ -130,6 +132,7 @@ class QuadSession final : public SessionBase {
         drop_graphs();
     }
     int run(int iters) override;
+    int run_pipelined(int target);
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
     void *device_x() override;
 
@@ -198,6 +201,9 @@ class QuadSession final : public SessionBase {
     R2<real> *xr_ = nullptr, *xw_ = nullptr;  // the sweeps' read / write (X, P)
     hipStream_t evs_ = nullptr;
     hipEvent_t evv_[2] = {}, evd_[2] = {};
+    // run_pipelined: the control block's snapshots after two chunks in flight
+    Ctrl<real> *snap_[2] = {};
+    hipEvent_t snapev_[2] = {};
     void body_spec(int i, int n);
     static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     std::unique_ptr<Halo> halo_;  // partition plan (null on one GPU)
@@ -1621,6 +1627,7 @@ template <typename real>
 int QuadSession<real>::run(int iters) {
     const bool gated = track_ || rec_obj_;
     const int target = (int)std::min<long>((long)it_ + std::max(iters, 0), (long)itMax_);
+    if (gated && !halo_ && !spec_) return run_pipelined(target);
     // every rank runs the same number of bodies: the decisions come from
     // all-reduced values, so the control blocks agree
     while (!stopped_ && it_ < target) {
@@ -1653,6 +1660,68 @@ int QuadSession<real>::run(int iters) {
             print_progress();
             next_print_ = it_ + verbose_;
         }
+    }
+    wait_stream();
+    if (prof.on) prof.resolve();
+    return it_;
+}
+
+// Gated single-GPU runs: chunk k + 1 is launched before the host reads the
+// control block chunk k left (a device-to-host snapshot ordered between the
+// two chunks), so the host's round trip -- ≈35-45 us per chunk, a tenth of
+// a 32-iteration chunk of C1 -- overlaps the GPU's work instead of idling
+// it.  A chunk launched after a stop or a reconditioning request runs with
+// the halt flag set: every kernel of it returns at once and changes nothing,
+// so the iterates, the iteration count and Dif are those of the one-chunk-
+// at-a-time loop.
+template <typename real>
+int QuadSession<real>::run_pipelined(int target) {
+    for (int k = 0; k < 2; k++) {
+        if (!snap_[k]) snap_[k] = static_cast<Ctrl<real> *>(pinned_small_get());
+        if (!snapev_[k]) PFDR_HIP(hipEventCreateWithFlags(&snapev_[k], hipEventDisableTiming));
+    }
+    int k = 0, nq = 0;  // slot of the oldest unread snapshot, chunks in flight
+    int ahead = it_;    // iterations launched so far, if none stops
+    while (!stopped_) {
+        while (nq < 2 && ahead < target) {
+            const int n = std::min(target - ahead, chunk_);
+            if (tiny_) tiny_chunk(n);
+            else run_bodies(n);
+            const int slot = (k + nq) & 1;
+            PFDR_HIP(hipMemcpyAsync(snap_[slot], ctrl_.p, sizeof(Ctrl<real>),
+                                    hipMemcpyDeviceToHost, stream));
+            PFDR_HIP(hipEventRecord(snapev_[slot], stream));
+            ahead += n;
+            nq++;
+        }
+        if (nq == 0) break;
+        PFDR_HIP(hipEventSynchronize(snapev_[k]));
+        *hctrl_ = *snap_[k];
+        k ^= 1;
+        nq--;
+        it_ = hctrl_->it;
+        if (hctrl_->stop) {
+            stopped_ = true;
+        } else if (hctrl_->recond) {
+            wait_stream();  // the chunk queued behind it ran halted
+            nq = 0;
+            ahead = it_;
+            if (verbose_) { print_progress(); printf("Reconditioning... "); fflush(stdout); }
+            precondition(false);
+            refresh_ends();
+            drop_graphs();
+            difRcd2_ *= real(0.01);  // ref :458
+            hctrl_->difRcd = difRcd2_;
+            hctrl_->recond = 0;
+            hctrl_->halt = 0;
+            push_ctrl();
+            if (verbose_) { printf("done.\n"); fflush(stdout); }
+        }
+        if (verbose_ && (it_ >= next_print_ || stopped_)) {
+            print_progress();
+            next_print_ = it_ + verbose_;
+        }
+        if (!stopped_ && nq == 0 && ahead >= target) break;
     }
     wait_stream();
     if (prof.on) prof.resolve();
