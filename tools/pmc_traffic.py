@@ -33,7 +33,26 @@ def counter(dirname, name):
     return vals
 
 
+def bench_size(root):
+    """(E, V) of the run, from the bench line the profiled command printed
+    (fetch.log / stats.log in the profile directory), or None"""
+    import re
+    for name in ("fetch.log", "write.log", "stats.log"):
+        try:
+            t = open(os.path.join(root, name)).read()
+        except OSError:
+            continue
+        e = re.search(r'"E_per_gpu": (\d+)', t)
+        v = re.search(r'"V_per_gpu": (\d+)', t)
+        if e and v:
+            return int(e.group(1)), int(v.group(1))
+    return None
+
+
 def main(root, workload="headline", E=60000000, V=10000000):
+    size = bench_size(root)  # the run's own size wins over the defaults
+    if size:
+        E, V = size
     fetch = counter(os.path.join(root, "fetch"), "FETCH_SIZE")
     write = counter(os.path.join(root, "write"), "WRITE_SIZE")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
