@@ -1096,6 +1096,8 @@ class SimplexSession final : public SessionBase {
             (void)hipStreamSynchronize(stream);  // no control-block copy in flight
             pinned_small_put(hctrl_);
         }
+        for (Ctrl<real> *c : snap_) if (c) pinned_small_put(c);
+        for (hipEvent_t e : snapev_) if (e) (void)hipEventDestroy(e);
         drop_graphs();
         for (hipEvent_t e : evv_) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : evd_) if (e) (void)hipEventDestroy(e);
@@ -1107,6 +1109,7 @@ class SimplexSession final : public SessionBase {
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
     void *device_x() override { return Pb(it_); }
+    void on_stop_or_recond();
 
   private:
     SxConst<real> c_;
@@ -1152,6 +1155,10 @@ class SimplexSession final : public SessionBase {
     SxR2<real> *PFb(int t) { return spec_ && (t & 1) ? PF2_.p : PF_.p; }
     hipStream_t evs_ = nullptr;
     hipEvent_t evv_[2] = {}, evd_[2] = {};
+    // pipelined gated runs (QuadSession::run_pipelined): control-block
+    // snapshots of two chunks in flight
+    Ctrl<real> *snap_[2] = {};
+    hipEvent_t snapev_[2] = {};
     void body_spec(int i, int n);
     void sweeps(const Ctrl<real> *c, int t);  // edge + vertex pass of iteration t
     DevBuf<int> Eu_, Ev_;
@@ -1706,6 +1713,46 @@ template <typename real>
 int SimplexSession<real>::run(int iters) {
     const bool gated = track_ || rec_obj_;
     const int target = (int)std::min<long>((long)it_ + std::max(iters, 0), (long)itMax_);
+    if (gated && !halo_ && !spec_) {
+        // two chunks in flight, as QuadSession::run_pipelined: chunk k + 1 is
+        // launched before the host reads chunk k's control-block snapshot; a
+        // chunk launched after a stop or a reconditioning request runs
+        // halted (every kernel returns at once)
+        for (int k = 0; k < 2; k++) {
+            if (!snap_[k]) snap_[k] = static_cast<Ctrl<real> *>(pinned_small_get());
+            if (!snapev_[k]) PFDR_HIP(hipEventCreateWithFlags(&snapev_[k], hipEventDisableTiming));
+        }
+        int k = 0, nq = 0, ahead = it_;
+        while (!stopped_) {
+            while (nq < 2 && ahead < target) {
+                const int n = std::min(target - ahead, chunk_);
+                if (tiny_) tiny_chunk(n);
+                else run_bodies(n);
+                const int slot = (k + nq) & 1;
+                PFDR_HIP(hipMemcpyAsync(snap_[slot], ctrl_.p, sizeof(Ctrl<real>),
+                                        hipMemcpyDeviceToHost, stream));
+                PFDR_HIP(hipEventRecord(snapev_[slot], stream));
+                ahead += n;
+                nq++;
+            }
+            if (nq == 0) break;
+            PFDR_HIP(hipEventSynchronize(snapev_[k]));
+            *hctrl_ = *snap_[k];
+            k ^= 1;
+            nq--;
+            it_ = hctrl_->it;
+            if (hctrl_->recond && !hctrl_->stop) {
+                wait_stream();  // the chunk queued behind it ran halted
+                nq = 0;
+                ahead = it_;
+            }
+            on_stop_or_recond();
+            if (!stopped_ && nq == 0 && ahead >= target) break;
+        }
+        wait_stream();
+        if (prof.on) prof.resolve();
+        return it_;
+    }
     while (!stopped_ && it_ < target) {
         const int n = std::min(target - it_, chunk_);
         if (tiny_) tiny_chunk(n);
@@ -1714,41 +1761,52 @@ int SimplexSession<real>::run(int iters) {
             PFDR_HIP(hipMemcpyAsync(hctrl_, ctrl_.p, sizeof(Ctrl<real>), hipMemcpyDeviceToHost, stream));
             wait_stream();
             it_ = hctrl_->it;
-            if (hctrl_->stop) {
-                stopped_ = true;
-            } else if (hctrl_->recond) {
-                if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
-                precondition(false);
-                drop_graphs();  // kernel arguments (A1_, stored weights) may have changed
-                k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
-                PFDR_HIP(hipGetLastError());
-                pullPF();
-                difRcd_ *= real(0.1);  // ref :563
-                hctrl_->difRcd = difRcd_;
-                hctrl_->recond = 0;
-                hctrl_->halt = 0;
-                PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, stream));
-                if (verbose_) { printf("done.\n"); fflush(stdout); }
-            }
+            on_stop_or_recond();
         } else {
             it_ += n;
             if (it_ >= itMax_) stopped_ = true;
-        }
-        if (verbose_ && (it_ >= next_print_ || stopped_)) {
-            printf("iteration %d (max. %d)\n", it_, itMax_);
-            if (track_ == 2)
-                printf("label evolution %d (recond. %d; tol. %d)\n", (int)hctrl_->dif,
-                       (int)hctrl_->difRcd, (int)difTol_);
-            else if (track_ == 1)
-                printf("iterate evolution %g (recond. %g; tol. %g)\n", (double)hctrl_->dif,
-                       (double)hctrl_->difRcd, (double)difTol_);
-            fflush(stdout);
-            next_print_ = it_ + verbose_;
+            on_stop_or_recond();
         }
     }
     wait_stream();
     if (prof.on) prof.resolve();
     return it_;
+}
+
+// after a chunk: the stop or reconditioning the control block (hctrl_, just
+// read) asks for, then the progress line
+template <typename real>
+void SimplexSession<real>::on_stop_or_recond() {
+    const bool gated = track_ || rec_obj_;
+    if (gated) {
+        if (hctrl_->stop) {
+            stopped_ = true;
+        } else if (hctrl_->recond) {
+            if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
+            precondition(false);
+            drop_graphs();  // kernel arguments (A1_, stored weights) may have changed
+            k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
+            PFDR_HIP(hipGetLastError());
+            pullPF();
+            difRcd_ *= real(0.1);  // ref :563
+            hctrl_->difRcd = difRcd_;
+            hctrl_->recond = 0;
+            hctrl_->halt = 0;
+            PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, stream));
+            if (verbose_) { printf("done.\n"); fflush(stdout); }
+        }
+    }
+    if (verbose_ && (it_ >= next_print_ || stopped_)) {
+        printf("iteration %d (max. %d)\n", it_, itMax_);
+        if (track_ == 2)
+            printf("label evolution %d (recond. %d; tol. %d)\n", (int)hctrl_->dif,
+                   (int)hctrl_->difRcd, (int)difTol_);
+        else if (track_ == 1)
+            printf("iterate evolution %g (recond. %g; tol. %g)\n", (double)hctrl_->dif,
+                   (double)hctrl_->difRcd, (double)difTol_);
+        fflush(stdout);
+        next_print_ = it_ + verbose_;
+    }
 }
 
 // host wait for the session stream (partitioned: under the transport's watchdog)
