@@ -187,6 +187,84 @@ def make_cases():
         Asum = (0.5 + uniform(15, np.arange(120))).astype(dt)
         cases["proj_simplex_" + nm] = dict(solver="proj", X=X, M=M, D=D, N=N,
                                            nm=200, A=Asum, na=120)
+    cases.update(make_wide_cases())
+    return cases
+
+
+def _grid_labels(shape, K):
+    """block labels of a 2-D grid: quadrants, a left band, spread over K"""
+    nx, ny = shape
+    v = np.arange(nx * ny)
+    lab = (v % nx >= nx // 2).astype(int) + 2 * (v // nx >= ny // 2) + 4 * ((v % nx) < nx // 5)
+    return (lab * max(1, K // 7) + v // (2 * nx)) % K
+
+
+def make_wide_cases():
+    """Round 5: the simplex and the metric projection beyond K = 10 / D = 7
+    (every label count the K-generic code paths take: the fused vertex
+    sweep's upper range K <= 64, odd K with stored prox weights, the
+    wave-per-vertex path from K = 65, and K, D > 1024 with the active set
+    outside registers).  The reference handles any K (alloca(D),
+    src/proj_simplex_metric.cpp:38, called with D = K from
+    src/PFDR_graph_loss_d1_simplex.cpp:651)."""
+    cases = {}
+    # (K, grid, loss variants) -- sizes keep V*K <= ~30K so the reference's
+    # single-threaded converged run finishes in about a second
+    plan = [
+        (16, (12, 12), [("kl", {})]),
+        (33, (10, 10), [("quad_laf_recond", dict(al=1.0, laf=True, difRcd=1e-2))]),
+        (63, (8, 8), [("linear", dict(al=0.0, difTol=1e-5))]),
+        (64, (8, 8), [("kl_recond", dict(difRcd=1e-2, difTol=1e-5))]),
+        (65, (8, 8), [("kl", {}), ("labels", dict(al=0.5, difTol=1.0, difRcd=8.0, uniform0=True))]),
+        (128, (8, 6), [("quad_laf", dict(al=1.0, laf=True)), ("linear", dict(al=0.0, difTol=1e-5))]),
+        (1024, (4, 4), [("kl", {})]),
+        (1500, (5, 4), [("kl_laf_recond", dict(laf=True, difRcd=1e-2, difTol=1e-5)),
+                        ("linear", dict(al=0.0, difTol=1e-5))]),
+    ]
+    for K, shape, variants in plan:
+        Eu, Ev = grid_graph(shape, 8)
+        V = int(np.prod(shape))
+        v = np.arange(V)
+        lab = _grid_labels(shape, K)
+        for tag, opt in variants:
+            dts = ((np.float32, "f32"), (np.float64, "f64"))
+            if tag in ("labels",) or (K == 128 and tag == "linear"):
+                dts = ((np.float32, "f32"),)
+            for dt, nm in dts:
+                Q = simplex_observation(V, K, 40 + K, lab, dt)
+                laf = (1.0 + np.floor(4 * uniform(41 + K, v))).astype(dt)
+                c = dict(solver="simplex", K=K, P0=Q.copy(), Q=Q, Eu=Eu, Ev=Ev,
+                         La_d1=np.full(Eu.size, 0.05, dt), La_f=None, al=0.1,
+                         rho=1.0, condMin=0.1, difRcd=0.0, difTol=1e-4,
+                         itMax=2000)
+                for k in ("al", "difRcd", "difTol"):
+                    if k in opt:
+                        c[k] = opt[k]
+                if opt.get("laf"):
+                    c["La_f"] = laf
+                if opt.get("uniform0"):
+                    c["P0"] = np.full(V * K, 1.0 / K, dt)
+                cases["simplex_k%d_%s_%s" % (K, tag, nm)] = c
+    # metric projection: one segment of G lanes per column (D <= 64), J
+    # registers per lane (D <= 1024), the active set in scratch (D > 1024);
+    # nm, na < N as in proj_simplex_D7
+    for D, N, nm, na in ((16, 90, 70, 33), (33, 80, 50, 21), (64, 60, 41, 17), (65, 60, 41, 17),
+                         (1024, 40, 30, 17), (2000, 30, 22, 9)):
+        for dt, tnm in ((np.float32, "f32"), (np.float64, "f64")):
+            X = (3.0 * uniform(50 + D, np.arange(D * N)) - 1.0).astype(dt)
+            M = (0.1 + uniform(51 + D, np.arange(D * nm))).astype(dt)
+            Asum = (0.5 + uniform(52 + D, np.arange(na))).astype(dt)
+            cases["proj_simplex_D%d_%s" % (D, tnm)] = dict(solver="proj", X=X, M=M, D=D, N=N,
+                                                          nm=nm, A=Asum, na=na)
+    # adversarial order: ascending columns (every coordinate enters the
+    # first pass, most leave again in the second) and a column of equal values
+    for D in (200, 1500):
+        N = 6
+        X = np.concatenate([np.sort(uniform(60 + D + n, np.arange(D)) * (n + 1)) for n in range(N - 1)]
+                           + [np.full(D, 0.25)])
+        M = (0.5 + uniform(61 + D, np.arange(D))).astype(np.float64)
+        cases["proj_simplex_sorted_D%d_f64" % D] = dict(solver="proj", X=X, M=M, D=D, N=N,
+                                                      nm=1, A=np.ones(1), na=1)
     return cases
 
 

@@ -13,6 +13,7 @@ Obj is stored only where the reference computes it without its stale-index
 read (src/PFDR_graph_quadratic_d1_l1.cpp:417): positivity or La_l1 == NULL.
 Single-threaded build, so no thread-count-dependent rounding
 (SURVEY.md §8(a) quirks).  Usage:  python tests/golden/make_golden.py
+[name prefix ...]  (no prefix: every case)
 """
 import os
 import sys
@@ -58,10 +59,14 @@ def obj_valid(c):
                 and not c["positivity"])
 
 
-def main():
+def main(prefixes=()):
+    """prefixes: regenerate only the cases whose name starts with one of
+    them (round 5 added the wide-K cases without rewriting the others)"""
     lib = Oracle("ref")
     cases = C.make_cases()
     for name, c in cases.items():
+        if prefixes and not name.startswith(tuple(prefixes)):
+            continue
         out = {}
         for k, v in c.items():
             if v is None:
@@ -87,4 +92,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])
