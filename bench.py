@@ -44,7 +44,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-CPU_REPEATS = 3        # CPU baseline: minimum of this many calls per T(k)
+CPU_PAIRS = 5          # CPU baseline: paired (T(k0), T(k1)) estimates, median reported
 CORE_GBS = 25.0        # one host core's streaming rate, upper bound (baseline floor)
 
 
@@ -115,10 +115,13 @@ def cpu_baseline_child(args):
         kw, V = inp["kw"], inp["V"]
         Eu, Ev = kw["Eu"], kw["Ev"]
     Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
-    # per-iteration time = (T(k1) - T(k0)) / (k1 - k0) with k1 - k0 >= 10, each
-    # T the minimum of REPEATS whole calls (setup varies run to run by more
-    # than a few iterations cost; a 1-2 iteration span made the number noise)
-    args.cpu_k0, args.cpu_k1 = {"c3": (1, 11), "c4": (1, 11)}.get(name, (2, 12))
+    # per-iteration time = (T(k1) - T(k0)) / (k1 - k0): the median of CPU_PAIRS
+    # paired estimates (T(k0) then T(k1), back to back) over a span of 40
+    # iterations (10 for the slow dense / simplex configurations), the OpenMP
+    # threads bound one per core (OMP_PROC_BIND / OMP_PLACES, set by the
+    # parent): a difference of two independently noisy minima over 10
+    # iterations had spread 0.55 (round 4's driver line)
+    args.cpu_k0, args.cpu_k1 = {"c3": (1, 11), "c4": (1, 11)}.get(name, (2, 42))
 
     def call(k):
         if name == "c4":
@@ -135,17 +138,17 @@ def cpu_baseline_child(args):
         else:
             lib.quadratic_d1_l1(kw["X0"].copy(), kw["Y"], None, 0, Eu, Ev, kw["La_d1"],
                                 kw["La_l1"], 0, 0, None, kw["rho"], kw["condMin"], 0.0, 0.0, k)
-    runs = {}
-    for rep in range(CPU_REPEATS):
+    span = args.cpu_k1 - args.cpu_k0
+    call(args.cpu_k0)  # warm: page-in of the inputs and the library, thread pool start
+    runs = {args.cpu_k0: [], args.cpu_k1: []}
+    for rep in range(CPU_PAIRS):
         for k in (args.cpu_k0, args.cpu_k1):
             t = time.perf_counter()
             call(k)
-            runs.setdefault(k, []).append(time.perf_counter() - t)
-    t0, t1 = min(runs[args.cpu_k0]), min(runs[args.cpu_k1])
-    span = args.cpu_k1 - args.cpu_k0
-    per_it = (t1 - t0) / span
-    # spread: the per-iteration times of the repeat pairs, relative to the min-based one
+            runs[k].append(time.perf_counter() - t)
     pairs = [(b - a) / span for a, b in zip(runs[args.cpu_k0], runs[args.cpu_k1])]
+    per_it = float(np.median(pairs))
+    t0 = float(np.median(runs[args.cpu_k0]))
     # floor: the reference's DR average is a serial scatter over 2E ends
     # (src/PFDR_graph_quadratic_d1_l1.cpp:492-497; simplex per label,
     # src/PFDR_graph_loss_d1_simplex.cpp:636-648): one core reads W and Z and
@@ -155,12 +158,14 @@ def cpu_baseline_child(args):
     floor = 16.0 * Eu.size * K / (CORE_GBS * 1e9)
     out = {"unit": "Medge-updates/s", "cores": len(cores) if kind == "reference" else 1,
            "kind": kind,
-           "sample": "%s (V=%d, E=%d) fp32, per-iteration time = (T(%d it) - T(%d it)) / %d, "
-                     "each T the minimum of %d calls, setup excluded" % (
-                         sample, V, Eu.size, args.cpu_k1, args.cpu_k0, span, CPU_REPEATS),
+           "sample": "%s (V=%d, E=%d) fp32, per-iteration time = median over %d back-to-back "
+                     "pairs of (T(%d it) - T(%d it)) / %d, OpenMP threads bound to cores, "
+                     "setup excluded" % (sample, V, Eu.size, CPU_PAIRS, args.cpu_k1, args.cpu_k0,
+                                         span),
            "per_iteration_s": per_it,
            "spread": {"pair_per_iteration_s": [round(x, 6) for x in pairs],
-                      "rel": round((max(pairs) - min(pairs)) / per_it, 4) if per_it > 0 else None},
+                      "rel": round((max(pairs) - min(pairs)) / per_it, 4) if per_it > 0 else None,
+                      "omp": {k: os.environ.get(k) for k in ("OMP_PROC_BIND", "OMP_PLACES")}},
            "bandwidth_floor_s": floor, **host}
     if per_it < floor:
         out.update(value=None, error="per-iteration time %.4g s below the serial-scatter floor "
@@ -175,9 +180,13 @@ def run_cpu_baseline(args):
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child",
            "--cpu-k0", str(args.cpu_k0), "--cpu-k1", str(args.cpu_k1),
            "--cpu-cores", str(args.cpu_cores), "--workload", args.workload]
+    # one OpenMP thread per core, kept there (the reference sets its thread
+    # count through num_threads clauses, src/PFDR_graph_quadratic_d1_l1.cpp:31-41;
+    # libgomp still honours the binding variables)
+    env = dict(os.environ, OMP_PROC_BIND="close", OMP_PLACES="cores")
     try:
         out = subprocess.run(cmd, check=True, capture_output=True, text=True,
-                             timeout=900).stdout
+                             timeout=900, env=env).stdout
         return json.loads(out.strip().splitlines()[-1])
     except Exception as ex:  # reported, never fatal for the GPU number
         return {"value": None, "error": repr(ex)[:300]}

@@ -29,6 +29,13 @@ bool comm_aborted(void *comm) {
     std::lock_guard<std::mutex> l(g_aborted_m);
     return g_aborted.count(comm) != 0;
 }
+
+// a communicator just created at the address of one the watchdog aborted
+// (released by ncclCommAbort, its handle never destroyed): the entry is stale
+void comm_created(void *comm) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    g_aborted.erase(comm);
+}
 }  // namespace pfdr
 
 int pfdr::report_rccl(const char *fn, ncclResult_t r) {
@@ -57,11 +64,7 @@ extern "C" int pfdr_comm_init(void **comm_out, int nranks, int rank, const void 
     ncclComm_t comm;
     ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
     if (r != ncclSuccess) return pfdr::report_rccl("pfdr_comm_init", r);
-    {   // a new communicator at the address of one the watchdog aborted (and
-        // the caller never destroyed): the old entry is stale
-        std::lock_guard<std::mutex> l(pfdr::g_aborted_m);
-        pfdr::g_aborted.erase(comm);
-    }
+    pfdr::comm_created(comm);
     *comm_out = comm;
     return PFDR_OK;
 }

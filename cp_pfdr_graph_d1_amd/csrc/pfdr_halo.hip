@@ -167,6 +167,8 @@ void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
 // ----------------------------------------------------------------- RCCL --
 class RcclTransport final : public Transport {
     ncclComm_t comm_;
+    bool owned_ = false;             // a split communicator: destroyed with the transport
+    std::vector<ncclComm_t> kids_;   // split from this one: aborted with it
     static void ck(ncclResult_t r, const char *what) {
         if (r != ncclSuccess) {
             char m[256];
@@ -177,10 +179,28 @@ class RcclTransport final : public Transport {
 
   public:
     RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) { nranks = n; rank = r; }
+    ~RcclTransport() override {
+        if (!owned_) return;
+        if (comm_aborted(comm_)) comm_created(comm_);  // released by the abort
+        else (void)ncclCommDestroy(comm_);
+    }
     // a stalled communicator cannot be used again: abort it so the peers'
     // operations fail too instead of waiting on this rank (recorded, so the
     // owner's pfdr_comm_destroy skips the freed handle)
-    void on_timeout() override { comm_abort(comm_); }
+    void on_timeout() override {
+        comm_abort(comm_);
+        for (ncclComm_t k : kids_) comm_abort(k);
+    }
+    std::unique_ptr<Transport> split(hipStream_t) override {
+        last_op = "communicator split";
+        ncclComm_t nc = nullptr;
+        ck(ncclCommSplit(comm_, 0, rank, &nc, nullptr), "comm split");
+        comm_created(nc);
+        kids_.push_back(nc);
+        std::unique_ptr<RcclTransport> t(new RcclTransport(nc, nranks, rank));
+        t->owned_ = true;
+        return std::unique_ptr<Transport>(t.release());
+    }
     bool capturable() const override { return true; }
     void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,
@@ -313,6 +333,9 @@ class LoopbackTransport final : public Transport {
         nranks = n;
         rank = r;
         if (hub_->k != n) throw std::runtime_error("loopback hub size differs from nranks");
+    }
+    std::unique_ptr<Transport> split(hipStream_t) override {
+        return std::unique_ptr<Transport>(new LoopbackTransport(hub_, nranks, rank));
     }
     void exchange(const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
                   const std::vector<void *> &recv, const std::vector<size_t> &rbytes,

@@ -18,7 +18,9 @@
 // device-to-device copies) — the latter lets the whole partitioned path be
 // tested on one GPU against the unpartitioned solver.
 #pragma once
+#include <algorithm>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -62,6 +64,13 @@ class Transport {
     // send `bytes` from dev to rank+1 (last rank: nothing)
     virtual void chain_send(const void *dev, size_t bytes, hipStream_t s) = 0;
     virtual void broadcast(void *dev, size_t bytes, int root, hipStream_t s) = 0;
+    // a second transport over the same ranks whose operations may run
+    // CONCURRENTLY with this one's, on another stream (a speculative
+    // session's evolution sums beside the next iteration's halo exchanges).
+    // RCCL: its own communicator (ncclCommSplit; collective, setup only),
+    // aborted with this one by the watchdog; loopback: the same hub (its
+    // exchanges are serialised by the host threads anyway)
+    virtual std::unique_ptr<Transport> split(hipStream_t s) = 0;
     // host-level allgather of one int64 per rank (setup only)
     void allgather_i64(int64_t mine, std::vector<int64_t> &all, hipStream_t s);
     // variable-size all-to-all of host arrays (setup only)
@@ -74,6 +83,7 @@ std::unique_ptr<Transport> make_rccl_transport(void *comm, int nranks, int rank)
 // once, remembered so that pfdr_comm_destroy does not free it a second time
 void comm_abort(void *comm);
 bool comm_aborted(void *comm);
+void comm_created(void *comm);  // forget a stale aborted entry at this address
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
 // wake every rank waiting on the hub with an error (a rank failed)
 void loopback_abort(void *hub, const char *reason);
@@ -218,6 +228,124 @@ struct ChainSum {
         PFDR_HIP(hipGetLastError());
         tr.chain_send(out, sizeof(real) * nsum, s);
         tr.broadcast(out, sizeof(real) * nsum, nranks - 1, s);
+    }
+};
+
+// item j of the route: its W terms of every sum into the send buffer (items
+// grouped by destination), and back out of the receive buffer at its slot
+template <typename real>
+__global__ void k_route_pack(long n, int W, int nsum, const int *__restrict__ sidx,
+                             const real *__restrict__ terms, long tstride,
+                             real *__restrict__ buf) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * W) return;
+    const long j = t / W;
+    const int w = (int)(t - j * W);
+    const long v = sidx[j];
+    for (int y = 0; y < nsum; y++) buf[(j * nsum + y) * W + w] = terms[y * tstride + v * W + w];
+}
+template <typename real>
+__global__ void k_route_unpack(long n, int W, int nsum, const int *__restrict__ rpos,
+                               const real *__restrict__ buf, real *__restrict__ slice,
+                               long sstride) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * W) return;
+    const long j = t / W;
+    const int w = (int)(t - j * W);
+    const long p = rpos[j];
+    for (int y = 0; y < nsum; y++) slice[y * sstride + p * W + w] = buf[(j * nsum + y) * W + w];
+}
+
+// Iterate-evolution sums of a RELABELLED partition (the ranks own ranges of
+// internal labels, while the reference sums in the caller's order).  The
+// caller's order is cut into contiguous slices, slice q = caller labels
+// [Vg q / N, Vg (q + 1) / N) on rank q; every owned vertex's W terms of each
+// sum travel, at positions fixed at setup, to the rank whose slice holds its
+// caller label -- one variable all-to-all of ~V/N items per rank per tracked
+// iteration, the vertex's own rank included when its label falls there -- and
+// ChainSum then runs over the slices in rank order, which IS the caller's
+// order: Dif bit-identical to one GPU, with O(V/N) bytes per rank on the
+// wire instead of an all-reduce of the whole V_global term vector.
+template <typename real>
+struct TermRoute {
+    int nsum = 1, W = 1, nranks = 1, rank = 0;
+    long nsend = 0, nrecv = 0, S = 0, sstride = 0;
+    std::vector<long> soff, roff;  // per peer, in items (nranks + 1)
+    DevBuf<int> sidx, rpos;
+    DevBuf<real> sbuf, rbuf, slice;
+    ChainSum<real> chain;
+    bool ready() const { return chain.ready(); }
+    // lab: caller labels of the V owned vertices (host), a permutation of
+    // [0, Vglob) over the ranks
+    void init(const std::vector<int> &lab, long Vglob, int nsum_, int W_, Transport &tr,
+              hipStream_t s) {
+        nsum = nsum_; W = W_; nranks = tr.nranks; rank = tr.rank;
+        const int n = nranks;
+        std::vector<int64_t> coff(n + 1);
+        for (int q = 0; q <= n; q++) coff[q] = Vglob * q / n;
+        S = coff[rank + 1] - coff[rank];
+        auto owner = [&](int64_t g) {
+            return (int)(std::upper_bound(coff.begin(), coff.end(), g) - coff.begin()) - 1;
+        };
+        std::vector<std::vector<int64_t>> pos(n), got;
+        std::vector<std::vector<int>> items(n);
+        for (size_t v = 0; v < lab.size(); v++) {
+            const int q = owner(lab[v]);
+            items[q].push_back((int)v);
+            pos[q].push_back(lab[v] - coff[q]);
+        }
+        tr.alltoallv_host(pos, got, s);
+        soff.assign(n + 1, 0);
+        roff.assign(n + 1, 0);
+        std::vector<int> hs, hr;
+        for (int q = 0; q < n; q++) {
+            soff[q + 1] = soff[q] + (long)items[q].size();
+            roff[q + 1] = roff[q] + (long)got[q].size();
+            hs.insert(hs.end(), items[q].begin(), items[q].end());
+            for (int64_t p : got[q]) hr.push_back((int)p);
+        }
+        nsend = soff[n];
+        nrecv = roff[n];
+        if (nrecv != S) throw std::runtime_error("vtx_label is not a permutation of [0, V_global)");
+        sidx.alloc(nsend ? nsend : 1);
+        rpos.alloc(nrecv ? nrecv : 1);
+        if (nsend) PFDR_HIP(hipMemcpy(sidx.p, hs.data(), sizeof(int) * nsend, hipMemcpyHostToDevice));
+        if (nrecv) PFDR_HIP(hipMemcpy(rpos.p, hr.data(), sizeof(int) * nrecv, hipMemcpyHostToDevice));
+        sbuf.alloc((size_t)(nsend ? nsend : 1) * nsum * W);
+        rbuf.alloc((size_t)(nrecv ? nrecv : 1) * nsum * W);
+        sstride = (S * W + 3) / 4 * 4;
+        slice.alloc((size_t)(sstride ? sstride : 4) * nsum);
+        chain.init(S * W, nsum, tr);
+    }
+    // terms: W per owned vertex of every sum (sum y at y * tstride); out[0 ..
+    // nsum) the whole sums on every rank, as ChainSum::run
+    void run(Transport &tr, const real *terms, long tstride, real *out, const int *halt,
+             hipStream_t s) {
+        const int n = nranks;
+        if (nsend) {
+            k_route_pack<real><<<grid_for(nsend * W), kBlock, 0, s>>>(nsend, W, nsum, sidx.p, terms,
+                                                                    tstride, sbuf.p);
+            PFDR_HIP(hipGetLastError());
+        }
+        const size_t ib = sizeof(real) * nsum * W;  // bytes per item
+        std::vector<const void *> sp(n);
+        std::vector<void *> rp(n);
+        std::vector<size_t> sb(n), rb(n);
+        for (int q = 0; q < n; q++) {
+            sp[q] = (const char *)sbuf.p + soff[q] * ib;
+            sb[q] = (size_t)(soff[q + 1] - soff[q]) * ib;
+            rp[q] = (char *)rbuf.p + roff[q] * ib;
+            rb[q] = (size_t)(roff[q + 1] - roff[q]) * ib;
+        }
+        tr.exchange(sp, sb, rp, rb, s);  // (skips this rank's own part)
+        if (rb[rank])
+            PFDR_HIP(hipMemcpyAsync(rp[rank], sp[rank], rb[rank], hipMemcpyDeviceToDevice, s));
+        if (nrecv) {
+            k_route_unpack<real><<<grid_for(nrecv * W), kBlock, 0, s>>>(nrecv, W, nsum, rpos.p,
+                                                                      rbuf.p, slice.p, sstride);
+            PFDR_HIP(hipGetLastError());
+        }
+        chain.run(tr, slice.p, sstride, out, halt, s);
     }
 };
 

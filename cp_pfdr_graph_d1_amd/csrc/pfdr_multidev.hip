@@ -142,20 +142,26 @@ bool distinct(const std::vector<int> &d) {
     return std::adjacent_find(s.begin(), s.end()) == s.end();
 }
 
-// the communicators of the device group (created on first use, re-created
-// after a watchdog abort); caller holds c.m
-std::vector<ncclComm_t> group_comms(DeviceConfig &c) {
-    bool ok = c.comm_devs == c.devs && c.comms.size() == c.devs.size();
+// the communicators of the device group `devs` (created on first use,
+// re-created after a watchdog abort or for another group); caller holds c.m.
+// comms[r] belongs to devs[r].
+std::vector<ncclComm_t> group_comms(DeviceConfig &c, const std::vector<int> &devs) {
+    bool ok = c.comm_devs == devs && c.comms.size() == devs.size();
     for (ncclComm_t cm : c.comms) ok = ok && !comm_aborted(cm);
     if (!ok) {
-        c.comms.clear();  // aborted ones were released by ncclCommAbort; others leak
+        for (ncclComm_t cm : c.comms) {  // aborted ones were released by ncclCommAbort
+            if (comm_aborted(cm)) comm_created(cm);  // forget the released handle
+            else (void)ncclCommDestroy(cm);
+        }
+        c.comms.clear();
         c.comm_devs.clear();
-        std::vector<ncclComm_t> cm(c.devs.size());
-        const ncclResult_t r = ncclCommInitAll(cm.data(), (int)c.devs.size(), c.devs.data());
+        std::vector<ncclComm_t> cm(devs.size());
+        const ncclResult_t r = ncclCommInitAll(cm.data(), (int)devs.size(), devs.data());
         if (r != ncclSuccess)
             throw std::runtime_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        for (ncclComm_t x : cm) comm_created(x);  // a new handle at an aborted one's address
         c.comms = cm;
-        c.comm_devs = c.devs;
+        c.comm_devs = devs;
     }
     return c.comms;
 }
@@ -244,6 +250,12 @@ void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it
     const long V = p->V, E = p->E;
     const int Kw = p->kind == PFDR_KIND_SIMPLEX ? p->K : 1;
     const size_t rsz = p->dtype == PFDR_F32 ? 4 : 8;
+    // the sessions' own preconditions, checked before the host split reads
+    // the caller's arrays
+    if (V <= 0 || E < 0 || (p->kind == PFDR_KIND_SIMPLEX && p->K <= 0))
+        throw std::runtime_error("V (and K) must be > 0 and E >= 0");
+    if (!p->X || !p->Y || (E > 0 && (!p->Eu || !p->Ev || !p->La_d1)))
+        throw std::runtime_error("X, Y, Eu, Ev and La_d1 are required");
     if (n > (int)V) throw std::runtime_error("more devices than vertices");
     std::vector<int64_t> off(n + 1);
     for (int r = 0; r <= n; r++) off[r] = V * r / n;
@@ -257,7 +269,7 @@ void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it
     } else {
         DeviceConfig &c = config();
         std::lock_guard<std::mutex> lk(c.m);
-        comms = group_comms(c);
+        comms = group_comms(c, devs);
     }
     const bool ata = p->N < 0, direct = p->N > 0;
     std::vector<std::string> err(n);
@@ -340,18 +352,23 @@ extern "C" int pfdr_set_devices(int n, const int *devices, int64_t min_vertices)
         return report_error("pfdr_set_devices", "invalid arguments");
     DeviceConfig &c = config();
     std::lock_guard<std::mutex> lk(c.m);
-    c.set = true;
-    c.devs.clear();
     int count = 0;
     if (n > 0 && hipGetDeviceCount(&count) != hipSuccess) {
         (void)hipGetLastError();
         return report_error("pfdr_set_devices", "no HIP device");
     }
+    std::vector<int> devs;
     for (int i = 0; i < n; i++) {
         const int d = devices ? devices[i] : 0;
         if (d < 0 || d >= count) return report_error("pfdr_set_devices", "device id out of range");
-        c.devs.push_back(d);
+        devs.push_back(d);
     }
+    // distinct devices (RCCL) or one device repeated (loopback ranks on it)
+    if (!distinct(devs) && std::count(devs.begin(), devs.end(), devs[0]) != n)
+        return report_error("pfdr_set_devices",
+                            "devices must be all distinct or all the same one");
+    c.set = true;
+    c.devs = devs;
     c.min_vertices = min_vertices >= 0 ? (long)min_vertices : kMultiMinVertices;
     return PFDR_OK;
 }

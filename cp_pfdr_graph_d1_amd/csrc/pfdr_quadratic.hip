@@ -179,17 +179,24 @@ class QuadSession final : public SessionBase {
     DevBuf<real> terms_;
     DevBuf<char> dws_;
     // partitioned sessions: the terms of the ranks in rank order are summed
-    // rank to rank (ChainSum); a relabelled partition (lab_) writes its terms
-    // at the caller's labels of a V_global-long array, all-reduced (one
-    // writer per position) into tall_ and summed whole on every rank
+    // rank to rank (ChainSum); a relabelled partition (lab_) first routes
+    // every vertex's terms to the rank whose caller-order slice holds its
+    // label (TermRoute: one all-to-all of ~V/N items per rank), then chains
     ChainSum<real> chain_;
-    DevBuf<real> tall_;
+    TermRoute<real> route_;
+    // the transport of the evolution sums: a speculative partition's own
+    // (Transport::split), so they run beside the next iteration's exchanges
+    std::unique_ptr<Transport> evtr_;
+    Transport &etr() { return evtr_ ? *evtr_ : *halo_->tr; }
     void seq_evolution(real *terms, const real *part, hipStream_t s);
-    // Speculative iteration (single GPU, sequential evolution, no
-    // reconditioning (difRcd = 0), no objective record, identity / diagonal
-    // A): the evolution sums and the decision on iteration t run on a second
-    // stream (evs_) while iteration t + 1 sweeps; iteration t + 2 waits for
-    // that decision.  X is ping-ponged (iteration t reads xpb(t - 1), writes
+    void sweeps(const Ctrl<real> *c);  // halo pull, edge sweep, halo push, vertex sweep
+    // Speculative iteration (sequential evolution, no reconditioning
+    // (difRcd = 0), no objective record, identity / diagonal A; one GPU or a
+    // partition): the evolution sums and the decision on iteration t run on
+    // a second stream (evs_) while iteration t + 1 sweeps; iteration t + 2
+    // waits for that decision.  A partition runs its rank-to-rank evolution
+    // chain there over a split transport (evtr_), beside the halo exchanges
+    // of t + 1, instead of on the critical path of every iteration.  X is ping-ponged (iteration t reads xpb(t - 1), writes
     // xpb(t)) and the terms are double-buffered, so when the decision on t
     // stops the loop, X_t is intact in xpb(t) and the speculative t + 1 (its
     // Z, its X in the other buffer) is simply discarded: the iterate,
@@ -649,20 +656,21 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     seqdif_ = track_ && !tiny_ && !fuse_ &&
               (want_seq || (evo_ == PFDR_EVOLUTION_AUTO && Vglob_ >= kSeqDifMin));
     if (seqdif_) {
-        const long nt = halo_ && lab_.p ? Vglob_ : (long)V_;  // terms per sum
+        const long nt = V_;  // terms per sum, in this rank's vertex order
         tstride_ = (nt + 3) / 4 * 4;  // 16-byte aligned second array
         terms_.alloc(2 * (size_t)tstride_);
-        if (!halo_ || lab_.p) dws_.alloc(mono_ws_bytes<real>(nt, 2));
-        if (halo_ && lab_.p) {
-            if (2 * tstride_ > 0x7fffffffL) throw std::runtime_error("V_global too large");
-            PFDR_HIP(hipMemsetAsync(terms_.p, 0, sizeof(real) * terms_.n, s));
-            tall_.alloc(terms_.n);
-        } else if (halo_) {
+        if (!halo_) {
+            dws_.alloc(mono_ws_bytes<real>(nt, 2));
+        } else if (lab_.p) {  // routed to caller-order slices, then chained
+            std::vector<int> hl(V_);
+            PFDR_HIP(hipMemcpy(hl.data(), lab_.p, sizeof(int) * V_, hipMemcpyDeviceToHost));
+            route_.init(hl, Vglob_, 2, 1, *halo_->tr, s);
+        } else {
             chain_.init(V_, 2, *halo_->tr);
         }
         seqdif = 1;
-        spec_ = !halo_ && difRcd2_ == real(0) && !rec_obj_ &&
-                (mode_ == A_IDENT || mode_ == A_DIAG);
+        spec_ = difRcd2_ == real(0) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG);
+        if (spec_ && halo_) evtr_ = halo_->tr->split(s);  // (a collective: every rank decides alike)
         if (spec_) {
             DevBuf<real> t2(4 * (size_t)tstride_);  // terms of both parities
             std::swap(terms_.p, t2.p);
@@ -689,7 +697,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (spec_) graphs_ok_ = capturable_ = false;
     if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
     acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
-    acc(tall_.n * sizeof(real) + chain_.ws.n + ampg_.n * sizeof(real) +
+    acc(route_.slice.n * sizeof(real) + route_.chain.ws.n + chain_.ws.n + ampg_.n * sizeof(real) +
         xp2_.n * sizeof(R2<real>));
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
     // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
@@ -1337,7 +1345,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.l1uni = l1_uniform_ ? 1 : 0;
     a.l1u = l1u_;
     a.terms = seqdif_ ? terms_.p : nullptr;
-    a.tmap = !seqdif_ ? nullptr : reordered_ ? order_.p : halo_ ? lab_.p : nullptr;
+    a.tmap = seqdif_ && reordered_ ? order_.p : nullptr;
     a.tstride = tstride_;
     a.bbeg = bbeg; a.nb = bend - bbeg; a.xcd = xcd_fit(a.nb, xcd_v_);
     a.bsplit = a.nb; a.bjump = 0;
@@ -1369,6 +1377,51 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
         k_vertex_sweep<real, 8><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(a);
 }
 
+// the sweeps of one iteration: (partitions) the ghosts' (X, P) pulled into
+// the buffer the edge sweep reads (xr_), the edge sweep, the ghost ends'
+// contributions pushed to their owners, the vertex sweep (into xw_)
+template <typename real>
+void QuadSession<real>::sweeps(const Ctrl<real> *c) {
+    hipStream_t s = stream;
+    if (overlap_) {
+        // pull ghosts (comm) || interior edges; boundary edges; push (comm)
+        // || interior vertices; boundary vertices
+        PFDR_HIP(hipEventRecord(ev_[0], s));
+        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[0], 0));
+        {
+            ProfScope ps(prof, "halo_pull", comm_);
+            halo_->pull(xr_, sizeof(R2<real>), comm_);
+        }
+        PFDR_HIP(hipEventRecord(ev_[1], comm_));
+        edge_sweep(elo_, ehi_, c, "edge_sweep");
+        PFDR_HIP(hipStreamWaitEvent(s, ev_[1], 0));
+        edge_sweep(0, elo_, c, "edge_sweep_b", ehi_, E_);  // both boundary ranges, one launch
+        PFDR_HIP(hipEventRecord(ev_[2], s));
+        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[2], 0));
+        {
+            ProfScope ps(prof, "halo_push", comm_);
+            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
+            halo_->push(src, src + 2 * E_, sizeof(real), comm_);
+        }
+        PFDR_HIP(hipEventRecord(ev_[3], comm_));
+        vertex_sweep(blo_, bhi_, c, "vertex_sweep");
+        PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
+        vertex_sweep(0, blo_, c, "vertex_sweep_b", bhi_, nbv_);
+    } else {
+        if (halo_) {
+            ProfScope ps(prof, "halo_pull", s);
+            halo_->pull(xr_, sizeof(R2<real>), s);
+        }
+        edge_sweep(0, E_, c, "edge_sweep");
+        if (halo_) {
+            ProfScope ps(prof, "halo_push", s);
+            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
+            halo_->push(src, src + 2 * E_, sizeof(real), s);
+        }
+        vertex_sweep(0, nbv_, c, "vertex_sweep");
+    }
+}
+
 // iteration t = it0_ + 1 + i of a speculative session (see spec_)
 template <typename real>
 void QuadSession<real>::body_spec(int i, int n) {
@@ -1382,8 +1435,7 @@ void QuadSession<real>::body_spec(int i, int n) {
     real *const keep = terms_.p, *const keepp = vpart_.p;
     terms_.p = terms;  // vargs() hands the sweep this iteration's terms
     vpart_.p = part;
-    edge_sweep(0, E_, c, "edge_sweep");
-    vertex_sweep(0, nbv_, c, "vertex_sweep");
+    sweeps(c);
     terms_.p = keep;
     vpart_.p = keepp;
     xr_ = xw_ = xp_.p;
@@ -1422,43 +1474,7 @@ void QuadSession<real>::body(int i, int n) {
         PFDR_HIP(hipGetLastError());
         return;
     }
-    if (overlap_) {
-        // pull ghosts (comm) || interior edges; boundary edges; push (comm)
-        // || interior vertices; boundary vertices
-        PFDR_HIP(hipEventRecord(ev_[0], s));
-        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[0], 0));
-        {
-            ProfScope ps(prof, "halo_pull", comm_);
-            halo_->pull(xp_.p, sizeof(R2<real>), comm_);
-        }
-        PFDR_HIP(hipEventRecord(ev_[1], comm_));
-        edge_sweep(elo_, ehi_, c, "edge_sweep");
-        PFDR_HIP(hipStreamWaitEvent(s, ev_[1], 0));
-        edge_sweep(0, elo_, c, "edge_sweep_b", ehi_, E_);  // both boundary ranges, one launch
-        PFDR_HIP(hipEventRecord(ev_[2], s));
-        PFDR_HIP(hipStreamWaitEvent(comm_, ev_[2], 0));
-        {
-            ProfScope ps(prof, "halo_push", comm_);
-            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
-            halo_->push(src, src + 2 * E_, sizeof(real), comm_);
-        }
-        PFDR_HIP(hipEventRecord(ev_[3], comm_));
-        vertex_sweep(blo_, bhi_, c, "vertex_sweep");
-        PFDR_HIP(hipStreamWaitEvent(s, ev_[3], 0));
-        vertex_sweep(0, blo_, c, "vertex_sweep_b", bhi_, nbv_);
-    } else {
-        if (halo_) {
-            ProfScope ps(prof, "halo_pull", s);
-            halo_->pull(xp_.p, sizeof(R2<real>), s);
-        }
-        edge_sweep(0, E_, c, "edge_sweep");
-        if (halo_) {
-            ProfScope ps(prof, "halo_push", s);
-            real *src = zdirect() ? Z2_.p : wz_.p;  // Z-direct ranks push Z
-            halo_->push(src, src + 2 * E_, sizeof(real), s);
-        }
-        vertex_sweep(0, nbv_, c, "vertex_sweep");
-    }
+    sweeps(c);
     if (seqdif_) {
         // the reference's two sequential sums (ref :518-526), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -1490,13 +1506,9 @@ void QuadSession<real>::seq_evolution(real *terms, const real *part, hipStream_t
         mono_sum<real>(V_, terms, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2, tstride_,
                        halt, reordered_ ? nullptr : part, nbv_);
     } else if (!lab_.p) {
-        chain_.run(*halo_->tr, terms_.p, tstride_, red_.p, halt, s);
+        chain_.run(etr(), terms, tstride_, red_.p, halt, s);
     } else {
-        PFDR_HIP(hipMemcpyAsync(tall_.p, terms_.p, sizeof(real) * terms_.n,
-                                hipMemcpyDeviceToDevice, s));
-        halo_->tr->allreduce_sum(tall_.p, (int)tall_.n, dtype_of<real>(), s);
-        mono_sum<real>(Vglob_, tall_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 2,
-                       tstride_, halt);
+        route_.run(etr(), terms, tstride_, red_.p, halt, s);
     }
 }
 

@@ -6,22 +6,23 @@
 //
 //   per iteration:
 //     k_sx_edge_sweep   : K-wide TV prox on every (edge, label) + relaxed Z
-//                         update + DR contributions W*Z      ref :589-634
+//                         update                              ref :589-634
 //     k_sx_vertex_sweep : (K <= 64) ordered per-(vertex, label) DR average
-//                         over the incidence CSR (the reference
-//                         parallelises it over labels only, :636-648),
-//                         per-vertex metric simplex projection, evolution
-//                         partials (l1 or label changes) and the NEXT
-//                         explicit step FP                  ref :651-691,
-//                                                               :567-587
-//     (K > 64: k_sx_average then k_sx_project, the same two halves)
+//                         over the incidence CSR, W*Z formed from Z (the
+//                         reference parallelises it over labels only,
+//                         :636-648), per-vertex metric simplex projection,
+//                         evolution partials (l1 or label changes) and the
+//                         NEXT explicit step FP          ref :651-691, :567-587
+//     k_sx_vertex_wide  : (K > 64) the same, one wave per vertex: coalesced
+//                         K-runs, sums in registers, the projection on the
+//                         whole wave (pfdr_proj.hpp); K > 1024 in memory
 //     k_sx_finalize     : stop / recondition flags (when tracked)
 // Layouts: P, Q, Ga, GaQ are K-by-V (index v*K + k) as in the reference; the
 // explicit step FP lives next to P in (P, FP) pairs PF[v*K + k] and the
 // splitting-weight factors in (Ga, 1/Aux) pairs GI[v*K + k], so the edge
 // sweep (bound by its texture-address work, not by bytes) gathers each end
-// with one 16-byte access per operand pair; edge state is K-by-E; the DR
-// contributions are wz[side][e][k].
+// with one 16-byte access per operand pair; edge state is K-by-E; the
+// preconditioner's weight sums run over wz[side][e][k].
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -30,6 +31,7 @@
 #include "pfdr_graph.hpp"
 #include "pfdr_halo.hpp"
 #include "pfdr_monosum.hpp"
+#include "pfdr_proj.hpp"
 #include "pfdr_session.hpp"
 
 namespace pfdr {
@@ -68,25 +70,24 @@ __device__ __forceinline__ void sx_prox_weights(real wu, real wv, real gu, real 
 }
 
 // ------------------------------------------------ metric projection ----
-// Projection of x (D values, stride 1) onto {x >= 0, sum x = a} in the
-// metric diag(1/m): active-set sweep of ref src/proj_simplex_metric.cpp:41-80,
-// operation for operation.  Works in place; the active set lives in a
-// register bit mask (D <= 64) or in a small local array (D <= 1024).
-template <typename real, int W>
+// Projection of x (D <= 64 values, stride 1, in LDS) onto {x >= 0, sum x = a}
+// in the metric diag(1/m) by one lane: the active-set sweep of ref
+// src/proj_simplex_metric.cpp:41-80, operation for operation, the active
+// set in a register bit mask.  Used by the fused vertex sweep (K <= 64),
+// whose vertices pack the lanes densely; wider columns are projected by a
+// whole segment of lanes (pfdr_proj.hpp).
+template <typename real>
 __device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
-    unsigned long long act[W];
-#pragma unroll
-    for (int w = 0; w < W; w++) act[w] = 0ull;
+    unsigned long long act = 1ull;
     real la = (x[0] - a) / m[0];
     x[0] = x[0] / m[0];
-    act[0] = 1ull;
     real s = m[0];
     for (int d = 1; d < D; d++) {
         const real md = m[d];
         const real xd = x[d] / md;
         x[d] = xd;
         if (xd > la) {
-            act[d >> 6] |= 1ull << (d & 63);
+            act |= 1ull << d;
             s += md;
             la += md * (xd - la) / s;
         }
@@ -95,10 +96,10 @@ __device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
     while (changed) {
         changed = false;
         for (int d = 0; d < D; d++) {
-            if ((act[d >> 6] >> (d & 63)) & 1ull) {
+            if ((act >> d) & 1ull) {
                 const real xd = x[d];
                 if (xd < la) {
-                    act[d >> 6] &= ~(1ull << (d & 63));
+                    act &= ~(1ull << d);
                     const real md = m[d];
                     s -= md;
                     la += md * (la - xd) / s;
@@ -107,19 +108,7 @@ __device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
             }
         }
     }
-    for (int d = 0; d < D; d++) {
-        x[d] = ((act[d >> 6] >> (d & 63)) & 1ull) ? (x[d] - la) * m[d] : real(0);
-    }
-}
-
-template <typename real, int W>
-__global__ void k_proj_simplex(real *X, const real *M, int D, int N, int nm,
-                               const real *A, int na) {
-    const int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= N) return;
-    const real *m = (nm > n) ? M + (size_t)D * n : M + (size_t)D * (nm - 1);
-    const real a = (na > n) ? A[n] : A[na - 1];
-    proj_simplex_column<real, W>(X + (size_t)D * n, m, D, a);
+    for (int d = 0; d < D; d++) x[d] = ((act >> d) & 1ull) ? (x[d] - la) * m[d] : real(0);
 }
 
 // ------------------------------------------------------------- kernels --
@@ -576,75 +565,6 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     sx_edge_lane<real, L>(i, EK, c, Eu, Ev, PF, Zu, Zv, A1, La_d1, GI, Wd1u, Wd1v, Th, wz, rho);
 }
 
-template <typename real>
-__global__ void k_sx_average(long VK, int K, const int *__restrict__ ptr,
-                             const unsigned *__restrict__ idx,
-                             const real *__restrict__ wz,
-                             real *__restrict__ Pavg, const Ctrl<real> *ctrl) {
-    if (ctrl && ctrl->halt) return;
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= VK) return;
-    Pavg[i] = sx_gather(i, K, ptr, idx, wz);
-}
-
-template <typename real>
-struct SxProjArgs {
-    int V;
-    SxConst<real> c;
-    const real *Pavg, *Ga, *GaQ, *Q;
-    real *P, *lab;
-    SxR2<real> *PF;  // (P, explicit step) pairs: the edge sweep's operands
-    int track;   // 0 none, 1 l1 evolution, 2 label changes
-    real *part;
-    const Ctrl<real> *ctrl;
-    real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
-    const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
-    real *Po;          // where the new P and (P, step) go (null: P, PF in place)
-    SxR2<real> *PFo;
-};
-
-// projection + evolution + next explicit step, one thread per vertex
-template <typename real, int W>
-__global__ __launch_bounds__(256) void k_sx_project(SxProjArgs<real> a) {
-    if (a.ctrl && a.ctrl->halt) return;
-    __shared__ real red[kBlock / kWave];
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    const int K = a.c.K;
-    real dif = real(0);
-    if (v < a.V) {
-        const long b = (long)v * K;
-        real *x = const_cast<real *>(a.Pavg) + b;  // projected in place
-        proj_simplex_column<real, W>(x, a.Ga + b, K, real(1));
-        if (a.track == 1) {
-            for (int k = 0; k < K; k++) {
-                real d = a.P[b + k] - x[k];
-                if (d < real(0)) d = -d;
-                dif += d;
-                if (a.terms) a.terms[(a.tmap ? (long)a.tmap[v] * K : b) + k] = d;
-            }
-        } else if (a.track == 2) {
-            real mx = x[0];
-            int l = 0;
-            for (int k = 1; k < K; k++) if (x[k] > mx) { mx = x[k]; l = k; }
-            const real fl = (real)l;
-            if (fl != a.lab[v]) { dif = real(1); a.lab[v] = fl; }
-            if (a.terms) a.terms[a.tmap ? a.tmap[v] : v] = dif;
-        }
-        for (int k = 0; k < K; k++) {
-            const real p = x[k];
-            (a.Po ? a.Po : a.P)[b + k] = p;
-            SxR2<real> q;
-            q.x = p;
-            q.y = sx_explicit(a.c, p, a.GaQ[b + k], a.Q[b + k]);
-            (a.PFo ? a.PFo : a.PF)[b + k] = q;
-        }
-    }
-    if (a.track) {
-        dif = block_sum(dif, red);
-        if (threadIdx.x == 0) a.part[blockIdx.x] = dif;
-    }
-}
-
 // Fused vertex sweep (K <= 64): ordered DR average, metric projection,
 // evolution partials and the next explicit step in one pass.  A block owns
 // vb = floor(256 / K) consecutive vertices and gives each (vertex, label)
@@ -673,9 +593,10 @@ struct SxVArgs {
     real *part;
     const Ctrl<real> *ctrl;
     real *terms;  // sequential evolution (null: off): |P_ - P| per (v, k) or 0/1 per v
-    const int *tmap;  // terms at vertex tmap[v] (a relabelled partition's caller labels)
     real *Po;          // where the new P and (P, step) go (null: P, PF in place)
     SxR2<real> *PFo;
+    real *xs;            // wide sweep, K > 1024: the averages, projected in place
+    unsigned char *act;  // its active flags (one byte per (v, k))
 };
 
 // One block of the fused vertex sweep: NT lanes (t = the lane within
@@ -742,14 +663,14 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     real dif = real(0);
     if (blk < a.nb && t < vb && v0 + t < a.V) {
         real *x = xs + t * K;
-        proj_simplex_column<real, 1>(x, ms + t * K, K, real(1));
+        proj_simplex_column<real>(x, ms + t * K, K, real(1));
         if (a.track == 2) {
             real mx = x[0];
             int l = 0;
             for (int d = 1; d < K; d++) if (x[d] > mx) { mx = x[d]; l = d; }
             const real fl = (real)l;
             if (fl != a.lab[v0 + t]) { dif = real(1); a.lab[v0 + t] = fl; }
-            if (a.terms) a.terms[a.tmap ? a.tmap[v0 + t] : v0 + t] = dif;
+            if (a.terms) a.terms[v0 + t] = dif;
         }
     }
     __syncthreads();
@@ -759,7 +680,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
             real d = a.P[i] - p;
             if (d < real(0)) d = -d;
             dif += d;
-            if (a.terms) a.terms[a.tmap ? (long)a.tmap[v] * K + k : i] = d;
+            if (a.terms) a.terms[i] = d;
         }
         (SPLIT ? a.Po : a.P)[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
@@ -787,6 +708,198 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
     sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+}
+
+// ------------------------------------------- wide vertex sweep (K > 64) --
+// One WAVE per vertex, lane l holding the labels k = l + 64 j: every
+// incidence is one K-contiguous run of Z read coalesced by the wave, the
+// ordered sums stay in registers, the metric projection runs on the whole
+// wave (pfdr_proj.hpp: one ballot per active-set event, bit-exact with
+// ref src/proj_simplex_metric.cpp:41-80), and P and (P, step) go back as
+// coalesced rows.  J registers per lane cover K <= 64 J; J = 0 (K > 1024)
+// keeps the averages in xs and the active set in act, 64 labels per chunk.
+constexpr int kSxWideVpw = 4;  // vertices per wave; a block's 4 waves interleave
+
+// ordered DR average (ref :636-648) of labels k = k0 + lane + 64 j of vertex
+// v (wave-uniform): the incidences in the reference's (e, side) order, W * Z
+// formed with the fused sweep's operations (sx_vertex_block); B incidences'
+// loads in flight, added in order
+template <typename real, int J>
+__device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int k0, int lane,
+                                             real (&s)[J]) {
+    constexpr int B = J >= 8 ? 1 : 8 / J;
+    const int K = a.c.K;
+    const long b = v * K;
+    real inv[J];
+    bool ok[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int k = k0 + lane + 64 * j;
+        ok[j] = k < K;
+        inv[j] = ok[j] ? a.invAux[b + k] : real(0);
+        s[j] = real(0);
+    }
+    const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
+    int q = j0;
+    for (; q + B <= j1; q += B) {
+        real z[B][J], an[B][J];
+        bool rq[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const long ad = a.idx[q + u];
+            const bool sv = ad >= a.E;
+            const long ea = sv ? ad - a.E : ad;
+            rq[u] = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
+            const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
+            const real la = (a.A1 || rq[u]) ? real(0) : a.La_d1[ea];
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                const long k = k0 + lane + 64 * j;
+                z[u][j] = ok[j] ? zp[k] : real(0);
+                an[u][j] = (a.A1 && !rq[u] && ok[j]) ? a.A1[ea * K + k] : la;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++)
+#pragma unroll
+            for (int j = 0; j < J; j++) s[j] += rq[u] ? z[u][j] : (an[u][j] * inv[j]) * z[u][j];
+    }
+    for (; q < j1; q++) {
+        const long ad = a.idx[q];
+        const bool sv = ad >= a.E;
+        const long ea = sv ? ad - a.E : ad;
+        const bool rq = ea >= a.E;
+        const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
+        const real la = (a.A1 || rq) ? real(0) : a.La_d1[ea];
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const long k = k0 + lane + 64 * j;
+            const real z = ok[j] ? zp[k] : real(0);
+            const real an = (a.A1 && !rq && ok[j]) ? a.A1[ea * K + k] : la;
+            s[j] += rq ? z : (an * inv[j]) * z;
+        }
+    }
+}
+
+// evolution term, new P and (P, step) of one (v, k); the label scan's candidate
+template <typename real, bool SPLIT>
+__device__ __forceinline__ void sx_wide_out(const SxVArgs<real> &a, long v, long b, int k, real p,
+                                            real &dif, real &mv, int &mi) {
+    const long i = b + k;
+    if (a.track == 1) {
+        real d = a.P[i] - p;
+        if (d < real(0)) d = -d;
+        dif += d;
+        if (a.terms) a.terms[i] = d;
+    } else if (a.track == 2) {
+        argmax_take(p, k, mv, mi);
+    }
+    (SPLIT ? a.Po : a.P)[i] = p;
+    SxR2<real> q;
+    q.x = p;
+    q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
+    (SPLIT ? a.PFo : a.PF)[i] = q;
+}
+
+template <typename real, int J, bool SPLIT>
+__global__ __launch_bounds__(kBlock) void k_sx_vertex_wide(SxVArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    __shared__ real red[kBlock / kWave];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & (kWave - 1));
+    const Seg<64> sg;
+    const int K = a.c.K;
+    real dif = real(0);
+    for (int q = 0; q < kSxWideVpw; q++) {
+        const long v = ((long)blockIdx.x * kSxWideVpw + q) * (kBlock / kWave) + w;
+        if (v >= a.V) break;  // wave-uniform
+        const long b = v * K;
+        real mv = real(0), p0;
+        int mi = 0x7fffffff;
+        if constexpr (J > 0) {
+            real x[J], m[J];
+            sx_wide_sums<real, J>(a, v, 0, lane, x);
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                const int k = lane + 64 * j;
+                m[j] = k < K ? a.Ga[b + k] : real(1);
+            }
+            proj_segment<real, 64, J>(sg, x, m, K, real(1));
+            p0 = lane_read(x[0], 0);
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                const int k = lane + 64 * j;
+                if (k < K) sx_wide_out<real, SPLIT>(a, v, b, k, x[j], dif, mv, mi);
+            }
+        } else {
+            for (int k0 = 0; k0 < K; k0 += 4 * 64) {
+                real s4[4];
+                sx_wide_sums<real, 4>(a, v, k0, lane, s4);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int k = k0 + lane + 64 * j;
+                    if (k < K) a.xs[b + k] = s4[j];
+                }
+            }
+            proj_wave_mem<real>(a.xs + b, a.Ga + b, K, real(1), a.act + b);
+            p0 = lane_read(lane == 0 ? a.xs[b] : real(0), 0);
+            for (int k = lane; k < K; k += 64) sx_wide_out<real, SPLIT>(a, v, b, k, a.xs[b + k], dif, mv, mi);
+        }
+        if (a.track == 2) {  // maximum-likelihood label (ref :656-676)
+            const int l = wave_argmax(mv, mi, p0 != p0);
+            if (lane == 0) {
+                real d = real(0);
+                const real fl = (real)l;
+                if (fl != a.lab[v]) { d = real(1); a.lab[v] = fl; }
+                if (a.terms) a.terms[v] = d;
+                dif += d;
+            }
+        }
+    }
+    if (a.track) {
+        dif = block_sum(dif, red);
+        if (threadIdx.x == 0) a.part[blockIdx.x] = dif;
+    }
+}
+
+// ------------------------------- standalone metric projection (any D) --
+// proj_simplex_metric (ref src/proj_simplex_metric.cpp:18-83): one segment
+// of G lanes per column, coordinates in J registers per lane
+template <typename real, int G, int J>
+__global__ __launch_bounds__(kBlock) void k_proj_wave(real *X, const real *M, int D, int N,
+                                                      int nm, const real *A, int na) {
+    const Seg<G> sg;
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((t - (t & (kWave - 1))) / G >= N) return;  // the whole wave is past the last column
+    const long col = t / G;
+    const bool live = col < N;
+    const real *m = M + (size_t)D * (live && nm > col ? col : nm - 1);
+    const real a = live ? (na > col ? A[col] : A[na - 1]) : real(1);
+    real x[J], mm[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int d = j * G + sg.sl;
+        const bool ok = live && d < D;
+        x[j] = ok ? X[(size_t)D * col + d] : real(0);
+        mm[j] = ok ? m[d] : real(1);
+    }
+    proj_segment<real, G, J>(sg, x, mm, live ? D : 0, a);
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int d = j * G + sg.sl;
+        if (live && d < D) X[(size_t)D * col + d] = x[j];
+    }
+}
+
+// D > 1024: one wave per column in memory, active flags in I (D bytes per column)
+template <typename real>
+__global__ __launch_bounds__(kBlock) void k_proj_mem(real *X, const real *M, int D, int N, int nm,
+                                                     const real *A, int na, unsigned char *I) {
+    const long col = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (col >= N) return;  // wave-uniform
+    const real *m = M + (size_t)D * (nm > col ? col : nm - 1);
+    const real a = na > col ? A[col] : A[na - 1];
+    proj_wave_mem<real>(X + (size_t)D * col, m, D, a, I + (size_t)D * col);
 }
 
 // ------------------------------------------ small problems, one launch --
@@ -1074,16 +1187,26 @@ static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipS
         pins.copy(d.p, src, n * sizeof(real), hipMemcpyHostToDevice);
 }
 
-static int mask_words(int D) { return (D + 63) / 64; }
-
+// proj_simplex_metric: a segment of G = 4..64 lanes per column with J
+// coordinates per lane (D <= 1024), else a wave per column in memory
 template <typename real>
-static void launch_proj(real *X, const real *M, int D, int N, int nm,
-                        const real *A, int na, hipStream_t s) {
-    const int w = mask_words(D);
-    const int g = grid_for(N);
-    if (w <= 1) k_proj_simplex<real, 1><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
-    else if (w <= 4) k_proj_simplex<real, 4><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
-    else k_proj_simplex<real, 16><<<g, kBlock, 0, s>>>(X, M, D, N, nm, A, na);
+static void launch_proj(real *X, const real *M, int D, int N, int nm, const real *A, int na,
+                        unsigned char *I, hipStream_t s) {
+    auto reg = [&](auto Gc, auto Jc) {
+        constexpr int G = decltype(Gc)::value, J = decltype(Jc)::value;
+        k_proj_wave<real, G, J><<<grid_for((long)N * G), kBlock, 0, s>>>(X, M, D, N, nm, A, na);
+    };
+    using std::integral_constant;
+    if (D <= 4) reg(integral_constant<int, 4>{}, integral_constant<int, 1>{});
+    else if (D <= 8) reg(integral_constant<int, 8>{}, integral_constant<int, 1>{});
+    else if (D <= 16) reg(integral_constant<int, 16>{}, integral_constant<int, 1>{});
+    else if (D <= 32) reg(integral_constant<int, 32>{}, integral_constant<int, 1>{});
+    else if (D <= 64) reg(integral_constant<int, 64>{}, integral_constant<int, 1>{});
+    else if (D <= 128) reg(integral_constant<int, 64>{}, integral_constant<int, 2>{});
+    else if (D <= 256) reg(integral_constant<int, 64>{}, integral_constant<int, 4>{});
+    else if (D <= 512) reg(integral_constant<int, 64>{}, integral_constant<int, 8>{});
+    else if (D <= 1024) reg(integral_constant<int, 64>{}, integral_constant<int, 16>{});
+    else k_proj_mem<real><<<grid_for((long)N * kWave), kBlock, 0, s>>>(X, M, D, N, nm, A, na, I);
     PFDR_HIP(hipGetLastError());
 }
 
@@ -1133,13 +1256,16 @@ class SimplexSession final : public SessionBase {
     DevBuf<char> dws_;
     static constexpr long kSeqDifMin = 1L << 17;  // AUTO: sums of at least this many terms
     // partitions: the ranks' terms summed rank to rank in the caller's order
-    // (ChainSum); a relabelled partition (vtx_label) writes them at its
-    // caller labels (tlab_) of a V_global * K array, all-reduced into tall_
-    // and summed whole on every rank.  Label counts (track 2) add 0 / 1:
-    // exact in any order, so partitions keep the tree for them.
+    // (ChainSum); a relabelled partition (vtx_label) first routes each
+    // vertex's K terms to the rank whose caller-order slice holds its label
+    // (TermRoute), then chains.  Label counts (track 2) add 0 / 1: exact in
+    // any order, so partitions keep the tree for them.
     ChainSum<real> chain_;
-    DevBuf<int> tlab_;
-    DevBuf<real> tall_;
+    TermRoute<real> route_;
+    // the evolution sums' transport: a speculative partition's own split one
+    // (beside the next iteration's exchanges, QuadSession::evtr_)
+    std::unique_ptr<Transport> evtr_;
+    Transport &etr() { return evtr_ ? *evtr_ : *halo_->tr; }
     void seq_evolution(real *terms, hipStream_t s);
     // Speculative iteration (one GPU, sequential evolution, difRcd = 0, no
     // objective record), as the quadratic session's spec_: the sum and the
@@ -1179,6 +1305,8 @@ class SimplexSession final : public SessionBase {
     HostPins pins_;  // caller arrays pinned for the setup copies
     int nbv_, nbe_;
     int vb_ = 0, nbs_ = 0;  // fused vertex sweep (K <= 64): vertices per block, blocks
+    int nbw_ = 0;           // wide vertex sweep (K > 64): blocks
+    DevBuf<unsigned char> act_;  // its active sets when K > 1024
     // the fused vertex sweep forms W*Z from the gathered Z and W (K contiguous
     // words per incidence), so the edge sweep neither reads W nor writes
     // contributions: 28 instead of 44 streamed bytes per (e, k) (C4: 2.42 ->
@@ -1214,7 +1342,6 @@ class SimplexSession final : public SessionBase {
     void precondition(bool init);
     void objective();
     void body();
-    void launch_project(const SxProjArgs<real> &a);
     // K-wide ghost rows of a [Vg][K] array from their owners
     void pullK(DevBuf<real> &b) {
         if (halo_) halo_->pull(b.p, K_ * (int)sizeof(real), stream);
@@ -1223,20 +1350,20 @@ class SimplexSession final : public SessionBase {
         if (halo_) halo_->pull(PF_.p, K_ * (int)sizeof(SxR2<real>), stream);
     }
     void push_wz();
+    template <bool SPLIT>
+    void launch_wide(const SxVArgs<real> &a) {
+        const int g = nbw_;
+        if (K_ <= 128) k_sx_vertex_wide<real, 2, SPLIT><<<g, kBlock, 0, stream>>>(a);
+        else if (K_ <= 256) k_sx_vertex_wide<real, 4, SPLIT><<<g, kBlock, 0, stream>>>(a);
+        else if (K_ <= 512) k_sx_vertex_wide<real, 8, SPLIT><<<g, kBlock, 0, stream>>>(a);
+        else if (K_ <= 1024) k_sx_vertex_wide<real, 16, SPLIT><<<g, kBlock, 0, stream>>>(a);
+        else k_sx_vertex_wide<real, 0, SPLIT><<<g, kBlock, 0, stream>>>(a);
+    }
 };
-
-template <typename real>
-void SimplexSession<real>::launch_project(const SxProjArgs<real> &a) {
-    const int w = mask_words(K_);
-    if (w <= 1) k_sx_project<real, 1><<<nbv_, kBlock, 0, stream>>>(a);
-    else if (w <= 4) k_sx_project<real, 4><<<nbv_, kBlock, 0, stream>>>(a);
-    else k_sx_project<real, 16><<<nbv_, kBlock, 0, stream>>>(a);
-}
 
 template <typename real>
 SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (p->K <= 0 || p->V <= 0 || p->E < 0) throw std::runtime_error("K, V must be > 0 and E >= 0");
-    if (p->K > 1024) throw std::runtime_error("K > 1024 labels is not supported");
     if (!p->X || !p->Y || !p->Eu || !p->Ev || !p->La_d1)
         throw std::runtime_error("P, Q, Eu, Ev and La_d1 are required");
     PFDR_HIP(hipGetDevice(&device));
@@ -1306,8 +1433,13 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64) {
         vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
-    } else {
-        Pavg_.alloc(VK_);
+    } else {  // wide vertex sweep: a wave per vertex
+        const long per = (long)kSxWideVpw * (kBlock / kWave);
+        nbw_ = (int)((V_ + per - 1) / per);
+        if (K_ > 1024) {  // averages and active sets in memory
+            Pavg_.alloc(VK_);
+            act_.alloc(VK_);
+        }
     }
     PF_.alloc(VgK); Ga_.alloc(VgK); GaQ_.alloc(VgK); invAux_.alloc(VgK);
     const size_t EKn = EK_ ? EK_ : 1;
@@ -1321,7 +1453,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
     nbe_ = grid_for(E_);
-    part_.alloc(std::max(nbv_, nbs_));
+    part_.alloc(std::max(std::max(nbv_, nbs_), nbw_));
     if (rec_obj_) { opart_.alloc((size_t)nbv_ + nbe_ + 1); Obj_.alloc((size_t)itMax_ + 1); }
     if (rec_dif_) Dif_.alloc(itMax_ > 0 ? itMax_ : 1);
     if (track_ == 2) {
@@ -1366,13 +1498,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
               (evo == PFDR_EVOLUTION_SEQUENTIAL ||
                (evo == PFDR_EVOLUTION_AUTO && nglob >= kSeqDifMin));
     if (seqdif_) {
-        const bool gathered = halo_ && p->vtx_label;
-        const long n = gathered ? nglob : nterms_;
+        const bool routed = halo_ && p->vtx_label;
+        const long n = nterms_;
         terms_.alloc((size_t)n);
-        if (!halo_ || gathered) dws_.alloc(mono_ws_bytes<real>(n, 1));
+        if (!halo_) dws_.alloc(mono_ws_bytes<real>(n, 1));
         red_.alloc(2);
-        if (gathered) {
-            if (n > 0x7fffffffL) throw std::runtime_error("V_global * K too large");
+        if (routed) {
             std::vector<int64_t> h64(V_);
             PFDR_HIP(hipMemcpy(h64.data(), p->vtx_label, sizeof(int64_t) * V_,
                                mem == PFDR_MEM_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
@@ -1382,16 +1513,16 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
                     throw std::runtime_error("vtx_label outside [0, V_global)");
                 h32[v] = (int)h64[v];
             }
-            tlab_.alloc(V_);
-            PFDR_HIP(hipMemcpy(tlab_.p, h32.data(), sizeof(int) * V_, hipMemcpyHostToDevice));
-            check_permutation(tlab_.p, V_, Vglob_, *halo_->tr, s);
-            PFDR_HIP(hipMemsetAsync(terms_.p, 0, sizeof(real) * n, s));
-            tall_.alloc((size_t)n);
+            DevBuf<int> dl(V_);
+            PFDR_HIP(hipMemcpy(dl.p, h32.data(), sizeof(int) * V_, hipMemcpyHostToDevice));
+            check_permutation(dl.p, V_, Vglob_, *halo_->tr, s);
+            route_.init(h32, Vglob_, 1, track_ == 1 ? K_ : 1, *halo_->tr, s);
         } else if (halo_) {
             chain_.init(nterms_, 1, *halo_->tr);
         }
         seqdif = 1;
-        spec_ = !halo_ && difRcd_ == real(0) && !rec_obj_;
+        spec_ = difRcd_ == real(0) && !rec_obj_;
+        if (spec_ && halo_) evtr_ = halo_->tr->split(s);  // (collective: every rank alike)
         if (spec_) {
             DevBuf<real> t2(2 * (size_t)n);  // terms of both parities
             std::swap(terms_.p, t2.p);
@@ -1420,7 +1551,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
-                            &Dif_, &terms_, &tall_, &P2_})
+                            &Dif_, &terms_, &P2_, &route_.slice})
         device_bytes += (int64_t)(b->n * sizeof(real));
     device_bytes += (int64_t)((GI_.n + PF_.n + PF2_.n) * sizeof(SxR2<real>));
 }
@@ -1504,7 +1635,7 @@ void SimplexSession<real>::body() {
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     sweeps(c, 0);
-    const int nparts = vb_ ? nbs_ : nbv_;
+    const int nparts = vb_ ? nbs_ : nbw_;
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -1544,52 +1675,42 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
             k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               vb_ ? nullptr : wz_.p,
+                                                               nullptr,
                                                                rho_, c, nb, xm);
         else
             k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
                                                                Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
-                                                               vb_ ? nullptr : wz_.p,
+                                                               nullptr,
                                                                rho_, c, nb, xm);
     }
     if (halo_) {
         ProfScope ps(prof, "halo_push", s);
         push_wz();
     }
+    SxVArgs<real> a{};
+    a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
+    a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = Pin; a.PF = PFin;
+    a.Po = Po; a.PFo = PFo;
+    a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
+    a.terms = seqdif_ ? terms_.p : nullptr;
+    a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
     if (vb_) {
-        SxVArgs<real> a{};
-        a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
-        a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = Pin; a.PF = PFin;
-        a.Po = Po; a.PFo = PFo;
-        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
-        a.terms = seqdif_ ? terms_.p : nullptr;
-        a.tmap = tlab_.p;
         ProfScope ps(prof, "sx_vertex_sweep", s);
-        a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
         if (Po) k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
         else k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
     } else {
-        {
-            ProfScope ps(prof, "sx_average", s);
-            k_sx_average<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, inc_.ptr.p,
-                                                                inc_.idx.p, wz_.p, Pavg_.p, c);
-        }
-        SxProjArgs<real> a{};
-        a.V = V_; a.c = c_; a.Pavg = Pavg_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p;
-        a.P = Pin; a.PF = PFin; a.Po = Po; a.PFo = PFo;
-        a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
-        a.terms = seqdif_ ? terms_.p : nullptr;
-        a.tmap = tlab_.p;
-        ProfScope ps(prof, "sx_project", s);
-        launch_project(a);
+        ProfScope ps(prof, "sx_vertex_wide", s);
+        a.nb = nbw_; a.xs = Pavg_.p; a.act = act_.p;
+        if (Po) launch_wide<true>(a);
+        else launch_wide<false>(a);
     }
-    if (halo_) {
+    if (halo_) {  // the ghosts of the buffers just written (speculative: Pb(t), PFb(t))
         ProfScope ps(prof, "halo_pull", s);
-        pullK(P_);
-        pullPF();
+        halo_->pull(Po ? Po : P_.p, K_ * (int)sizeof(real), s);
+        halo_->pull(PFo ? PFo : PF_.p, K_ * (int)sizeof(SxR2<real>), s);
     }
     PFDR_HIP(hipGetLastError());
 }
@@ -1602,14 +1723,10 @@ void SimplexSession<real>::seq_evolution(real *terms, hipStream_t s) {
     if (!halo_) {
         mono_sum<real>(nterms_, terms, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1, 0,
                        halt);
-    } else if (!tlab_.p) {
-        chain_.run(*halo_->tr, terms, 0, red_.p, halt, s);
+    } else if (!route_.ready()) {
+        chain_.run(etr(), terms, 0, red_.p, halt, s);
     } else {
-        PFDR_HIP(hipMemcpyAsync(tall_.p, terms_.p, sizeof(real) * terms_.n,
-                                hipMemcpyDeviceToDevice, s));
-        halo_->tr->allreduce_sum(tall_.p, (int)tall_.n, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
-        mono_sum<real>((long)tall_.n, tall_.p, nullptr, 0, nullptr, red_.p, nullptr, dws_.p, s, 1,
-                       0, halt);
+        route_.run(etr(), terms, 0, red_.p, halt, s);
     }
 }
 
@@ -1617,11 +1734,6 @@ void SimplexSession<real>::seq_evolution(real *terms, hipStream_t s) {
 template <typename real>
 void SimplexSession<real>::push_wz() {
     const int eb = K_ * (int)sizeof(real);
-    real *tail = wz_.p + 2 * EK_;
-    if (!vb_) {  // the edge sweep stored W*Z
-        halo_->push(wz_.p, tail, eb, stream);
-        return;
-    }
     const long n = halo_->push_send_off[halo_->tr->nranks];
     real *buf = (real *)halo_->push_buffer(eb);
     if (n) {
@@ -1888,19 +2000,20 @@ static int proj_host(const char *fn, real *X, const real *M, int D, int N, int n
                      int na) {
     if (D <= 0 || N < 0 || nm <= 0 || na <= 0 || !X || !M || !A)
         return report_error(fn, "invalid arguments");
-    if (D > 1024) return report_error(fn, "D > 1024 is not supported");
     if (N == 0) return PFDR_OK;
     try {
         hipStream_t s = lib_stream();
         const int mm = std::min(nm, N), aa = std::min(na, N);
         DevBuf<real> dX, dM, dA;
+        DevBuf<unsigned char> dI;  // active flags of the in-memory columns
+        if (D > 1024) dI.alloc((size_t)D * N);
         dX.alloc((size_t)D * N);
         dM.alloc((size_t)D * mm);
         dA.alloc(aa);
         PFDR_HIP(hipMemcpyAsync(dX.p, X, sizeof(real) * D * (size_t)N, hipMemcpyHostToDevice, s));
         PFDR_HIP(hipMemcpyAsync(dM.p, M, sizeof(real) * D * (size_t)mm, hipMemcpyHostToDevice, s));
         PFDR_HIP(hipMemcpyAsync(dA.p, A, sizeof(real) * aa, hipMemcpyHostToDevice, s));
-        launch_proj<real>(dX.p, dM.p, D, N, mm, dA.p, aa, s);
+        launch_proj<real>(dX.p, dM.p, D, N, mm, dA.p, aa, dI.p, s);
         PFDR_HIP(hipMemcpyAsync(X, dX.p, sizeof(real) * D * (size_t)N, hipMemcpyDeviceToHost, s));
         PFDR_HIP(hipStreamSynchronize(s));
     } catch (const HipError &h) {

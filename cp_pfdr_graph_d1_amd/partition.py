@@ -202,7 +202,7 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e,
                              vtx_label=None if order is None else order[v0:v1],
                              evolution=evolution)
-            queries[r] = {"ghosts": s.query("ghosts")}
+            queries[r] = {q: s.query(q) for q in ("ghosts", "speculative", "seqdif")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
                 queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks",
                                                             "record_blocks")})

@@ -138,9 +138,13 @@ int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
  * SEQUENTIAL on one GPU for sums of at least 2^17 terms, except on the
  * small-graph paths that decide inside a sweep (quadratic: identity /
  * diagonal A, no objective record, <= 1,024 vertex blocks of 256; both
- * solvers' one-workgroup paths), which keep TREE; a partitioned session
- * always uses TREE (SEQUENTIAL there is refused).  SEQUENTIAL forced on a
- * small graph takes the multi-launch loop instead of those paths. */
+ * solvers' one-workgroup paths), which keep TREE.  A partitioned session
+ * applies the same rule to its global term count: SEQUENTIAL sums the terms
+ * rank to rank in the caller's order (ChainSum, pfdr_halo.hpp; a relabelled
+ * split first routes every term to the rank owning that caller-order
+ * slice), bit-identical to one GPU; the simplex's label counts (0 / 1 terms,
+ * exact in any order) keep TREE there.  SEQUENTIAL forced on a small graph
+ * takes the multi-launch loop instead of those paths. */
 #define PFDR_EVOLUTION_AUTO 0
 #define PFDR_EVOLUTION_SEQUENTIAL 1
 #define PFDR_EVOLUTION_TREE 2
@@ -441,9 +445,11 @@ int pfdr_loopback_destroy(void *hub);
  * once and cached across calls): the drop-in calls of this process with at
  * least min_vertices vertices (< 0: the default 2^20) are vertex-range
  * partitioned across devices[0 .. n) -- bit-identical to the one-GPU solve.
- * n = 0 returns to one GPU.  A list that repeats one device runs the ranks
- * as threads on it (loopback transport; for tests).  Without this call the
- * PFDR_DEVICES environment variable (N or "all") selects devices 0 .. N-1. */
+ * n = 0 returns to one GPU.  The devices must be all distinct (RCCL), or one
+ * device repeated, which runs the ranks as threads on it (loopback transport;
+ * for tests); a mixed list is refused and leaves the configuration as it was.
+ * Without this call the PFDR_DEVICES environment variable (N or "all")
+ * selects devices 0 .. N-1. */
 int pfdr_set_devices(int n, const int *devices, int64_t min_vertices);
 
 /* Host-only partition planner (what the partitioned session runs at setup;

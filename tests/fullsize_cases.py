@@ -13,6 +13,16 @@ with the library's native generators (splitmix64 laws, no device needed):
   c4_k2                simplex K = 10, KL al = 0.1, 2236^2 8-nbr (V 5.0M,
                        E 20.0M), f32, 2 iterations
   c5_k1                bounds [0, 1], 640^3 6-NN (V 262M, E 785M), f32, 1 it
+  c4k64_k2             C4's law at K = 64 labels (the fused sweep's widest),
+                       768^2 8-nbr (V 590K, E 2.35M, 151M (edge, label)), 2 its
+  c4k100_k2 / _conv    K = 100 (one wave per vertex): 512^2 (2 its) and 256^2
+                       converged to difTol 1e-4
+  c3_direct_conv       C3's law (N = 1024) converged to difTol 1e-4 on a 512^2
+                       grid (V = 262,144): at V = 2M one reference iteration
+                       takes ~50 s on one core here, so a converged solve
+                       would take hours; the f32 and f64 reference runs are
+                       both kept (the dense yardstick, below)
+  c3_ata_conv          the A^tA mode (V = 32,768) converged to difTol 1e-4
   headline_conv        the headline solved to difTol 1e-5 (C2's
   c2_conv              parity tolerance), C2 to difTol 1e-5 and C4 to its
   c4_conv              difTol 1e-4: the north star's
@@ -31,10 +41,11 @@ from cp_pfdr_graph_d1_amd import pfdr
 # C3 scalar Lipschitz constant L = ||A||^2: computed once by
 # make_fullsize.py (power method in float64) and stored with the digest
 CASES = ("c1_fixk25", "c1_conv", "headline_k3", "c2_k2", "c3_direct_k2", "c3_ata_k3",
-         "c4_k2", "c5_k1", "headline_conv", "c2_conv", "c4_conv")
-CONVERGED = ("c1_conv", "headline_conv", "c2_conv", "c4_conv")
+         "c4_k2", "c5_k1", "headline_conv", "c2_conv", "c4_conv", "c4k64_k2", "c4k100_k2",
+         "c4k100_conv", "c3_direct_conv", "c3_ata_conv")
+CONVERGED = ("c1_conv", "headline_conv", "c2_conv", "c4_conv", "c4k100_conv")
 SAMPLE_SEED = 0x5EED
-DENSE = ("c3_direct_k2", "c3_ata_k3")
+DENSE = ("c3_direct_k2", "c3_ata_k3", "c3_direct_conv", "c3_ata_conv")
 
 
 def sample_index(n, m, seed=SAMPLE_SEED):
@@ -86,8 +97,9 @@ def build(name, L_c3=None):
                  condMin=1e-3, difRcd=0.0, difTol=1e-5 if conv else 0.0,
                  itMax=10000 if conv else 2)
         return dict(solver="l1", dtype=np.float32, args=a, sample_m=65536 if conv else 4096)
-    if name == "c3_direct_k2":
-        N, nx, ny = 1024, 2000, 1000
+    if name in ("c3_direct_k2", "c3_direct_conv"):
+        conv = name == "c3_direct_conv"
+        N, nx, ny = (1024, 512, 512) if conv else (1024, 2000, 1000)
         V = nx * ny
         h = (3.0 / N) ** 0.5  # U(-h, h): variance 1/N
         A = pfdr.gen_uniform(3, N * V, -h, h, np.float32)  # column-major N x V
@@ -101,9 +113,10 @@ def build(name, L_c3=None):
         a = dict(X0=np.zeros(V, np.float32), Y=Y, A=A, N=N, Eu=Eu, Ev=Ev,
                  La_d1=np.full(E, 0.05, np.float32), La_l1=np.full(V, 0.005, np.float32),
                  positivity=0, Ltype=pfdr.SCAL, L=L, rho=1.5, condMin=1e-3, difRcd=0.0,
-                 difTol=0.0, itMax=2)
+                 difTol=1e-4 if conv else 0.0, itMax=5000 if conv else 2)
         return dict(solver="l1", dtype=np.float32, args=a, sample_m=65536)
-    if name == "c3_ata_k3":
+    if name in ("c3_ata_k3", "c3_ata_conv"):
+        conv = name == "c3_ata_conv"
         nx, ny = 256, 128
         V = nx * ny
         G = pfdr.gen_symmetric(V, 33, 1.0 / V, 1.0, np.float32)
@@ -114,7 +127,8 @@ def build(name, L_c3=None):
         a = dict(X0=np.zeros(V, np.float32), Y=AtY, A=G, N=-V, Eu=Eu, Ev=Ev,
                  La_d1=np.full(E, 0.05, np.float32), La_l1=np.full(V, 0.005, np.float32),
                  positivity=0, Ltype=pfdr.SCAL, L=np.array([2.0], np.float32), rho=1.5,
-                 condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=3)
+                 condMin=1e-3, difRcd=0.0, difTol=1e-4 if conv else 0.0,
+                 itMax=5000 if conv else 3)
         return dict(solver="l1", dtype=np.float32, args=a, sample_m=V)
     if name in ("c4_k2", "c4_conv"):
         from cp_pfdr_graph_d1_amd.graphs import simplex_observation
@@ -131,6 +145,21 @@ def build(name, L_c3=None):
                  difTol=1e-4 if conv else 0.0, itMax=10000 if conv else 2)
         return dict(solver="simplex", dtype=np.float32, args=a,
                     sample_m=65536 if conv else 16384)
+    if name in ("c4k64_k2", "c4k100_k2", "c4k100_conv"):
+        from cp_pfdr_graph_d1_amd.graphs import simplex_observation
+        K = 64 if name == "c4k64_k2" else 100
+        n = {"c4k64_k2": 768, "c4k100_k2": 512, "c4k100_conv": 256}[name]
+        V = n * n
+        Eu, Ev = pfdr.gen_grid_edges((n, n), 8)
+        v = np.arange(V)
+        lab = (((v % n) * 4 // n) + 4 * ((v // n) * 3 // n)) * (K // 12)
+        Q = simplex_observation(V, K, 4, lab, np.float32)
+        E = Eu.size
+        conv = name.endswith("conv")
+        a = dict(P0=Q.copy(), Q=Q, K=K, Eu=Eu, Ev=Ev, La_d1=np.full(E, 0.05, np.float32),
+                 al=0.1, La_f=None, rho=1.0, condMin=0.1, difRcd=0.0,
+                 difTol=1e-4 if conv else 0.0, itMax=10000 if conv else 2)
+        return dict(solver="simplex", dtype=np.float32, args=a, sample_m=65536)
     if name == "c5_k1":
         shape = (640, 640, 640)
         Eu, Ev = pfdr.gen_grid_edges(shape, 6)

@@ -57,7 +57,7 @@ def main():
         t0 = time.perf_counter()
         extra = {}
         L = None
-        if name == "c3_direct_k2":
+        if name in ("c3_direct_k2", "c3_direct_conv"):
             case = F.build(name)
             a = case["args"]
             L = power_norm(a["A"], a["N"], a["X0"].size)
@@ -83,8 +83,9 @@ def main():
                     a[k] = a[k].astype(np.float64)
             del X
             t3 = time.perf_counter()
-            X64, it64, _ = F.run(ref, case)
+            X64, it64, Dif64 = F.run(ref, case)
             d64 = F.digest(X64, it64, np.zeros(0), case["sample_m"])
+            extra["ref64_Dif"] = np.asarray(Dif64)
             extra["ref64_sample"] = d64["sample"]
             extra["ref64_norm2"] = d64["norm2"]
             extra["ref64_it"] = d64["it"]

@@ -33,12 +33,12 @@ def test_invalid_inputs_fail_cleanly(gpu_lib):
             gpu_lib.quadratic_d1_l1(np.zeros(V, np.float32), Y, None, 0,
                                     np.asarray(Eu, np.int32), np.asarray(Ev, np.int32), La,
                                     None, 0, 0, None, 1.5, 1e-3, 0.0, 0.0, 5)
-    # more labels than the simplex solver supports (K <= 1024)
+    # a negative loss parameter (the reference's al is >= 0); any K is served
     K = 1025
     Q = np.full(2 * K, 1.0 / K, np.float32)
     with pytest.raises(pfdr.PFDRError):
         gpu_lib.loss_d1_simplex(Q.copy(), Q, K, np.array([0], np.int32), np.array([1], np.int32),
-                                np.array([0.1], np.float32), 0.1, None, 1.5, 1e-3, 0.0, 0.0, 3)
+                                np.array([0.1], np.float32), -0.5, None, 1.5, 1e-3, 0.0, 0.0, 3)
     # the library still works afterwards
     X, it, _, _ = gpu_lib.quadratic_d1_l1(np.zeros(V, np.float32), np.ones(V, np.float32), None,
                                           0, np.array([0, 1, 2], np.int32),

@@ -75,8 +75,12 @@ def test_fullsize_matches_reference(gpu_lib, name):
     if name in F.DENSE:
         r64 = g["ref64_sample"].astype(np.float64)
         e_gpu, e_ref = rel(samp, r64), rel(gs, r64)
-        print("  vs reference f64: GPU f32 %.3e, reference f32 %.3e" % (e_gpu, e_ref))
-        assert it == git == int(g["ref64_it"])
+        print("  vs reference f64: GPU f32 %.3e, reference f32 %.3e (it %d / f32 %d / f64 %d)" % (
+            e_gpu, e_ref, it, git, int(g["ref64_it"])))
+        if name.endswith("conv"):  # converged: the stopping iteration within one
+            assert abs(it - int(g["ref64_it"])) <= 1 and abs(it - git) <= 1
+        else:
+            assert it == git == int(g["ref64_it"])
         assert e_gpu <= 1e-5
         assert e_gpu <= 1.5 * e_ref + 1e-7
         return
@@ -102,16 +106,22 @@ def test_fullsize_matches_reference(gpu_lib, name):
         assert below.size and below[0] == it - 1
 
 
-@pytest.mark.parametrize("name,k", [("headline_conv", 2), ("c4_conv", 2), ("headline_conv", 3),
-                                    ("c2_conv", 4), ("c5_k1", 8)])
-def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
+@pytest.mark.parametrize("name,k,relabel", [("headline_conv", 2, False), ("c4_conv", 2, False),
+                                            ("headline_conv", 3, False), ("c2_conv", 4, False),
+                                            ("c5_k1", 8, False), ("headline_conv", 2, True),
+                                            ("c4k100_conv", 3, False)])
+def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k, relabel):
     """The converged full-size solves split over k ranks (loopback threads on
     one GPU: the RCCL session code with device-copy exchanges), and C5 (640^3,
     262M vertices, the 8-GPU configuration) split over 8 ranks: the iterate
     evolution is summed rank to rank with the reference's sequential rounding
     (ChainSum, pfdr_halo.hpp), so the stopping iteration, every Dif and X's
     sha256 equal the reference's (src/PFDR_graph_quadratic_d1_l1.cpp:429,
-    514-529; simplex src/PFDR_graph_loss_d1_simplex.cpp:653-691)."""
+    514-529; simplex src/PFDR_graph_loss_d1_simplex.cpp:653-691).  With
+    difRcd = 0 the ranks decide speculatively (the evolution chain of t on a
+    split transport beside t + 1's exchanges); relabel: the headline's
+    vertices renumbered breadth-first before the split, the evolution terms
+    routed back to caller-order slices (TermRoute) before the chain."""
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
     g = _gold(name)
@@ -122,7 +132,8 @@ def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_SIMPLEX, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["P0"], a["Q"],
             La_l1=a["La_f"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
-            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, K=a["K"], al=a["al"])
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, K=a["K"], al=a["al"],
+            relabel=relabel)
     elif case["solver"] == "bounds":  # C5: 640^3, the 8-GPU configuration, as 8 ranks
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_BOUNDS, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
@@ -132,10 +143,11 @@ def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k):
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_L1, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
             La_l1=a["La_l1"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
-            difTol=a["difTol"], itMax=a["itMax"], record_dif=True)
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, relabel=relabel)
     d = F.digest(X, it, Dif[:it], case["sample_m"])
-    print("%s k=%d: it %d/%d sha256 equal %s" % (name, k, it, int(g["it"]),
-                                                  str(d["sha256"]) == str(g["sha256"])))
+    print("%s k=%d relabel=%s: it %d/%d sha256 equal %s speculative %s" % (
+        name, k, relabel, it, int(g["it"]), str(d["sha256"]) == str(g["sha256"]),
+        [q["speculative"] for q in info["queries"]]))
     assert it == int(g["it"])
     assert np.array_equal(Dif[:it], g["Dif"][:it]), "partitioned Dif differs from the reference"
     assert str(d["sha256"]) == str(g["sha256"])

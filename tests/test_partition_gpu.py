@@ -15,7 +15,7 @@ CASES = ["l1_grid2d_f64", "l1_grid2d_f32", "l1_knn_shuffled_f32", "l1_l22_f64",
          "bounds_upper_recond_f32", "l1_chain_kat_f64"] + G.names("simplex_")
 
 
-def _solve(c, k, fixed, evolution=0):
+def _solve(c, k, fixed, evolution=0, record_obj=True):
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
     a = dict(c)
@@ -27,7 +27,7 @@ def _solve(c, k, fixed, evolution=0):
             k, pfdr.PFDR_KIND_SIMPLEX, P0.dtype, a["Eu"], a["Ev"], a["La_d1"], P0, a["Q"],
             La_l1=a["La_f"], rho=float(a["rho"]), condMin=float(a["condMin"]),
             difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
-            record_obj=True, record_dif=True, K=int(a["K"]), al=float(a["al"]),
+            record_obj=record_obj, record_dif=True, K=int(a["K"]), al=float(a["al"]),
             evolution=evolution)
     kind = pfdr.PFDR_KIND_L1 if str(a["solver"]) == "l1" else pfdr.PFDR_KIND_BOUNDS
     X0 = a["X0"]
@@ -37,7 +37,7 @@ def _solve(c, k, fixed, evolution=0):
         lo=float(a.get("lo", -np.inf)), hi=float(a.get("hi", np.inf)), Ltype=int(a["Ltype"]),
         L=a["L"], rho=float(a["rho"]), condMin=float(a["condMin"]),
         difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
-        record_obj=True, record_dif=True, evolution=evolution)
+        record_obj=record_obj, record_dif=True, evolution=evolution)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -77,6 +77,29 @@ def test_partitioned_sequential_evolution_equals_reference(gpu_lib, name, k):
         pytest.skip("graph too small for %d ranks" % k)
     X, it, Obj, Dif, info = _solve(c, k, False, pfdr.EVOLUTION_SEQUENTIAL)
     print("%s k=%d it=%d/%d" % (name, k, it, int(g["conv_it"])))
+    assert it == int(g["conv_it"])
+    assert np.array_equal(X, g["conv_X"])
+    assert np.array_equal(Dif[:it], g["conv_Dif"][:it])
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("k", [2, 3])
+def test_partitioned_speculative_equals_reference(gpu_lib, name, k):
+    """difRcd = 0 and no objective record: the partition decides
+    speculatively -- the evolution chain and decision of iteration t run on a
+    second stream over the split transport, beside the halo exchanges and
+    sweeps of t + 1 (X / P ping-ponged) -- and the stopping iteration, every
+    Dif and X still equal the reference's bit for bit"""
+    from cp_pfdr_graph_d1_amd import pfdr
+    c, g = G.load(name)
+    V = c["X0"].size if "X0" in c else c["P0"].size // int(c["K"])
+    if V < 4 * k:
+        pytest.skip("graph too small for %d ranks" % k)
+    if float(c["difRcd"]) != 0.0:
+        pytest.skip("reconditioning: no speculation")
+    X, it, _, Dif, info = _solve(c, k, False, pfdr.EVOLUTION_SEQUENTIAL, record_obj=False)
+    print("%s k=%d it=%d/%d" % (name, k, it, int(g["conv_it"])))
+    assert all(q["speculative"] == 1 for q in info["queries"])
     assert it == int(g["conv_it"])
     assert np.array_equal(X, g["conv_X"])
     assert np.array_equal(Dif[:it], g["conv_Dif"][:it])
@@ -314,8 +337,10 @@ def test_relabelled_partition_random_labels(gpu_lib, k, kind):
     s.run(kw["itMax"])
     X1, it1, _, D1 = s.result()
     s.close()
-    Xr, itr, _, Dr, _ = P.solve_loopback(*args, relabel=True, **kw)
+    Xr, itr, _, Dr, info = P.solve_loopback(*args, relabel=True, **kw)
     print("%s k=%d converged: it %d / %d" % (kind, k, it1, itr))
+    # difRcd = 0: speculative ranks, their terms routed to caller-order slices
+    assert all(q["speculative"] == 1 and q["seqdif"] == 1 for q in info["queries"])
     assert 0 < it1 < kw["itMax"] and itr == it1
     assert np.array_equal(Dr[:itr], D1[:it1])
     assert np.array_equal(Xr, X1)
