@@ -226,7 +226,8 @@ def pmc_summary(wl, E):
 # boundary launches (edge_sweep_b, vertex_sweep_b) complete the interior ones
 FAMILIES = {"edge_sweep": ("edge_sweep", "edge_sweep_b"),
             "vertex_sweep": ("vertex_sweep", "vertex_sweep_b"),
-            "sx_edge_sweep": ("sx_edge_sweep",), "sx_vertex_sweep": ("sx_vertex_sweep",),
+            "sx_edge_sweep": ("sx_edge_sweep",),
+            "sx_vertex_sweep": ("sx_vertex_sweep", "sx_vertex_wide"),  # K <= 64 / K > 64
             "gemv_cols": ("gemv_cols",), "gemv_rows": ("gemv_rows",), "symv": ("symv",)}
 
 
@@ -366,7 +367,7 @@ def main():
     # profiles/r2/r2d_launch_gap.log); a small solve timed to tolerance is
     # timed bare and a second, profiled solve gives the kernel means
     timed = sorted({wl.dominant, "edge_sweep", "vertex_sweep", "sx_edge_sweep",
-                    "sx_vertex_sweep", "gemv_cols", "gemv_rows"})
+                    "sx_vertex_sweep", "sx_vertex_wide", "gemv_cols", "gemv_rows"})
     period = 4 if world == 1 else 8
     torch.cuda.synchronize()
     barrier()
@@ -398,7 +399,7 @@ def main():
         torch.cuda.synchronize()
         del kw
     names = (wl.dominant, "edge_sweep", "edge_sweep_b", "vertex_sweep", "vertex_sweep_b",
-             "sx_edge_sweep", "sx_vertex_sweep", "sx_average", "sx_project", "gemv_rows",
+             "sx_edge_sweep", "sx_vertex_sweep", "sx_vertex_wide", "gemv_rows",
              "gemv_cols", "halo_pull", "halo_push", "seq_evolution")
     stats = {k: sess.kernel_stats(k) for k in names}
     res = res_timed if converge else sess.result()
@@ -419,6 +420,8 @@ def main():
         knames["edge_sweep"] = ["k_edge_sweep_tl"]
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
+    if not quad and getattr(wl, "K", 0) > 64:  # one wave per vertex
+        knames["sx_vertex_sweep"] = ["k_sx_vertex_wide"]
     sess.close()
     if comm:
         from cp_pfdr_graph_d1_amd import partition

@@ -70,12 +70,61 @@ __device__ __forceinline__ void sx_prox_weights(real wu, real wv, real gu, real 
 }
 
 // ------------------------------------------------ metric projection ----
+// The metric simplex projection's sweep (ref src/proj_simplex_metric.cpp:41-80)
+// down a column of LDS (stride `st` between coordinates),
+// split for the group vertex sweep (k_sx_vertex_group): the coordinates
+// arrive already divided by their metric (x[d] / m[d], the reference's own
+// division, done by the item lanes) with the raw x[0] beside them, the
+// active set goes to bytes I[d * st], and the final threshold is returned --
+// the item lanes then form (x - la) m or 0 in parallel (ref :74-80).  The
+// walk itself is the reference's sequence of comparisons and updates
+// (ref :43-72), the next coordinate's loads issued before the current one's
+// arithmetic.
+template <typename real>
+__device__ real proj_simplex_walk(const real *x, const real *m, unsigned char *I, int D, int st,
+                                  real x0, real a) {
+    const real m0 = m[0];
+    real la = (x0 - a) / m0;
+    real s = m0;
+    I[0] = 1;
+    real xn = D > 1 ? x[st] : real(0), mn = D > 1 ? m[st] : real(1);
+    for (int d = 1; d < D; d++) {  // first pass (ref :48-57)
+        const real xd = xn, md = mn;
+        if (d + 1 < D) { xn = x[(d + 1) * st]; mn = m[(d + 1) * st]; }
+        unsigned char in = 0;
+        if (xd > la) {
+            in = 1;
+            s += md;
+            la += md * (xd - la) / s;
+        }
+        I[d * st] = in;
+    }
+    bool changed = true;
+    while (changed) {  // later passes (ref :59-72)
+        changed = false;
+        unsigned char in_n = I[0];
+        real xm = x[0];
+        for (int d = 0; d < D; d++) {
+            const unsigned char in = in_n;
+            const real xd = xm;
+            if (d + 1 < D) { in_n = I[(d + 1) * st]; xm = x[(d + 1) * st]; }
+            if (in && xd < la) {
+                I[d * st] = 0;
+                const real md = m[d * st];
+                s -= md;
+                la += md * (la - xd) / s;
+                changed = true;
+            }
+        }
+    }
+    return la;
+}
+
 // Projection of x (D <= 64 values, stride 1, in LDS) onto {x >= 0, sum x = a}
 // in the metric diag(1/m) by one lane: the active-set sweep of ref
 // src/proj_simplex_metric.cpp:41-80, operation for operation, the active
 // set in a register bit mask.  Used by the fused vertex sweep (K <= 64),
-// whose vertices pack the lanes densely; wider columns are projected by a
-// whole segment of lanes (pfdr_proj.hpp).
+// whose vertices pack the lanes densely.
 template <typename real>
 __device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
     unsigned long long act = 1ull;
@@ -599,6 +648,55 @@ struct SxVArgs {
     unsigned char *act;  // its active flags (one byte per (v, k))
 };
 
+// ordered DR average of item (v, k) (ref :636-648): the incidences in the
+// reference's (e, side) order, W * Z formed from Z with the reference's
+// products; consecutive lanes take consecutive labels, so each incidence is
+// a K-contiguous run read coalesced
+template <typename real>
+__device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int k) {
+    const int K = a.c.K;
+    const real inv = a.invAux[v * K + k];  // 1/Aux of this (v, k)
+    const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
+    real s = real(0);
+    int j = j0;
+    // 8 slots, then 8 contributions in flight per lane; summed in order
+    for (; j + 8 <= j1; j += 8) {
+        unsigned sl[8];
+        real w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
+        {   // W * Z formed here (the reference's products, same rounding)
+            // branch-free: received entries (address 2E + j) sit in the
+            // tail of Zv as the sender's W*Z (factor 1), so all 16 loads
+            // issue together
+            real zq[8], aq[8];
+            bool rq[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const long ad = sl[q];
+                const bool sv = ad >= a.E;
+                const long ea = sv ? ad - a.E : ad;
+                rq[q] = ea >= a.E;
+                zq[q] = (sv ? a.Zv : a.Zu)[ea * K + k];
+                aq[q] = a.A1 ? a.A1[rq[q] ? 0 : ea * K + k] : a.La_d1[rq[q] ? 0 : ea];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) w[q] = rq[q] ? zq[q] : (aq[q] * inv) * zq[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) s += w[q];
+    }
+    for (; j < j1; j++) {
+        const long ad = a.idx[j];
+        const bool sv = ad >= a.E;
+        const long ea = sv ? ad - a.E : ad;
+        const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
+        if (ea >= a.E) s += z;
+        else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
+    }
+    return s;
+}
+
 // One block of the fused vertex sweep: NT lanes (t = the lane within
 // them) with their own xs / ms / red in LDS.  Every lane of the calling
 // workgroup reaches the same barriers (a block past the last, blk >= nb, has
@@ -617,46 +715,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     const bool live = blk < a.nb && vl < vb && v < a.V;
     const long i = v * K + k;
     if (live) {
-        const real inv = a.invAux[i];  // 1/Aux of this (v, k)
-        const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
-        real s = real(0);
-        int j = j0;
-        // 8 slots, then 8 contributions in flight per lane; summed in order
-        for (; j + 8 <= j1; j += 8) {
-            unsigned sl[8];
-            real w[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
-            {   // W * Z formed here (the reference's products, same rounding)
-                // branch-free: received entries (address 2E + j) sit in the
-                // tail of Zv as the sender's W*Z (factor 1), so all 16 loads
-                // issue together
-                real zq[8], aq[8];
-                bool rq[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const long ad = sl[q];
-                    const bool sv = ad >= a.E;
-                    const long ea = sv ? ad - a.E : ad;
-                    rq[q] = ea >= a.E;
-                    zq[q] = (sv ? a.Zv : a.Zu)[ea * K + k];
-                    aq[q] = a.A1 ? a.A1[rq[q] ? 0 : ea * K + k] : a.La_d1[rq[q] ? 0 : ea];
-                }
-#pragma unroll
-                for (int q = 0; q < 8; q++) w[q] = rq[q] ? zq[q] : (aq[q] * inv) * zq[q];
-            }
-#pragma unroll
-            for (int q = 0; q < 8; q++) s += w[q];
-        }
-        for (; j < j1; j++) {
-            const long ad = a.idx[j];
-            const bool sv = ad >= a.E;
-            const long ea = sv ? ad - a.E : ad;
-            const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
-            if (ea >= a.E) s += z;
-            else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
-        }
-        xs[t] = s;
+        xs[t] = sx_item_sum(a, v, k);
         ms[t] = a.Ga[i];
     }
     __syncthreads();
@@ -710,19 +769,230 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
 }
 
-// ------------------------------------------- wide vertex sweep (K > 64) --
+// ------------------------------------------ group vertex sweep (K > 64) --
+// NV vertices per workgroup (NV <= 64, sized so that their K-long columns
+// fit in LDS).  (1) sums: the block's 256 lanes take the group's (vertex,
+// label) items, consecutive lanes consecutive labels, two items per lane in
+// flight, each item's ordered sum over its incidences (K-contiguous runs of
+// Z, read coalesced), divided by its metric, into LDS COLUMNS
+// xs[k * (NV + 1) + v]; (2) projection: lane v < NV walks its vertex down its
+// column -- the reference's comparisons and threshold updates
+// (src/proj_simplex_metric.cpp:41-72), its sequential arithmetic SIMT across
+// the group's vertices, conflict-free (consecutive lanes, consecutive words);
+// (3) the items again: (x - la) m or 0 (ref :74-80), evolution terms, P and
+// (P, step) written back as coalesced rows (then the label scan, if asked).  The metric
+// projection costs K steps of one lane per vertex: a typical column (an
+// averaged distribution, which enters the active set element by element)
+// has ~K events, so a whole wave per vertex (one ballot per event) spent 64
+// lanes' issue slots on each step and ran the C4 law at K = 100 at 5.2 ms
+// (0.9 TB/s) where this layout shares them among NV vertices.
+template <typename real>
+struct SxGroup {
+    static constexpr int kMaxNV = 64;
+    // vertices per group, at most: C4's law at K = 100 (1M vertices), group
+    // sweep 1.69 / 1.73 / 1.75 ms at 16 / 32 / 64 -- the walking lanes per CU
+    // are set by the LDS whatever the split, and smaller groups keep more
+    // workgroups' loads in flight
+    static constexpr int kNV = 16;
+    static constexpr int kInc = 16;            // staged incidences per vertex, on average
+    static constexpr size_t kLds = 60 * 1024;  // bytes of dynamic LDS per workgroup, at most
+    // per (vertex, label): x and m (reals) and the active flag (a byte);
+    // per staged incidence: its Z offset (int64, side and received bits on top)
+    // and its weight a_e (real)
+    static size_t bytes(int K, int nv) {
+        const size_t col = (size_t)K * (nv + 1) * (2 * sizeof(real) + 1);
+        return (col + 7) / 8 * 8 + (size_t)kInc * nv * (8 + sizeof(real));
+    }
+    // vertices per group for K labels (0: K too wide for LDS)
+    static int nv_for(int K, int want) {
+        int nv = want;
+        while (nv > 1 && bytes(K, nv) > kLds) nv >>= 1;
+        return bytes(K, nv) <= kLds ? nv : 0;
+    }
+};
+
+constexpr long kZv = 1L << 62, kRecv = 1L << 61;  // staged Z offset: v-side / received
+
+// items per lane in flight in the group sweep's sums: C4's law at K = 100
+// (1M vertices), group sweep ms: 1 item 2.0, 2 items 1.69, 4 items 2.2-3.1
+constexpr int SXU = 2;
+
+template <typename real, bool SPLIT>
+__global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    extern __shared__ double lds_group[];
+    __shared__ real red[kBlock / kWave];
+    __shared__ real x0s[SxGroup<real>::kMaxNV], las[SxGroup<real>::kMaxNV];
+    __shared__ int lptr[SxGroup<real>::kMaxNV + 1];
+    const int K = a.c.K, NV = a.vb, st = NV + 1, t = threadIdx.x;
+    real *xs = reinterpret_cast<real *>(lds_group);
+    real *ms = xs + (size_t)K * st;
+    unsigned char *I = reinterpret_cast<unsigned char *>(ms + (size_t)K * st);
+    long *zo = reinterpret_cast<long *>(lds_group) +
+               ((size_t)K * st * (2 * sizeof(real) + 1) + 7) / 8;
+    real *wa = reinterpret_cast<real *>(zo + SxGroup<real>::kInc * NV);
+    const long v0 = (long)blockIdx.x * NV;
+    const int nv = (int)(a.V - v0 < NV ? a.V - v0 : NV);  // this group's vertices
+    const int nitems = nv * K;
+    // (0) the group's incidence lists (one contiguous CSR range), decoded once
+    // into LDS: every item of a vertex then issues its K-run loads of Z at once
+    if (t <= nv) lptr[t] = a.ptr[v0 + t];
+    __syncthreads();
+    const int jb = lptr[0], nj = lptr[nv] - jb;
+    const bool staged = nj <= SxGroup<real>::kInc * NV;
+    if (staged) {
+        for (int q = t; q < nj; q += kBlock) {
+            const long ad = a.idx[jb + q];
+            const bool sv = ad >= a.E;
+            const long ea = sv ? ad - a.E : ad;
+            const bool rq = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
+            zo[q] = ea * K | (sv ? kZv : 0) | (rq ? kRecv : 0);
+            wa[q] = (rq || a.A1) ? real(0) : a.La_d1[ea];
+        }
+        __syncthreads();
+    }
+    // (1) ordered sums (ref :636-648), divided by their metric (the first
+    // pass's x[d] / m[d], ref :44, :49), raw x[0] aside; SXU items per lane,
+    // their SXU x 8 K-run loads of Z in flight together
+    for (int it0 = t; it0 < nitems; it0 += SXU * kBlock) {
+        real x[SXU];
+        int vl[SXU], k[SXU];
+        long i[SXU];
+        bool ok[SXU];
+#pragma unroll
+        for (int u = 0; u < SXU; u++) {
+            const int it = it0 + u * kBlock;
+            ok[u] = it < nitems;
+            vl[u] = ok[u] ? it / K : 0;
+            k[u] = ok[u] ? it - vl[u] * K : 0;
+            i[u] = v0 * K + (ok[u] ? it : 0);
+            x[u] = real(0);
+        }
+        if (staged) {
+            real inv[SXU];
+            int j[SXU], j1[SXU];
+#pragma unroll
+            for (int u = 0; u < SXU; u++) {
+                inv[u] = ok[u] ? a.invAux[i[u]] : real(0);
+                j[u] = ok[u] ? lptr[vl[u]] - jb : 0;
+                j1[u] = ok[u] ? lptr[vl[u] + 1] - jb : 0;
+            }
+            for (;;) {
+                bool more = false;
+#pragma unroll
+                for (int u = 0; u < SXU; u++) more |= j[u] < j1[u];
+                if (!more) break;  // 8 K-run loads per item, added in order
+                real zq[SXU][8], aq[SXU][8];
+                bool rq[SXU][8];
+#pragma unroll
+                for (int u = 0; u < SXU; u++)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        rq[u][q] = true;
+                        zq[u][q] = aq[u][q] = real(0);
+                        if (j[u] + q < j1[u]) {
+                            const long o = zo[j[u] + q];
+                            const long e = o & (kRecv - 1);
+                            rq[u][q] = (o & kRecv) != 0;
+                            zq[u][q] = ((o & kZv) ? a.Zv : a.Zu)[e + k[u]];
+                            aq[u][q] = (a.A1 && !rq[u][q]) ? a.A1[e + k[u]] : wa[j[u] + q];
+                        }
+                    }
+#pragma unroll
+                for (int u = 0; u < SXU; u++) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (j[u] + q < j1[u])
+                            x[u] += rq[u][q] ? zq[u][q] : (aq[u][q] * inv[u]) * zq[u][q];
+                    j[u] += 8;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < SXU; u++)  // (a hub-sized group: the CSR from memory)
+                if (ok[u]) x[u] = sx_item_sum(a, v0 + vl[u], k[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < SXU; u++) {
+            if (!ok[u]) continue;
+            const real m = a.Ga[i[u]];
+            if (k[u] == 0) x0s[vl[u]] = x[u];
+            xs[k[u] * st + vl[u]] = x[u] / m;
+            ms[k[u] * st + vl[u]] = m;
+        }
+    }
+    __syncthreads();
+    real dif = real(0);
+    if (t < nv)  // (2) one lane per vertex down its column
+        las[t] = proj_simplex_walk<real>(xs + t, ms + t, I + t, K, st, x0s[t], real(1));
+    __syncthreads();
+    // (3) finalise (ref :74-80), rows back out; 4 items per lane, loads first
+    for (int it0 = t; it0 < nitems; it0 += 4 * kBlock) {
+        real pold[4], gq[4], qq[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int it = it0 + u * kBlock;
+            pold[u] = gq[u] = qq[u] = real(0);
+            if (it < nitems) {
+                const long i = v0 * K + it;  // (items are the group's rows, in order)
+                if (a.track == 1) pold[u] = a.P[i];
+                gq[u] = a.GaQ[i];
+                if (a.c.loss == LOSS_QUAD) qq[u] = a.Q[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int it = it0 + u * kBlock;
+            if (it >= nitems) break;
+            const int vl = it / K, k = it - vl * K;
+            const long i = v0 * K + it;
+            const int c = k * st + vl;
+            const real p = I[c] ? (xs[c] - las[vl]) * ms[c] : real(0);
+            if (a.track == 2) xs[c] = p;  // for the label scan
+            if (a.track == 1) {
+                real d = pold[u] - p;
+                if (d < real(0)) d = -d;
+                dif += d;
+                if (a.terms) a.terms[i] = d;
+            }
+            (SPLIT ? a.Po : a.P)[i] = p;
+            SxR2<real> q;
+            q.x = p;
+            q.y = sx_explicit(a.c, p, gq[u], qq[u]);
+            (SPLIT ? a.PFo : a.PF)[i] = q;
+        }
+    }
+    if (a.track == 2) {  // maximum-likelihood label of each vertex (ref :656-676)
+        __syncthreads();
+        if (t < nv) {
+            const real *x = xs + t;
+            real mx = x[0];
+            int l = 0;
+            for (int d = 1; d < K; d++) if (x[d * st] > mx) { mx = x[d * st]; l = d; }
+            const real fl = (real)l;
+            if (fl != a.lab[v0 + t]) { dif = real(1); a.lab[v0 + t] = fl; }
+            if (a.terms) a.terms[v0 + t] = dif;
+        }
+    }
+    if (a.track) {
+        dif = block_sum(dif, red);
+        if (t == 0) a.part[blockIdx.x] = dif;
+    }
+}
+
+// ------------------------ wide vertex sweep in memory (K past the LDS) --
 // One WAVE per vertex, lane l holding the labels k = l + 64 j: every
 // incidence is one K-contiguous run of Z read coalesced by the wave, the
-// ordered sums stay in registers, the metric projection runs on the whole
-// wave (pfdr_proj.hpp: one ballot per active-set event, bit-exact with
-// ref src/proj_simplex_metric.cpp:41-80), and P and (P, step) go back as
-// coalesced rows.  J registers per lane cover K <= 64 J; J = 0 (K > 1024)
-// keeps the averages in xs and the active set in act, 64 labels per chunk.
+// averages go to xs (projected in place by the whole wave, pfdr_proj.hpp:
+// one ballot per active-set event, bit-exact with ref
+// src/proj_simplex_metric.cpp:41-80, the active set in act), and P and
+// (P, step) go back as coalesced rows.  For K whose column does not fit a
+// group's LDS (f32 K > 3,413, f64 K > 1,807).
 constexpr int kSxWideVpw = 4;  // vertices per wave; a block's 4 waves interleave
 
 // ordered DR average (ref :636-648) of labels k = k0 + lane + 64 j of vertex
 // v (wave-uniform): the incidences in the reference's (e, side) order, W * Z
-// formed with the fused sweep's operations (sx_vertex_block); B incidences'
+// formed with the fused sweep's operations (sx_item_sum); B incidences'
 // loads in flight, added in order
 template <typename real, int J>
 __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int k0, int lane,
@@ -783,7 +1053,7 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
 
 // evolution term, new P and (P, step) of one (v, k); the label scan's candidate
 template <typename real, bool SPLIT>
-__device__ __forceinline__ void sx_wide_out(const SxVArgs<real> &a, long v, long b, int k, real p,
+__device__ __forceinline__ void sx_wide_out(const SxVArgs<real> &a, long b, int k, real p,
                                             real &dif, real &mv, int &mi) {
     const long i = b + k;
     if (a.track == 1) {
@@ -801,50 +1071,32 @@ __device__ __forceinline__ void sx_wide_out(const SxVArgs<real> &a, long v, long
     (SPLIT ? a.PFo : a.PF)[i] = q;
 }
 
-template <typename real, int J, bool SPLIT>
+template <typename real, bool SPLIT>
 __global__ __launch_bounds__(kBlock) void k_sx_vertex_wide(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real red[kBlock / kWave];
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & (kWave - 1));
-    const Seg<64> sg;
     const int K = a.c.K;
     real dif = real(0);
     for (int q = 0; q < kSxWideVpw; q++) {
         const long v = ((long)blockIdx.x * kSxWideVpw + q) * (kBlock / kWave) + w;
         if (v >= a.V) break;  // wave-uniform
         const long b = v * K;
-        real mv = real(0), p0;
+        real mv = real(0);
         int mi = 0x7fffffff;
-        if constexpr (J > 0) {
-            real x[J], m[J];
-            sx_wide_sums<real, J>(a, v, 0, lane, x);
+        for (int k0 = 0; k0 < K; k0 += 4 * 64) {
+            real s4[4];
+            sx_wide_sums<real, 4>(a, v, k0, lane, s4);
 #pragma unroll
-            for (int j = 0; j < J; j++) {
-                const int k = lane + 64 * j;
-                m[j] = k < K ? a.Ga[b + k] : real(1);
+            for (int j = 0; j < 4; j++) {
+                const int k = k0 + lane + 64 * j;
+                if (k < K) a.xs[b + k] = s4[j];
             }
-            proj_segment<real, 64, J>(sg, x, m, K, real(1));
-            p0 = lane_read(x[0], 0);
-#pragma unroll
-            for (int j = 0; j < J; j++) {
-                const int k = lane + 64 * j;
-                if (k < K) sx_wide_out<real, SPLIT>(a, v, b, k, x[j], dif, mv, mi);
-            }
-        } else {
-            for (int k0 = 0; k0 < K; k0 += 4 * 64) {
-                real s4[4];
-                sx_wide_sums<real, 4>(a, v, k0, lane, s4);
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int k = k0 + lane + 64 * j;
-                    if (k < K) a.xs[b + k] = s4[j];
-                }
-            }
-            proj_wave_mem<real>(a.xs + b, a.Ga + b, K, real(1), a.act + b);
-            p0 = lane_read(lane == 0 ? a.xs[b] : real(0), 0);
-            for (int k = lane; k < K; k += 64) sx_wide_out<real, SPLIT>(a, v, b, k, a.xs[b + k], dif, mv, mi);
         }
+        proj_wave_mem<real>(a.xs + b, a.Ga + b, K, real(1), a.act + b);
+        const real p0 = lane_read(lane == 0 ? a.xs[b] : real(0), 0);
+        for (int k = lane; k < K; k += 64) sx_wide_out<real, SPLIT>(a, b, k, a.xs[b + k], dif, mv, mi);
         if (a.track == 2) {  // maximum-likelihood label (ref :656-676)
             const int l = wave_argmax(mv, mi, p0 != p0);
             if (lane == 0) {
@@ -1306,6 +1558,7 @@ class SimplexSession final : public SessionBase {
     int nbv_, nbe_;
     int vb_ = 0, nbs_ = 0;  // fused vertex sweep (K <= 64): vertices per block, blocks
     int nbw_ = 0;           // wide vertex sweep (K > 64): blocks
+    int gnv_ = 0;           // its vertices per group (0: a wave per vertex, in memory)
     DevBuf<unsigned char> act_;  // its active sets when K > 1024
     // the fused vertex sweep forms W*Z from the gathered Z and W (K contiguous
     // words per incidence), so the edge sweep neither reads W nor writes
@@ -1351,13 +1604,13 @@ class SimplexSession final : public SessionBase {
     }
     void push_wz();
     template <bool SPLIT>
-    void launch_wide(const SxVArgs<real> &a) {
-        const int g = nbw_;
-        if (K_ <= 128) k_sx_vertex_wide<real, 2, SPLIT><<<g, kBlock, 0, stream>>>(a);
-        else if (K_ <= 256) k_sx_vertex_wide<real, 4, SPLIT><<<g, kBlock, 0, stream>>>(a);
-        else if (K_ <= 512) k_sx_vertex_wide<real, 8, SPLIT><<<g, kBlock, 0, stream>>>(a);
-        else if (K_ <= 1024) k_sx_vertex_wide<real, 16, SPLIT><<<g, kBlock, 0, stream>>>(a);
-        else k_sx_vertex_wide<real, 0, SPLIT><<<g, kBlock, 0, stream>>>(a);
+    void launch_wide(SxVArgs<real> a) {
+        if (gnv_) {  // groups of gnv_ vertices, columns in LDS
+            a.vb = gnv_;
+            k_sx_vertex_group<real, SPLIT><<<nbw_, kBlock, SxGroup<real>::bytes(K_, gnv_), stream>>>(a);
+        } else {
+            k_sx_vertex_wide<real, SPLIT><<<nbw_, kBlock, 0, stream>>>(a);
+        }
     }
 };
 
@@ -1433,10 +1686,11 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64) {
         vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
-    } else {  // wide vertex sweep: a wave per vertex
-        const long per = (long)kSxWideVpw * (kBlock / kWave);
+    } else {  // groups of vertices with their columns in LDS, or a wave per vertex
+        gnv_ = SxGroup<real>::nv_for(K_, SxGroup<real>::kNV);
+        const long per = gnv_ ? gnv_ : (long)kSxWideVpw * (kBlock / kWave);
         nbw_ = (int)((V_ + per - 1) / per);
-        if (K_ > 1024) {  // averages and active sets in memory
+        if (!gnv_) {  // averages and active sets in memory
             Pavg_.alloc(VK_);
             act_.alloc(VK_);
         }

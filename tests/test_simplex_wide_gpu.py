@@ -29,12 +29,16 @@ def _problem(n, K, dt, seed=4, weak=False):
     return V, Eu.astype(np.int32), Ev.astype(np.int32), Q
 
 
-@pytest.mark.parametrize("K,n", [(130, 40), (1100, 12)], ids=["K130", "K1100"])
+@pytest.mark.parametrize("K,n,dt", [(130, 40, np.float32), (1100, 12, np.float32),
+                                    (2000, 9, np.float64), (3500, 7, np.float32)],
+                         ids=["K130", "K1100", "K2000-f64", "K3500"])
 @pytest.mark.parametrize("difTol", [1e-3, 1.0], ids=["l1", "labels"])
-def test_wide_speculative_matches_restatement(gpu_lib, K, n, difTol):
+def test_wide_speculative_matches_restatement(gpu_lib, K, n, dt, difTol):
+    """K = 130 and 1,100: groups of vertices with their columns in LDS (64
+    and 4 per group); K = 2,000 (f64) and 3,500 (f32): past the LDS, one wave
+    per vertex with the columns and active sets in memory"""
     import oracle
     from cp_pfdr_graph_d1_amd import pfdr
-    dt = np.float32
     labels = difTol >= 1
     V, Eu, Ev, Q = _problem(n, K, dt, weak=labels)
     La = np.full(Eu.size, 0.3 if labels else 0.05, dt)
@@ -57,7 +61,7 @@ def test_wide_speculative_matches_restatement(gpu_lib, K, n, difTol):
     assert np.array_equal(P, Po)
 
 
-@pytest.mark.parametrize("K,n", [(100, 24), (1030, 9)], ids=["K100", "K1030"])
+@pytest.mark.parametrize("K,n", [(100, 24), (1030, 9), (3500, 6)], ids=["K100", "K1030", "K3500"])
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 def test_wide_partitioned_matches_single(gpu_lib, K, n, dt):
     """3 loopback ranks with K-wide halos (the pushed W*Z packed per label,

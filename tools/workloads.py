@@ -113,13 +113,15 @@ class HeadlineConv(Headline):
     """The headline solved to difTol 1e-5 (the parity run):
     time to tolerance and the converged iteration count; the evolution sums
     round as the reference's (PFDR_EVOLUTION_AUTO -> sequential at this size),
-    so the count is the reference's (248, tests/golden/fullsize/headline_conv)."""
+    so the count is the reference's (248, tests/golden/fullsize/headline_conv).
+    N > 1 (or --dist-selftest): z-slabs as the headline, the evolution summed
+    rank to rank (ChainSum) and decided speculatively beside the next
+    iteration's halo exchanges."""
     name = "headline_conv"
-    partitionable = False
     steps = 10000
 
     def inputs(self, rank, world, strong=True):
-        d = Headline.inputs(self, 0, 1)
+        d = Headline.inputs(self, rank, world, strong)
         d["kw"].update(difTol=1e-5, record_dif=True)
         d["converge"] = True
         d["desc"] += ", solved to difTol 1e-5"
@@ -335,6 +337,23 @@ class C4(Workload):
                     graph="%dx%d" % g)
 
 
+class C4K100(C4):
+    """C4's law at K = 100 labels (one wave per vertex, k_sx_vertex_wide) on
+    a 1000^2 8-neighbour grid (V = 1M, E = 4M, 400M (edge, label) entries):
+    the wide simplex path's throughput, for DESIGN.md"""
+    name = "c4k100"
+    metric = "PFDR_graph_loss_d1_simplex<float> K=100 KL 1M-vertex 8-NN: Medge-updates/s"
+    K = 100
+    SIDE = 1000
+    edge_bytes = 8 + 9 * 100 * 4
+    vertex_bytes = 100 * 4 * 4
+
+    def inputs(self, rank, world, strong=True):
+        d = C4.inputs(self, rank, world, strong)
+        d["desc"] = d["desc"].replace("2236^2", "1000^2").replace("K=10", "K=100")
+        return d
+
+
 class C5(Workload):
     """config 5: bounds [0,1], 640^3 6-NN, fp32, split across the GPUs
     (strong scaling: the 262M-vertex graph is fixed)"""
@@ -427,4 +446,4 @@ class C3AtA(Workload):
 
 WORKLOADS = {w.name: w for w in (Headline(), HeadlineConv(), HeadlineSlab8(), HeadlineShuffled(),
                                   C1(), C2(), C3(),
-                                  C3AtA(), C4(), C5())}
+                                  C3AtA(), C4(), C4K100(), C5())}
