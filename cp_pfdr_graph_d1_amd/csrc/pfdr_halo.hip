@@ -194,7 +194,11 @@ class RcclTransport final : public Transport {
     std::unique_ptr<Transport> split(hipStream_t) override {
         last_op = "communicator split";
         ncclComm_t nc = nullptr;
-        ck(ncclCommSplit(comm_, 0, rank, &nc, nullptr), "comm split");
+        // its own resources (streams, buffers): operations on the two
+        // communicators must not be ordered behind each other
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.splitShare = 0;
+        ck(ncclCommSplit(comm_, 0, rank, &nc, &cfg), "comm split");
         comm_created(nc);
         kids_.push_back(nc);
         std::unique_ptr<RcclTransport> t(new RcclTransport(nc, nranks, rank));
@@ -207,6 +211,9 @@ class RcclTransport final : public Transport {
                   hipStream_t s) override {
         last_op = "grouped send/recv, send " + peers_bytes(sbytes, rank) + " recv " +
                   peers_bytes(rbytes, rank);
+        bool any = false;  // (an exchange with nothing to move issues no RCCL call)
+        for (int q = 0; q < nranks; q++) any = any || (q != rank && (sbytes[q] || rbytes[q]));
+        if (!any) return;
         ck(ncclGroupStart(), "group start");
         for (int q = 0; q < nranks; q++) {
             if (q == rank) continue;
@@ -218,6 +225,7 @@ class RcclTransport final : public Transport {
     void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
         ncclDataType_t t = dtype == PFDR_F32 ? ncclFloat32 : dtype == PFDR_F64 ? ncclFloat64 : ncclInt64;
         last_op = "all-reduce of " + std::to_string(n) + " values, all peers";
+        if (nranks == 1) return;  // (in place: the sum over one rank is the data)
         ck(ncclAllReduce(dev, dev, n, t, ncclSum, comm_, s), "allreduce");
     }
     void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
@@ -234,6 +242,7 @@ class RcclTransport final : public Transport {
     }
     void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
         last_op = "broadcast of " + std::to_string(bytes) + " B from " + std::to_string(root);
+        if (nranks == 1) return;
         ck(ncclBroadcast(dev, dev, bytes, ncclChar, root, comm_, s), "broadcast");
     }
 };
