@@ -193,21 +193,25 @@ class QuadSession final : public SessionBase {
     // Speculative iteration (sequential evolution, no reconditioning
     // (difRcd = 0), no objective record, identity / diagonal A; one GPU or a
     // partition): the evolution sums and the decision on iteration t run on
-    // a second stream (evs_) while iteration t + 1 sweeps; iteration t + 2
-    // waits for that decision.  A partition runs its rank-to-rank evolution
-    // chain there over a split transport (evtr_), beside the halo exchanges
-    // of t + 1, instead of on the critical path of every iteration.  X is ping-ponged (iteration t reads xpb(t - 1), writes
-    // xpb(t)) and the terms are double-buffered, so when the decision on t
-    // stops the loop, X_t is intact in xpb(t) and the speculative t + 1 (its
-    // Z, its X in the other buffer) is simply discarded: the iterate,
-    // iteration count and Dif are the sequential loop's, bit for bit.
+    // a second stream (evs_) while iterations t + 1 ... t + D - 1 sweep;
+    // iteration t + D waits for that decision (depth D = sd_: 2 on one GPU;
+    // 4 on a partition of three or more ranks, whose rank-to-rank evolution
+    // chain, run there over a split transport (evtr_) beside the halo
+    // exchanges, takes several of a rank's iterations).  X cycles through D
+    // buffers (iteration t reads xpb(t - 1), writes xpb(t)) and the terms
+    // through D, so when the decision on t stops the loop, X_t is intact in
+    // xpb(t) and the speculative iterations after it (their Z, their X in the
+    // other buffers) are simply discarded: the iterate, iteration count and
+    // Dif are the sequential loop's, bit for bit.
+    static constexpr int kSpecMax = 4;
     bool spec_ = false;
+    int sd_ = 2;
     int it0_ = 0;  // completed iterations when the captured / launched bodies start
-    DevBuf<R2<real>> xp2_;
-    R2<real> *xpb(int t) { return spec_ && (t & 1) ? xp2_.p : xp_.p; }
+    DevBuf<R2<real>> xpx_[kSpecMax - 1];  // X buffers 1 .. D - 1 (0 is xp_)
+    R2<real> *xpb(int t) { return spec_ && t % sd_ ? xpx_[t % sd_ - 1].p : xp_.p; }
     R2<real> *xr_ = nullptr, *xw_ = nullptr;  // the sweeps' read / write (X, P)
     hipStream_t evs_ = nullptr;
-    hipEvent_t evv_[2] = {}, evd_[2] = {};
+    hipEvent_t evv_[kSpecMax] = {}, evd_[kSpecMax] = {};
     // run_pipelined: the control block's snapshots after two chunks in flight
     Ctrl<real> *snap_[2] = {};
     hipEvent_t snapev_[2] = {};
@@ -679,17 +683,20 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             overlap_ = false;
         }
         if (spec_) {
-            DevBuf<real> t2(4 * (size_t)tstride_);  // terms of both parities
+            sd_ = halo_ && halo_->tr->nranks >= 3 ? 4 : 2;
+            DevBuf<real> t2((size_t)sd_ * 2 * tstride_);  // terms of D iterations
             std::swap(terms_.p, t2.p);
             std::swap(terms_.n, t2.n);
-            DevBuf<real> p2(4 * (size_t)nbv_);  // and their block sums
+            DevBuf<real> p2((size_t)sd_ * 2 * nbv_);  // and their block sums
             std::swap(vpart_.p, p2.p);
             std::swap(vpart_.n, p2.n);
-            xp2_.alloc(Vg_ + 2);  // (+2 as xp_)
-            PFDR_HIP(hipMemcpyAsync(xp2_.p, xp_.p, sizeof(R2<real>) * (Vg_ + 2),
-                                    hipMemcpyDeviceToDevice, s));
+            for (int k = 0; k + 1 < sd_; k++) {
+                xpx_[k].alloc(Vg_ + 2);  // (+2 as xp_)
+                PFDR_HIP(hipMemcpyAsync(xpx_[k].p, xp_.p, sizeof(R2<real>) * (Vg_ + 2),
+                                        hipMemcpyDeviceToDevice, s));
+            }
             PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < sd_; k++) {
                 PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
                 PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
             }
@@ -705,7 +712,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     if (!seqdif_ || !reordered_) order_.release();  // inputs are in the internal labels now
     acc(where_.n * 4 + amp_orig_.n * sizeof(real) + order_.n * 4 + terms_.n * sizeof(real) + dws_.n);
     acc(route_.slice.n * sizeof(real) + route_.chain.ws.n + chain_.ws.n + ampg_.n * sizeof(real) +
-        xp2_.n * sizeof(R2<real>));
+        (xpx_[0].n + xpx_[1].n + xpx_[2].n) * sizeof(R2<real>));
     acc(sl_.n * 4 + wzp_.n * sizeof(real) + pidx_.n * 4 + (xpe_.n + gie_.n) * sizeof(R2<real>));
     // the chunk graph is part of the setup (instantiation costs ~0.1-1 ms,
     // which a small solve timed to tolerance would otherwise pay in its loop)
@@ -1435,10 +1442,11 @@ void QuadSession<real>::body_spec(int i, int n) {
     hipStream_t s = stream;
     const int t = it0_ + 1 + i;
     const Ctrl<real> *c = ctrl_.p;
-    if (i >= 2) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // the decision on t - 2
+    const int b = t % sd_;
+    if (i >= sd_) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // the decision on t - D
     xr_ = xpb(t - 1);
     xw_ = xpb(t);
-    real *terms = terms_.p + (t & 1) * 2 * tstride_, *part = vpart_.p + (t & 1) * 2 * nbv_;
+    real *terms = terms_.p + (long)b * 2 * tstride_, *part = vpart_.p + (long)b * 2 * nbv_;
     real *const keep = terms_.p, *const keepp = vpart_.p;
     terms_.p = terms;  // vargs() hands the sweep this iteration's terms
     vpart_.p = part;
@@ -1446,13 +1454,13 @@ void QuadSession<real>::body_spec(int i, int n) {
     terms_.p = keep;
     vpart_.p = keepp;
     xr_ = xw_ = xp_.p;
-    PFDR_HIP(hipEventRecord(evv_[t & 1], s));
-    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[t & 1], 0));
+    PFDR_HIP(hipEventRecord(evv_[b], s));
+    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[b], 0));
     seq_evolution(terms, part, evs_);  // overlaps the sweeps of t + 1
     k_decide<real><<<1, 64, 0, evs_>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipEventRecord(evd_[t & 1], evs_));
-    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // join: the chunk's last
+    PFDR_HIP(hipEventRecord(evd_[b], evs_));
+    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // join: the chunk's last
 }
 
 template <typename real>
@@ -1578,7 +1586,7 @@ void QuadSession<real>::plan_overlap() {
 // again after a reconditioning dropped them
 template <typename real>
 hipGraphExec_t QuadSession<real>::chunk_graph(int n) {
-    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);  // speculative: X buffers by parity
+    const int key = kSpecMax * n + (spec_ ? it0_ % sd_ : 0);  // speculative: X buffers by t mod D
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     hipGraph_t g = nullptr;
@@ -1608,7 +1616,7 @@ hipGraphExec_t QuadSession<real>::chunk_graph(int n) {
 template <typename real>
 void QuadSession<real>::run_bodies(int n) {
     it0_ = it_;
-    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);
+    const int key = kSpecMax * n + (spec_ ? it0_ % sd_ : 0);
     if (!prof.on && capturable_ && graphs_.count(key)) {
         PFDR_HIP(hipGraphLaunch(graphs_[key], stream));
         return;

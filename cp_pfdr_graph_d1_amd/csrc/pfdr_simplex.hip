@@ -1519,20 +1519,23 @@ class SimplexSession final : public SessionBase {
     std::unique_ptr<Transport> evtr_;
     Transport &etr() { return evtr_ ? *evtr_ : *halo_->tr; }
     void seq_evolution(real *terms, hipStream_t s);
-    // Speculative iteration (one GPU, sequential evolution, difRcd = 0, no
-    // objective record), as the quadratic session's spec_: the sum and the
-    // decision on iteration t run on evs_ beside the sweeps of t + 1, P and
-    // (P, step) are ping-ponged (iteration t reads Pb(t - 1), writes Pb(t)),
-    // the terms double-buffered; a stop at t leaves P_t in Pb(t) and the
-    // speculative t + 1 is discarded.
+    // Speculative iteration (sequential evolution, difRcd = 0, no objective
+    // record; one GPU or a partition), as the quadratic session's spec_: the
+    // sum and the decision on iteration t run on evs_ beside the sweeps of
+    // t + 1 ... t + D - 1 (depth D = sd_: 2, or 4 on three or more ranks), P
+    // and (P, step) cycle through D buffers (iteration t reads Pb(t - 1),
+    // writes Pb(t)), the terms through D; a stop at t leaves P_t in Pb(t) and
+    // the speculative iterations after it are discarded.
+    static constexpr int kSpecMax = 4;
     bool spec_ = false;
+    int sd_ = 2;
     int it0_ = 0;
-    DevBuf<real> P2_;
-    DevBuf<SxR2<real>> PF2_;
-    real *Pb(int t) { return spec_ && (t & 1) ? P2_.p : P_.p; }
-    SxR2<real> *PFb(int t) { return spec_ && (t & 1) ? PF2_.p : PF_.p; }
+    DevBuf<real> Px_[kSpecMax - 1];           // P buffers 1 .. D - 1 (0 is P_)
+    DevBuf<SxR2<real>> PFx_[kSpecMax - 1];    // (P, step) likewise
+    real *Pb(int t) { return spec_ && t % sd_ ? Px_[t % sd_ - 1].p : P_.p; }
+    SxR2<real> *PFb(int t) { return spec_ && t % sd_ ? PFx_[t % sd_ - 1].p : PF_.p; }
     hipStream_t evs_ = nullptr;
-    hipEvent_t evv_[2] = {}, evd_[2] = {};
+    hipEvent_t evv_[kSpecMax] = {}, evd_[kSpecMax] = {};
     // pipelined gated runs (QuadSession::run_pipelined): control-block
     // snapshots of two chunks in flight
     Ctrl<real> *snap_[2] = {};
@@ -1778,13 +1781,16 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         spec_ = difRcd_ == real(0) && !rec_obj_;
         if (spec_ && halo_) evtr_ = halo_->tr->split(s);  // (collective: every rank alike)
         if (spec_) {
-            DevBuf<real> t2(2 * (size_t)n);  // terms of both parities
+            sd_ = halo_ && halo_->tr->nranks >= 3 ? 4 : 2;
+            DevBuf<real> t2((size_t)sd_ * n);  // terms of D iterations
             std::swap(terms_.p, t2.p);
             std::swap(terms_.n, t2.n);
-            P2_.alloc((size_t)Vg_ * K_);
-            PF2_.alloc((size_t)Vg_ * K_);
+            for (int k = 0; k + 1 < sd_; k++) {
+                Px_[k].alloc((size_t)Vg_ * K_);
+                PFx_[k].alloc((size_t)Vg_ * K_);
+            }
             PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < sd_; k++) {
                 PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
                 PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
             }
@@ -1805,9 +1811,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
                             &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
-                            &Dif_, &terms_, &P2_, &route_.slice})
+                            &Dif_, &terms_, &Px_[0], &Px_[1], &Px_[2], &route_.slice})
         device_bytes += (int64_t)(b->n * sizeof(real));
-    device_bytes += (int64_t)((GI_.n + PF_.n + PF2_.n) * sizeof(SxR2<real>));
+    device_bytes += (int64_t)((GI_.n + PF_.n + PFx_[0].n + PFx_[1].n + PFx_[2].n) *
+                              sizeof(SxR2<real>));
 }
 
 // ref :64-370
@@ -1867,20 +1874,21 @@ template <typename real>
 void SimplexSession<real>::body_spec(int i, int n) {
     hipStream_t s = stream;
     const int t = it0_ + 1 + i;
-    if (i >= 2) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // the decision on t - 2
-    real *terms = terms_.p + (t & 1) * (terms_.n / 2);
+    const int b = t % sd_;
+    if (i >= sd_) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // the decision on t - D
+    real *terms = terms_.p + (long)b * (terms_.n / sd_);
     real *const keep = terms_.p;
     terms_.p = terms;
     sweeps(ctrl_.p, t);
     terms_.p = keep;
-    PFDR_HIP(hipEventRecord(evv_[t & 1], s));
-    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[t & 1], 0));
+    PFDR_HIP(hipEventRecord(evv_[b], s));
+    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[b], 0));
     seq_evolution(terms, evs_);  // overlaps the sweeps of t + 1
     k_sx_finalize<real><<<1, kBlock, 0, evs_>>>(0, nullptr, Vglob_, track_, ctrl_.p,
                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
     PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipEventRecord(evd_[t & 1], evs_));
-    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[t & 1], 0));  // join: the chunk's last
+    PFDR_HIP(hipEventRecord(evd_[b], evs_));
+    if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // join: the chunk's last
 }
 
 template <typename real>
@@ -2026,7 +2034,7 @@ void SimplexSession<real>::tiny_chunk(int n) {
 // at the end of the setup, and again after a reconditioning dropped it
 template <typename real>
 hipGraphExec_t SimplexSession<real>::chunk_graph(int n) {
-    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);  // speculative: P buffers by parity
+    const int key = kSpecMax * n + (spec_ ? it0_ % sd_ : 0);  // speculative: P buffers by t mod D
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     hipGraph_t g = nullptr;
@@ -2053,7 +2061,7 @@ hipGraphExec_t SimplexSession<real>::chunk_graph(int n) {
 template <typename real>
 void SimplexSession<real>::run_bodies(int n) {
     it0_ = it_;
-    const int key = 2 * n + (spec_ ? (it0_ & 1) : 0);
+    const int key = kSpecMax * n + (spec_ ? it0_ % sd_ : 0);
     if (!prof.on && capturable_ && graphs_.count(key)) {  // prepared (or whole) chunk
         PFDR_HIP(hipGraphLaunch(graphs_[key], stream));
         return;
