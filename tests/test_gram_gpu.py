@@ -24,8 +24,10 @@ def _mat(M, N, seed, dt):
 # (64, 3000) / (96, 4096) with which = 0: hundreds of output tiles and one
 # contraction chunk -- every XCD takes an eighth of the tiles (gram_block),
 # ragged (300 tiles over 8 x 38 slots) and even (528 over 8 x 66)
+# (256, 1024), (384, 4096): whole 128-wide tiles, one and many contraction
+# chunks
 @pytest.mark.parametrize("shape", [(100, 37), (333, 129), (64, 300), (1000, 257), (20000, 96),
-                                   (64, 3000), (96, 4096)])
+                                   (64, 3000), (96, 4096), (256, 1024), (384, 4096)])
 @pytest.mark.parametrize("which", [0, 1])
 def test_gram_matches_numpy(gpu_lib, dt, shape, which):
     A = _mat(*shape, seed=sum(shape) + which, dt=dt)
@@ -37,6 +39,19 @@ def test_gram_matches_numpy(gpu_lib, dt, shape, which):
     assert G.shape == ref.shape
     assert np.array_equal(G, G.T)
     assert err <= (2e-6 if dt == np.float32 else 1e-13)
+
+
+def test_gram_short_last_chunk(gpu_lib):
+    """A A^t of a 2048 x 20000 f32 A: 16 contraction chunks of 1280, the
+    last one 800 long (20000 = 15 x 1280 + 800)"""
+    A = _mat(2048, 20000, seed=7, dt=np.float32)
+    G, ms = pfdr.gram(A, 1)
+    A64 = A.astype(np.float64)
+    ref = A64 @ A64.T
+    err = np.linalg.norm(G - ref) / np.linalg.norm(ref)
+    print("gram 2048 x 20000 err=%.2e %.3f ms" % (err, ms))
+    assert np.array_equal(G, G.T)
+    assert err <= 2e-6
 
 
 def _spectral(M, N, s, seed, dt):
