@@ -2297,8 +2297,15 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     __shared__ real red[2][kBlock / kWave];
     __shared__ int scan[3 * kTileRuns + kBlock / kWave];  // block scan (split_sum) / run table
                                                          // and degree totals (tile_sum)
+    // the logical blocks LAST to first: the edge sweep before this one walked
+    // its tiles first to last, so the contributions it wrote last are the
+    // ones still in the 256 MB Infinity Cache when this sweep starts, and the
+    // blocks this sweep ends on are the ones the next edge sweep starts with
+    // (headline: vertex sweep 0.180 -> 0.167 ms, edge sweep 0.283 -> 0.277;
+    // C2 0.482 -> 0.468 ms/iter, r6a / r6c)
     int lb = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (lb >= a.nb) return;
+    lb = a.nb - 1 - lb;
     if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB, ZD>(a, a.bbeg + lb, lds, red, scan, halt);
 }
