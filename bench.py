@@ -420,8 +420,9 @@ def main():
         knames["edge_sweep"] = ["k_edge_sweep_tl"]
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
-    if not quad and getattr(wl, "K", 0) > 64:  # one wave per vertex
-        knames["sx_vertex_sweep"] = ["k_sx_vertex_wide"]
+    if not quad and getattr(wl, "K", 0) > 64:  # group sweep (LDS columns), or a wave per vertex
+        knames["sx_vertex_sweep"] = ["k_sx_vertex_group", "k_sx_vertex_wide"]
+        knames["sx_vertex_wide"] = ["k_sx_vertex_group", "k_sx_vertex_wide"]
     sess.close()
     if comm:
         from cp_pfdr_graph_d1_amd import partition
@@ -445,11 +446,14 @@ def main():
         # replaces.  The layout moves fewer (Z-direct: no W*Z stores), so that
         # figure can pass 1; frac is the kernel's own measured HBM bytes (PMC,
         # when a summary taken on these sources exists) over time and peak.
-        row = {"kernel": "+".join(knames[fam]), "algorithmic_bytes": int(alg_b),
+        # the family's kernels that ran in the profiled pass (a K > 64
+        # simplex runs the group sweep or, past the LDS, the wide one)
+        ks = [k for k in knames[fam] if pmc is None or k in pmc] or knames[fam]
+        row = {"kernel": "+".join(ks), "algorithmic_bytes": int(alg_b),
                "mean_ms": round(ms, 5), "effective_GBps": round(gbs, 1),
                "effective_frac": round(gbs / HBM_PEAK_GBS, 4)}
-        if pmc is not None and all(k in pmc for k in knames[fam]):
-            t = sum(pmc[k]["hbm_bytes_per_launch"] for k in knames[fam])
+        if pmc is not None and all(k in pmc for k in ks):
+            t = sum(pmc[k]["hbm_bytes_per_launch"] for k in ks)
             row["pmc_bytes"] = int(t)
             row["pmc_over_algorithmic"] = round(t / alg_b, 3)
             row["achieved_GBps"] = round(t / (ms * 1e-3) / 1e9, 1)
