@@ -15,6 +15,10 @@
 //     computed, the epilogue mirrors it; the contraction is split into
 //     chunks (deterministic second pass) so that a 1024-wide Gram over two
 //     million columns still fills the 256 CUs.
+//   * f32 A^t A on the bf16 matrix cores (k_gram_b): each element split
+//     exactly into three bf16 pieces, six piece products per f32 product,
+//     f32 accumulation -- f32 accuracy at up to 2.7x the f32 MFMA rate per
+//     flop (PFDR_GRAM_SPLIT selects, see gram()).
 //   * the power method runs all starts at once: X is S-by-B, one apply is
 //     a skinny product (HBM-bound: each pass streams the matrix once for
 //     all B starts); each start keeps the reference's stopping rule
@@ -309,6 +313,238 @@ __global__ __launch_bounds__(64 * WG) void k_gram_v(int P, long K, const real *_
 }
 
 
+// f32 Gram on the bf16 matrix cores, f32-accurate: every element is split
+// exactly into three bf16 pieces, x = h + m + l (h = x rounded to 8
+// significant bits, m the same of x - h, l = x - h - m: no bits lost), and
+// a product x y is formed from the six pieces whose weight reaches 2^-16 of
+// it (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16, accumulated in
+// f32; the pieces left out (ml, lm, ll) weigh <= 2^-24 of each product,
+// below the f32 rounding of the sum.  Six bf16 MFMAs of 16 k do the work of
+// eight f32 ones of 2 k at a sixteenth of the rate per flop: 2.7x the f32
+// matrix-core throughput.  Same blocks, tiles and chunks
+// as k_gram_v; the staging splits each element once, into three bf16
+// planes [row][k] (rows of BK + 8: 16-byte fragment reads conflict-free).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+    unsigned u = __builtin_bit_cast(unsigned, x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bf16_val(unsigned short h) {
+    return __builtin_bit_cast(float, (unsigned)h << 16);
+}
+template <int LAYOUT, int BK, bool VEC>
+__device__ __forceinline__ void gram_b_body(int P, long K, const float *__restrict__ A, long ld,
+                                            long kchunk, int nchunk, float *__restrict__ Gpart) {
+    using M = Mfma<float>;
+    constexpr int BT = 128, T = 32, RS = BK + 8, PL = BT * RS, NK = BK / 2;
+    static_assert(BK == 16 || BK == 32, "slices of one or two 16-k MFMA steps");
+    int bi, bj, z;
+    if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
+    const long k0 = (long)z * kchunk;
+    const long k1 = min(K, k0 + kchunk);
+    float *G = Gpart + (size_t)z * P * P;
+    // [side][piece][row][RS] bf16; the epilogue's tiles reuse it
+    __shared__ alignas(16) unsigned short sm[2 * 3 * PL];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wi = w & 1, wj = w >> 1;
+    const long i0 = (long)bi * BT, j0 = (long)bj * BT;
+    M::acc_t acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) acc[a][b][r] = 0.f;
+    // staging: lane t holds row ri of both sides, k = kg NK ... kg NK + NK - 1
+    const int ri = t & (BT - 1), kg = t >> 7;
+    float st[2][NK];
+    const int ld32 = (int)ld;  // (gram() checks 16 ld + 128 < 2^31)
+    auto load = [&](long kb) {
+        const long kk = kb + kg * NK;
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const long rb0 = side ? j0 : i0, row = rb0 + ri;
+            const bool rin = row < P;
+            if (LAYOUT == GRAM_NT && VEC) {
+                // rows 2 rp, 2 rp + 1 (one 8-byte load per k), k = kq4 ... kq4
+                // + BK / 4 - 1: st[side][2 q + r] = (row 2 rp + r, k kq4 + q);
+                // a wave-uniform base and 32-bit lane offsets, out-of-range
+                // elements from a clamped in-range address, zeroed
+                const float *base = A + rb0 + kb * ld;
+                const int rp = t & 63, kq4 = (t >> 6) * (BK / 4);
+                const int kl = (int)(k1 - kb) - 1;  // last k of the chunk, from kb
+                const bool whole = rb0 + BT <= P && kb + BK <= k1;  // block-uniform
+#pragma unroll
+                for (int q = 0; q < BK / 4; q++) {
+                    const int kq = min(kq4 + q, kl);
+                    const int r2 = whole ? 2 * rp : min(2 * rp, (int)(P - rb0) - 2);
+                    if (whole || (rb0 + 2 * rp + 1 < P && kq4 + q <= kl)) {
+                        const Pk<float, 2> v = ldv<float, 2>(base + r2 + kq * ld32);
+                        st[side][2 * q] = v.v[0];
+                        st[side][2 * q + 1] = v.v[1];
+                    } else {
+                        st[side][2 * q] = (rb0 + 2 * rp < P && kq4 + q <= kl) ? base[2 * rp + kq * ld32] : 0.f;
+                        st[side][2 * q + 1] = 0.f;
+                    }
+                }
+            } else if (LAYOUT == GRAM_NT) {
+                const float *base = A + rb0 + kb * ld;
+                const int rc = (int)min(row, (long)P - 1) - (int)rb0;
+                const int kl = (int)(k1 - kb) - 1;
+#pragma unroll
+                for (int q = 0; q < NK; q++) {
+                    const int kq = kg * NK + q;
+                    const float v = base[rc + min(kq, kl) * ld32];
+                    st[side][q] = (rin && kq <= kl) ? v : 0.f;
+                }
+            } else if (VEC && rin && kk + NK <= k1) {
+#pragma unroll
+                for (int q = 0; q < NK / 4; q++) {
+                    const Pk<float, 4> v = ldv<float, 4>(A + kk + 4 * q + row * ld);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) st[side][4 * q + u] = v.v[u];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NK; q++)
+                    st[side][q] = (rin && kk + q < k1) ? gram_elem<float, LAYOUT>(A, ld, row, kk + q) : 0.f;
+            }
+        }
+    };
+    auto store = [&]() {
+        if (LAYOUT == GRAM_NT && VEC) {  // two rows of BK / 4 k per lane
+            typedef unsigned short u16xq __attribute__((ext_vector_type(BK / 4)));
+            const int rp = t & 63, kq4 = (t >> 6) * (BK / 4);
+#pragma unroll
+            for (int side = 0; side < 2; side++)
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    u16xq ph, pm, pl;
+#pragma unroll
+                    for (int q = 0; q < BK / 4; q++) {
+                        const float x = st[side][2 * q + r];
+                        const unsigned short h = bf16_rne(x);
+                        const float r1 = x - bf16_val(h);
+                        const unsigned short m = bf16_rne(r1);
+                        ph[q] = h;
+                        pm[q] = m;
+                        pl[q] = bf16_rne(r1 - bf16_val(m));
+                    }
+                    unsigned short *d = sm + side * 3 * PL + (2 * rp + r) * RS + kq4;
+                    *reinterpret_cast<u16xq *>(d) = ph;
+                    *reinterpret_cast<u16xq *>(d + PL) = pm;
+                    *reinterpret_cast<u16xq *>(d + 2 * PL) = pl;
+                }
+            return;
+        }
+#pragma unroll
+        for (int side = 0; side < 2; side++)
+#pragma unroll
+            for (int c = 0; c < NK / 8; c++) {
+                u16x8 ph, pm, pl;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float x = st[side][8 * c + u];
+                    const unsigned short h = bf16_rne(x);
+                    const float r1 = x - bf16_val(h);
+                    const unsigned short m = bf16_rne(r1);
+                    ph[u] = h;
+                    pm[u] = m;
+                    pl[u] = bf16_rne(r1 - bf16_val(m));
+                }
+                unsigned short *d = sm + side * 3 * PL + ri * RS + kg * NK + 8 * c;
+                *reinterpret_cast<u16x8 *>(d) = ph;
+                *reinterpret_cast<u16x8 *>(d + PL) = pm;
+                *reinterpret_cast<u16x8 *>(d + 2 * PL) = pl;
+            }
+    };
+    auto frag = [&](int side, int piece, int row, int ks) {
+        return *reinterpret_cast<const bf16x8 *>(sm + (side * 3 + piece) * PL + row * RS + 16 * ks +
+                                                 8 * (lane >> 5));
+    };
+    const int ra = wi * 64 + (lane & 31), rb = wj * 64 + (lane & 31);
+    if (k0 < k1) load(k0);
+    for (long kb = k0; kb < k1; kb += BK) {
+        store();
+        __syncthreads();
+        if (kb + BK < k1) load(kb + BK);  // in flight during the MFMAs below
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ks++) {
+            bf16x8 ah[2], bh[2], am[2], bm[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                ah[q] = frag(0, 0, ra + 32 * q, ks);
+                bh[q] = frag(1, 0, rb + 32 * q, ks);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                am[q] = frag(0, 1, ra + 32 * q, ks);
+                bm[q] = frag(1, 1, rb + 32 * q, ks);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++) {
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bm[y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[x], bh[y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[x], bm[y], acc[x][y], 0, 0, 0);
+                }
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                am[q] = frag(0, 2, ra + 32 * q, ks);  // the l pieces
+                bm[q] = frag(1, 2, rb + 32 * q, ks);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++) {
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bm[y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[x], bh[y], acc[x][y], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    // epilogue as k_gram_v's, its tiles in the staging array
+    float(*O)[T + 1] = reinterpret_cast<float(*)[T + 1]>(reinterpret_cast<float *>(sm) + w * T * (T + 1));
+    const int li = lane % T, lj = lane / T;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) {
+            const long ib = i0 + wi * 64 + x * T, jb = j0 + wj * 64 + y * T;
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) O[M::row(lane, r)][M::col(lane, r)] = acc[x][y][r];
+            __syncthreads();
+            // the pieces' cross products (hm, mh) are added in row-column
+            // order, so G(i, j) and G(j, i) of a diagonal block may round
+            // apart: there the upper triangle is written and mirrored
+            const bool diag = bi == bj;
+            for (int j = lj; j < T; j += 2)
+                if (ib + li < P && jb + j < P && (!diag || ib + li <= jb + j))
+                    G[(ib + li) + (jb + j) * P] = O[li][j];
+            for (int i = lj; i < T; i += 2)
+                if (jb + li < P && ib + i < P && (!diag || ib + i < jb + li))
+                    G[(jb + li) + (ib + i) * P] = O[i][li];
+            __syncthreads();
+        }
+}
+
+// four blocks per CU (LDS 36 KB, <= 128 registers; loading two slices
+// ahead needs three waves per SIMD and measured slower: C3 26.7 vs 21.6 ms)
+template <int LAYOUT, int BK, bool VEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_b(
+    int P, long K, const float *__restrict__ A, long ld, long kchunk, int nchunk,
+    float *__restrict__ Gpart) {
+    gram_b_body<LAYOUT, BK, VEC>(P, K, A, ld, kchunk, nchunk, Gpart);
+}
+
 // G = sum of the chunk partials, in chunk order
 template <typename real>
 __global__ void k_gram_sum(long PP, int nchunk, const real *__restrict__ part,
@@ -346,7 +582,27 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     const long nblk = gram_slots(nb, nchunk);  // see gram_block
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
-    if (vec) {
+    // f32: A^t A (TN) on the bf16 matrix cores (k_gram_b: C3-like A^t A
+    // 9.1 vs 11.0 ms); A A^t (NT) stays on the exact-f32 tile, which the
+    // split tile only ties on C3 (21.0-21.6 vs 20.7-21.1 ms).
+    // PFDR_GRAM_SPLIT: 0 = never split, 2 = both layouts
+    static const int split = [] {
+        const char *e = getenv("PFDR_GRAM_SPLIT");
+        return e ? atoi(e) : 1;
+    }();
+    if (sizeof(real) == 4 && (split == 2 || (split == 1 && which == 0)) &&
+        16 * ld + 128 < 0x7fffffffL) {
+        const float *Af = reinterpret_cast<const float *>(A);
+        float *of = reinterpret_cast<float *>(out);
+        constexpr int BKS = 16;  // (BK = 32: 61 KB of LDS, two blocks per CU, slower)
+        if (which == 0) {
+            if (vec) k_gram_b<GRAM_TN, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+            else k_gram_b<GRAM_TN, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+        } else {
+            if (vec) k_gram_b<GRAM_NT, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+            else k_gram_b<GRAM_NT, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+        }
+    } else if (vec) {
         if (which == 0)
             k_gram_v<real, GRAM_TN><<<grid, 64 * kGramWaves, 0, s>>>(P, K, A, ld, kchunk,
                                                                     (int)nchunk, out);
