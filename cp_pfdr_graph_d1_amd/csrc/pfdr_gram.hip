@@ -15,10 +15,10 @@
 //     computed, the epilogue mirrors it; the contraction is split into
 //     chunks (deterministic second pass) so that a 1024-wide Gram over two
 //     million columns still fills the 256 CUs.
-//   * f32 A^t A on the bf16 matrix cores (k_gram_b): each element split
-//     exactly into three bf16 pieces, six piece products per f32 product,
-//     f32 accumulation -- f32 accuracy at up to 2.7x the f32 MFMA rate per
-//     flop (PFDR_GRAM_SPLIT selects, see gram()).
+//   * f32 on the bf16 matrix cores (k_gram_b): each element split exactly
+//     into three bf16 pieces, six piece products per f32 product, f32
+//     accumulation -- f32 accuracy at up to 2.7x the f32 MFMA rate per flop
+//     (PFDR_GRAM_SPLIT=0: the exact-f32 tile k_gram_v).
 //   * the power method runs all starts at once: X is S-by-B, one apply is
 //     a skinny product (HBM-bound: each pass streams the matrix once for
 //     all B starts); each start keeps the reference's stopping rule
@@ -334,11 +334,12 @@ __device__ __forceinline__ unsigned short bf16_rne(float x) {
 __device__ __forceinline__ float bf16_val(unsigned short h) {
     return __builtin_bit_cast(float, (unsigned)h << 16);
 }
-template <int LAYOUT, int BK, bool VEC>
+template <int LAYOUT, int BK, bool VEC, int RW>
 __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restrict__ A, long ld,
                                             long kchunk, int nchunk, float *__restrict__ Gpart) {
     using M = Mfma<float>;
     constexpr int BT = 128, T = 32, RS = BK + 8, PL = BT * RS, NK = BK / 2;
+    constexpr int KQ = BK / (2 * RW);  // NT staging: k per lane (RW rows each)
     static_assert(BK == 16 || BK == 32, "slices of one or two 16-k MFMA steps");
     int bi, bj, z;
     if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
@@ -368,25 +369,26 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
             const long rb0 = side ? j0 : i0, row = rb0 + ri;
             const bool rin = row < P;
             if (LAYOUT == GRAM_NT && VEC) {
-                // rows 2 rp, 2 rp + 1 (one 8-byte load per k), k = kq4 ... kq4
-                // + BK / 4 - 1: st[side][2 q + r] = (row 2 rp + r, k kq4 + q);
-                // a wave-uniform base and 32-bit lane offsets, out-of-range
-                // elements from a clamped in-range address, zeroed
+                // rows RW rp ... RW rp + RW - 1 (one RW-wide load per k), k =
+                // kq ... kq + KQ - 1: st[side][RW q + r] = (row RW rp + r, k
+                // kq + q); a wave-uniform base and 32-bit lane offsets,
+                // out-of-range elements from a clamped address, zeroed
                 const float *base = A + rb0 + kb * ld;
-                const int rp = t & 63, kq4 = (t >> 6) * (BK / 4);
+                const int rp = t % (BT / RW), kq = (t / (BT / RW)) * KQ;
                 const int kl = (int)(k1 - kb) - 1;  // last k of the chunk, from kb
                 const bool whole = rb0 + BT <= P && kb + BK <= k1;  // block-uniform
 #pragma unroll
-                for (int q = 0; q < BK / 4; q++) {
-                    const int kq = min(kq4 + q, kl);
-                    const int r2 = whole ? 2 * rp : min(2 * rp, (int)(P - rb0) - 2);
-                    if (whole || (rb0 + 2 * rp + 1 < P && kq4 + q <= kl)) {
-                        const Pk<float, 2> v = ldv<float, 2>(base + r2 + kq * ld32);
-                        st[side][2 * q] = v.v[0];
-                        st[side][2 * q + 1] = v.v[1];
+                for (int q = 0; q < KQ; q++) {
+                    const int kc = min(kq + q, kl);
+                    if (whole || (rb0 + RW * rp + RW - 1 < P && kq + q <= kl)) {
+                        const Pk<float, RW> v = ldv<float, RW>(base + RW * rp + kc * ld32);
+#pragma unroll
+                        for (int r = 0; r < RW; r++) st[side][RW * q + r] = v.v[r];
                     } else {
-                        st[side][2 * q] = (rb0 + 2 * rp < P && kq4 + q <= kl) ? base[2 * rp + kq * ld32] : 0.f;
-                        st[side][2 * q + 1] = 0.f;
+#pragma unroll
+                        for (int r = 0; r < RW; r++)
+                            st[side][RW * q + r] = (rb0 + RW * rp + r < P && kq + q <= kl)
+                                                       ? base[RW * rp + r + kc * ld32] : 0.f;
                     }
                 }
             } else if (LAYOUT == GRAM_NT) {
@@ -414,17 +416,17 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
         }
     };
     auto store = [&]() {
-        if (LAYOUT == GRAM_NT && VEC) {  // two rows of BK / 4 k per lane
-            typedef unsigned short u16xq __attribute__((ext_vector_type(BK / 4)));
-            const int rp = t & 63, kq4 = (t >> 6) * (BK / 4);
+        if (LAYOUT == GRAM_NT && VEC) {  // RW rows of KQ k per lane
+            typedef unsigned short u16xq __attribute__((ext_vector_type(KQ)));
+            const int rp = t % (BT / RW), kq = (t / (BT / RW)) * KQ;
 #pragma unroll
             for (int side = 0; side < 2; side++)
 #pragma unroll
-                for (int r = 0; r < 2; r++) {
+                for (int r = 0; r < RW; r++) {
                     u16xq ph, pm, pl;
 #pragma unroll
-                    for (int q = 0; q < BK / 4; q++) {
-                        const float x = st[side][2 * q + r];
+                    for (int q = 0; q < KQ; q++) {
+                        const float x = st[side][RW * q + r];
                         const unsigned short h = bf16_rne(x);
                         const float r1 = x - bf16_val(h);
                         const unsigned short m = bf16_rne(r1);
@@ -432,7 +434,7 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
                         pm[q] = m;
                         pl[q] = bf16_rne(r1 - bf16_val(m));
                     }
-                    unsigned short *d = sm + side * 3 * PL + (2 * rp + r) * RS + kq4;
+                    unsigned short *d = sm + side * 3 * PL + (RW * rp + r) * RS + kq;
                     *reinterpret_cast<u16xq *>(d) = ph;
                     *reinterpret_cast<u16xq *>(d + PL) = pm;
                     *reinterpret_cast<u16xq *>(d + 2 * PL) = pl;
@@ -538,11 +540,11 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
 
 // four blocks per CU (LDS 36 KB, <= 128 registers; loading two slices
 // ahead needs three waves per SIMD and measured slower: C3 26.7 vs 21.6 ms)
-template <int LAYOUT, int BK, bool VEC>
+template <int LAYOUT, int BK, bool VEC, int RW = 2>  // (RW = 4: C3 28.4 ms)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_b(
     int P, long K, const float *__restrict__ A, long ld, long kchunk, int nchunk,
     float *__restrict__ Gpart) {
-    gram_b_body<LAYOUT, BK, VEC>(P, K, A, ld, kchunk, nchunk, Gpart);
+    gram_b_body<LAYOUT, BK, VEC, RW>(P, K, A, ld, kchunk, nchunk, Gpart);
 }
 
 // G = sum of the chunk partials, in chunk order
@@ -582,16 +584,14 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     const long nblk = gram_slots(nb, nchunk);  // see gram_block
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
-    // f32: A^t A (TN) on the bf16 matrix cores (k_gram_b: C3-like A^t A
-    // 9.1 vs 11.0 ms); A A^t (NT) stays on the exact-f32 tile, which the
-    // split tile only ties on C3 (21.0-21.6 vs 20.7-21.1 ms).
-    // PFDR_GRAM_SPLIT: 0 = never split, 2 = both layouts
-    static const int split = [] {
+    // f32 on the bf16 matrix cores (k_gram_b; paired on one box: c3_ata's
+    // A^t A 9.1 vs 11.0 ms, C3's A A^t 19.7 vs 21.1 ms); PFDR_GRAM_SPLIT=0
+    // keeps the exact-f32 tile (k_gram_v)
+    static const bool split = [] {
         const char *e = getenv("PFDR_GRAM_SPLIT");
-        return e ? atoi(e) : 1;
+        return !(e && e[0] == '0');
     }();
-    if (sizeof(real) == 4 && (split == 2 || (split == 1 && which == 0)) &&
-        16 * ld + 128 < 0x7fffffffL) {
+    if (sizeof(real) == 4 && split && 16 * ld + 128 < 0x7fffffffL) {
         const float *Af = reinterpret_cast<const float *>(A);
         float *of = reinterpret_cast<float *>(out);
         constexpr int BKS = 16;  // (BK = 32: 61 KB of LDS, two blocks per CU, slower)
