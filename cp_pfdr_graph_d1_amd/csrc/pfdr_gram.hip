@@ -567,7 +567,17 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     // 16-byte operand loads when the layout allows (k_gram_v), else k_gram
     const bool vec = (ld % (16 / sizeof(real))) == 0 && ((uintptr_t)A % 16) == 0;
     const int BT = M::BT, BK = M::BK;
-    const long target = 2048;  // blocks to aim for
+    // f32 on the bf16 matrix cores (k_gram_b; paired on one box: c3_ata's
+    // A^t A 9.1 vs 11.0 ms, C3's A A^t 19.7 vs 21.1 ms); PFDR_GRAM_SPLIT=0
+    // keeps the exact-f32 tile (k_gram_v)
+    static const bool split_on = [] {
+        const char *e = getenv("PFDR_GRAM_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    const bool split = sizeof(real) == 4 && split_on && 16 * ld + 128 < 0x7fffffffL;
+    // blocks to aim for: the split tile's shorter blocks want more of them
+    // (C3: 128 chunks 19.2-19.4 ms against 64 chunks' 19.9-20.0, r6n)
+    const long target = split ? 4096 : 2048;
     const int nb = (P + BT - 1) / BT;
     const long tiles = (long)nb * (nb + 1) / 2;
     long nchunk = std::max(1L, std::min((target + tiles - 1) / tiles, (K + 4 * BK - 1) / (4 * BK)));
@@ -584,14 +594,7 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     const long nblk = gram_slots(nb, nchunk);  // see gram_block
     if (nblk > 0x7fffffffL) throw std::runtime_error("gram: grid too large");
     const dim3 grid((unsigned)nblk);
-    // f32 on the bf16 matrix cores (k_gram_b; paired on one box: c3_ata's
-    // A^t A 9.1 vs 11.0 ms, C3's A A^t 19.7 vs 21.1 ms); PFDR_GRAM_SPLIT=0
-    // keeps the exact-f32 tile (k_gram_v)
-    static const bool split = [] {
-        const char *e = getenv("PFDR_GRAM_SPLIT");
-        return !(e && e[0] == '0');
-    }();
-    if (sizeof(real) == 4 && split && 16 * ld + 128 < 0x7fffffffL) {
+    if (split) {
         const float *Af = reinterpret_cast<const float *>(A);
         float *of = reinterpret_cast<float *>(out);
         constexpr int BKS = 16;  // (BK = 32: 61 KB of LDS, two blocks per CU, slower)
