@@ -326,6 +326,7 @@ __global__ __launch_bounds__(64 * WG) void k_gram_v(int P, long K, const real *_
 // planes [row][k] (rows of BK + 8: 16-byte fragment reads conflict-free).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float x) {
     unsigned u = __builtin_bit_cast(unsigned, x);
     u += 0x7fffu + ((u >> 16) & 1u);
@@ -338,8 +339,17 @@ template <int LAYOUT, int BK, bool VEC, int RW>
 __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restrict__ A, long ld,
                                             long kchunk, int nchunk, float *__restrict__ Gpart) {
     using M = Mfma<float>;
-    constexpr int BT = 128, T = 32, RS = BK + 8, PL = BT * RS, NK = BK / 2;
+    constexpr int BT = 128, T = 32, RS = BK + 8, NK = BK / 2;
     constexpr int KQ = BK / (2 * RW);  // NT staging: k per lane (RW rows each)
+    // piece planes: [row][k] (rows of RS) -- or, for NT staged from row
+    // loads, [k][row] (rows of RK = 160: the 4 k rows a transposed read
+    // gathers sit 80 dwords apart, on distinct banks) read back with
+    // ds_read_b64_tr_b16: a wave's staging writes are then 256 contiguous
+    // bytes, where [row][k] put them 48 B apart on a quarter of the banks
+    // (SQ_LDS_BANK_CONFLICT 2.6e9 cycles on C3, r6q)
+    constexpr bool KI = LAYOUT == GRAM_NT && VEC && RW == 2;
+    constexpr int RK = 160;
+    constexpr int PL = KI ? BK * RK : BT * RS;
     static_assert(BK == 16 || BK == 32, "slices of one or two 16-k MFMA steps");
     int bi, bj, z;
     if (!gram_block((P + BT - 1) / BT, nchunk, bi, bj, z)) return;
@@ -416,6 +426,31 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
         }
     };
     auto store = [&]() {
+        if (KI) {  // rows 2 rp, 2 rp + 1 at each of the lane's KQ k: 4 B per piece
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            const int rp = t % (BT / RW), kq = (t / (BT / RW)) * KQ;
+#pragma unroll
+            for (int side = 0; side < 2; side++)
+#pragma unroll
+                for (int q = 0; q < KQ; q++) {
+                    u16x2 ph, pm, pl;
+#pragma unroll
+                    for (int r = 0; r < 2; r++) {
+                        const float x = st[side][2 * q + r];
+                        const unsigned short h = bf16_rne(x);
+                        const float r1 = x - bf16_val(h);
+                        const unsigned short m = bf16_rne(r1);
+                        ph[r] = h;
+                        pm[r] = m;
+                        pl[r] = bf16_rne(r1 - bf16_val(m));
+                    }
+                    unsigned short *d = sm + side * 3 * PL + (kq + q) * RK + 2 * rp;
+                    *reinterpret_cast<u16x2 *>(d) = ph;
+                    *reinterpret_cast<u16x2 *>(d + PL) = pm;
+                    *reinterpret_cast<u16x2 *>(d + 2 * PL) = pl;
+                }
+            return;
+        }
         if (LAYOUT == GRAM_NT && VEC) {  // RW rows of KQ k per lane
             typedef unsigned short u16xq __attribute__((ext_vector_type(KQ)));
             const int rp = t % (BT / RW), kq = (t / (BT / RW)) * KQ;
@@ -462,11 +497,28 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
                 *reinterpret_cast<u16x8 *>(d + 2 * PL) = pl;
             }
     };
-    auto frag = [&](int side, int piece, int row, int ks) {
-        return *reinterpret_cast<const bf16x8 *>(sm + (side * 3 + piece) * PL + row * RS + 16 * ks +
-                                                 8 * (lane >> 5));
+    // the 32x32x16 operand of rows tb ... tb + 31: lane l holds row tb + (l
+    // & 31), k = 16 ks + 8 (l >> 5) ... + 7
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    auto frag = [&](int side, int piece, int tb, int ks) {
+        const unsigned short *pl = sm + (side * 3 + piece) * PL;
+        if constexpr (KI) {
+            // two transposed reads of 4 k rows each: in lane group g = l >>
+            // 4, lane 4 q + p names k row 16 ks + 8 (g >> 1) + q (+ 4) at
+            // columns tb + 16 (g & 1) + 4 p ...; lane i of the group gets
+            // column tb + 16 (g & 1) + i of the 4 rows
+            const int g = lane >> 4, li = lane & 15;
+            const unsigned short *a = pl + (16 * ks + 8 * (g >> 1) + (li >> 2)) * RK + tb +
+                                      16 * (g & 1) + 4 * (li & 3);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)a);
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a + 4 * RK));
+            return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        } else {
+            return *reinterpret_cast<const bf16x8 *>(pl + (tb + (lane & 31)) * RS + 16 * ks +
+                                                     8 * (lane >> 5));
+        }
     };
-    const int ra = wi * 64 + (lane & 31), rb = wj * 64 + (lane & 31);
+    const int ra = wi * 64, rb = wj * 64;
     if (k0 < k1) load(k0);
     for (long kb = k0; kb < k1; kb += BK) {
         store();
