@@ -335,19 +335,19 @@ __device__ __forceinline__ unsigned short bf16_rne(float x) {
 __device__ __forceinline__ float bf16_val(unsigned short h) {
     return __builtin_bit_cast(float, (unsigned)h << 16);
 }
-template <int LAYOUT, int BK, bool VEC, int RW>
+template <int LAYOUT, int BK, bool VEC>
 __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restrict__ A, long ld,
                                             long kchunk, int nchunk, float *__restrict__ Gpart) {
     using M = Mfma<float>;
     constexpr int BT = 128, T = 32, RS = BK + 8, NK = BK / 2;
-    constexpr int KQ = BK / (2 * RW);  // NT staging: k per lane (RW rows each)
+    constexpr int RW = 2, KQ = BK / (2 * RW);  // NT staging: RW rows of KQ k per lane
     // piece planes: [row][k] (rows of RS) -- or, for NT staged from row
     // loads, [k][row] (rows of RK = 160: the 4 k rows a transposed read
     // gathers sit 80 dwords apart, on distinct banks) read back with
     // ds_read_b64_tr_b16: a wave's staging writes are then 256 contiguous
     // bytes, where [row][k] put them 48 B apart on a quarter of the banks
     // (SQ_LDS_BANK_CONFLICT 2.6e9 cycles on C3, r6q)
-    constexpr bool KI = LAYOUT == GRAM_NT && VEC && RW == 2;
+    constexpr bool KI = LAYOUT == GRAM_NT && VEC;
     constexpr int RK = 160;
     constexpr int PL = KI ? BK * RK : BT * RS;
     static_assert(BK == 16 || BK == 32, "slices of one or two 16-k MFMA steps");
@@ -448,31 +448,6 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
                     *reinterpret_cast<u16x2 *>(d) = ph;
                     *reinterpret_cast<u16x2 *>(d + PL) = pm;
                     *reinterpret_cast<u16x2 *>(d + 2 * PL) = pl;
-                }
-            return;
-        }
-        if (LAYOUT == GRAM_NT && VEC) {  // RW rows of KQ k per lane
-            typedef unsigned short u16xq __attribute__((ext_vector_type(KQ)));
-            const int rp = t % (BT / RW), kq = (t / (BT / RW)) * KQ;
-#pragma unroll
-            for (int side = 0; side < 2; side++)
-#pragma unroll
-                for (int r = 0; r < RW; r++) {
-                    u16xq ph, pm, pl;
-#pragma unroll
-                    for (int q = 0; q < KQ; q++) {
-                        const float x = st[side][RW * q + r];
-                        const unsigned short h = bf16_rne(x);
-                        const float r1 = x - bf16_val(h);
-                        const unsigned short m = bf16_rne(r1);
-                        ph[q] = h;
-                        pm[q] = m;
-                        pl[q] = bf16_rne(r1 - bf16_val(m));
-                    }
-                    unsigned short *d = sm + side * 3 * PL + (RW * rp + r) * RS + kq;
-                    *reinterpret_cast<u16xq *>(d) = ph;
-                    *reinterpret_cast<u16xq *>(d + PL) = pm;
-                    *reinterpret_cast<u16xq *>(d + 2 * PL) = pl;
                 }
             return;
         }
@@ -592,11 +567,11 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
 
 // four blocks per CU (LDS 36 KB, <= 128 registers; loading two slices
 // ahead needs three waves per SIMD and measured slower: C3 26.7 vs 21.6 ms)
-template <int LAYOUT, int BK, bool VEC, int RW = 2>  // (RW = 4: C3 28.4 ms)
+template <int LAYOUT, int BK, bool VEC>  // (NT from 16-byte four-row loads: C3 28.4 ms)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_b(
     int P, long K, const float *__restrict__ A, long ld, long kchunk, int nchunk,
     float *__restrict__ Gpart) {
-    gram_b_body<LAYOUT, BK, VEC, RW>(P, K, A, ld, kchunk, nchunk, Gpart);
+    gram_b_body<LAYOUT, BK, VEC>(P, K, A, ld, kchunk, nchunk, Gpart);
 }
 
 // G = sum of the chunk partials, in chunk order
