@@ -328,9 +328,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float x) {
-    unsigned u = __builtin_bit_cast(unsigned, x);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (unsigned short)(u >> 16);
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const unsigned r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+    // a finite x that rounds past the largest bf16 (|x| > 3.39e38) keeps
+    // its truncation: the split stays exact instead of turning into inf - inf
+    return (unsigned short)(((r & 0x7f80u) == 0x7f80u && (u & 0x7f800000u) != 0x7f800000u) ? u >> 16 : r);
 }
 __device__ __forceinline__ float bf16_val(unsigned short h) {
     return __builtin_bit_cast(float, (unsigned)h << 16);

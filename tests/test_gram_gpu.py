@@ -54,6 +54,28 @@ def test_gram_short_last_chunk(gpu_lib):
     assert err <= 2e-6
 
 
+@pytest.mark.parametrize("which", [0, 1])
+def test_gram_huge_entries(gpu_lib, which):
+    """an entry past the largest bf16 (3.4e38) is split by truncation, not
+    rounded to inf: its finite products stay finite and exact to f32.  A
+    product that overflows f32 is inf on the exact-f32 tile and may be NaN
+    on the split one (its pieces' products overflow with both signs)"""
+    rng = np.random.default_rng(3)
+    B = rng.uniform(-1, 1, (128, 64)).astype(np.float32)  # rows = Gram index
+    B[:, 0] = 0.0
+    B[0, 0] = np.float32(3.4e38)
+    B[1, 0] = np.float32(1e-30)  # (normal: MFMA inputs may flush subnormals)
+    A = B if which == 1 else np.ascontiguousarray(B.T)  # A A^t of B, or A^t A of B^t
+    G, _ = pfdr.gram(A, which)
+    B64 = B.astype(np.float64)
+    ref = B64 @ B64.T
+    assert not np.isfinite(G[0, 0])
+    assert abs(G[0, 1] - ref[0, 1]) <= 1e-6 * abs(ref[0, 1]) and G[0, 1] == G[1, 0]
+    sub, rsub = G[1:, 1:].astype(np.float64), ref[1:, 1:]
+    assert np.linalg.norm(sub - rsub) <= 2e-6 * np.linalg.norm(rsub)
+    assert np.all(np.isfinite(G[0, 1:]))
+
+
 def _spectral(M, N, s, seed, dt):
     """A = U diag(s) V^t with orthonormal U, V: ||A||^2 = max(s)^2"""
     rng = np.random.default_rng(seed)
