@@ -314,11 +314,11 @@ __global__ __launch_bounds__(64 * WG) void k_gram_v(int P, long K, const real *_
 
 
 // f32 Gram on the bf16 matrix cores, f32-accurate: every element is split
-// exactly into three bf16 pieces, x = h + m + l (h = x rounded to 8
-// significant bits, m the same of x - h, l = x - h - m: no bits lost), and
+// exactly into three bf16 pieces, x = h + m + l (h = x truncated to 8
+// significant bits, m = x - h rounded to 8, l = x - h - m: no bits lost), and
 // a product x y is formed from the six pieces whose weight reaches 2^-16 of
 // it (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16, accumulated in
-// f32; the pieces left out (ml, lm, ll) weigh <= 2^-24 of each product,
+// f32; the pieces left out (ml, lm, ll) weigh <= 2^-23 of each product,
 // below the f32 rounding of the sum.  Six bf16 MFMAs of 16 k do the work of
 // eight f32 ones of 2 k at a sixteenth of the rate per flop: 2.7x the f32
 // matrix-core throughput.  Same blocks, tiles and chunks
@@ -328,11 +328,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf16_rne(float x) {
-    const unsigned u = __builtin_bit_cast(unsigned, x);
-    const unsigned r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-    // a finite x that rounds past the largest bf16 (|x| > 3.39e38) keeps
-    // its truncation: the split stays exact instead of turning into inf - inf
-    return (unsigned short)(((r & 0x7f80u) == 0x7f80u && (u & 0x7f800000u) != 0x7f800000u) ? u >> 16 : r);
+    unsigned u = __builtin_bit_cast(unsigned, x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+// the leading piece: x's top 16 bits (truncation never overflows to inf,
+// and x - h is exact with at most 16 significant bits)
+__device__ __forceinline__ unsigned short bf16_trunc(float x) {
+    return (unsigned short)(__builtin_bit_cast(unsigned, x) >> 16);
 }
 __device__ __forceinline__ float bf16_val(unsigned short h) {
     return __builtin_bit_cast(float, (unsigned)h << 16);
@@ -439,7 +442,7 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
 #pragma unroll
                     for (int r = 0; r < 2; r++) {
                         const float x = st[side][2 * q + r];
-                        const unsigned short h = bf16_rne(x);
+                        const unsigned short h = bf16_trunc(x);
                         const float r1 = x - bf16_val(h);
                         const unsigned short m = bf16_rne(r1);
                         ph[r] = h;
@@ -461,7 +464,7 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const float x = st[side][8 * c + u];
-                    const unsigned short h = bf16_rne(x);
+                    const unsigned short h = bf16_trunc(x);
                     const float r1 = x - bf16_val(h);
                     const unsigned short m = bf16_rne(r1);
                     ph[u] = h;

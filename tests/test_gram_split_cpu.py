@@ -1,30 +1,35 @@
 """CPU: the numerics the split Gram tile (k_gram_b, csrc/pfdr_gram.hip) rests
 on, restated in numpy with the kernel's bit operations: every f32 x splits
-EXACTLY into three bf16 pieces x = h + m + l (h = x rounded to nearest even at
-8 significant bits, m the same of x - h, l = x - h - m), and a product x y
-formed from the six pieces hh, hm, mh, hl, lh, mm -- each exact in f32 --
-differs from the exact product by the three pieces left out (ml, lm, ll),
-at most ~2^-22 of |x y|: below the f32 rounding of the Gram's sums, which
-the GPU test (tests/test_gram_gpu.py) holds to 2e-6 relative Frobenius."""
+EXACTLY into three bf16 pieces x = h + m + l (h = x truncated to 8
+significant bits, m = x - h rounded to nearest even at 8, l = x - h - m), and
+a product x y formed from the six pieces hh, hm, mh, hl, lh, mm -- each exact
+in f32 -- differs from the exact product by the three pieces left out (ml,
+lm, ll), at most ~2^-21 of |x y|: at the f32 rounding of the Gram's sums,
+which the GPU test (tests/test_gram_gpu.py) holds to 2e-6 relative
+Frobenius."""
 import numpy as np
 
 
 def bf16_rne(x):
     """the kernel's bf16_rne: round the f32 bit pattern to its top 16 bits,
-    to nearest even -- truncated where a finite x would round to inf"""
+    to nearest even"""
     u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
-    r = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFFFFFF) >> 16
-    over = ((r & 0x7F80) == 0x7F80) & ((u & 0x7F800000) != 0x7F800000)
-    return np.where(over, u >> 16, r).astype(np.uint32)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFFFFFF) >> 16
+    return u.astype(np.uint32)
 
 
 def bf16_val(h):
     return (h.astype(np.uint32) << 16).view(np.float32)
 
 
+def bf16_trunc(x):
+    """the kernel's leading piece: the top 16 bits of x"""
+    return (np.asarray(x, np.float32).view(np.uint32) >> 16).astype(np.uint32)
+
+
 def split3(x):
     x = np.asarray(x, np.float32)
-    h = bf16_val(bf16_rne(x))
+    h = bf16_val(bf16_trunc(x))
     r1 = (x - h).astype(np.float32)
     m = bf16_val(bf16_rne(r1))
     r2 = (r1 - m).astype(np.float32)
