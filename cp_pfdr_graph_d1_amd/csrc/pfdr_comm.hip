@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <set>
 
@@ -17,12 +18,38 @@ int report_rccl(const char *fn, ncclResult_t r);
 // (pfdr_comm_destroy in a finally block) must then not destroy it again.
 static std::mutex g_aborted_m;
 static std::set<void *> g_aborted;
+// communicators split from another (Transport::split): aborted with it, so a
+// failed rank's abort of its partition's communicators also releases the
+// peers waiting on a speculative session's evolution chain
+static std::map<void *, std::set<void *>> g_children;
+
+static void abort_locked(void *comm) {
+    if (!comm || g_aborted.count(comm)) return;
+    auto it = g_children.find(comm);
+    if (it != g_children.end()) {
+        const std::set<void *> kids = it->second;
+        for (void *k : kids) abort_locked(k);
+    }
+    (void)ncclCommAbort((ncclComm_t)comm);
+    g_aborted.insert(comm);
+}
 
 void comm_abort(void *comm) {
     std::lock_guard<std::mutex> l(g_aborted_m);
-    if (!comm || g_aborted.count(comm)) return;
-    (void)ncclCommAbort((ncclComm_t)comm);
-    g_aborted.insert(comm);
+    abort_locked(comm);
+}
+
+void comm_add_child(void *parent, void *child) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    g_children[parent].insert(child);
+}
+
+void comm_forget_child(void *parent, void *child) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    auto it = g_children.find(parent);
+    if (it == g_children.end()) return;
+    it->second.erase(child);
+    if (it->second.empty()) g_children.erase(it);
 }
 
 bool comm_aborted(void *comm) {

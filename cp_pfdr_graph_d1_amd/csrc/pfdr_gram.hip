@@ -342,7 +342,8 @@ __device__ __forceinline__ float bf16_val(unsigned short h) {
 }
 template <int LAYOUT, int BK, bool VEC>
 __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restrict__ A, long ld,
-                                            long kchunk, int nchunk, float *__restrict__ Gpart) {
+                                            long kchunk, int nchunk, float *__restrict__ Gpart,
+                                            int *__restrict__ nanflag) {
     using M = Mfma<float>;
     constexpr int BT = 128, T = 32, RS = BK + 8, NK = BK / 2;
     constexpr int RW = 2, KQ = BK / (2 * RW);  // NT staging: RW rows of KQ k per lane
@@ -548,6 +549,18 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
     // epilogue as k_gram_v's, its tiles in the staging array
     float(*O)[T + 1] = reinterpret_cast<float(*)[T + 1]>(reinterpret_cast<float *>(sm) + w * T * (T + 1));
     const int li = lane % T, lj = lane / T;
+    // a NaN here where no input was NaN is an overflow the split turned into
+    // inf - inf (pieces of both signs, or an infinite element split as
+    // h = inf, m = NaN): gram() then recomputes G on the exact-f32 tile,
+    // whose inf the reference's f32 sums give (one lane's vector store)
+    bool bad = false;
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++)
+#pragma unroll
+            for (int r = 0; r < M::NR; r++) bad |= acc[x][y][r] != acc[x][y][r];
+    if (bad) nanflag[0] = 1;
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -575,8 +588,8 @@ __device__ __forceinline__ void gram_b_body(int P, long K, const float *__restri
 template <int LAYOUT, int BK, bool VEC>  // (NT from 16-byte four-row loads: C3 28.4 ms)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_b(
     int P, long K, const float *__restrict__ A, long ld, long kchunk, int nchunk,
-    float *__restrict__ Gpart) {
-    gram_b_body<LAYOUT, BK, VEC>(P, K, A, ld, kchunk, nchunk, Gpart);
+    float *__restrict__ Gpart, int *__restrict__ nanflag) {
+    gram_b_body<LAYOUT, BK, VEC>(P, K, A, ld, kchunk, nchunk, Gpart, nanflag);
 }
 
 // G = sum of the chunk partials, in chunk order
@@ -629,13 +642,31 @@ void gram(int which, int P, long K, const real *A, long ld, real *G, hipStream_t
     if (split) {
         const float *Af = reinterpret_cast<const float *>(A);
         float *of = reinterpret_cast<float *>(out);
+        DevBuf<int> nanflag(1);
+        PFDR_HIP(hipMemsetAsync(nanflag.p, 0, sizeof(int), s));
         constexpr int BKS = 16;  // (BK = 32: 61 KB of LDS, two blocks per CU, slower)
         if (which == 0) {
-            if (vec) k_gram_b<GRAM_TN, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
-            else k_gram_b<GRAM_TN, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+            if (vec) k_gram_b<GRAM_TN, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of, nanflag.p);
+            else k_gram_b<GRAM_TN, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of, nanflag.p);
         } else {
-            if (vec) k_gram_b<GRAM_NT, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
-            else k_gram_b<GRAM_NT, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of);
+            if (vec) k_gram_b<GRAM_NT, BKS, true><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of, nanflag.p);
+            else k_gram_b<GRAM_NT, BKS, false><<<grid, 256, 0, s>>>(P, K, Af, ld, kchunk, (int)nchunk, of, nanflag.p);
+        }
+        PFDR_HIP(hipGetLastError());
+        int h = 0;
+        PFDR_HIP(hipMemcpyAsync(&h, nanflag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        if (h) {  // an overflow (or a non-finite input): the exact-f32 tile's semantics
+            if (vec && which == 0)
+                k_gram_v<real, GRAM_TN><<<grid, 64 * kGramWaves, 0, s>>>(P, K, A, ld, kchunk,
+                                                                        (int)nchunk, out);
+            else if (vec)
+                k_gram_v<real, GRAM_NT><<<grid, 64 * kGramWaves, 0, s>>>(P, K, A, ld, kchunk,
+                                                                        (int)nchunk, out);
+            else if (which == 0)
+                k_gram<real, GRAM_TN><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
+            else
+                k_gram<real, GRAM_NT><<<grid, 256, 0, s>>>(P, K, A, ld, kchunk, (int)nchunk, out);
         }
     } else if (vec) {
         if (which == 0)

@@ -168,7 +168,26 @@ void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
 class RcclTransport final : public Transport {
     ncclComm_t comm_;
     bool owned_ = false;             // a split communicator: destroyed with the transport
-    std::vector<ncclComm_t> kids_;   // split from this one: aborted with it
+    ncclComm_t parent_ = nullptr;    // the communicator it was split from (comm_add_child)
+    // PFDR_RCCL_SELF=1 (test flag): operations that move nothing still issue
+    // real RCCL calls -- a 1-rank all-reduce / broadcast, and a grouped
+    // send / receive of a 4-byte token to this rank itself where an exchange
+    // or a chain step has no peer -- so that a 1-rank communicator runs
+    // (and hipGraph-captures) the same RCCL operations as the ranks of a
+    // real partition, instead of returning early
+    bool self_ = false;
+    DevBuf<int> tok_;
+    void self_token(hipStream_t s) {
+        ck(ncclGroupStart(), "group start");
+        ck(ncclSend(tok_.p, 4, ncclChar, rank, comm_, s), "self send");
+        ck(ncclRecv(tok_.p + 1, 4, ncclChar, rank, comm_, s), "self recv");
+        ck(ncclGroupEnd(), "group end");
+    }
+    void init_self() {
+        const char *e = getenv("PFDR_RCCL_SELF");
+        self_ = e && e[0] == '1';
+        if (self_) tok_.alloc(2);
+    }
     static void ck(ncclResult_t r, const char *what) {
         if (r != ncclSuccess) {
             char m[256];
@@ -178,19 +197,21 @@ class RcclTransport final : public Transport {
     }
 
   public:
-    RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) { nranks = n; rank = r; }
+    RcclTransport(void *comm, int n, int r) : comm_((ncclComm_t)comm) {
+        nranks = n;
+        rank = r;
+        init_self();
+    }
     ~RcclTransport() override {
         if (!owned_) return;
+        comm_forget_child(parent_, comm_);  // (no abort through the parent after this)
         if (comm_aborted(comm_)) comm_created(comm_);  // released by the abort
         else (void)ncclCommDestroy(comm_);
     }
     // a stalled communicator cannot be used again: abort it so the peers'
     // operations fail too instead of waiting on this rank (recorded, so the
     // owner's pfdr_comm_destroy skips the freed handle)
-    void on_timeout() override {
-        comm_abort(comm_);
-        for (ncclComm_t k : kids_) comm_abort(k);
-    }
+    void on_timeout() override { comm_abort(comm_); }  // (its split ones first)
     std::unique_ptr<Transport> split(hipStream_t) override {
         last_op = "communicator split";
         ncclComm_t nc = nullptr;
@@ -200,9 +221,10 @@ class RcclTransport final : public Transport {
         cfg.splitShare = 0;
         ck(ncclCommSplit(comm_, 0, rank, &nc, &cfg), "comm split");
         comm_created(nc);
-        kids_.push_back(nc);
+        comm_add_child(comm_, nc);
         std::unique_ptr<RcclTransport> t(new RcclTransport(nc, nranks, rank));
         t->owned_ = true;
+        t->parent_ = comm_;
         return std::unique_ptr<Transport>(t.release());
     }
     bool capturable() const override { return true; }
@@ -213,7 +235,10 @@ class RcclTransport final : public Transport {
                   peers_bytes(rbytes, rank);
         bool any = false;  // (an exchange with nothing to move issues no RCCL call)
         for (int q = 0; q < nranks; q++) any = any || (q != rank && (sbytes[q] || rbytes[q]));
-        if (!any) return;
+        if (!any) {
+            if (self_) self_token(s);
+            return;
+        }
         ck(ncclGroupStart(), "group start");
         for (int q = 0; q < nranks; q++) {
             if (q == rank) continue;
@@ -225,24 +250,28 @@ class RcclTransport final : public Transport {
     void allreduce_sum(void *dev, int n, int dtype, hipStream_t s) override {
         ncclDataType_t t = dtype == PFDR_F32 ? ncclFloat32 : dtype == PFDR_F64 ? ncclFloat64 : ncclInt64;
         last_op = "all-reduce of " + std::to_string(n) + " values, all peers";
-        if (nranks == 1) return;  // (in place: the sum over one rank is the data)
+        if (nranks == 1 && !self_) return;  // (in place: the sum over one rank is the data)
         ck(ncclAllReduce(dev, dev, n, t, ncclSum, comm_, s), "allreduce");
     }
     void chain_recv(void *dev, size_t bytes, hipStream_t s) override {
         if (rank > 0) {
             last_op = "chain recv of " + std::to_string(bytes) + " B from " + std::to_string(rank - 1);
             ck(ncclRecv(dev, bytes, ncclChar, rank - 1, comm_, s), "chain recv");
+        } else if (self_) {
+            self_token(s);
         }
     }
     void chain_send(const void *dev, size_t bytes, hipStream_t s) override {
         if (rank + 1 < nranks) {
             last_op = "chain send of " + std::to_string(bytes) + " B to " + std::to_string(rank + 1);
             ck(ncclSend(dev, bytes, ncclChar, rank + 1, comm_, s), "chain send");
+        } else if (self_) {
+            self_token(s);
         }
     }
     void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {
         last_op = "broadcast of " + std::to_string(bytes) + " B from " + std::to_string(root);
-        if (nranks == 1) return;
+        if (nranks == 1 && !self_) return;
         ck(ncclBroadcast(dev, dev, bytes, ncclChar, root, comm_, s), "broadcast");
     }
 };

@@ -84,6 +84,10 @@ std::unique_ptr<Transport> make_rccl_transport(void *comm, int nranks, int rank)
 void comm_abort(void *comm);
 bool comm_aborted(void *comm);
 void comm_created(void *comm);  // forget a stale aborted entry at this address
+// a communicator split from `parent`: comm_abort(parent) aborts it first;
+// forget it before destroying it
+void comm_add_child(void *parent, void *child);
+void comm_forget_child(void *parent, void *child);
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
 // wake every rank waiting on the hub with an error (a rank failed)
 void loopback_abort(void *hub, const char *reason);

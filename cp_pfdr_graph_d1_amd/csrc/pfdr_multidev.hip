@@ -264,6 +264,11 @@ void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it
     const bool loop = !distinct(devs);
     std::vector<ncclComm_t> comms;
     void *hub = nullptr;
+    // one partitioned call at a time, from fetching the group's communicators
+    // to the end of the solve: another thread's call for another device group
+    // (pfdr_set_devices in between) re-creates the cached communicators, which
+    // must not happen while these are in use
+    std::lock_guard<std::mutex> call(multidev_call_mutex());
     if (loop) {
         if (pfdr_loopback_create(&hub, n) != PFDR_OK) throw std::runtime_error(pfdr_last_error());
     } else {
@@ -326,10 +331,7 @@ void multidev_solve(const pfdr_problem *p, const std::vector<int> &devs, int *it
             else for (ncclComm_t cm : comms) comm_abort(cm);
         }
     };
-    {
-        std::lock_guard<std::mutex> call(multidev_call_mutex());
-        rank_pool().run(n, rank_main);
-    }
+    rank_pool().run(n, rank_main);
     if (hub) pfdr_loopback_destroy(hub);
     // the first failure is the cause, the others its consequence
     std::string first;

@@ -210,7 +210,8 @@ class QuadSession final : public SessionBase {
     DevBuf<R2<real>> xpx_[kSpecMax - 1];  // X buffers 1 .. D - 1 (0 is xp_)
     R2<real> *xpb(int t) { return spec_ && t % sd_ ? xpx_[t % sd_ - 1].p : xp_.p; }
     R2<real> *xr_ = nullptr, *xw_ = nullptr;  // the sweeps' read / write (X, P)
-    hipStream_t evs_ = nullptr;
+    hipStream_t evs_ = nullptr;  // the decisions' stream (null: PFDR_SPEC_SERIAL, the session's)
+    hipStream_t evs() const { return evs_ ? evs_ : stream; }
     hipEvent_t evv_[kSpecMax] = {}, evd_[kSpecMax] = {};
     // run_pipelined: the control block's snapshots after two chunks in flight
     Ctrl<real> *snap_[2] = {};
@@ -235,7 +236,8 @@ class QuadSession final : public SessionBase {
     DevBuf<real> A1_;
     DevBuf<R2<real>> gi_;
     real cw_ = real(0);
-    DevBuf<real> R_, Rpart_, vpart_, opart_, Obj_, Dif_, red_, csum_;
+    DevBuf<real> R_, vpart_, opart_, Obj_, Dif_, red_, csum_;
+    DevBuf<double> Rpart_;  // k_rows_partial's double partials
     DevBuf<real> Rsum_, xfull_;  // dense A on a partition: summed A X, gathered X
     // relabelled partition (pfdr_problem.vtx_label): the caller's label of
     // each owned vertex; the amplitudes are all-reduced into ampg_ at those
@@ -630,9 +632,10 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
-                            &pre_, &Z2_, &A1_, &wz_, &R_, &Rpart_,
+                            &pre_, &Z2_, &A1_, &wz_, &R_,
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_, &spart_})
         acc(b->n * sizeof(real));
+    acc(Rpart_.n * sizeof(double));
     acc((xp_.n + gi_.n) * sizeof(R2<real>) + inc_.ptr.n * 4 + inc_.idx.n * 4);
     acc((uptr_.n + mask_.n + oidx_.n + blkok_.n) * 4);
     acc(slots_.n * sizeof(Slots12) + luv_.n * 2 + deg8_.n +
@@ -673,8 +676,11 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             chain_.init(V_, 2, *halo_->tr);
         }
         seqdif = 1;
-        spec_ = difRcd2_ == real(0) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG);
-        if (spec_ && halo_) {
+        const int smode = spec_mode(p);
+        spec_ = difRcd2_ == real(0) && !rec_obj_ && (mode_ == A_IDENT || mode_ == A_DIAG) &&
+                smode != PFDR_SPEC_OFF;
+        const bool serial = smode == PFDR_SPEC_SERIAL;
+        if (spec_ && halo_ && !serial) {
             evtr_ = halo_->tr->split(s);  // (a collective: every rank decides alike)
             // the halo exchanges stay on the session stream: a third stream
             // for them (overlap_) shared a hardware queue with the evolution
@@ -695,12 +701,12 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
                 PFDR_HIP(hipMemcpyAsync(xpx_[k].p, xp_.p, sizeof(R2<real>) * (Vg_ + 2),
                                         hipMemcpyDeviceToDevice, s));
             }
-            PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
+            if (!serial) PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
             for (int k = 0; k < sd_; k++) {
                 PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
                 PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
             }
-            speculative = 1;
+            speculative = serial ? 2 : 1;
         }
     }
     xr_ = xw_ = xp_.p;
@@ -1455,11 +1461,12 @@ void QuadSession<real>::body_spec(int i, int n) {
     vpart_.p = keepp;
     xr_ = xw_ = xp_.p;
     PFDR_HIP(hipEventRecord(evv_[b], s));
-    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[b], 0));
-    seq_evolution(terms, part, evs_);  // overlaps the sweeps of t + 1
-    k_decide<real><<<1, 64, 0, evs_>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
+    const hipStream_t es = evs();
+    PFDR_HIP(hipStreamWaitEvent(es, evv_[b], 0));
+    seq_evolution(terms, part, es);  // overlaps the sweeps of t + 1 (not when serial)
+    k_decide<real><<<1, 64, 0, es>>>(ctrl_.p, red_.p, rec_dif_ ? Dif_.p : nullptr, 1);
     PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipEventRecord(evd_[b], evs_));
+    PFDR_HIP(hipEventRecord(evd_[b], es));
     if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // join: the chunk's last
 }
 

@@ -822,6 +822,10 @@ __device__ __forceinline__ void col_epilogue(const ColArgs<real> &a, long col, r
 
 // One wave64 per column: 16-byte loads of the column (and of w, which
 // every wave re-reads from L2), wave-shuffle reduction, fused epilogue.
+// The products and sums run in double whatever `real` (HBM-bound: the f64
+// arithmetic is free), so a tree-reduced f32 dot product lies closer to the
+// exact one than the reference's sequential f32 sum, not just as close
+// (tests/test_fullsize_pin_gpu.py: the yardstick is the reference's f64 run).
 // ref: diag of A^tA :102-110, pseudo-inverse :126-134, apply A^tA
 // :368-376, gradient -A^t R :432-440, forward :462-464.
 template <typename real, int EPI>
@@ -833,21 +837,21 @@ __global__ __launch_bounds__(256) void k_col_dot(ColArgs<real> a) {
     const real *c = a.A + (size_t)a.len * col;
     const real *w = (EPI == EPI_SELF) ? c : a.w;
     constexpr int VW = Vec<real>::kPer16B;
-    real acc = real(0);
+    double acc = 0.0;
     if ((a.len % VW) == 0) {
         const int nv = a.len / VW;
         for (int i = lane; i < nv; i += 64) {
             Pk<real, VW> x = ldv<real, VW>(c + (size_t)i * VW);
             Pk<real, VW> y = ldv<real, VW>(w + (size_t)i * VW);
 #pragma unroll
-            for (int j = 0; j < VW; j++) acc += x.v[j] * y.v[j];
+            for (int j = 0; j < VW; j++) acc += (double)x.v[j] * (double)y.v[j];
         }
     } else {
-        for (int i = lane; i < a.len; i += 64) acc += c[i] * w[i];
+        for (int i = lane; i < a.len; i += 64) acc += (double)c[i] * (double)w[i];
     }
     acc = wave_sum(acc);
     if (lane != 0) return;
-    col_epilogue<real, EPI>(a, col, acc);
+    col_epilogue<real, EPI>(a, col, (real)acc);
 }
 
 // Sequential-order column dots for small dense problems (the reduced
@@ -1062,72 +1066,74 @@ __global__ __launch_bounds__(256) void k_sym_check(int V, const real *__restrict
 }
 
 // R partials: part[b][n] = sum_{v in block b} A[n + N v] X[v]
-// (column-major A streamed once, 16-byte loads, 4 columns in flight)
+// (column-major A streamed once, 16-byte loads, 4 columns in flight);
+// products and partials in double (as k_col_dot)
 template <typename real>
 __global__ __launch_bounds__(256) void k_rows_partial(
     int N, int V, const real *__restrict__ A, const R2<real> *__restrict__ xp,
-    int cpb, real *__restrict__ part, const Ctrl<real> *ctrl, int gate) {
+    int cpb, double *__restrict__ part, const Ctrl<real> *ctrl, int gate) {
     if (gated(ctrl, gate)) return;
     const int b = blockIdx.x;
     const int v0 = b * cpb, v1 = min(v0 + cpb, V);
     constexpr int VW = Vec<real>::kPer16B;
     if ((N % VW) == 0) {
         for (int n0 = threadIdx.x * VW; n0 < N; n0 += kBlock * VW) {
-            real acc[VW];
+            double acc[VW];
 #pragma unroll
-            for (int j = 0; j < VW; j++) acc[j] = real(0);
+            for (int j = 0; j < VW; j++) acc[j] = 0.0;
             int v = v0;
             for (; v + 4 <= v1; v += 4) {
                 Pk<real, VW> c[4];
-                real x[4];
+                double x[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     c[q] = ldv<real, VW>(A + (size_t)N * (v + q) + n0);
-                    x[q] = xp[v + q].x;
+                    x[q] = (double)xp[v + q].x;
                 }
 #pragma unroll
                 for (int q = 0; q < 4; q++)
 #pragma unroll
-                    for (int j = 0; j < VW; j++) acc[j] += c[q].v[j] * x[q];
+                    for (int j = 0; j < VW; j++) acc[j] += (double)c[q].v[j] * x[q];
             }
             for (; v < v1; v++) {
                 Pk<real, VW> c = ldv<real, VW>(A + (size_t)N * v + n0);
-                real x = xp[v].x;
+                const double x = (double)xp[v].x;
 #pragma unroll
-                for (int j = 0; j < VW; j++) acc[j] += c.v[j] * x;
+                for (int j = 0; j < VW; j++) acc[j] += (double)c.v[j] * x;
             }
 #pragma unroll
             for (int j = 0; j < VW; j++) part[(size_t)b * N + n0 + j] = acc[j];
         }
     } else {
         for (int n = threadIdx.x; n < N; n += kBlock) {
-            real acc = real(0);
-            for (int v = v0; v < v1; v++) acc += A[(size_t)N * v + n] * xp[v].x;
+            double acc = 0.0;
+            for (int v = v0; v < v1; v++) acc += (double)A[(size_t)N * v + n] * (double)xp[v].x;
             part[(size_t)b * N + n] = acc;
         }
     }
 }
 
-// R[n] = Y[n] - sum_b part[b][n]   (ref :356-367)
+// R[n] = Y[n] - sum_b part[b][n]   (ref :356-367), in double, rounded once
 template <typename real>
-__global__ void k_rows_finish(int N, int nb, const real *__restrict__ part,
+__global__ void k_rows_finish(int N, int nb, const double *__restrict__ part,
                               const real *__restrict__ Y,
                               real *__restrict__ R, const Ctrl<real> *ctrl,
                               int gate) {
     if (gated(ctrl, gate)) return;
     int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
-    real s = real(0);
+    double s = 0.0;
     int b = 0;
     for (; b + 8 <= nb; b += 8) {
-        real t[8];
+        double t[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) t[q] = part[(size_t)(b + q) * N + n];
 #pragma unroll
         for (int q = 0; q < 8; q++) s += t[q];
     }
     for (; b < nb; b++) s += part[(size_t)b * N + n];
-    R[n] = Y ? Y[n] - s : s;  // Y == NULL: this rank's partial A X (all-reduced next)
+    // Y == NULL: this rank's partial A X (all-reduced next)
+    R[n] = Y ? (real)((double)Y[n] - s) : (real)s;
 }
 
 // R = Y - (A X summed over the ranks)

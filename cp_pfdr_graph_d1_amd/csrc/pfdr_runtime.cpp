@@ -377,7 +377,7 @@ using namespace pfdr;
     }
 
 extern "C" const char *pfdr_last_error(void) { return g_last_error.c_str(); }
-extern "C" int pfdr_abi_version(void) { return 3; }
+extern "C" int pfdr_abi_version(void) { return 4; }
 extern "C" int pfdr_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return -1;

@@ -3,6 +3,7 @@
 // iteration loop bookkeeping.
 #pragma once
 #include <map>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -74,12 +75,30 @@ class SessionBase {
     int64_t dense_exact = 0;   // dense A: dot products in the reference's order
     int64_t ghosts = 0;        // partitioned: ghost (halo) vertices of this rank
     int64_t graphs = 0;        // chunks of iterations replayed as hipGraphs
-    int64_t speculative = 0;   // evolution decision overlapped with the next iteration
+    int64_t speculative = 0;   // 1: evolution decision overlapped with the next iteration
+                               // (its own stream / split communicator), 2: serial (PFDR_SPEC_SERIAL)
     int64_t interior_edges = -1;  // edges of the "edge_sweep" launch (E unless halo overlap)
     hipStream_t stream = nullptr;
     Profiler prof;
     int device = 0;
 };
+
+// the speculation mode of a problem: p->spec, or the env PFDR_SPEC (auto |
+// serial | off) when set
+inline int spec_mode(const pfdr_problem *p) {
+    const char *e = getenv("PFDR_SPEC");
+    int m = p->spec;
+    if (e && *e) {
+        const std::string v(e);
+        if (v == "auto") m = PFDR_SPEC_AUTO;
+        else if (v == "serial") m = PFDR_SPEC_SERIAL;
+        else if (v == "off") m = PFDR_SPEC_OFF;
+        else throw std::runtime_error("PFDR_SPEC must be auto, serial or off");
+    }
+    if (m < PFDR_SPEC_AUTO || m > PFDR_SPEC_OFF)
+        throw std::runtime_error("spec must be PFDR_SPEC_AUTO, _SERIAL or _OFF");
+    return m;
+}
 
 // PFDR_TRACE=1: one stderr line per drop-in call (sizes, iterations, setup /
 // iteration / copy-back wall times) -- the view of a CP caller's inner loop.

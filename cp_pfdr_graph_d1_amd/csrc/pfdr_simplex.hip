@@ -33,6 +33,7 @@
 #include "pfdr_monosum.hpp"
 #include "pfdr_proj.hpp"
 #include "pfdr_session.hpp"
+#include "pfdr_sort.hpp"
 
 namespace pfdr {
 
@@ -646,7 +647,31 @@ struct SxVArgs {
     SxR2<real> *PFo;
     real *xs;            // wide sweep, K > 1024: the averages, projected in place
     unsigned char *act;  // its active flags (one byte per (v, k))
+    // 1/Aux per VERTEX (null: per (v, k) in invAux): before any reconditioning
+    // every label of a vertex sums the same weights La_d1[e] in the same
+    // order (ref :196-217), so its K values are one value
+    const real *invV;
+    real la0;  // La_d1 when it is one value for every edge (la_u), before A1
+    int la_u;
+    // P lives in the .x half of PF only (no P store; the evolution reads
+    // the old P from PF; SimplexSession::sync_p extracts it when asked)
+    int nop;
 };
+
+template <typename real>
+__device__ __forceinline__ real sx_inv(const SxVArgs<real> &a, long v, long i) {
+    return a.invV ? a.invV[v] : a.invAux[i];
+}
+// the splitting-weight factor of a local incidence (ref :199-217): A1 after
+// a reconditioning, else La_d1 (one kernel argument when uniform)
+template <typename real>
+__device__ __forceinline__ real sx_wa(const SxVArgs<real> &a, long i, long e) {
+    return a.A1 ? a.A1[i] : (a.la_u ? a.la0 : a.La_d1[e]);
+}
+template <typename real>
+__device__ __forceinline__ real sx_pold(const SxVArgs<real> &a, long i) {
+    return a.nop ? a.PF[i].x : a.P[i];
+}
 
 // ordered DR average of item (v, k) (ref :636-648): the incidences in the
 // reference's (e, side) order, W * Z formed from Z with the reference's
@@ -655,7 +680,7 @@ struct SxVArgs {
 template <typename real>
 __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int k) {
     const int K = a.c.K;
-    const real inv = a.invAux[v * K + k];  // 1/Aux of this (v, k)
+    const real inv = sx_inv(a, v, v * K + k);  // 1/Aux of this (v, k)
     const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
     real s = real(0);
     int j = j0;
@@ -678,7 +703,7 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
                 const long ea = sv ? ad - a.E : ad;
                 rq[q] = ea >= a.E;
                 zq[q] = (sv ? a.Zv : a.Zu)[ea * K + k];
-                aq[q] = a.A1 ? a.A1[rq[q] ? 0 : ea * K + k] : a.La_d1[rq[q] ? 0 : ea];
+                aq[q] = sx_wa(a, rq[q] ? 0 : ea * K + k, rq[q] ? 0 : ea);
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) w[q] = rq[q] ? zq[q] : (aq[q] * inv) * zq[q];
@@ -692,7 +717,7 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
         const long ea = sv ? ad - a.E : ad;
         const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
         if (ea >= a.E) s += z;
-        else s += (sx_a(ea * K + k, ea, a.A1, a.La_d1) * inv) * z;
+        else s += (sx_wa(a, ea * K + k, ea) * inv) * z;
     }
     return s;
 }
@@ -736,12 +761,12 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     if (live) {
         const real p = xs[t];
         if (a.track == 1) {
-            real d = a.P[i] - p;
+            real d = sx_pold(a, i) - p;
             if (d < real(0)) d = -d;
             dif += d;
             if (a.terms) a.terms[i] = d;
         }
-        (SPLIT ? a.Po : a.P)[i] = p;
+        if (!a.nop) (SPLIT ? a.Po : a.P)[i] = p;
         // Q enters the quadratic loss's step only (no load otherwise)
         SxR2<real> q;
         q.x = p;
@@ -847,7 +872,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
             const long ea = sv ? ad - a.E : ad;
             const bool rq = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
             zo[q] = ea * K | (sv ? kZv : 0) | (rq ? kRecv : 0);
-            wa[q] = (rq || a.A1) ? real(0) : a.La_d1[ea];
+            wa[q] = (rq || a.A1) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
         }
         __syncthreads();
     }
@@ -873,7 +898,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
             int j[SXU], j1[SXU];
 #pragma unroll
             for (int u = 0; u < SXU; u++) {
-                inv[u] = ok[u] ? a.invAux[i[u]] : real(0);
+                inv[u] = ok[u] ? sx_inv(a, v0 + vl[u], i[u]) : real(0);
                 j[u] = ok[u] ? lptr[vl[u]] - jb : 0;
                 j1[u] = ok[u] ? lptr[vl[u] + 1] - jb : 0;
             }
@@ -935,7 +960,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
             pold[u] = gq[u] = qq[u] = real(0);
             if (it < nitems) {
                 const long i = v0 * K + it;  // (items are the group's rows, in order)
-                if (a.track == 1) pold[u] = a.P[i];
+                if (a.track == 1) pold[u] = sx_pold(a, i);
                 gq[u] = a.GaQ[i];
                 if (a.c.loss == LOSS_QUAD) qq[u] = a.Q[i];
             }
@@ -955,7 +980,7 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
                 dif += d;
                 if (a.terms) a.terms[i] = d;
             }
-            (SPLIT ? a.Po : a.P)[i] = p;
+            if (!a.nop) (SPLIT ? a.Po : a.P)[i] = p;
             SxR2<real> q;
             q.x = p;
             q.y = sx_explicit(a.c, p, gq[u], qq[u]);
@@ -1006,7 +1031,7 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
     for (int j = 0; j < J; j++) {
         const int k = k0 + lane + 64 * j;
         ok[j] = k < K;
-        inv[j] = ok[j] ? a.invAux[b + k] : real(0);
+        inv[j] = ok[j] ? sx_inv(a, v, b + k) : real(0);
         s[j] = real(0);
     }
     const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
@@ -1021,7 +1046,7 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
             const long ea = sv ? ad - a.E : ad;
             rq[u] = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
             const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
-            const real la = (a.A1 || rq[u]) ? real(0) : a.La_d1[ea];
+            const real la = (a.A1 || rq[u]) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
 #pragma unroll
             for (int j = 0; j < J; j++) {
                 const long k = k0 + lane + 64 * j;
@@ -1040,7 +1065,7 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
         const long ea = sv ? ad - a.E : ad;
         const bool rq = ea >= a.E;
         const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
-        const real la = (a.A1 || rq) ? real(0) : a.La_d1[ea];
+        const real la = (a.A1 || rq) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
 #pragma unroll
         for (int j = 0; j < J; j++) {
             const long k = k0 + lane + 64 * j;
@@ -1057,14 +1082,14 @@ __device__ __forceinline__ void sx_wide_out(const SxVArgs<real> &a, long b, int 
                                             real &dif, real &mv, int &mi) {
     const long i = b + k;
     if (a.track == 1) {
-        real d = a.P[i] - p;
+        real d = sx_pold(a, i) - p;
         if (d < real(0)) d = -d;
         dif += d;
         if (a.terms) a.terms[i] = d;
     } else if (a.track == 2) {
         argmax_take(p, k, mv, mi);
     }
-    (SPLIT ? a.Po : a.P)[i] = p;
+    if (!a.nop) (SPLIT ? a.Po : a.P)[i] = p;
     SxR2<real> q;
     q.x = p;
     q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
@@ -1428,6 +1453,66 @@ __global__ void k_sx_obj_write(const real *__restrict__ sums, int quad, Ctrl<rea
 }
 
 // ---------------------------------------------------------------- session
+// --------------------------------------- tile order (K <= 64, one GPU) --
+// Large single-GPU sessions keep their edges in TILE order: stably sorted
+// by (u block, v block), the blocks the fused vertex sweep's workgroups own
+// (vb vertices).  Every edge-indexed array (Zu, Zv, A1, La_d1, Eu, Ev)
+// follows, so block b's u-end rows of Z are one contiguous run and its v-end
+// rows a few runs, one per (u block, b) tile, each read by workgroup b alone:
+// on a grid in its natural order the v ends of a row's edges interleave
+// with the in-row ones, so the K-wide Z runs of one 128-byte line belonged
+// to two workgroups a grid row apart and were fetched twice.  The
+// incidence keys keep the original edge ids, so every per-(v, k) sum still
+// runs in the reference's (e, side) order (ref :636-648).
+__global__ void k_sx_tile_keys(long E, int vb, int vbits, const int *__restrict__ Eu,
+                               const int *__restrict__ Ev, unsigned long long *__restrict__ keys,
+                               unsigned *__restrict__ vals) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    keys[e] = ((unsigned long long)(Eu[e] / vb) << vbits) | (unsigned)(Ev[e] / vb);
+    vals[e] = (unsigned)e;
+}
+
+// position p takes edge perm[p] (its original id: the incidence keys)
+__global__ void k_sx_tile_order(long E, const unsigned *__restrict__ perm,
+                                const int *__restrict__ Eu, const int *__restrict__ Ev,
+                                int *__restrict__ nEu, int *__restrict__ nEv) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const unsigned q = perm[p];
+    nEu[p] = Eu[q];
+    nEv[p] = Ev[q];
+}
+
+template <typename real>
+__global__ void k_sx_permute(long E, const unsigned *__restrict__ perm, const real *__restrict__ src,
+                             real *__restrict__ dst) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < E) dst[p] = src[perm[p]];
+}
+
+// *bad += the entries of La_d1 that differ from La_d1[0]
+template <typename real>
+__global__ void k_sx_uniform_check(long E, const real *__restrict__ x, int *__restrict__ bad) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < E && x[e] != x[0]) atomicAdd(bad, 1);
+}
+
+// 1/Aux per vertex: label 0's (every label's, before a reconditioning)
+template <typename real>
+__global__ void k_sx_inv_vertex(int V, int K, const real *__restrict__ invAux,
+                                real *__restrict__ invV) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) invV[v] = invAux[(long)v * K];
+}
+
+// P from the .x half of the (P, step) pairs (SxVArgs::nop)
+template <typename real>
+__global__ void k_sx_p_from_pf(long n, const SxR2<real> *__restrict__ PF, real *__restrict__ P) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) P[i] = PF[i].x;
+}
+
 template <typename real>
 static void sx_copy_in(DevBuf<real> &d, const void *src, size_t n, int mem, hipStream_t s,
                        HostPins &pins) {
@@ -1483,7 +1568,11 @@ class SimplexSession final : public SessionBase {
     }
     int run(int iters) override;
     void result(void *X_host, int *it, void *Obj_host, void *Dif_host) override;
-    void *device_x() override { return Pb(it_); }
+    void *device_x() override {
+        sync_p(it_);
+        PFDR_HIP(hipStreamSynchronize(stream));
+        return Pb(it_);
+    }
     void on_stop_or_recond();
 
   private:
@@ -1534,7 +1623,8 @@ class SimplexSession final : public SessionBase {
     DevBuf<SxR2<real>> PFx_[kSpecMax - 1];    // (P, step) likewise
     real *Pb(int t) { return spec_ && t % sd_ ? Px_[t % sd_ - 1].p : P_.p; }
     SxR2<real> *PFb(int t) { return spec_ && t % sd_ ? PFx_[t % sd_ - 1].p : PF_.p; }
-    hipStream_t evs_ = nullptr;
+    hipStream_t evs_ = nullptr;  // the decisions' stream (null: PFDR_SPEC_SERIAL, the session's)
+    hipStream_t evs() const { return evs_ ? evs_ : stream; }
     hipEvent_t evv_[kSpecMax] = {}, evd_[kSpecMax] = {};
     // pipelined gated runs (QuadSession::run_pipelined): control-block
     // snapshots of two chunks in flight
@@ -1563,6 +1653,19 @@ class SimplexSession final : public SessionBase {
     int nbw_ = 0;           // wide vertex sweep (K > 64): blocks
     int gnv_ = 0;           // its vertices per group (0: a wave per vertex, in memory)
     DevBuf<unsigned char> act_;  // its active sets when K > 1024
+    // tile order (k_sx_tile_keys; PFDR_SX_TILE = 0 off, 1 on, default from
+    // kSxTileMinVK (edge, label) entries)
+    bool sxtile_ = false;
+    static constexpr long kSxTileMinVK = 1L << 21;
+    // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
+    bool la_u_ = false;
+    real la0_ = real(0);
+    DevBuf<real> invV_;  // 1/Aux per vertex (SxVArgs::invV), before any reconditioning
+    // P kept only in PF's .x half by the sweeps (SxVArgs::nop): every session
+    // but the one-workgroup one; sync_p(t) writes Pb(t) from PFb(t) for the
+    // readers of P (objective, reconditioning, result)
+    bool plazy_ = false;
+    void sync_p(int t);
     // the fused vertex sweep forms W*Z from the gathered Z and W (K contiguous
     // words per incidence), so the edge sweep neither reads W nor writes
     // contributions: 28 instead of 44 streamed bytes per (e, k) (C4: 2.42 ->
@@ -1676,9 +1779,54 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         }
     }
     check_endpoints(Eu_.p, Ev_.p, E_, Vg_, s);
-    contribution_incidence(Eu_.p, Ev_.p, E_, V_, eg.p, e_offset, halo_.get(), inc_, s);
+    DevBuf<unsigned> perm;  // tile order: position -> original edge id
+    {
+        const char *t = getenv("PFDR_SX_TILE");
+        const int want = t ? atoi(t) : -1;
+        const int vb = K_ <= 64 ? kBlock / K_ : 0;
+        const long nb = vb ? ((long)V_ + vb - 1) / vb : 0;
+        sxtile_ = !halo_ && vb && E_ > 1 && want != 0 && (want > 0 || VK_ >= kSxTileMinVK);
+        if (sxtile_) {
+            int vbits = 1;
+            while (vbits < 31 && (1L << vbits) < nb) vbits++;
+            DevBuf<unsigned long long> k(E_), ks(E_);
+            DevBuf<unsigned> v(E_);
+            perm.alloc(E_);
+            k_sx_tile_keys<<<grid_for(E_), kBlock, 0, s>>>(E_, vb, vbits, Eu_.p, Ev_.p, k.p, v.p);
+            PFDR_HIP(hipGetLastError());
+            radix_sort_pairs_stable<unsigned long long>(k.p, ks.p, v.p, perm.p, E_, 2 * vbits, s);
+            DevBuf<int> nu(E_), nv(E_);
+            k_sx_tile_order<<<grid_for(E_), kBlock, 0, s>>>(E_, perm.p, Eu_.p, Ev_.p, nu.p, nv.p);
+            PFDR_HIP(hipGetLastError());
+            std::swap(Eu_.p, nu.p);
+            std::swap(Ev_.p, nv.p);
+            PFDR_HIP(hipStreamSynchronize(s));
+        }
+        tiled_blocks = sxtile_ ? nb : 0;  // (every fused-sweep block reads tile runs)
+    }
+    contribution_incidence(Eu_.p, Ev_.p, E_, V_, sxtile_ ? perm.p : eg.p, e_offset, halo_.get(),
+                           inc_, s);
     const size_t VgK = (size_t)Vg_ * K_;
     sx_copy_in(La_d1_, p->La_d1, E_, mem, s, pins_);
+    if (sxtile_) {
+        DevBuf<real> t(E_);
+        k_sx_permute<real><<<grid_for(E_), kBlock, 0, s>>>(E_, perm.p, La_d1_.p, t.p);
+        PFDR_HIP(hipGetLastError());
+        std::swap(La_d1_.p, t.p);
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+    if (E_) {
+        DevBuf<int> bad(1);
+        PFDR_HIP(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+        k_sx_uniform_check<real><<<grid_for(E_), kBlock, 0, s>>>(E_, La_d1_.p, bad.p);
+        PFDR_HIP(hipGetLastError());
+        int h = 1;
+        PFDR_HIP(hipMemcpyAsync(&h, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipMemcpyAsync(&la0_, La_d1_.p, sizeof(real), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        la_u_ = h == 0;
+        la_uniform = la_u_ ? 1 : 0;
+    }
     if (c_.loss != LOSS_LINEAR) sx_copy_in(La_f_, p->La_l1, V_, mem, s, pins_);
     for (auto q : {std::make_pair(&Q_, p->Y), std::make_pair(&P_, (const void *)p->X)}) {
         q.first->alloc(VgK);  // owned rows, then the ghosts' from their owners
@@ -1731,6 +1879,8 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
 
     if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, Zv_.p);
     precondition(true);
+    invV_.alloc(V_);
+    k_sx_inv_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, K_, invAux_.p, invV_.p);
     k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
     PFDR_HIP(hipGetLastError());
     pullPF();
@@ -1749,6 +1899,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
                 !(track_ && evo == PFDR_EVOLUTION_SEQUENTIAL);
         tiny = tiny_ ? 1 : 0;
         if (tiny_) graphs_ok_ = capturable_ = false;
+        plazy_ = !tiny_;
     }
     const long nglob = track_ == 2 ? Vglob_ : Vglob_ * K_;  // terms over all ranks
     seqdif_ = track_ && !tiny_ && !(halo_ && track_ == 2) &&
@@ -1778,8 +1929,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
             chain_.init(nterms_, 1, *halo_->tr);
         }
         seqdif = 1;
-        spec_ = difRcd_ == real(0) && !rec_obj_;
-        if (spec_ && halo_) evtr_ = halo_->tr->split(s);  // (collective: every rank alike)
+        const int smode = spec_mode(p);
+        const bool serial = smode == PFDR_SPEC_SERIAL;
+        spec_ = difRcd_ == real(0) && !rec_obj_ && smode != PFDR_SPEC_OFF;
+        if (spec_ && halo_ && !serial) evtr_ = halo_->tr->split(s);  // (collective: every rank alike)
         if (spec_) {
             sd_ = halo_ && halo_->tr->nranks >= 3 ? 4 : 2;
             DevBuf<real> t2((size_t)sd_ * n);  // terms of D iterations
@@ -1789,12 +1942,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
                 Px_[k].alloc((size_t)Vg_ * K_);
                 PFx_[k].alloc((size_t)Vg_ * K_);
             }
-            PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
+            if (!serial) PFDR_HIP(hipStreamCreateWithFlags(&evs_, hipStreamNonBlocking));
             for (int k = 0; k < sd_; k++) {
                 PFDR_HIP(hipEventCreateWithFlags(&evv_[k], hipEventDisableTiming));
                 PFDR_HIP(hipEventCreateWithFlags(&evd_[k], hipEventDisableTiming));
             }
-            speculative = 1;
+            speculative = serial ? 2 : 1;
             graphs_ok_ = capturable_ = false;  // launched directly (see QuadSession)
         }
     }
@@ -1856,6 +2009,7 @@ void SimplexSession<real>::precondition(bool init) {
 template <typename real>
 void SimplexSession<real>::objective() {
     hipStream_t s = stream;
+    sync_p(0);  // (no objective record in a speculative session: P_)
     k_sx_obj_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, c_, La_f_.p, P_.p, Q_.p, opart_.p, ctrl_.p);
     if (E_) k_sx_obj_edge<real><<<nbe_, kBlock, 0, s>>>(E_, K_, Eu_.p, Ev_.p, La_d1_.p, P_.p,
                                                         opart_.p + nbv_, ctrl_.p);
@@ -1866,6 +2020,16 @@ void SimplexSession<real>::objective() {
         halo_->tr->allreduce_sum(red_.p, 2, sizeof(real) == 4 ? PFDR_F32 : PFDR_F64, s);
         k_sx_obj_write<real><<<1, 1, 0, s>>>(red_.p, c_.loss == LOSS_QUAD, ctrl_.p, Obj_.p);
     }
+    PFDR_HIP(hipGetLastError());
+}
+
+// Pb(t) from the (P, step) pairs the sweeps wrote (plazy_), ghost rows
+// included (their PF rows were pulled)
+template <typename real>
+void SimplexSession<real>::sync_p(int t) {
+    if (!plazy_) return;
+    const long n = (long)Vg_ * K_;
+    k_sx_p_from_pf<real><<<grid_for(n), kBlock, 0, stream>>>(n, PFb(t), Pb(t));
     PFDR_HIP(hipGetLastError());
 }
 
@@ -1882,12 +2046,13 @@ void SimplexSession<real>::body_spec(int i, int n) {
     sweeps(ctrl_.p, t);
     terms_.p = keep;
     PFDR_HIP(hipEventRecord(evv_[b], s));
-    PFDR_HIP(hipStreamWaitEvent(evs_, evv_[b], 0));
-    seq_evolution(terms, evs_);  // overlaps the sweeps of t + 1
-    k_sx_finalize<real><<<1, kBlock, 0, evs_>>>(0, nullptr, Vglob_, track_, ctrl_.p,
+    const hipStream_t es = evs();
+    PFDR_HIP(hipStreamWaitEvent(es, evv_[b], 0));
+    seq_evolution(terms, es);  // overlaps the sweeps of t + 1 (not when serial)
+    k_sx_finalize<real><<<1, kBlock, 0, es>>>(0, nullptr, Vglob_, track_, ctrl_.p,
                                                 rec_dif_ ? Dif_.p : nullptr, red_.p);
     PFDR_HIP(hipGetLastError());
-    PFDR_HIP(hipEventRecord(evd_[b], evs_));
+    PFDR_HIP(hipEventRecord(evd_[b], es));
     if (i == n - 1) PFDR_HIP(hipStreamWaitEvent(s, evd_[b], 0));  // join: the chunk's last
 }
 
@@ -1957,6 +2122,9 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
     a.terms = seqdif_ ? terms_.p : nullptr;
     a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
+    a.invV = A1_.p ? nullptr : invV_.p;
+    a.la0 = la0_; a.la_u = la_u_ ? 1 : 0;
+    a.nop = plazy_ ? 1 : 0;
     if (vb_) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
@@ -1971,7 +2139,7 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     }
     if (halo_) {  // the ghosts of the buffers just written (speculative: Pb(t), PFb(t))
         ProfScope ps(prof, "halo_pull", s);
-        halo_->pull(Po ? Po : P_.p, K_ * (int)sizeof(real), s);
+        if (!plazy_) halo_->pull(Po ? Po : P_.p, K_ * (int)sizeof(real), s);
         halo_->pull(PFo ? PFo : PF_.p, K_ * (int)sizeof(SxR2<real>), s);
     }
     PFDR_HIP(hipGetLastError());
@@ -2157,6 +2325,7 @@ void SimplexSession<real>::on_stop_or_recond() {
             stopped_ = true;
         } else if (hctrl_->recond) {
             if (verbose_) { printf("Reconditioning... "); fflush(stdout); }
+            sync_p(it_);
             precondition(false);
             drop_graphs();  // kernel arguments (A1_, stored weights) may have changed
             k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, stream>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
@@ -2196,7 +2365,10 @@ template <typename real>
 void SimplexSession<real>::result(void *X_host, int *it, void *Obj_host, void *Dif_host) {
     hipStream_t s = stream;
     HostPins hp(s);
-    if (X_host) hp.copy(X_host, Pb(it_), sizeof(real) * VK_, hipMemcpyDeviceToHost);
+    if (X_host) {
+        sync_p(it_);
+        hp.copy(X_host, Pb(it_), sizeof(real) * VK_, hipMemcpyDeviceToHost);
+    }
     if (it) *it = it_;
     if (Obj_host && rec_obj_)
         hp.copy(Obj_host, Obj_.p, sizeof(real) * (it_ + 1), hipMemcpyDeviceToHost);

@@ -139,14 +139,16 @@ class Plan:
 def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                    positivity=0, lo=-np.inf, hi=np.inf, Ltype=0, L=None, rho=1.5,
                    condMin=1e-3, difRcd=0.0, difTol=0.0, itMax=100, record_obj=False,
-                   record_dif=False, off=None, K=0, al=0.0, N=0, relabel=False, evolution=0):
+                   record_dif=False, off=None, K=0, al=0.0, N=0, relabel=False, evolution=0,
+                   spec=0):
     """Partitioned solve with k ranks as k threads on the current GPU.
     Simplex (kind PFDR_KIND_SIMPLEX): X0 = P0 and Y = Q are K-by-V (v*K + k),
     La_l1 = La_f.  Dense A: N > 0 (A is N-by-V column-major, each rank gets
     its vertices' columns, Y stays whole) or N = -V (A^tA, column blocks).
     relabel (graph modes): split the locality order instead of the labels
     (locality_order, relabelled_split).  evolution: pfdr.EVOLUTION_* (AUTO:
-    sequential rounding from 2^17 vertices, as one GPU).  Returns (X, it, Obj, Dif, info)
+    sequential rounding from 2^17 vertices, as one GPU).  spec: pfdr.SPEC_* (the
+    speculative decisions' concurrency).  Returns (X, it, Obj, Dif, info)
     with X for all vertices in the caller's labels."""
     lib = pfdr.load()
     Kw = max(int(K), 1)
@@ -201,7 +203,7 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
                              record_dif=record_dif, K=K, al=al, nranks=k, rank=r, comm=hub.value,
                              comm_kind=COMM_LOOPBACK, vtx_begin=v0, V_global=V, e_global=e,
                              vtx_label=None if order is None else order[v0:v1],
-                             evolution=evolution)
+                             evolution=evolution, spec=spec)
             queries[r] = {q: s.query(q) for q in ("ghosts", "speculative", "seqdif")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
                 queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks",

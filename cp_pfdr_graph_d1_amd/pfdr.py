@@ -29,7 +29,10 @@ SCAL, DIAG = 0, 1
 REORDER_AUTO, REORDER_ON, REORDER_OFF = 0, 1, 2
 # iterate-evolution statistic (include/pfdr_mi355x.h PFDR_EVOLUTION_*)
 EVOLUTION_AUTO, EVOLUTION_SEQUENTIAL, EVOLUTION_TREE = 0, 1, 2
-ABI_VERSION = 3  # pfdr_abi_version() of the matching library
+# speculative decisions (PFDR_SPEC_*): own stream / split communicator,
+# serial on the session stream over one communicator, or none
+SPEC_AUTO, SPEC_SERIAL, SPEC_OFF = 0, 1, 2
+ABI_VERSION = 4  # pfdr_abi_version() of the matching library
 
 # every C entry point of include/pfdr_mi355x.h
 EXPORTED = (
@@ -94,6 +97,7 @@ class Problem(C.Structure):
         ("reorder", C.c_int),
         ("evolution", C.c_int),
         ("vtx_label", C.c_void_p),
+        ("spec", C.c_int),
     ]
 
 
@@ -136,7 +140,10 @@ def load():
         lib.pfdr_comm_init.argtypes = [C.POINTER(C.c_void_p), C.c_int,
                                        C.c_int, C.c_void_p]
         lib.pfdr_comm_destroy.argtypes = [C.c_void_p]
-        if lib.pfdr_abi_version() != ABI_VERSION:
+        # (PFDR_LIB_PATH: an A/B against a build of the previous ABI, 3, which
+        # reads the problem without its trailing `spec` field)
+        old_ok = bool(os.environ.get("PFDR_LIB_PATH")) and lib.pfdr_abi_version() == 3
+        if lib.pfdr_abi_version() != ABI_VERSION and not old_ok:
             raise PFDRError("%s has ABI %d, this module expects %d: rebuild it" % (
                 LIB_PATH, lib.pfdr_abi_version(), ABI_VERSION))
         _LIB = lib
@@ -479,7 +486,7 @@ class Session:
                  record_dif=False, verbose=0, device=False, nranks=0, rank=0,
                  comm=None, comm_kind=0, vtx_begin=0, V_global=0, e_global=None,
                  e_offset=0, reorder=REORDER_AUTO, evolution=EVOLUTION_AUTO,
-                 vtx_label=None):
+                 vtx_label=None, spec=SPEC_AUTO):
         self.lib = load()
         ct, _, dcode = _real(dtype)
         self._keep = []
@@ -514,6 +521,7 @@ class Session:
         p.vtx_begin, p.V_global, p.e_offset = vtx_begin, V_global, e_offset
         p.reorder = reorder
         p.evolution = evolution
+        p.spec = spec
         if vtx_label is not None:
             vl = np.ascontiguousarray(vtx_label, np.int64)
             self._keep.append(vl)

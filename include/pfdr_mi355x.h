@@ -56,7 +56,7 @@ extern "C" {
 #define PFDR_LIPSCHITZ_DIAG 1
 
 const char *pfdr_last_error(void);
-int pfdr_abi_version(void);          /* 3 (pfdr_problem.evolution added) */
+int pfdr_abi_version(void);          /* 4 (pfdr_problem.spec added) */
 int pfdr_device_count(void);         /* visible HIP devices, <0 on error */
 
 /* ------------------------------------------------------------------ l1 -- */
@@ -148,6 +148,21 @@ int pfdr_proj_simplex_metric_f64(double *X, const double *M, int D, int N,
 #define PFDR_EVOLUTION_AUTO 0
 #define PFDR_EVOLUTION_SEQUENTIAL 1
 #define PFDR_EVOLUTION_TREE 2
+/* speculative decisions (pfdr_problem.spec; env PFDR_SPEC = auto | serial |
+ * off overrides): sessions with a sequential evolution statistic, difRcd = 0
+ * and no objective record decide on iteration t while t + 1 sweeps.
+ *   AUTO   the evolution sums and the decision run on a second stream; a
+ *          partition runs them over a communicator split from its own
+ *          (ncclCommSplit) beside the next iteration's halo exchanges --
+ *          concurrent operations on two communicators, which NCCL/RCCL do
+ *          not guarantee to co-schedule;
+ *   SERIAL the same buffers and decisions on the session stream over the one
+ *          communicator: no split, no second stream, no concurrency; results
+ *          identical bit for bit, the decision no longer overlapped;
+ *   OFF    the plain sequential loop (identical results). */
+#define PFDR_SPEC_AUTO 0
+#define PFDR_SPEC_SERIAL 1
+#define PFDR_SPEC_OFF 2
 
 typedef struct pfdr_problem {
     int kind;             /* PFDR_KIND_* */
@@ -190,6 +205,8 @@ typedef struct pfdr_problem {
                              the caller's label order (all-reduced, then summed
                              in that order on every rank), as the reference's
                              one-thread loop does (quadratic solvers). */
+    /* --- speculative decisions ---------------------------------------------- */
+    int spec;             /* PFDR_SPEC_* (0: AUTO) */
 } pfdr_problem;
 
 typedef struct pfdr_session pfdr_session;

@@ -69,7 +69,7 @@ def test_dropin_symbols_equal_reference_build():
 
 
 def test_abi_version():
-    assert pfdr.load().pfdr_abi_version() == pfdr.ABI_VERSION == 3
+    assert pfdr.load().pfdr_abi_version() == pfdr.ABI_VERSION == 4
 
 
 @pytest.mark.parametrize("shape", [(7, 5, 4), (12, 9, 6), (3, 3, 3)])

@@ -46,6 +46,7 @@ import fullsize_cases as F
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize")
 DENSE = ("c3_direct_k2", "c3_ata_k3")
+SPEC = {"auto": 0, "serial": 1, "off": 2}  # pfdr.SPEC_*
 
 
 def _gold(name):
@@ -106,11 +107,15 @@ def test_fullsize_matches_reference(gpu_lib, name):
         assert below.size and below[0] == it - 1
 
 
-@pytest.mark.parametrize("name,k,relabel", [("headline_conv", 2, False), ("c4_conv", 2, False),
-                                            ("headline_conv", 3, False), ("c2_conv", 4, False),
-                                            ("c5_k1", 8, False), ("headline_conv", 2, True),
-                                            ("c4k100_conv", 3, False)])
-def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k, relabel):
+@pytest.mark.parametrize("name,k,relabel,spec", [
+    ("headline_conv", 2, False, "auto"), ("c4_conv", 2, False, "auto"),
+    ("headline_conv", 3, False, "auto"), ("c2_conv", 4, False, "auto"),
+    ("c5_k1", 8, False, "auto"), ("headline_conv", 2, True, "auto"),
+    ("c4k100_conv", 3, False, "auto"),
+    # the speculative pipeline on one stream and one transport (PFDR_SPEC_SERIAL)
+    ("headline_conv", 2, False, "serial"), ("headline_conv", 3, False, "serial"),
+    ("c4k100_conv", 2, False, "serial"), ("c4k100_conv", 3, False, "serial")])
+def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k, relabel, spec):
     """The converged full-size solves split over k ranks (loopback threads on
     one GPU: the RCCL session code with device-copy exchanges), and C5 (640^3,
     262M vertices, the 8-GPU configuration) split over 8 ranks: the iterate
@@ -121,7 +126,9 @@ def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k, rela
     difRcd = 0 the ranks decide speculatively (the evolution chain of t on a
     split transport beside t + 1's exchanges); relabel: the headline's
     vertices renumbered breadth-first before the split, the evolution terms
-    routed back to caller-order slices (TermRoute) before the chain."""
+    routed back to caller-order slices (TermRoute) before the chain.  spec
+    "serial": the same speculative buffers and decisions on each rank's
+    session stream over its one transport (no split, no second stream)."""
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
     g = _gold(name)
@@ -133,21 +140,24 @@ def test_fullsize_partitioned_converged_matches_reference(gpu_lib, name, k, rela
             k, pfdr.PFDR_KIND_SIMPLEX, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["P0"], a["Q"],
             La_l1=a["La_f"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
             difTol=a["difTol"], itMax=a["itMax"], record_dif=True, K=a["K"], al=a["al"],
-            relabel=relabel)
+            relabel=relabel, spec=SPEC[spec])
     elif case["solver"] == "bounds":  # C5: 640^3, the 8-GPU configuration, as 8 ranks
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_BOUNDS, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
             lo=a["lo"], hi=a["hi"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
-            difTol=a["difTol"], itMax=a["itMax"], record_dif=True)
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, spec=SPEC[spec])
     else:
         X, it, _, Dif, info = P.solve_loopback(
             k, pfdr.PFDR_KIND_L1, np.float32, a["Eu"], a["Ev"], a["La_d1"], a["X0"], a["Y"],
             La_l1=a["La_l1"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
-            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, relabel=relabel)
+            difTol=a["difTol"], itMax=a["itMax"], record_dif=True, relabel=relabel,
+            spec=SPEC[spec])
     d = F.digest(X, it, Dif[:it], case["sample_m"])
-    print("%s k=%d relabel=%s: it %d/%d sha256 equal %s speculative %s" % (
-        name, k, relabel, it, int(g["it"]), str(d["sha256"]) == str(g["sha256"]),
+    print("%s k=%d relabel=%s spec=%s: it %d/%d sha256 equal %s speculative %s" % (
+        name, k, relabel, spec, it, int(g["it"]), str(d["sha256"]) == str(g["sha256"]),
         [q["speculative"] for q in info["queries"]]))
     assert it == int(g["it"])
     assert np.array_equal(Dif[:it], g["Dif"][:it]), "partitioned Dif differs from the reference"
     assert str(d["sha256"]) == str(g["sha256"])
+    if a["difRcd"] == 0 and a["difTol"] > 0:  # every rank speculates: 1 split, 2 serial
+        assert [q["speculative"] for q in info["queries"]] == [2 if spec == "serial" else 1] * k

@@ -58,8 +58,9 @@ def test_gram_short_last_chunk(gpu_lib):
 def test_gram_huge_entries(gpu_lib, which):
     """an entry past the largest bf16 (3.4e38) is split by truncation, not
     rounded to inf: its finite products stay finite and exact to f32.  A
-    product that overflows f32 is inf on the exact-f32 tile and may be NaN
-    on the split one (its pieces' products overflow with both signs)"""
+    product that overflows f32 is +inf, as in the reference's f32 sums: the
+    split tile's pieces would overflow with both signs (NaN), so its NaN
+    flag sends the Gram to the exact-f32 tile (pfdr_gram.hip gram())"""
     rng = np.random.default_rng(3)
     B = rng.uniform(-1, 1, (128, 64)).astype(np.float32)  # rows = Gram index
     B[:, 0] = 0.0
@@ -69,11 +70,34 @@ def test_gram_huge_entries(gpu_lib, which):
     G, _ = pfdr.gram(A, which)
     B64 = B.astype(np.float64)
     ref = B64 @ B64.T
-    assert not np.isfinite(G[0, 0])
+    assert np.isposinf(G[0, 0])
     assert abs(G[0, 1] - ref[0, 1]) <= 1e-6 * abs(ref[0, 1]) and G[0, 1] == G[1, 0]
     sub, rsub = G[1:, 1:].astype(np.float64), ref[1:, 1:]
     assert np.linalg.norm(sub - rsub) <= 2e-6 * np.linalg.norm(rsub)
     assert np.all(np.isfinite(G[0, 1:]))
+
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_gram_infinite_entry(gpu_lib, which):
+    """an infinite entry gives the exact-f32 tile's signed infinities (the
+    split would give NaN: h = inf, m = inf - inf); rows and columns away from
+    it stay finite and accurate"""
+    rng = np.random.default_rng(4)
+    B = rng.uniform(0.5, 1.0, (96, 48)).astype(np.float32)
+    B *= np.where(rng.random(B.shape) < 0.5, -1, 1).astype(np.float32)
+    B[2, 5] = np.inf
+    A = B if which == 1 else np.ascontiguousarray(B.T)
+    G, _ = pfdr.gram(A, which)
+    want = np.sign(B[:, 5]).astype(np.float32) * np.float32(np.inf)
+    want[2] = np.inf
+    assert np.array_equal(G[2], want) and np.array_equal(G[:, 2], want)
+    keep = np.arange(96) != 2
+    sub = G[np.ix_(keep, keep)].astype(np.float64)
+    B64 = B[keep].astype(np.float64)
+    ref = B64 @ B64.T
+    assert np.all(np.isfinite(sub))
+    assert np.linalg.norm(sub - ref) <= 2e-6 * np.linalg.norm(ref)
 
 
 def _spectral(M, N, s, seed, dt):

@@ -15,7 +15,7 @@ CASES = ["l1_grid2d_f64", "l1_grid2d_f32", "l1_knn_shuffled_f32", "l1_l22_f64",
          "bounds_upper_recond_f32", "l1_chain_kat_f64"] + G.names("simplex_")
 
 
-def _solve(c, k, fixed, evolution=0, record_obj=True):
+def _solve(c, k, fixed, evolution=0, record_obj=True, spec=0):
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
     a = dict(c)
@@ -28,7 +28,7 @@ def _solve(c, k, fixed, evolution=0, record_obj=True):
             La_l1=a["La_f"], rho=float(a["rho"]), condMin=float(a["condMin"]),
             difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
             record_obj=record_obj, record_dif=True, K=int(a["K"]), al=float(a["al"]),
-            evolution=evolution)
+            evolution=evolution, spec=spec)
     kind = pfdr.PFDR_KIND_L1 if str(a["solver"]) == "l1" else pfdr.PFDR_KIND_BOUNDS
     X0 = a["X0"]
     return P.solve_loopback(
@@ -37,7 +37,7 @@ def _solve(c, k, fixed, evolution=0, record_obj=True):
         lo=float(a.get("lo", -np.inf)), hi=float(a.get("hi", np.inf)), Ltype=int(a["Ltype"]),
         L=a["L"], rho=float(a["rho"]), condMin=float(a["condMin"]),
         difRcd=float(a["difRcd"]), difTol=float(a["difTol"]), itMax=int(a["itMax"]),
-        record_obj=record_obj, record_dif=True, evolution=evolution)
+        record_obj=record_obj, record_dif=True, evolution=evolution, spec=spec)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -84,12 +84,14 @@ def test_partitioned_sequential_evolution_equals_reference(gpu_lib, name, k):
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("k", [2, 3])
-def test_partitioned_speculative_equals_reference(gpu_lib, name, k):
+@pytest.mark.parametrize("spec", ["auto", "serial"])
+def test_partitioned_speculative_equals_reference(gpu_lib, name, k, spec):
     """difRcd = 0 and no objective record: the partition decides
     speculatively -- the evolution chain and decision of iteration t run on a
     second stream over the split transport, beside the halo exchanges and
-    sweeps of t + 1 (X / P ping-ponged) -- and the stopping iteration, every
-    Dif and X still equal the reference's bit for bit"""
+    sweeps of t + 1 (X / P ping-ponged); serial: the same on the session
+    stream over the one transport -- and the stopping iteration, every Dif
+    and X still equal the reference's bit for bit"""
     from cp_pfdr_graph_d1_amd import pfdr
     c, g = G.load(name)
     V = c["X0"].size if "X0" in c else c["P0"].size // int(c["K"])
@@ -97,9 +99,11 @@ def test_partitioned_speculative_equals_reference(gpu_lib, name, k):
         pytest.skip("graph too small for %d ranks" % k)
     if float(c["difRcd"]) != 0.0:
         pytest.skip("reconditioning: no speculation")
-    X, it, _, Dif, info = _solve(c, k, False, pfdr.EVOLUTION_SEQUENTIAL, record_obj=False)
-    print("%s k=%d it=%d/%d" % (name, k, it, int(g["conv_it"])))
-    assert all(q["speculative"] == 1 for q in info["queries"])
+    mode = pfdr.SPEC_SERIAL if spec == "serial" else pfdr.SPEC_AUTO
+    X, it, _, Dif, info = _solve(c, k, False, pfdr.EVOLUTION_SEQUENTIAL, record_obj=False,
+                                 spec=mode)
+    print("%s k=%d spec=%s it=%d/%d" % (name, k, spec, it, int(g["conv_it"])))
+    assert all(q["speculative"] == (2 if spec == "serial" else 1) for q in info["queries"])
     assert it == int(g["conv_it"])
     assert np.array_equal(X, g["conv_X"])
     assert np.array_equal(Dif[:it], g["conv_Dif"][:it])
@@ -344,3 +348,133 @@ def test_relabelled_partition_random_labels(gpu_lib, k, kind):
     assert 0 < it1 < kw["itMax"] and itr == it1
     assert np.array_equal(Dr[:itr], D1[:it1])
     assert np.array_equal(Xr, X1)
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        import os
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        import os
+        for k, v in self.old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("kind", ["l1", "simplex"])
+def test_rccl_single_rank_real_calls_graph_replay(gpu_lib, kind):
+    """PFDR_RCCL_SELF=1: a 1-rank communicator issues every RCCL operation a
+    real partition would (the exchanges and chain steps as grouped
+    send / receive pairs to itself, the all-reduces and broadcasts as 1-rank
+    collectives) instead of returning early, and the chunks of iterations
+    capture them in hipGraphs: the iterates, counts and Dif equal the
+    single-GPU session's bit for bit"""
+    import ctypes as C
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation, simplex_observation
+    lib = pfdr.load()
+    dt = np.float32
+    shape = (128, 96)
+    V = int(np.prod(shape))
+    if kind == "l1":
+        Eu, Ev = grid_graph(shape, 4)
+        args = (pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                np.zeros(V, dt), piecewise_observation(shape, 3, dt))
+        kw = dict(La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=1e-5, difRcd=1e-2)
+    else:
+        Eu, Ev = grid_graph(shape, 8)
+        v = np.arange(V)
+        Q = simplex_observation(V, 4, 4, (v * 4) // V, dt)
+        args = (pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.05, dt),
+                Q.copy(), Q)
+        kw = dict(K=4, al=0.1, rho=1.0, condMin=0.1, difTol=1e-5, difRcd=1e-2)
+    kw.update(itMax=1000, record_dif=True, evolution=pfdr.EVOLUTION_SEQUENTIAL)
+    out = []
+    with _env(PFDR_RCCL_SELF="1"):
+        idb = (C.c_char * 128)()
+        assert lib.pfdr_comm_unique_id(idb) == 0
+        comm = C.c_void_p()
+        assert lib.pfdr_comm_init(C.byref(comm), 1, 0, idb) == 0, lib.pfdr_last_error()
+        try:
+            for part in (False, True):
+                extra = dict(nranks=1, rank=0, comm=comm.value, comm_kind=P.COMM_RCCL,
+                             vtx_begin=0, V_global=V) if part else {}
+                s = pfdr.Session(*args, **kw, **extra)
+                try:
+                    if part:
+                        assert s.query("graphs") == 1
+                    for n in (50, 950):
+                        s.run(n)
+                    out.append(s.result())
+                finally:
+                    s.close()
+        finally:
+            lib.pfdr_comm_destroy(comm)
+    (X0, it0, _, D0), (X1, it1, _, D1) = out
+    print("%s: it %d / %d" % (kind, it0, it1))
+    assert 0 < it0 < 1000 and it1 == it0
+    assert np.array_equal(X1, X0)
+    assert np.array_equal(D1[:it1], D0[:it0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("spec", ["auto", "serial", "off"])
+def test_rccl_single_rank_real_calls_headline_conv(gpu_lib, spec):
+    """the converged full-size headline (10M vertices, 60M edges, difTol
+    1e-5) as a 1-rank RCCL partition with PFDR_RCCL_SELF=1, in every
+    speculation mode: auto (the evolution chain on a split communicator and a
+    second stream), serial (one stream, one communicator), off (the plain
+    loop, its chunks captured in hipGraphs with the RCCL calls inside):
+    sha256 of X, the iteration count and every Dif equal the reference's"""
+    import ctypes as C
+    import fullsize_cases as F
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize",
+                             "headline_conv.npz"))
+    case = F.build("headline_conv")
+    assert F.input_digest(case) == str(g["in_sha256"])
+    a = case["args"]
+    lib = pfdr.load()
+    mode = {"auto": pfdr.SPEC_AUTO, "serial": pfdr.SPEC_SERIAL, "off": pfdr.SPEC_OFF}[spec]
+    V = a["X0"].size
+    with _env(PFDR_RCCL_SELF="1"):
+        idb = (C.c_char * 128)()
+        assert lib.pfdr_comm_unique_id(idb) == 0
+        comm = C.c_void_p()
+        assert lib.pfdr_comm_init(C.byref(comm), 1, 0, idb) == 0, lib.pfdr_last_error()
+        try:
+            s = pfdr.Session(pfdr.PFDR_KIND_L1, np.float32, V, a["Eu"].size, a["Eu"], a["Ev"],
+                             a["La_d1"], a["X0"], a["Y"], La_l1=a["La_l1"], Ltype=a["Ltype"],
+                             L=a["L"], rho=a["rho"], condMin=a["condMin"], difRcd=a["difRcd"],
+                             difTol=a["difTol"], itMax=a["itMax"], record_dif=True, nranks=1,
+                             rank=0, comm=comm.value, comm_kind=P.COMM_RCCL, vtx_begin=0,
+                             V_global=V, spec=mode)
+            try:
+                q = {k: s.query(k) for k in ("speculative", "graphs", "seqdif")}
+                s.prepare(a["itMax"])
+                s.run(a["itMax"])
+                X, it, _, Dif = s.result()
+            finally:
+                s.close()
+        finally:
+            lib.pfdr_comm_destroy(comm)
+    d = F.digest(X, it, Dif[:it], case["sample_m"])
+    print("headline_conv 1-rank RCCL (self calls) spec=%s %s: it %d/%d sha256 equal %s" % (
+        spec, q, it, int(g["it"]), str(d["sha256"]) == str(g["sha256"])))
+    assert q["seqdif"] == 1
+    assert q["speculative"] == {"auto": 1, "serial": 2, "off": 0}[spec]
+    if spec == "off":
+        assert q["graphs"] == 1  # the RCCL calls replayed inside captured chunks
+    assert it == int(g["it"])
+    assert np.array_equal(Dif[:it], g["Dif"][:it])
+    assert str(d["sha256"]) == str(g["sha256"])

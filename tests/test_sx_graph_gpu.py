@@ -42,7 +42,8 @@ class _env:
 def test_sx_graph_golden_identical(gpu_lib, name, fixed):
     c, g = G.load(name)
     res = []
-    for env in ({}, {"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "100000000"}):
+    for env in ({}, {"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "100000000"},
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1"}):  # edges in tile order
         with _env(**env):
             res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
     X0, it0, _, D0 = res[0]
@@ -77,7 +78,9 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
     Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
     res = []
     for env in ({"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "0", "launch": "direct"},
-                {"PFDR_SX_TINY": "100000000"}, {}):
+                {"PFDR_SX_TINY": "100000000"}, {},
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1"},
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "launch": "direct"}):
         direct = env.pop("launch", None) == "direct"
         with _env(**env):
             s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev,
@@ -90,6 +93,8 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
                 assert s.query("tiny") == (1 if nb <= 32 else 0)
             elif env.get("PFDR_SX_TINY") == "0":
                 assert s.query("tiny") == 0
+            if env.get("PFDR_SX_TILE") == "1":
+                assert s.query("tiled_blocks") == (nb if K <= 64 else 0)
             if direct:  # profiled: every chunk launched directly, no graph replay
                 s.profile(True)
             for n in runs:
@@ -103,3 +108,47 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
         assert it1 == it0
         assert np.array_equal(X1, X0)
         assert np.array_equal(D1[:it1], D0[:it0])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("K,al,difRcd", [(10, 0.1, 1e-2), (8, 1.0, 0.0), (3, 0.0, 1e-1),
+                                         (64, 0.2, 0.0), (7, 0.1, 1e-2)])
+def test_sx_tile_order_identical(gpu_lib, dt, K, al, difRcd):
+    """Edges in tile order (PFDR_SX_TILE=1: stably sorted by (u block, v
+    block), La_d1 permuted with them, the incidence keys the original ids)
+    against the caller's order, on a shuffled k-NN-like graph with
+    duplicates, self-loops, both end orders and per-edge weights, with and
+    without reconditionings: identical iterates, counts and Dif."""
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    rng = np.random.default_rng(K * 7 + int(al * 10))
+    Eu, Ev = grid_graph((70, 60), 8)
+    V = 70 * 60
+    flip = rng.random(Eu.size) < 0.3
+    Eu, Ev = np.where(flip, Ev, Eu), np.where(flip, Eu, Ev)
+    extra = rng.integers(0, V, (2, 500)).astype(np.int32)
+    extra[1, :50] = extra[0, :50]  # self-loops
+    Eu = np.concatenate([Eu, extra[0], Eu[:300]]).astype(np.int32)  # + duplicates
+    Ev = np.concatenate([Ev, extra[1], Ev[:300]]).astype(np.int32)
+    p = rng.permutation(Eu.size)
+    Eu, Ev = Eu[p], Ev[p]
+    La = (0.02 + 0.06 * rng.random(Eu.size)).astype(dt)
+    Q = rng.random((V, K))
+    Q[: V // 3, 1 % K] += 1.5
+    Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
+    res = []
+    for tile in ("0", "1"):
+        with _env(PFDR_SX_TINY="0", PFDR_SX_TILE=tile):
+            s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, La, Q.copy(), Q,
+                             K=K, al=al, rho=1.0, condMin=0.1, difRcd=difRcd, difTol=1e-6,
+                             itMax=150, record_dif=True)
+        try:
+            assert (s.query("tiled_blocks") > 0) == (tile == "1")
+            s.run(150)
+            res.append(s.result())
+        finally:
+            s.close()
+    (X0, it0, _, D0), (X1, it1, _, D1) = res
+    assert it0 == it1 and it0 > 0
+    assert np.array_equal(X0, X1)
+    assert np.array_equal(D0[:it0], D1[:it1])
