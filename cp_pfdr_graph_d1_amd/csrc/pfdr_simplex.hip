@@ -161,6 +161,43 @@ __device__ void proj_simplex_column(real *x, const real *m, int D, real a) {
     for (int d = 0; d < D; d++) x[d] = ((act >> d) & 1ull) ? (x[d] - la) * m[d] : real(0);
 }
 
+// The same projection with the coordinates already divided by their metric
+// (x[d] / m[d], the reference's division, done in parallel by the item
+// lanes) and the raw x[0] aside: the walk keeps only the active-set
+// updates' divisions (bit-identical to proj_simplex_column)
+template <typename real>
+__device__ void proj_simplex_column_div(real *x, const real *m, int D, real x0, real a) {
+    unsigned long long act = 1ull;
+    real la = (x0 - a) / m[0];
+    real s = m[0];
+    for (int d = 1; d < D; d++) {
+        const real xd = x[d];
+        if (xd > la) {
+            const real md = m[d];
+            act |= 1ull << d;
+            s += md;
+            la += md * (xd - la) / s;
+        }
+    }
+    bool changed = true;
+    while (changed) {
+        changed = false;
+        for (int d = 0; d < D; d++) {
+            if ((act >> d) & 1ull) {
+                const real xd = x[d];
+                if (xd < la) {
+                    act &= ~(1ull << d);
+                    const real md = m[d];
+                    s -= md;
+                    la += md * (la - xd) / s;
+                    changed = true;
+                }
+            }
+        }
+    }
+    for (int d = 0; d < D; d++) x[d] = ((act >> d) & 1ull) ? (x[d] - la) * m[d] : real(0);
+}
+
 // ------------------------------------------------------------- kernels --
 template <typename real>
 __global__ void k_sx_z_init(long EK, int K, const int *__restrict__ Eu,
@@ -656,6 +693,11 @@ struct SxVArgs {
     // P lives in the .x half of PF only (no P store; the evolution reads
     // the old P from PF; SimplexSession::sync_p extracts it when asked)
     int nop;
+    // tile-ordered sessions (sx_tile_sum): per vertex block a 32-int record
+    // of its runs (null: no tiles; a block whose record says 0 runs takes
+    // the CSR gather) and the slot of every edge end in its block's list
+    const int *trec;
+    const unsigned short *sl;
 };
 
 template <typename real>
@@ -663,10 +705,15 @@ __device__ __forceinline__ real sx_inv(const SxVArgs<real> &a, long v, long i) {
     return a.invV ? a.invV[v] : a.invAux[i];
 }
 // the splitting-weight factor of a local incidence (ref :199-217): A1 after
-// a reconditioning, else La_d1 (one kernel argument when uniform)
+// a reconditioning, else La_d1 (one kernel argument la0 when uniform: the
+// caller passes it by value -- a conditional between the argument and an
+// array element written as one lvalue made the compiler copy the argument
+// to scratch and load the element through a selected pointer)
 template <typename real>
-__device__ __forceinline__ real sx_wa(const SxVArgs<real> &a, long i, long e) {
-    return a.A1 ? a.A1[i] : (a.la_u ? a.la0 : a.La_d1[e]);
+__device__ __forceinline__ real sx_wa(const SxVArgs<real> &a, long i, long e, bool lu, real la0) {
+    if (a.A1) return a.A1[i];
+    if (lu) return la0;
+    return a.La_d1[e];
 }
 template <typename real>
 __device__ __forceinline__ real sx_pold(const SxVArgs<real> &a, long i) {
@@ -681,6 +728,8 @@ template <typename real>
 __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int k) {
     const int K = a.c.K;
     const real inv = sx_inv(a, v, v * K + k);  // 1/Aux of this (v, k)
+    const bool lu = a.la_u != 0;
+    const real la0 = a.la0;
     const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
     real s = real(0);
     int j = j0;
@@ -703,7 +752,7 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
                 const long ea = sv ? ad - a.E : ad;
                 rq[q] = ea >= a.E;
                 zq[q] = (sv ? a.Zv : a.Zu)[ea * K + k];
-                aq[q] = sx_wa(a, rq[q] ? 0 : ea * K + k, rq[q] ? 0 : ea);
+                aq[q] = sx_wa(a, rq[q] ? 0 : ea * K + k, rq[q] ? 0 : ea, lu, la0);
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) w[q] = rq[q] ? zq[q] : (aq[q] * inv) * zq[q];
@@ -717,7 +766,106 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
         const long ea = sv ? ad - a.E : ad;
         const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
         if (ea >= a.E) s += z;
-        else s += (sx_wa(a, ea * K + k, ea) * inv) * z;
+        else s += (sx_wa(a, ea * K + k, ea, lu, la0) * inv) * z;
+    }
+    return s;
+}
+
+// ---------------------------------------- tile-ordered sums (K <= 64) ---
+// Ordered DR averages of vertex block blk from its tile runs (SxVArgs::trec,
+// see k_sx_tile_keys): the u-end rows of Z of the block's own edges (one
+// run) and the v-end rows of the (u block, blk) tiles (a few runs), read
+// once, coalesced, by this workgroup alone, and written into LDS at their
+// SLOT -- the (e, side) rank in the block's CSR-ordered list (sl) -- so
+// that each (vertex, label) lane then adds its vertex's entries in the
+// reference's order (ref :636-648) with the products of sx_item_sum: the
+// same sums bit for bit, one round of loads (record, then the runs) where
+// the CSR gather had two dependent ones (pointers, addresses, values).
+// Record: [runs n, u start, u count, (v start, count) x (n - 1)] in edge
+// units, n <= kSxRuns; the lane's slots [my0, my1) from the CSR pointers.
+constexpr int kSxRuns = 15, kSxRec = 32;
+template <typename real> struct SxTileCap { static constexpr int v = 3072; };  // LDS reals
+template <> struct SxTileCap<double> { static constexpr int v = 1536; };
+
+// WA: per-incidence weights staged too (per-edge La_d1: one per slot in
+// al[]; A1: K per slot in al[]); else the one weight la0
+template <typename real, bool WA>
+__device__ __forceinline__ real sx_tile_sum(const SxVArgs<real> &a, int blk, int t, bool live,
+                                            long v, int k, real inv, real *zl, real *al,
+                                            int *rt) {
+    const int K = a.c.K;
+    const int lane = t & (kWave - 1);
+    const long v0 = (long)blk * a.vb;
+    const int rv = lane < kSxRec ? a.trec[(long)blk * kSxRec + lane] : 0;
+    const int nr = __builtin_amdgcn_readfirstlane(__shfl(rv, 0, kWave));
+    // run r in lane r: start, length (edge ends); values K per end
+    const int st = __shfl(rv, min(1 + 2 * lane, kWave - 1), kWave);
+    const int ln = lane < nr ? __shfl(rv, min(2 + 2 * lane, kWave - 1), kWave) : 0;
+    int P = ln * K;  // inclusive prefix of the runs' values
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(P, o, kWave);
+        if (lane >= o) P += y;
+    }
+    const int tot = __builtin_amdgcn_readlane(P, kWave - 1);
+    // the run table in LDS for the item loop below (its lanes diverge)
+    if (t < kSxRuns + 1) {
+        rt[t] = t < nr ? st : 0;
+        rt[kSxRuns + 1 + t] = t < nr ? P : 0x7fffffff;
+    }
+    __syncthreads();
+    int my0 = 0, my1 = 0;
+    if (live) {
+        const int b0 = a.ptr[v0];
+        my0 = a.ptr[v] - b0;
+        my1 = a.ptr[v + 1] - b0;
+    }
+    const long E = a.E;
+    const bool per_e = WA && !a.A1;  // per-edge La_d1: one weight per slot
+    // each lane walks values q = t, t + NT, ...: its run only advances
+    const int *rst = rt, *rpr = rt + kSxRuns + 1;
+    int r = 0, pend = rpr[0], pbeg = 0;
+    constexpr int U = 4;
+    for (int q0 = t; q0 < tot; q0 += U * kBlock) {
+        real z[U], w[U];
+        int sl[U], kk[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int q = q0 + u * kBlock;
+            ok[u] = q < tot;
+            const int qq = ok[u] ? q : tot - 1;
+            while (pend <= qq) {
+                pbeg = pend;
+                pend = rpr[++r];
+            }
+            const int sr = rst[r];
+            const unsigned off = (unsigned)(qq - pbeg);
+            const unsigned ei = off / (unsigned)K;
+            kk[u] = (int)(off - ei * (unsigned)K);
+            const long p = (long)sr + ei;
+            const bool sv = r > 0;
+            z[u] = (sv ? a.Zv : a.Zu)[p * K + kk[u]];
+            sl[u] = a.sl[(sv ? E : 0) + p];
+            w[u] = real(0);
+            if (WA) w[u] = a.A1 ? a.A1[p * K + kk[u]] : (kk[u] == 0 ? a.La_d1[p] : real(0));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (ok[u]) {
+                zl[sl[u] * K + kk[u]] = z[u];
+                if (WA) {
+                    if (!per_e) al[sl[u] * K + kk[u]] = w[u];
+                    else if (kk[u] == 0) al[sl[u]] = w[u];
+                }
+            }
+    }
+    __syncthreads();
+    real s = real(0);
+    const real la0 = a.la0;
+    for (int j = my0; j < my1; j++) {
+        const real an = !WA ? la0 : (per_e ? al[j] : al[j * K + k]);
+        s += (an * inv) * zl[j * K + k];
     }
     return s;
 }
@@ -729,9 +877,13 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
 // The body of k_sx_vertex_sweep, shared with the one-workgroup
 // k_sx_tiny_iterate (four blocks side by side).
 // SPLIT (speculative sessions): the new P and (P, step) go to Po / PFo
-template <typename real, int NT, bool SPLIT = false>
+// TL: the block sums from its tile runs (sx_tile_sum; zl / al its LDS
+// lists, WA its staged weights) when its record has runs, else the CSR gather
+template <typename real, int NT, bool SPLIT = false, bool TL = false, bool WA = false>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
-                                                real *ms, real *red, real *part_out) {
+                                                real *ms, real *red, real *part_out,
+                                                real *x0s = nullptr, real *zl = nullptr,
+                                                real *al = nullptr, int *rt = nullptr) {
     const int K = a.c.K, vb = a.vb;
     const int vl = t / K;
     const int k = t - vl * K;
@@ -739,15 +891,37 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     const long v = v0 + vl;
     const bool live = blk < a.nb && vl < vb && v < a.V;
     const long i = v * K + k;
+    // the item's operands before the sum (their latency hides under it)
+    real ga = real(0), gaq = real(0), qv = real(0), pold = real(0);
     if (live) {
-        xs[t] = sx_item_sum(a, v, k);
-        ms[t] = a.Ga[i];
+        ga = a.Ga[i];
+        gaq = a.GaQ[i];
+        if (a.c.loss == LOSS_QUAD) qv = a.Q[i];
+        if (a.track == 1) pold = sx_pold(a, i);
+    }
+    real x = real(0);
+    const bool tiled = TL && a.trec[(long)blk * kSxRec] > 0;  // block-uniform
+    if (tiled) {
+        const real inv = live ? sx_inv(a, v, i) : real(0);
+        x = sx_tile_sum<real, WA>(a, blk, t, live, v, k, inv, zl, al, rt);
+    } else if (live) {
+        x = sx_item_sum(a, v, k);
+    }
+    if (live) {
+        if (TL) {  // divided by the metric here (ref src/proj_simplex_metric.cpp:44, :49)
+            xs[t] = x / ga;
+            if (k == 0) x0s[vl] = x;
+        } else {
+            xs[t] = x;
+        }
+        ms[t] = ga;
     }
     __syncthreads();
     real dif = real(0);
     if (blk < a.nb && t < vb && v0 + t < a.V) {
         real *x = xs + t * K;
-        proj_simplex_column<real>(x, ms + t * K, K, real(1));
+        if (TL) proj_simplex_column_div<real>(x, ms + t * K, K, x0s[t], real(1));
+        else proj_simplex_column<real>(x, ms + t * K, K, real(1));
         if (a.track == 2) {
             real mx = x[0];
             int l = 0;
@@ -761,7 +935,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     if (live) {
         const real p = xs[t];
         if (a.track == 1) {
-            real d = sx_pold(a, i) - p;
+            real d = pold - p;
             if (d < real(0)) d = -d;
             dif += d;
             if (a.terms) a.terms[i] = d;
@@ -770,7 +944,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
         // Q enters the quadratic loss's step only (no load otherwise)
         SxR2<real> q;
         q.x = p;
-        q.y = sx_explicit(a.c, p, a.GaQ[i], a.c.loss == LOSS_QUAD ? a.Q[i] : real(0));
+        q.y = sx_explicit(a.c, p, gaq, qv);
         (SPLIT ? a.PFo : a.PF)[i] = q;
     }
     if (a.track) {
@@ -792,6 +966,22 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
     sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+}
+
+// tile-ordered sessions (sx_tile_sum)
+template <typename real, bool SPLIT, bool WA>
+__global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
+    if (a.ctrl && a.ctrl->halt) return;
+    constexpr int CAP = SxTileCap<real>::v;
+    __shared__ real xs[kBlock], ms[kBlock], x0s[kBlock];
+    __shared__ real red[kBlock / kWave];
+    __shared__ real zl[CAP];
+    __shared__ real al[WA ? CAP : 1];
+    __shared__ int rt[2 * (kSxRuns + 1)];
+    const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
+    if (blk >= a.nb) return;
+    sx_vertex_block<real, kBlock, SPLIT, true, WA>(a, blk, threadIdx.x, xs, ms, red, a.part + blk,
+                                                    x0s, zl, al, rt);
 }
 
 // ------------------------------------------ group vertex sweep (K > 64) --
@@ -866,13 +1056,17 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
     const int jb = lptr[0], nj = lptr[nv] - jb;
     const bool staged = nj <= SxGroup<real>::kInc * NV;
     if (staged) {
+        const bool lu = a.la_u != 0;
+        const real la0 = a.la0;
         for (int q = t; q < nj; q += kBlock) {
             const long ad = a.idx[jb + q];
             const bool sv = ad >= a.E;
             const long ea = sv ? ad - a.E : ad;
             const bool rq = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
             zo[q] = ea * K | (sv ? kZv : 0) | (rq ? kRecv : 0);
-            wa[q] = (rq || a.A1) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
+            real w = real(0);
+            if (!rq && !a.A1) w = lu ? la0 : a.La_d1[ea];
+            wa[q] = w;
         }
         __syncthreads();
     }
@@ -1025,6 +1219,8 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
     constexpr int B = J >= 8 ? 1 : 8 / J;
     const int K = a.c.K;
     const long b = v * K;
+    const bool lu = a.la_u != 0;
+    const real la0 = a.la0;
     real inv[J];
     bool ok[J];
 #pragma unroll
@@ -1046,7 +1242,8 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
             const long ea = sv ? ad - a.E : ad;
             rq[u] = ea >= a.E;  // received: the sender's W * Z in the tail of Zv
             const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
-            const real la = (a.A1 || rq[u]) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
+            real la = real(0);
+            if (!a.A1 && !rq[u]) la = lu ? la0 : a.La_d1[ea];
 #pragma unroll
             for (int j = 0; j < J; j++) {
                 const long k = k0 + lane + 64 * j;
@@ -1065,7 +1262,8 @@ __device__ __forceinline__ void sx_wide_sums(const SxVArgs<real> &a, long v, int
         const long ea = sv ? ad - a.E : ad;
         const bool rq = ea >= a.E;
         const real *zp = (sv ? a.Zv : a.Zu) + ea * K;
-        const real la = (a.A1 || rq) ? real(0) : (a.la_u ? a.la0 : a.La_d1[ea]);
+        real la = real(0);
+        if (!a.A1 && !rq) la = lu ? la0 : a.La_d1[ea];
 #pragma unroll
         for (int j = 0; j < J; j++) {
             const long k = k0 + lane + 64 * j;
@@ -1491,6 +1689,77 @@ __global__ void k_sx_permute(long E, const unsigned *__restrict__ perm, const re
     if (p < E) dst[p] = src[perm[p]];
 }
 
+// sl[address] = the slot of the edge end at that address (e: u end, E + e:
+// v end) in its vertex block's CSR list (vb vertices per block; clamped:
+// a block past 65,535 entries has no record)
+__global__ void k_sxt_slots(int V, int vb, const int *__restrict__ ptr,
+                            const unsigned *__restrict__ idx, unsigned short *__restrict__ sl) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const int base = ptr[v - v % vb];
+    for (int j = ptr[v]; j < ptr[v + 1]; j++) {
+        const int d = j - base;
+        sl[idx[j]] = (unsigned short)(d < 65535 ? d : 65535);
+    }
+}
+
+// ustart[b] = first position whose u end lies in block >= b (edges sorted
+// by u block), ustart[nb] = E
+__global__ void k_sxt_ustart(long E, int nb, int vb, const int *__restrict__ Eu,
+                             int *__restrict__ ustart) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > E) return;
+    const int lo = p == 0 ? 0 : Eu[p - 1] / vb + 1;
+    const int hi = p == E ? nb : Eu[p] / vb;
+    for (int b = lo; b <= hi; b++) ustart[b] = (int)p;
+}
+
+// v-end runs: maximal stretches of positions whose v end lies in one block
+__global__ void k_sxt_runs_count(long E, int vb, const int *__restrict__ Ev, int *__restrict__ cnt) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const int b = Ev[i] / vb;
+    if (i == 0 || Ev[i - 1] / vb != b) atomicAdd(cnt + b, 1);
+}
+__global__ void k_sxt_runs_fill(long E, int vb, const int *__restrict__ Ev,
+                                const int *__restrict__ tptr, int *__restrict__ fill,
+                                int *__restrict__ tstart, int *__restrict__ tlen) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const int b = Ev[i] / vb;
+    if (i != 0 && Ev[i - 1] / vb == b) return;
+    long q = i + 1;
+    while (q < E && Ev[q] / vb == b) q++;
+    const int j = tptr[b] + atomicAdd(fill + b, 1);
+    tstart[j] = (int)i;
+    tlen[j] = (int)(q - i);
+}
+
+// block b's record (sx_tile_sum): [runs, u start, u count, (v start, v
+// count) x runs - 1]; 0 runs (the CSR gather) when it has more than kSxRuns
+// runs or its list exceeds the LDS (cap reals, K per entry)
+__global__ void k_sxt_rec(int nb, int V, int vb, int K, int cap, const int *__restrict__ ptr,
+                          const int *__restrict__ ustart, const int *__restrict__ tptr,
+                          const int *__restrict__ tstart, const int *__restrict__ tlen,
+                          int *__restrict__ rec, int *__restrict__ nok) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    int *r = rec + (long)b * kSxRec;
+    for (int q = 0; q < kSxRec; q++) r[q] = 0;
+    const long v0 = (long)b * vb, v1 = min(v0 + vb, (long)V);
+    const long n = (long)ptr[v1] - ptr[v0];
+    const int t0 = tptr[b], nt = tptr[b + 1] - t0;
+    if (nt + 1 > kSxRuns || n * K > cap) return;
+    r[0] = nt + 1;
+    r[1] = ustart[b];
+    r[2] = ustart[b + 1] - ustart[b];
+    for (int q = 0; q < nt; q++) {
+        r[3 + 2 * q] = tstart[t0 + q];
+        r[4 + 2 * q] = tlen[t0 + q];
+    }
+    atomicAdd(nok, 1);
+}
+
 // *bad += the entries of La_d1 that differ from La_d1[0]
 template <typename real>
 __global__ void k_sx_uniform_check(long E, const real *__restrict__ x, int *__restrict__ bad) {
@@ -1657,6 +1926,9 @@ class SimplexSession final : public SessionBase {
     // kSxTileMinVK (edge, label) entries)
     bool sxtile_ = false;
     static constexpr long kSxTileMinVK = 1L << 21;
+    DevBuf<int> trec_;              // per vertex block: its runs (k_sxt_rec)
+    DevBuf<unsigned short> sl_;     // slot of every edge end (k_sxt_slots)
+    void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
     bool la_u_ = false;
     real la0_ = real(0);
@@ -1837,6 +2109,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64) {
         vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
+        if (sxtile_) build_sx_tiles();
     } else {  // groups of vertices with their columns in LDS, or a wave per vertex
         gnv_ = SxGroup<real>::nv_for(K_, SxGroup<real>::kNV);
         const long per = gnv_ ? gnv_ : (long)kSxWideVpw * (kBlock / kWave);
@@ -1968,6 +2241,38 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         device_bytes += (int64_t)(b->n * sizeof(real));
     device_bytes += (int64_t)((GI_.n + PF_.n + PFx_[0].n + PFx_[1].n + PFx_[2].n) *
                               sizeof(SxR2<real>));
+}
+
+// the runs and slots of every vertex block of a tile-ordered session (see
+// sx_tile_sum); blocks whose runs or list do not fit keep the CSR gather
+template <typename real>
+void SimplexSession<real>::build_sx_tiles() {
+    hipStream_t s = stream;
+    const int nb = nbs_, vb = vb_;
+    sl_.alloc((size_t)2 * E_);
+    k_sxt_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, vb, inc_.ptr.p, inc_.idx.p, sl_.p);
+    DevBuf<int> ustart((size_t)nb + 1), cnt(nb), fill(nb), nok(1);
+    k_sxt_ustart<<<grid_for(E_ + 1), kBlock, 0, s>>>(E_, nb, vb, Eu_.p, ustart.p);
+    PFDR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * nb, s));
+    PFDR_HIP(hipMemsetAsync(fill.p, 0, sizeof(int) * nb, s));
+    PFDR_HIP(hipMemsetAsync(nok.p, 0, sizeof(int), s));
+    k_sxt_runs_count<<<grid_for(E_), kBlock, 0, s>>>(E_, vb, Ev_.p, cnt.p);
+    PFDR_HIP(hipGetLastError());
+    std::vector<int> h(nb), tp((size_t)nb + 1, 0);
+    PFDR_HIP(hipMemcpyAsync(h.data(), cnt.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < nb; b++) tp[b + 1] = tp[b] + h[b];
+    DevBuf<int> tptr((size_t)nb + 1), tstart(tp[nb] ? tp[nb] : 1), tlen(tp[nb] ? tp[nb] : 1);
+    PFDR_HIP(hipMemcpyAsync(tptr.p, tp.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice, s));
+    k_sxt_runs_fill<<<grid_for(E_), kBlock, 0, s>>>(E_, vb, Ev_.p, tptr.p, fill.p, tstart.p, tlen.p);
+    trec_.alloc((size_t)nb * kSxRec);
+    k_sxt_rec<<<grid_for(nb), kBlock, 0, s>>>(nb, V_, vb, K_, SxTileCap<real>::v, inc_.ptr.p,
+                                              ustart.p, tptr.p, tstart.p, tlen.p, trec_.p, nok.p);
+    PFDR_HIP(hipGetLastError());
+    int n = 0;
+    PFDR_HIP(hipMemcpyAsync(&n, nok.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    record_blocks = n;  // (tiled_blocks: every block's edges are in tile order)
 }
 
 // ref :64-370
@@ -2129,8 +2434,22 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
-        if (Po) k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
-        else k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
+        if (trec_.p) {  // tile runs staged by slot (sx_tile_sum)
+            a.trec = trec_.p;
+            a.sl = sl_.p;
+            const bool wa = A1_.p || !la_u_;  // weights staged with the runs
+            if (Po) {
+                if (wa) k_sx_vertex_tile<real, true, true><<<g, kBlock, 0, s>>>(a);
+                else k_sx_vertex_tile<real, true, false><<<g, kBlock, 0, s>>>(a);
+            } else {
+                if (wa) k_sx_vertex_tile<real, false, true><<<g, kBlock, 0, s>>>(a);
+                else k_sx_vertex_tile<real, false, false><<<g, kBlock, 0, s>>>(a);
+            }
+        } else if (Po) {
+            k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
+        } else {
+            k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
+        }
     } else {
         ProfScope ps(prof, "sx_vertex_wide", s);
         a.nb = nbw_; a.xs = Pavg_.p; a.act = act_.p;
