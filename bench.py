@@ -409,7 +409,7 @@ def main():
     quad = wl.kind != pfdr.PFDR_KIND_SIMPLEX
     split_blocks = sess.query("split_blocks") if quad else 0
     tiled_blocks = sess.query("tiled_blocks")  # (simplex: edges in tile order)
-    record_blocks = sess.query("record_blocks") if quad else 0
+    record_blocks = sess.query("record_blocks")  # (simplex: tile blocks staged from their runs)
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     seqdif = sess.query("seqdif")
     # which speculative mode ran (PFDR_SPEC / pfdr_problem.spec): the decision

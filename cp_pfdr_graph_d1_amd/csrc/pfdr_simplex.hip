@@ -787,21 +787,22 @@ constexpr int kSxRuns = 15, kSxRec = 32;
 template <typename real> struct SxTileCap { static constexpr int v = 3072; };  // LDS reals
 template <> struct SxTileCap<double> { static constexpr int v = 1536; };
 
-// WA: per-incidence weights staged too (per-edge La_d1: one per slot in
-// al[]; A1: K per slot in al[]); else the one weight la0
-template <typename real, bool WA>
-__device__ __forceinline__ real sx_tile_sum(const SxVArgs<real> &a, int blk, int t, bool live,
-                                            long v, int k, real inv, real *zl, real *al,
-                                            int *rt) {
+// Stage block blk's runs into LDS by slot: zl[slot * K + k] = Z, and with
+// WA the weights (per-edge La_d1: al[slot]; A1: al[slot * K + k]).  All
+// lanes of the workgroup take part (barriers).
+template <typename real, bool WA, int M>
+__device__ __forceinline__ void sx_tile_stage(const SxVArgs<real> &a, int blk, int t, real *zl,
+                                              real *al, int *rt) {
     const int K = a.c.K;
     const int lane = t & (kWave - 1);
-    const long v0 = (long)blk * a.vb;
     const int rv = lane < kSxRec ? a.trec[(long)blk * kSxRec + lane] : 0;
     const int nr = __builtin_amdgcn_readfirstlane(__shfl(rv, 0, kWave));
-    // run r in lane r: start, length (edge ends); values K per end
+    // run r in lane r: start, length (edge ends); values K per end (the
+    // shuffles run with the whole wave active: a lane reads another's
+    // register only while that lane is active)
     const int st = __shfl(rv, min(1 + 2 * lane, kWave - 1), kWave);
-    const int ln = lane < nr ? __shfl(rv, min(2 + 2 * lane, kWave - 1), kWave) : 0;
-    int P = ln * K;  // inclusive prefix of the runs' values
+    const int lnr = __shfl(rv, min(2 + 2 * lane, kWave - 1), kWave);
+    int P = (lane < nr ? lnr : 0) * K;  // inclusive prefix of the runs' values
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
         const int y = __shfl_up(P, o, kWave);
@@ -814,18 +815,12 @@ __device__ __forceinline__ real sx_tile_sum(const SxVArgs<real> &a, int blk, int
         rt[kSxRuns + 1 + t] = t < nr ? P : 0x7fffffff;
     }
     __syncthreads();
-    int my0 = 0, my1 = 0;
-    if (live) {
-        const int b0 = a.ptr[v0];
-        my0 = a.ptr[v] - b0;
-        my1 = a.ptr[v + 1] - b0;
-    }
     const long E = a.E;
     const bool per_e = WA && !a.A1;  // per-edge La_d1: one weight per slot
-    // each lane walks values q = t, t + NT, ...: its run only advances
     const int *rst = rt, *rpr = rt + kSxRuns + 1;
+    // each lane walks values q = t, t + 256, ...: its run only advances
     int r = 0, pend = rpr[0], pbeg = 0;
-    constexpr int U = 4;
+    constexpr int U = 4 * M;
     for (int q0 = t; q0 < tot; q0 += U * kBlock) {
         real z[U], w[U];
         int sl[U], kk[U];
@@ -861,10 +856,22 @@ __device__ __forceinline__ real sx_tile_sum(const SxVArgs<real> &a, int blk, int
             }
     }
     __syncthreads();
-    real s = real(0);
+}
+
+// the ordered sum of item (v, k) from the staged list: its vertex's slots
+// [ptr[v] - ptr[v0], ptr[v + 1] - ptr[v0]) in the reference's order, each
+// term (a * 1/Aux) * z as sx_item_sum forms it
+template <typename real>
+__device__ __forceinline__ real sx_tile_item(const SxVArgs<real> &a, long v0, long v, int k,
+                                             real inv, const real *zl, const real *al, bool wa) {
+    const int K = a.c.K;
+    const int b0 = a.ptr[v0];
+    const int my0 = a.ptr[v] - b0, my1 = a.ptr[v + 1] - b0;
+    const bool per_e = !a.A1;
     const real la0 = a.la0;
+    real s = real(0);
     for (int j = my0; j < my1; j++) {
-        const real an = !WA ? la0 : (per_e ? al[j] : al[j * K + k]);
+        const real an = !wa ? la0 : (per_e ? al[j] : al[j * K + k]);
         s += (an * inv) * zl[j * K + k];
     }
     return s;
@@ -877,13 +884,9 @@ __device__ __forceinline__ real sx_tile_sum(const SxVArgs<real> &a, int blk, int
 // The body of k_sx_vertex_sweep, shared with the one-workgroup
 // k_sx_tiny_iterate (four blocks side by side).
 // SPLIT (speculative sessions): the new P and (P, step) go to Po / PFo
-// TL: the block sums from its tile runs (sx_tile_sum; zl / al its LDS
-// lists, WA its staged weights) when its record has runs, else the CSR gather
-template <typename real, int NT, bool SPLIT = false, bool TL = false, bool WA = false>
+template <typename real, int NT, bool SPLIT = false>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
-                                                real *ms, real *red, real *part_out,
-                                                real *x0s = nullptr, real *zl = nullptr,
-                                                real *al = nullptr, int *rt = nullptr) {
+                                                real *ms, real *red, real *part_out) {
     const int K = a.c.K, vb = a.vb;
     const int vl = t / K;
     const int k = t - vl * K;
@@ -899,29 +902,15 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
         if (a.c.loss == LOSS_QUAD) qv = a.Q[i];
         if (a.track == 1) pold = sx_pold(a, i);
     }
-    real x = real(0);
-    const bool tiled = TL && a.trec[(long)blk * kSxRec] > 0;  // block-uniform
-    if (tiled) {
-        const real inv = live ? sx_inv(a, v, i) : real(0);
-        x = sx_tile_sum<real, WA>(a, blk, t, live, v, k, inv, zl, al, rt);
-    } else if (live) {
-        x = sx_item_sum(a, v, k);
-    }
     if (live) {
-        if (TL) {  // divided by the metric here (ref src/proj_simplex_metric.cpp:44, :49)
-            xs[t] = x / ga;
-            if (k == 0) x0s[vl] = x;
-        } else {
-            xs[t] = x;
-        }
+        xs[t] = sx_item_sum(a, v, k);
         ms[t] = ga;
     }
     __syncthreads();
     real dif = real(0);
     if (blk < a.nb && t < vb && v0 + t < a.V) {
         real *x = xs + t * K;
-        if (TL) proj_simplex_column_div<real>(x, ms + t * K, K, x0s[t], real(1));
-        else proj_simplex_column<real>(x, ms + t * K, K, real(1));
+        proj_simplex_column<real>(x, ms + t * K, K, real(1));
         if (a.track == 2) {
             real mx = x[0];
             int l = 0;
@@ -968,20 +957,111 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
 }
 
-// tile-ordered sessions (sx_tile_sum)
-template <typename real, bool SPLIT, bool WA>
+// Tile-ordered sessions: one workgroup per tile block of M * vb vertices (M
+// items per lane), its sums from the block's tile runs (sx_tile_sum) or,
+// for a block without a record, the CSR gather.  M > 1 gives each
+// workgroup's load rounds and projection walk M times the work: the sweep
+// is bound by the latency of those serial phases, not by its bytes.
+template <typename real, int M>
+struct SxTileLds {
+    static constexpr int items = M * kBlock;
+    static constexpr int cap = M * SxTileCap<real>::v;  // staged reals (K per list entry)
+};
+
+template <typename real, bool SPLIT, bool WA, int M>
 __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
-    constexpr int CAP = SxTileCap<real>::v;
-    __shared__ real xs[kBlock], ms[kBlock], x0s[kBlock];
+    using L = SxTileLds<real, M>;
+    __shared__ real xs[L::items], ms[L::items], x0s[L::items];
     __shared__ real red[kBlock / kWave];
-    __shared__ real zl[CAP];
-    __shared__ real al[WA ? CAP : 1];
+    __shared__ real zl[L::cap];
+    __shared__ real al[WA ? L::cap : 1];
     __shared__ int rt[2 * (kSxRuns + 1)];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
-    sx_vertex_block<real, kBlock, SPLIT, true, WA>(a, blk, threadIdx.x, xs, ms, red, a.part + blk,
-                                                    x0s, zl, al, rt);
+    const int t = threadIdx.x;
+    const int K = a.c.K, nv = a.vb;  // (a.vb: the tile block's vertices, M * 256 / K at most)
+    const long v0 = (long)blk * nv;
+    // the items' operands before the sum (their latency hides under it)
+    real ga[M], gaq[M], qv[M], pold[M], x[M], inv[M];
+    long vi[M];
+    int kk[M];
+    bool live[M];
+#pragma unroll
+    for (int u = 0; u < M; u++) {
+        const int it = t + u * kBlock;
+        const int vl = it / K;
+        kk[u] = it - vl * K;
+        vi[u] = v0 + vl;
+        live[u] = vl < nv && vi[u] < a.V;
+        ga[u] = gaq[u] = qv[u] = pold[u] = x[u] = inv[u] = real(0);
+        if (live[u]) {
+            const long i = vi[u] * K + kk[u];
+            ga[u] = a.Ga[i];
+            gaq[u] = a.GaQ[i];
+            if (a.c.loss == LOSS_QUAD) qv[u] = a.Q[i];
+            if (a.track == 1) pold[u] = sx_pold(a, i);
+            inv[u] = sx_inv(a, vi[u], i);
+        }
+    }
+    if (a.trec[(long)blk * kSxRec] > 0) {  // block-uniform
+        sx_tile_stage<real, WA, M>(a, blk, t, zl, al, rt);
+#pragma unroll
+        for (int u = 0; u < M; u++)
+            if (live[u]) x[u] = sx_tile_item(a, v0, vi[u], kk[u], inv[u], zl, al, WA);
+    } else {
+#pragma unroll
+        for (int u = 0; u < M; u++)
+            if (live[u]) x[u] = sx_item_sum(a, vi[u], kk[u]);
+    }
+    // divided by the metric here, the raw x[0] aside (ref
+    // src/proj_simplex_metric.cpp:44, :49; proj_simplex_column_div)
+#pragma unroll
+    for (int u = 0; u < M; u++)
+        if (live[u]) {
+            const int it = t + u * kBlock;
+            xs[it] = x[u] / ga[u];
+            ms[it] = ga[u];
+            if (kk[u] == 0) x0s[it / K] = x[u];
+        }
+    __syncthreads();
+    real dif = real(0);
+    for (int vl = t; vl < nv && v0 + vl < a.V; vl += kBlock) {  // one lane per vertex
+        real *xc = xs + vl * K;
+        proj_simplex_column_div<real>(xc, ms + vl * K, K, x0s[vl], real(1));
+        if (a.track == 2) {
+            real mx = xc[0];
+            int l = 0;
+            for (int d = 1; d < K; d++) if (xc[d] > mx) { mx = xc[d]; l = d; }
+            const real fl = (real)l;
+            real dl = real(0);
+            if (fl != a.lab[v0 + vl]) { dl = real(1); a.lab[v0 + vl] = fl; }
+            if (a.terms) a.terms[v0 + vl] = dl;
+            dif += dl;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < M; u++) {
+        if (!live[u]) continue;
+        const long i = vi[u] * K + kk[u];
+        const real p = xs[t + u * kBlock];
+        if (a.track == 1) {
+            real d = pold[u] - p;
+            if (d < real(0)) d = -d;
+            dif += d;
+            if (a.terms) a.terms[i] = d;
+        }
+        if (!a.nop) (SPLIT ? a.Po : a.P)[i] = p;
+        SxR2<real> q;
+        q.x = p;
+        q.y = sx_explicit(a.c, p, gaq[u], qv[u]);
+        (SPLIT ? a.PFo : a.PF)[i] = q;
+    }
+    if (a.track) {
+        dif = block_sum(dif, red);
+        if (t == 0) a.part[blk] = dif;
+    }
 }
 
 // ------------------------------------------ group vertex sweep (K > 64) --
@@ -1926,7 +2006,8 @@ class SimplexSession final : public SessionBase {
     // kSxTileMinVK (edge, label) entries)
     bool sxtile_ = false;
     static constexpr long kSxTileMinVK = 1L << 21;
-    DevBuf<int> trec_;              // per vertex block: its runs (k_sxt_rec)
+    int sxtm_ = 2, tbv_ = 0, nbt_ = 0;  // items per lane, tile block vertices, tile blocks
+    DevBuf<int> trec_;              // per tile block: its runs (k_sxt_rec)
     DevBuf<unsigned short> sl_;     // slot of every edge end (k_sxt_slots)
     void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
@@ -1981,6 +2062,17 @@ class SimplexSession final : public SessionBase {
         if (halo_) halo_->pull(PF_.p, K_ * (int)sizeof(SxR2<real>), stream);
     }
     void push_wz();
+    template <bool SPLIT, bool WA>
+    void launch_tile_m(const SxVArgs<real> &a) {
+        const int g = xcd_grid(a.nb, a.xcd);
+        if (sxtm_ == 1) k_sx_vertex_tile<real, SPLIT, WA, 1><<<g, kBlock, 0, stream>>>(a);
+        else if (sxtm_ == 2) k_sx_vertex_tile<real, SPLIT, WA, 2><<<g, kBlock, 0, stream>>>(a);
+        else k_sx_vertex_tile<real, SPLIT, WA, 4><<<g, kBlock, 0, stream>>>(a);
+    }
+    void launch_tile(const SxVArgs<real> &a, bool split, bool wa) {
+        if (split) wa ? launch_tile_m<true, true>(a) : launch_tile_m<true, false>(a);
+        else wa ? launch_tile_m<false, true>(a) : launch_tile_m<false, false>(a);
+    }
     template <bool SPLIT>
     void launch_wide(SxVArgs<real> a) {
         if (gnv_) {  // groups of gnv_ vertices, columns in LDS
@@ -2055,8 +2147,14 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     {
         const char *t = getenv("PFDR_SX_TILE");
         const int want = t ? atoi(t) : -1;
-        const int vb = K_ <= 64 ? kBlock / K_ : 0;
+        // tile blocks of M vertex blocks (k_sx_vertex_tile; PFDR_SX_TILEM = 1, 2, 4)
+        const char *tm = getenv("PFDR_SX_TILEM");
+        sxtm_ = tm ? atoi(tm) : 2;
+        if (sxtm_ != 1 && sxtm_ != 2 && sxtm_ != 4) throw std::runtime_error("PFDR_SX_TILEM: 1, 2 or 4");
+        const int vb = K_ <= 64 ? sxtm_ * (kBlock / K_) : 0;
         const long nb = vb ? ((long)V_ + vb - 1) / vb : 0;
+        tbv_ = vb;
+        nbt_ = (int)nb;
         sxtile_ = !halo_ && vb && E_ > 1 && want != 0 && (want > 0 || VK_ >= kSxTileMinVK);
         if (sxtile_) {
             int vbits = 1;
@@ -2074,7 +2172,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
             std::swap(Ev_.p, nv.p);
             PFDR_HIP(hipStreamSynchronize(s));
         }
-        tiled_blocks = sxtile_ ? nb : 0;  // (every fused-sweep block reads tile runs)
+        tiled_blocks = sxtile_ ? nb : 0;  // tile blocks (every one's edges in tile order)
     }
     contribution_incidence(Eu_.p, Ev_.p, E_, V_, sxtile_ ? perm.p : eg.p, e_offset, halo_.get(),
                            inc_, s);
@@ -2131,7 +2229,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
     nbv_ = grid_for(V_);
     nbe_ = grid_for(E_);
-    part_.alloc(std::max(std::max(nbv_, nbs_), nbw_));
+    part_.alloc(std::max(std::max(nbv_, nbs_), nbw_));  // (nbt_ <= nbs_)
     if (rec_obj_) { opart_.alloc((size_t)nbv_ + nbe_ + 1); Obj_.alloc((size_t)itMax_ + 1); }
     if (rec_dif_) Dif_.alloc(itMax_ > 0 ? itMax_ : 1);
     if (track_ == 2) {
@@ -2248,7 +2346,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
 template <typename real>
 void SimplexSession<real>::build_sx_tiles() {
     hipStream_t s = stream;
-    const int nb = nbs_, vb = vb_;
+    const int nb = nbt_, vb = tbv_;
     sl_.alloc((size_t)2 * E_);
     k_sxt_slots<<<grid_for(V_), kBlock, 0, s>>>(V_, vb, inc_.ptr.p, inc_.idx.p, sl_.p);
     DevBuf<int> ustart((size_t)nb + 1), cnt(nb), fill(nb), nok(1);
@@ -2266,7 +2364,7 @@ void SimplexSession<real>::build_sx_tiles() {
     PFDR_HIP(hipMemcpyAsync(tptr.p, tp.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice, s));
     k_sxt_runs_fill<<<grid_for(E_), kBlock, 0, s>>>(E_, vb, Ev_.p, tptr.p, fill.p, tstart.p, tlen.p);
     trec_.alloc((size_t)nb * kSxRec);
-    k_sxt_rec<<<grid_for(nb), kBlock, 0, s>>>(nb, V_, vb, K_, SxTileCap<real>::v, inc_.ptr.p,
+    k_sxt_rec<<<grid_for(nb), kBlock, 0, s>>>(nb, V_, vb, K_, sxtm_ * SxTileCap<real>::v, inc_.ptr.p,
                                               ustart.p, tptr.p, tstart.p, tlen.p, trec_.p, nok.p);
     PFDR_HIP(hipGetLastError());
     int n = 0;
@@ -2367,7 +2465,7 @@ void SimplexSession<real>::body() {
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     sweeps(c, 0);
-    const int nparts = vb_ ? nbs_ : nbw_;
+    const int nparts = trec_.p ? nbt_ : vb_ ? nbs_ : nbw_;  // (the sweep's blocks)
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -2434,17 +2532,13 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
         const int g = xcd_grid(nbs_, a.xcd);
-        if (trec_.p) {  // tile runs staged by slot (sx_tile_sum)
+        if (trec_.p) {  // tile runs staged by slot (sx_tile_stage)
             a.trec = trec_.p;
             a.sl = sl_.p;
-            const bool wa = A1_.p || !la_u_;  // weights staged with the runs
-            if (Po) {
-                if (wa) k_sx_vertex_tile<real, true, true><<<g, kBlock, 0, s>>>(a);
-                else k_sx_vertex_tile<real, true, false><<<g, kBlock, 0, s>>>(a);
-            } else {
-                if (wa) k_sx_vertex_tile<real, false, true><<<g, kBlock, 0, s>>>(a);
-                else k_sx_vertex_tile<real, false, false><<<g, kBlock, 0, s>>>(a);
-            }
+            a.vb = tbv_;
+            a.nb = nbt_;
+            a.xcd = xcd_fit(nbt_, sx_xcd_v_);
+            launch_tile(a, Po != nullptr, A1_.p || !la_u_);  // (weights staged with the runs)
         } else if (Po) {
             k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
         } else {

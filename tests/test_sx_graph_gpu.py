@@ -94,7 +94,7 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
             elif env.get("PFDR_SX_TINY") == "0":
                 assert s.query("tiny") == 0
             if env.get("PFDR_SX_TILE") == "1":
-                assert s.query("tiled_blocks") == (nb if K <= 64 else 0)
+                assert (s.query("tiled_blocks") > 0) == (K <= 64)
             if direct:  # profiled: every chunk launched directly, no graph replay
                 s.profile(True)
             for n in runs:
