@@ -698,6 +698,7 @@ struct SxVArgs {
     // the CSR gather) and the slot of every edge end in its block's list
     const int *trec;
     const unsigned short *sl;
+    int nparts;  // the fused sweep's blocks (the tile sweep's sub-blocks)
 };
 
 template <typename real>
@@ -973,27 +974,30 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     using L = SxTileLds<real, M>;
     __shared__ real xs[L::items], ms[L::items], x0s[L::items];
-    __shared__ real red[kBlock / kWave];
+    __shared__ real red[M][kBlock / kWave];
     __shared__ real zl[L::cap];
     __shared__ real al[WA ? L::cap : 1];
     __shared__ int rt[2 * (kSxRuns + 1)];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
     const int t = threadIdx.x;
-    const int K = a.c.K, nv = a.vb;  // (a.vb: the tile block's vertices, M * 256 / K at most)
+    // M sub-blocks of vb vertices (the fused sweep's blocks): lane t takes
+    // item t of each, so every sub-block's evolution partial is formed by
+    // the lanes and tree of k_sx_vertex_sweep -- the same partials bit for
+    // bit, written where that sweep writes them (part[blk * M + u])
+    const int K = a.c.K, vb = a.vb, vbK = vb * K, nv = M * vb;
     const long v0 = (long)blk * nv;
     // the items' operands before the sum (their latency hides under it)
     real ga[M], gaq[M], qv[M], pold[M], x[M], inv[M];
     long vi[M];
     int kk[M];
     bool live[M];
+    const int vt = t / K, kt = t - vt * K;
 #pragma unroll
     for (int u = 0; u < M; u++) {
-        const int it = t + u * kBlock;
-        const int vl = it / K;
-        kk[u] = it - vl * K;
-        vi[u] = v0 + vl;
-        live[u] = vl < nv && vi[u] < a.V;
+        kk[u] = kt;
+        vi[u] = v0 + u * vb + vt;
+        live[u] = t < vbK && vi[u] < a.V;
         ga[u] = gaq[u] = qv[u] = pold[u] = x[u] = inv[u] = real(0);
         if (live[u]) {
             const long i = vi[u] * K + kk[u];
@@ -1019,14 +1023,17 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
 #pragma unroll
     for (int u = 0; u < M; u++)
         if (live[u]) {
-            const int it = t + u * kBlock;
+            const int it = u * vbK + t;
             xs[it] = x[u] / ga[u];
             ms[it] = ga[u];
-            if (kk[u] == 0) x0s[it / K] = x[u];
+            if (kk[u] == 0) x0s[u * vb + vt] = x[u];
         }
     __syncthreads();
-    real dif = real(0);
-    for (int vl = t; vl < nv && v0 + vl < a.V; vl += kBlock) {  // one lane per vertex
+    // one lane per vertex walks its column (all M sub-blocks side by side);
+    // a label change is 0 / 1, so its count is exact in any order: x0s
+    // takes it for the sub-block sums below
+    for (int vl = t; vl < nv; vl += kBlock) {
+        if (v0 + vl >= a.V) break;
         real *xc = xs + vl * K;
         proj_simplex_column_div<real>(xc, ms + vl * K, K, x0s[vl], real(1));
         if (a.track == 2) {
@@ -1037,19 +1044,21 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
             real dl = real(0);
             if (fl != a.lab[v0 + vl]) { dl = real(1); a.lab[v0 + vl] = fl; }
             if (a.terms) a.terms[v0 + vl] = dl;
-            dif += dl;
+            x0s[vl] = dl;
         }
     }
     __syncthreads();
+    real dif[M];
 #pragma unroll
     for (int u = 0; u < M; u++) {
+        dif[u] = real(0);
         if (!live[u]) continue;
         const long i = vi[u] * K + kk[u];
-        const real p = xs[t + u * kBlock];
+        const real p = xs[u * vbK + t];
         if (a.track == 1) {
             real d = pold[u] - p;
             if (d < real(0)) d = -d;
-            dif += d;
+            dif[u] = d;
             if (a.terms) a.terms[i] = d;
         }
         if (!a.nop) (SPLIT ? a.Po : a.P)[i] = p;
@@ -1058,9 +1067,23 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
         q.y = sx_explicit(a.c, p, gaq[u], qv[u]);
         (SPLIT ? a.PFo : a.PF)[i] = q;
     }
+    if (a.track == 2) {  // sub-block u's vertices [u vb, u vb + vb): lane t < vb, as the fused sweep
+#pragma unroll
+        for (int u = 0; u < M; u++) dif[u] = (t < vb && v0 + u * vb + t < a.V) ? x0s[u * vb + t] : real(0);
+    }
     if (a.track) {
-        dif = block_sum(dif, red);
-        if (t == 0) a.part[blk] = dif;
+#pragma unroll
+        for (int u = 0; u < M; u++) {
+            const real w = wave_sum(dif[u]);
+            if ((t & (kWave - 1)) == 0) red[u][t / kWave] = w;
+        }
+        __syncthreads();
+        if (t < M) {  // (((w0 + w1) + w2) + w3), k_sx_vertex_sweep's order
+            const long sb = (long)blk * M + t;
+            real d = red[t][0];
+            for (int q = 1; q < kBlock / kWave; q++) d += red[t][q];
+            if (sb < a.nparts) a.part[sb] = d;
+        }
     }
 }
 
@@ -2465,7 +2488,7 @@ void SimplexSession<real>::body() {
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     sweeps(c, 0);
-    const int nparts = trec_.p ? nbt_ : vb_ ? nbs_ : nbw_;  // (the sweep's blocks)
+    const int nparts = vb_ ? nbs_ : nbw_;  // (the tile sweep writes the fused sweep's partials)
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -2535,7 +2558,7 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
         if (trec_.p) {  // tile runs staged by slot (sx_tile_stage)
             a.trec = trec_.p;
             a.sl = sl_.p;
-            a.vb = tbv_;
+            a.nparts = nbs_;  // (a.vb stays the fused sweep's: the tile blocks are M of them)
             a.nb = nbt_;
             a.xcd = xcd_fit(nbt_, sx_xcd_v_);
             launch_tile(a, Po != nullptr, A1_.p || !la_u_);  // (weights staged with the runs)
