@@ -785,8 +785,14 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
 // Record: [runs n, u start, u count, (v start, count) x (n - 1)] in edge
 // units, n <= kSxRuns; the lane's slots [my0, my1) from the CSR pointers.
 constexpr int kSxRuns = 15, kSxRec = 32;
-template <typename real> struct SxTileCap { static constexpr int v = 3072; };  // LDS reals
-template <> struct SxTileCap<double> { static constexpr int v = 1536; };
+template <typename real> struct SxTileCap { static constexpr int v = 2560; };  // LDS reals
+template <> struct SxTileCap<double> { static constexpr int v = 1280; };
+
+template <typename real, int M>
+struct SxTileLds {
+    static constexpr int items = M * kBlock;
+    static constexpr int cap = M * SxTileCap<real>::v;  // staged reals (K per list entry)
+};
 
 // Stage block blk's runs into LDS by slot: zl[slot * K + k] = Z, and with
 // WA the weights (per-edge La_d1: al[slot]; A1: al[slot * K + k]).  All
@@ -819,9 +825,13 @@ __device__ __forceinline__ void sx_tile_stage(const SxVArgs<real> &a, int blk, i
     const long E = a.E;
     const bool per_e = WA && !a.A1;  // per-edge La_d1: one weight per slot
     const int *rst = rt, *rpr = rt + kSxRuns + 1;
-    // each lane walks values q = t, t + 256, ...: its run only advances
+    // off / K as umulhi(off, ceil(2^32 / K)): exact for off < 2^20, K < 4096
+    const unsigned mK = (unsigned)((0x100000000ull + K - 1) / K);
+    // each lane walks values q = t, t + 256, ...: its run only advances;
+    // a block's list fits the LDS (k_sxt_rec), so all of its loads issue in
+    // ONE round (U values per lane in flight)
     int r = 0, pend = rpr[0], pbeg = 0;
-    constexpr int U = 4 * M;
+    constexpr int U = SxTileLds<real, M>::cap / kBlock;
     for (int q0 = t; q0 < tot; q0 += U * kBlock) {
         real z[U], w[U];
         int sl[U], kk[U];
@@ -837,7 +847,7 @@ __device__ __forceinline__ void sx_tile_stage(const SxVArgs<real> &a, int blk, i
             }
             const int sr = rst[r];
             const unsigned off = (unsigned)(qq - pbeg);
-            const unsigned ei = off / (unsigned)K;
+            const unsigned ei = __umulhi(off, mK);
             kk[u] = (int)(off - ei * (unsigned)K);
             const long p = (long)sr + ei;
             const bool sv = r > 0;
@@ -863,11 +873,9 @@ __device__ __forceinline__ void sx_tile_stage(const SxVArgs<real> &a, int blk, i
 // [ptr[v] - ptr[v0], ptr[v + 1] - ptr[v0]) in the reference's order, each
 // term (a * 1/Aux) * z as sx_item_sum forms it
 template <typename real>
-__device__ __forceinline__ real sx_tile_item(const SxVArgs<real> &a, long v0, long v, int k,
+__device__ __forceinline__ real sx_tile_item(const SxVArgs<real> &a, int my0, int my1, int k,
                                              real inv, const real *zl, const real *al, bool wa) {
     const int K = a.c.K;
-    const int b0 = a.ptr[v0];
-    const int my0 = a.ptr[v] - b0, my1 = a.ptr[v + 1] - b0;
     const bool per_e = !a.A1;
     const real la0 = a.la0;
     real s = real(0);
@@ -963,11 +971,6 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
 // for a block without a record, the CSR gather.  M > 1 gives each
 // workgroup's load rounds and projection walk M times the work: the sweep
 // is bound by the latency of those serial phases, not by its bytes.
-template <typename real, int M>
-struct SxTileLds {
-    static constexpr int items = M * kBlock;
-    static constexpr int cap = M * SxTileCap<real>::v;  // staged reals (K per list entry)
-};
 
 template <typename real, bool SPLIT, bool WA, int M>
 __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
@@ -990,9 +993,10 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
     // the items' operands before the sum (their latency hides under it)
     real ga[M], gaq[M], qv[M], pold[M], x[M], inv[M];
     long vi[M];
-    int kk[M];
+    int kk[M], j0[M], j1[M];
     bool live[M];
     const int vt = t / K, kt = t - vt * K;
+    const int b0 = a.ptr[v0];  // (the list's slots are relative to the tile block's first)
 #pragma unroll
     for (int u = 0; u < M; u++) {
         kk[u] = kt;
@@ -1006,13 +1010,15 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
             if (a.c.loss == LOSS_QUAD) qv[u] = a.Q[i];
             if (a.track == 1) pold[u] = sx_pold(a, i);
             inv[u] = sx_inv(a, vi[u], i);
+            j0[u] = a.ptr[vi[u]];
+            j1[u] = a.ptr[vi[u] + 1];
         }
     }
     if (a.trec[(long)blk * kSxRec] > 0) {  // block-uniform
         sx_tile_stage<real, WA, M>(a, blk, t, zl, al, rt);
 #pragma unroll
         for (int u = 0; u < M; u++)
-            if (live[u]) x[u] = sx_tile_item(a, v0, vi[u], kk[u], inv[u], zl, al, WA);
+            if (live[u]) x[u] = sx_tile_item(a, j0[u] - b0, j1[u] - b0, kk[u], inv[u], zl, al, WA);
     } else {
 #pragma unroll
         for (int u = 0; u < M; u++)
@@ -2170,9 +2176,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     {
         const char *t = getenv("PFDR_SX_TILE");
         const int want = t ? atoi(t) : -1;
-        // tile blocks of M vertex blocks (k_sx_vertex_tile; PFDR_SX_TILEM = 1, 2, 4)
+        // tile blocks of M vertex blocks (the staged sweep k_sx_vertex_tile,
+        // PFDR_SX_STAGE=1; PFDR_SX_TILEM = 1, 2, 4; the CSR gather's blocks
+        // are the M = 1 ones)
         const char *tm = getenv("PFDR_SX_TILEM");
-        sxtm_ = tm ? atoi(tm) : 2;
+        const char *stg = getenv("PFDR_SX_STAGE");
+        sxtm_ = tm ? atoi(tm) : (stg && stg[0] == '1') ? 2 : 1;
         if (sxtm_ != 1 && sxtm_ != 2 && sxtm_ != 4) throw std::runtime_error("PFDR_SX_TILEM: 1, 2 or 4");
         const int vb = K_ <= 64 ? sxtm_ * (kBlock / K_) : 0;
         const long nb = vb ? ((long)V_ + vb - 1) / vb : 0;
@@ -2230,7 +2239,12 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64) {
         vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
-        if (sxtile_) build_sx_tiles();
+        // the staged tile sweep (k_sx_vertex_tile) is opt-in: PFDR_SX_STAGE=1.
+        // On C4 it measured slower than the CSR gather over the same
+        // tile-ordered edges (1.10 vs 0.69 ms: its staging costs more issue
+        // and LDS work than the gather's one extra load round)
+        const char *st = getenv("PFDR_SX_STAGE");
+        if (sxtile_ && st && st[0] == '1') build_sx_tiles();
     } else {  // groups of vertices with their columns in LDS, or a wave per vertex
         gnv_ = SxGroup<real>::nv_for(K_, SxGroup<real>::kNV);
         const long per = gnv_ ? gnv_ : (long)kSxWideVpw * (kBlock / kWave);

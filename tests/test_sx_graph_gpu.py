@@ -43,7 +43,8 @@ def test_sx_graph_golden_identical(gpu_lib, name, fixed):
     c, g = G.load(name)
     res = []
     for env in ({}, {"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "100000000"},
-                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1"}):  # edges in tile order
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1"},  # edges in tile order
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "PFDR_SX_STAGE": "1"}):  # staged sweep
         with _env(**env):
             res.append(G.replay(gpu_lib, c, fixed, obj=False, dif=True))
     X0, it0, _, D0 = res[0]
@@ -80,7 +81,10 @@ def test_sx_graph_sessions_identical(gpu_lib, case):
     for env in ({"PFDR_SX_TINY": "0"}, {"PFDR_SX_TINY": "0", "launch": "direct"},
                 {"PFDR_SX_TINY": "100000000"}, {},
                 {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1"},
-                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "launch": "direct"}):
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "launch": "direct"},
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "PFDR_SX_STAGE": "1"},
+                {"PFDR_SX_TINY": "0", "PFDR_SX_TILE": "1", "PFDR_SX_STAGE": "1",
+                 "PFDR_SX_TILEM": "1"}):
         direct = env.pop("launch", None) == "direct"
         with _env(**env):
             s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev,
@@ -137,8 +141,8 @@ def test_sx_tile_order_identical(gpu_lib, dt, K, al, difRcd):
     Q[: V // 3, 1 % K] += 1.5
     Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
     res = []
-    for tile in ("0", "1"):
-        with _env(PFDR_SX_TINY="0", PFDR_SX_TILE=tile):
+    for tile, stage in (("0", "0"), ("1", "0"), ("1", "1")):
+        with _env(PFDR_SX_TINY="0", PFDR_SX_TILE=tile, PFDR_SX_STAGE=stage):
             s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, La, Q.copy(), Q,
                              K=K, al=al, rho=1.0, condMin=0.1, difRcd=difRcd, difTol=1e-6,
                              itMax=150, record_dif=True)
@@ -148,7 +152,9 @@ def test_sx_tile_order_identical(gpu_lib, dt, K, al, difRcd):
             res.append(s.result())
         finally:
             s.close()
-    (X0, it0, _, D0), (X1, it1, _, D1) = res
-    assert it0 == it1 and it0 > 0
-    assert np.array_equal(X0, X1)
-    assert np.array_equal(D0[:it0], D1[:it1])
+    X0, it0, _, D0 = res[0]
+    assert it0 > 0
+    for X1, it1, _, D1 in res[1:]:
+        assert it0 == it1
+        assert np.array_equal(X0, X1)
+        assert np.array_equal(D0[:it0], D1[:it1])
