@@ -699,6 +699,12 @@ struct SxVArgs {
     const int *trec;
     const unsigned short *sl;
     int nparts;  // the fused sweep's blocks (the tile sweep's sub-blocks)
+    // the fused sweep's per-block incidence lists, padded to capb entries
+    // (idxp[blk * capb + j] = idx[ptr[v0] + j]; null: read idx through ptr):
+    // a block loads its list with addresses that depend on nothing loaded,
+    // beside its CSR pointers -- one round of loads fewer before the gathers
+    const unsigned *idxp;
+    int capb;
 };
 
 template <typename real>
@@ -725,13 +731,14 @@ __device__ __forceinline__ real sx_pold(const SxVArgs<real> &a, long i) {
 // reference's (e, side) order, W * Z formed from Z with the reference's
 // products; consecutive lanes take consecutive labels, so each incidence is
 // a K-contiguous run read coalesced
+// (the incidence addresses idx[j0 .. j1): the CSR in memory, or the
+// block's list staged in LDS)
 template <typename real>
-__device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int k) {
+__device__ __forceinline__ real sx_item_sum_from(const SxVArgs<real> &a, long v, int k,
+                                                 const unsigned *idx, int j0, int j1, real inv) {
     const int K = a.c.K;
-    const real inv = sx_inv(a, v, v * K + k);  // 1/Aux of this (v, k)
     const bool lu = a.la_u != 0;
     const real la0 = a.la0;
-    const int j0 = a.ptr[v], j1 = a.ptr[v + 1];
     real s = real(0);
     int j = j0;
     // 8 slots, then 8 contributions in flight per lane; summed in order
@@ -739,7 +746,7 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
         unsigned sl[8];
         real w[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) sl[q] = a.idx[j + q];
+        for (int q = 0; q < 8; q++) sl[q] = idx[j + q];
         {   // W * Z formed here (the reference's products, same rounding)
             // branch-free: received entries (address 2E + j) sit in the
             // tail of Zv as the sender's W*Z (factor 1), so all 16 loads
@@ -762,7 +769,7 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
         for (int q = 0; q < 8; q++) s += w[q];
     }
     for (; j < j1; j++) {
-        const long ad = a.idx[j];
+        const long ad = idx[j];
         const bool sv = ad >= a.E;
         const long ea = sv ? ad - a.E : ad;
         const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
@@ -770,6 +777,11 @@ __device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int 
         else s += (sx_wa(a, ea * K + k, ea, lu, la0) * inv) * z;
     }
     return s;
+}
+
+template <typename real>
+__device__ __forceinline__ real sx_item_sum(const SxVArgs<real> &a, long v, int k) {
+    return sx_item_sum_from(a, v, k, a.idx, a.ptr[v], a.ptr[v + 1], sx_inv(a, v, v * a.c.K + k));
 }
 
 // ---------------------------------------- tile-ordered sums (K <= 64) ---
@@ -895,7 +907,8 @@ __device__ __forceinline__ real sx_tile_item(const SxVArgs<real> &a, int my0, in
 // SPLIT (speculative sessions): the new P and (P, step) go to Po / PFo
 template <typename real, int NT, bool SPLIT = false>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
-                                                real *ms, real *red, real *part_out) {
+                                                real *ms, real *red, real *part_out,
+                                                unsigned *lidx = nullptr) {
     const int K = a.c.K, vb = a.vb;
     const int vl = t / K;
     const int k = t - vl * K;
@@ -911,7 +924,25 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
         if (a.c.loss == LOSS_QUAD) qv = a.Q[i];
         if (a.track == 1) pold = sx_pold(a, i);
     }
-    if (live) {
+    if (lidx && a.idxp) {  // the padded list into LDS beside the pointers (SxVArgs::idxp)
+        const int b0 = a.ptr[v0];
+        int j0 = 0, j1 = 0;
+        real inv = real(0);
+        if (live) {
+            j0 = a.ptr[v];
+            j1 = a.ptr[v + 1];
+            inv = sx_inv(a, v, i);
+        }
+        const long lb = (long)blk * a.capb;
+        for (int q = t; q < a.capb; q += NT) lidx[q] = a.idxp[lb + q];
+        j0 -= b0;
+        j1 -= b0;
+        __syncthreads();
+        if (live) {
+            xs[t] = sx_item_sum_from(a, v, k, lidx, j0, j1, inv);
+            ms[t] = ga;
+        }
+    } else if (live) {
         xs[t] = sx_item_sum(a, v, k);
         ms[t] = ga;
     }
@@ -956,14 +987,36 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     }
 }
 
+constexpr int kSxPadCap = 2048;  // entries of a padded block list, at most
 template <typename real, int NT, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real xs[NT], ms[NT];
     __shared__ real red[NT / kWave];
+    __shared__ unsigned lidx[kSxPadCap];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
-    sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk);
+    sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk, lidx);
+}
+
+// the padded lists (SxVArgs::idxp) and their width: the largest block's
+// list (*capb, atomicMax) first
+__global__ void k_sx_block_max(int nb, int vb, int V, const int *__restrict__ ptr,
+                               int *__restrict__ capb) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const long v0 = (long)b * vb, v1 = min(v0 + vb, (long)V);
+    atomicMax(capb, ptr[v1] - ptr[v0]);
+}
+__global__ void k_sx_pad_idx(long n, int capb, int vb, int V, const int *__restrict__ ptr,
+                             const unsigned *__restrict__ idx, unsigned *__restrict__ idxp) {
+    const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const long b = q / capb;
+    const int j = (int)(q - b * capb);
+    const long v0 = b * vb, v1 = min(v0 + vb, (long)V);
+    const int j0 = ptr[v0];
+    idxp[q] = j < ptr[v1] - j0 ? idx[j0 + j] : 0u;
 }
 
 // Tile-ordered sessions: one workgroup per tile block of M * vb vertices (M
@@ -2038,6 +2091,8 @@ class SimplexSession final : public SessionBase {
     int sxtm_ = 2, tbv_ = 0, nbt_ = 0;  // items per lane, tile block vertices, tile blocks
     DevBuf<int> trec_;              // per tile block: its runs (k_sxt_rec)
     DevBuf<unsigned short> sl_;     // slot of every edge end (k_sxt_slots)
+    DevBuf<unsigned> idxp_;         // padded block lists (SxVArgs::idxp), capb_ wide
+    int capb_ = 0;
     void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
     bool la_u_ = false;
@@ -2245,6 +2300,27 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
         // and LDS work than the gather's one extra load round)
         const char *st = getenv("PFDR_SX_STAGE");
         if (sxtile_ && st && st[0] == '1') build_sx_tiles();
+        // padded block lists for the one-GPU fused sweep (PFDR_SX_PAD=0 off):
+        // when the widest block's list is at most kSxPadCap and the padding
+        // costs at most half the lists' size (regular graphs)
+        const char *pd = getenv("PFDR_SX_PAD");
+        if (!halo_ && E_ > 0 && !(pd && pd[0] == '0')) {
+            DevBuf<int> cb(1);
+            PFDR_HIP(hipMemsetAsync(cb.p, 0, sizeof(int), s));
+            k_sx_block_max<<<grid_for(nbs_), kBlock, 0, s>>>(nbs_, vb_, V_, inc_.ptr.p, cb.p);
+            PFDR_HIP(hipGetLastError());
+            int h = 0;
+            PFDR_HIP(hipMemcpyAsync(&h, cb.p, sizeof(int), hipMemcpyDeviceToHost, s));
+            PFDR_HIP(hipStreamSynchronize(s));
+            const long n = (long)nbs_ * h;
+            if (h > 0 && h <= kSxPadCap && n <= 3 * E_) {  // (2E list entries, at most 1.5 x)
+                capb_ = h;
+                idxp_.alloc((size_t)n);
+                k_sx_pad_idx<<<grid_for(n), kBlock, 0, s>>>(n, h, vb_, V_, inc_.ptr.p, inc_.idx.p,
+                                                            idxp_.p);
+                PFDR_HIP(hipGetLastError());
+            }
+        }
     } else {  // groups of vertices with their columns in LDS, or a wave per vertex
         gnv_ = SxGroup<real>::nv_for(K_, SxGroup<real>::kNV);
         const long per = gnv_ ? gnv_ : (long)kSxWideVpw * (kBlock / kWave);
@@ -2565,6 +2641,8 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     a.invV = A1_.p ? nullptr : invV_.p;
     a.la0 = la0_; a.la_u = la_u_ ? 1 : 0;
     a.nop = plazy_ ? 1 : 0;
+    a.idxp = idxp_.p;
+    a.capb = capb_;
     if (vb_) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
