@@ -1249,6 +1249,9 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
             i[u] = v0 * K + (ok[u] ? it : 0);
             x[u] = real(0);
         }
+        real m[SXU];  // the metric, loaded with the first round of the sum's loads
+#pragma unroll
+        for (int u = 0; u < SXU; u++) m[u] = ok[u] ? a.Ga[i[u]] : real(1);
         if (staged) {
             real inv[SXU];
             int j[SXU], j1[SXU];
@@ -1296,22 +1299,18 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
 #pragma unroll
         for (int u = 0; u < SXU; u++) {
             if (!ok[u]) continue;
-            const real m = a.Ga[i[u]];
             if (k[u] == 0) x0s[vl[u]] = x[u];
-            xs[k[u] * st + vl[u]] = x[u] / m;
-            ms[k[u] * st + vl[u]] = m;
+            xs[k[u] * st + vl[u]] = x[u] / m[u];
+            ms[k[u] * st + vl[u]] = m[u];
         }
     }
-    __syncthreads();
-    real dif = real(0);
-    if (t < nv)  // (2) one lane per vertex down its column
-        las[t] = proj_simplex_walk<real>(xs + t, ms + t, I + t, K, st, x0s[t], real(1));
-    __syncthreads();
-    // (3) finalise (ref :74-80), rows back out; 4 items per lane, loads first
-    for (int it0 = t; it0 < nitems; it0 += 4 * kBlock) {
-        real pold[4], gq[4], qq[4];
+    // (3)'s first FU items per lane: their operands loaded now, their latency
+    // under the walk
+    constexpr int FU = 8;
+    real pold[FU], gq[FU], qq[FU];
+    auto fin_load = [&](int it0) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < FU; u++) {
             const int it = it0 + u * kBlock;
             pold[u] = gq[u] = qq[u] = real(0);
             if (it < nitems) {
@@ -1321,8 +1320,18 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
                 if (a.c.loss == LOSS_QUAD) qq[u] = a.Q[i];
             }
         }
+    };
+    fin_load(t);
+    __syncthreads();
+    real dif = real(0);
+    if (t < nv)  // (2) one lane per vertex down its column
+        las[t] = proj_simplex_walk<real>(xs + t, ms + t, I + t, K, st, x0s[t], real(1));
+    __syncthreads();
+    // (3) finalise (ref :74-80), rows back out; FU items per lane, loads first
+    for (int it0 = t; it0 < nitems; it0 += FU * kBlock) {
+        if (it0 != t) fin_load(it0);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < FU; u++) {
             const int it = it0 + u * kBlock;
             if (it >= nitems) break;
             const int vl = it / K, k = it - vl * K;
