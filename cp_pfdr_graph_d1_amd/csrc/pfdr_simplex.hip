@@ -987,13 +987,14 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
     }
 }
 
-constexpr int kSxPadCap = 2048;  // entries of a padded block list, at most
+constexpr int kSxPadPer = 8;  // entries of a padded block list per lane, at most
+constexpr int kSxNtDefault = 256;  // the fused sweep's workgroup width (fused_sweep_setup)
 template <typename real, int NT, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     __shared__ real xs[NT], ms[NT];
     __shared__ real red[NT / kWave];
-    __shared__ unsigned lidx[kSxPadCap];
+    __shared__ unsigned lidx[kSxPadPer * NT];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
     sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk, lidx);
@@ -2102,6 +2103,10 @@ class SimplexSession final : public SessionBase {
     DevBuf<unsigned short> sl_;     // slot of every edge end (k_sxt_slots)
     DevBuf<unsigned> idxp_;         // padded block lists (SxVArgs::idxp), capb_ wide
     int capb_ = 0;
+    // the one-GPU fused sweep's workgroups: snt_ lanes, svb_ vertices,
+    // snb_ blocks (PFDR_SX_NT = 64, 128, 256; fused_sweep_setup)
+    int snt_ = kBlock, svb_ = 0, snb_ = 0;
+    void fused_sweep_setup();
     void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
     bool la_u_ = false;
@@ -2155,6 +2160,12 @@ class SimplexSession final : public SessionBase {
         if (halo_) halo_->pull(PF_.p, K_ * (int)sizeof(SxR2<real>), stream);
     }
     void push_wz();
+    template <bool SPLIT>
+    void launch_fused(const SxVArgs<real> &a, int g) {
+        if (snt_ == 64) k_sx_vertex_sweep<real, 64, SPLIT><<<g, 64, 0, stream>>>(a);
+        else if (snt_ == 128) k_sx_vertex_sweep<real, 128, SPLIT><<<g, 128, 0, stream>>>(a);
+        else k_sx_vertex_sweep<real, kBlock, SPLIT><<<g, kBlock, 0, stream>>>(a);
+    }
     template <bool SPLIT, bool WA>
     void launch_tile_m(const SxVArgs<real> &a) {
         const int g = xcd_grid(a.nb, a.xcd);
@@ -2303,33 +2314,14 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     if (K_ <= 64) {
         vb_ = kBlock / K_;
         nbs_ = (int)((V_ + vb_ - 1) / vb_);
+        svb_ = vb_;  // (fused_sweep_setup may narrow the one-GPU sweep's blocks)
+        snb_ = nbs_;
         // the staged tile sweep (k_sx_vertex_tile) is opt-in: PFDR_SX_STAGE=1.
         // On C4 it measured slower than the CSR gather over the same
         // tile-ordered edges (1.10 vs 0.69 ms: its staging costs more issue
         // and LDS work than the gather's one extra load round)
         const char *st = getenv("PFDR_SX_STAGE");
         if (sxtile_ && st && st[0] == '1') build_sx_tiles();
-        // padded block lists for the one-GPU fused sweep (PFDR_SX_PAD=0 off):
-        // when the widest block's list is at most kSxPadCap and the padding
-        // costs at most half the lists' size (regular graphs)
-        const char *pd = getenv("PFDR_SX_PAD");
-        if (!halo_ && E_ > 0 && !(pd && pd[0] == '0')) {
-            DevBuf<int> cb(1);
-            PFDR_HIP(hipMemsetAsync(cb.p, 0, sizeof(int), s));
-            k_sx_block_max<<<grid_for(nbs_), kBlock, 0, s>>>(nbs_, vb_, V_, inc_.ptr.p, cb.p);
-            PFDR_HIP(hipGetLastError());
-            int h = 0;
-            PFDR_HIP(hipMemcpyAsync(&h, cb.p, sizeof(int), hipMemcpyDeviceToHost, s));
-            PFDR_HIP(hipStreamSynchronize(s));
-            const long n = (long)nbs_ * h;
-            if (h > 0 && h <= kSxPadCap && n <= 3 * E_) {  // (2E list entries, at most 1.5 x)
-                capb_ = h;
-                idxp_.alloc((size_t)n);
-                k_sx_pad_idx<<<grid_for(n), kBlock, 0, s>>>(n, h, vb_, V_, inc_.ptr.p, inc_.idx.p,
-                                                            idxp_.p);
-                PFDR_HIP(hipGetLastError());
-            }
-        }
     } else {  // groups of vertices with their columns in LDS, or a wave per vertex
         gnv_ = SxGroup<real>::nv_for(K_, SxGroup<real>::kNV);
         const long per = gnv_ ? gnv_ : (long)kSxWideVpw * (kBlock / kWave);
@@ -2444,6 +2436,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
             graphs_ok_ = capturable_ = false;  // launched directly (see QuadSession)
         }
     }
+    if (vb_ && !tiny_ && !halo_) fused_sweep_setup();
     if (graphs_ok_) {  // instantiated with the setup
         try {
             (void)chunk_graph(chunk_);
@@ -2548,6 +2541,51 @@ void SimplexSession<real>::objective() {
     PFDR_HIP(hipGetLastError());
 }
 
+// The one-GPU fused sweep (K <= 64, not the one-workgroup path): its
+// workgroup width and the padded block lists.  Narrower workgroups put more
+// of them on a CU: the sweep's time is the latency of each block's chain
+// (list and pointers, gathers, projection walk, stores), hidden by the other
+// blocks in flight.  Its evolution partials are per workgroup, so a tracked
+// solve with the tree statistic keeps the 256-lane blocks (its Dif rounds as
+// before); the sequential statistic and untracked solves take PFDR_SX_NT.
+template <typename real>
+void SimplexSession<real>::fused_sweep_setup() {
+    hipStream_t s = stream;
+    snt_ = kBlock;
+    svb_ = vb_;
+    snb_ = nbs_;
+    const char *ntv = getenv("PFDR_SX_NT");
+    const int nt = ntv ? atoi(ntv) : kSxNtDefault;
+    if (nt != 64 && nt != 128 && nt != 256) throw std::runtime_error("PFDR_SX_NT: 64, 128 or 256");
+    if ((!track_ || seqdif_) && !trec_.p && K_ <= nt) {
+        snt_ = nt;
+        svb_ = nt / K_;
+        snb_ = (int)((V_ + svb_ - 1) / svb_);
+        if ((size_t)snb_ > part_.n) part_.alloc((size_t)snb_);
+    }
+    // padded block lists (PFDR_SX_PAD=0 off): when the widest block's list
+    // fits the sweep's LDS list and the padding costs at most half the lists'
+    // size (regular graphs)
+    const char *pd = getenv("PFDR_SX_PAD");
+    if (E_ > 0 && !(pd && pd[0] == '0')) {
+        DevBuf<int> cb(1);
+        PFDR_HIP(hipMemsetAsync(cb.p, 0, sizeof(int), s));
+        k_sx_block_max<<<grid_for(snb_), kBlock, 0, s>>>(snb_, svb_, V_, inc_.ptr.p, cb.p);
+        PFDR_HIP(hipGetLastError());
+        int h = 0;
+        PFDR_HIP(hipMemcpyAsync(&h, cb.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        const long n = (long)snb_ * h;
+        if (h > 0 && h <= kSxPadPer * snt_ && n <= 3 * E_) {  // (2E list entries, at most 1.5 x)
+            capb_ = h;
+            idxp_.alloc((size_t)n);
+            k_sx_pad_idx<<<grid_for(n), kBlock, 0, s>>>(n, h, svb_, V_, inc_.ptr.p, inc_.idx.p,
+                                                        idxp_.p);
+            PFDR_HIP(hipGetLastError());
+        }
+    }
+}
+
 // Pb(t) from the (P, step) pairs the sweeps wrote (plazy_), ghost rows
 // included (their PF rows were pulled)
 template <typename real>
@@ -2587,7 +2625,8 @@ void SimplexSession<real>::body() {
     const bool gated = track_ || rec_obj_;
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     sweeps(c, 0);
-    const int nparts = vb_ ? nbs_ : nbw_;  // (the tile sweep writes the fused sweep's partials)
+    // (the staged tile sweep writes the 256-lane fused sweep's partials)
+    const int nparts = trec_.p ? nbs_ : vb_ ? snb_ : nbw_;
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -2654,19 +2693,21 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     a.capb = capb_;
     if (vb_) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
-        a.nb = nbs_; a.xcd = xcd_fit(nbs_, sx_xcd_v_);
-        const int g = xcd_grid(nbs_, a.xcd);
+        a.vb = svb_;
+        a.nb = snb_; a.xcd = xcd_fit(snb_, sx_xcd_v_);
+        const int g = xcd_grid(snb_, a.xcd);
         if (trec_.p) {  // tile runs staged by slot (sx_tile_stage)
             a.trec = trec_.p;
             a.sl = sl_.p;
-            a.nparts = nbs_;  // (a.vb stays the fused sweep's: the tile blocks are M of them)
+            a.nparts = nbs_;  // (a.vb: the 256-lane sweep's; the tile blocks are M of them)
+            a.vb = vb_;
             a.nb = nbt_;
             a.xcd = xcd_fit(nbt_, sx_xcd_v_);
             launch_tile(a, Po != nullptr, A1_.p || !la_u_);  // (weights staged with the runs)
         } else if (Po) {
-            k_sx_vertex_sweep<real, kBlock, true><<<g, kBlock, 0, s>>>(a);
+            launch_fused<true>(a, g);
         } else {
-            k_sx_vertex_sweep<real, kBlock><<<g, kBlock, 0, s>>>(a);
+            launch_fused<false>(a, g);
         }
     } else {
         ProfScope ps(prof, "sx_vertex_wide", s);

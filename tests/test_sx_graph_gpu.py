@@ -158,3 +158,40 @@ def test_sx_tile_order_identical(gpu_lib, dt, K, al, difRcd):
         assert it0 == it1
         assert np.array_equal(X0, X1)
         assert np.array_equal(D0[:it0], D1[:it1])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("K,al", [(10, 0.1), (3, 0.0), (64, 1.0), (7, 0.1)])
+def test_sx_fused_widths_identical(gpu_lib, dt, K, al):
+    """The one-GPU fused sweep on workgroups of 64, 128 or 256 lanes
+    (PFDR_SX_NT), with and without the padded block lists (PFDR_SX_PAD=0):
+    identical iterates, counts and (sequential) Dif, tracked to a tolerance
+    with reconditionings and at a fixed iteration count"""
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph
+    rng = np.random.default_rng(K + 11)
+    Eu, Ev = grid_graph((90, 70), 8)
+    V = 90 * 70
+    Q = rng.random((V, K))
+    Q[: V // 2, 0] += 1.0
+    Q = (Q / Q.sum(axis=1, keepdims=True)).reshape(-1).astype(dt)
+    La = np.full(Eu.size, 0.05, dt)
+    for kw in (dict(difTol=1e-6, difRcd=1e-2, evolution=pfdr.EVOLUTION_SEQUENTIAL),
+               dict(difTol=0.0, difRcd=0.0)):
+        res = []
+        for env in ({"PFDR_SX_NT": "256"}, {"PFDR_SX_NT": "128"}, {"PFDR_SX_NT": "64"},
+                    {"PFDR_SX_NT": "64", "PFDR_SX_PAD": "0"}, {"PFDR_SX_NT": "256", "PFDR_SX_PAD": "0"}):
+            with _env(PFDR_SX_TINY="0", **env):
+                s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, La, Q.copy(), Q,
+                                 K=K, al=al, rho=1.0, condMin=0.1, itMax=120, record_dif=True, **kw)
+            try:
+                s.run(120)
+                res.append(s.result())
+            finally:
+                s.close()
+        X0, it0, _, D0 = res[0]
+        assert it0 > 0
+        for X1, it1, _, D1 in res[1:]:
+            assert it1 == it0
+            assert np.array_equal(X1, X0)
+            assert np.array_equal(D1[:it1], D0[:it0])
