@@ -705,6 +705,11 @@ struct SxVArgs {
     // beside its CSR pointers -- one round of loads fewer before the gathers
     const unsigned *idxp;
     int capb;
+    // zoff: the padded lists hold Z element offsets (u end e: e K, v end e:
+    // EK + e K, Zv = Zu + EK) instead of contribution addresses: one add per
+    // term, no side / received tests (one GPU, 2 EK + K < 2^32)
+    int zoff;
+    unsigned EK;
 };
 
 template <typename real>
@@ -775,6 +780,46 @@ __device__ __forceinline__ real sx_item_sum_from(const SxVArgs<real> &a, long v,
         const real z = (sv ? a.Zv : a.Zu)[ea * K + k];
         if (ea >= a.E) s += z;
         else s += (sx_wa(a, ea * K + k, ea, lu, la0) * inv) * z;
+    }
+    return s;
+}
+
+// the same sum from a list of Z offsets (SxVArgs::zoff): with one edge
+// weight and no A1, every term's splitting weight is the one product
+// la0 * 1/Aux, formed once (the reference's product, same rounding)
+template <typename real>
+__device__ __forceinline__ real sx_item_sum_off(const SxVArgs<real> &a, int k, const unsigned *off,
+                                                int j0, int j1, real inv) {
+    const real *Z = a.Zu;
+    real s = real(0);
+    int j = j0;
+    if (!a.A1) {
+        const real w = a.la0 * inv;
+        for (; j + 8 <= j1; j += 8) {
+            real z[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) z[q] = Z[off[j + q] + k];
+#pragma unroll
+            for (int q = 0; q < 8; q++) s += w * z[q];
+        }
+        for (; j < j1; j++) s += w * Z[off[j] + k];
+    } else {
+        const unsigned EK = a.EK;
+        for (; j + 8 <= j1; j += 8) {
+            real z[8], an[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const unsigned o = off[j + q];
+                z[q] = Z[o + k];
+                an[q] = a.A1[(o >= EK ? o - EK : o) + k];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) s += (an[q] * inv) * z[q];
+        }
+        for (; j < j1; j++) {
+            const unsigned o = off[j];
+            s += (a.A1[(o >= EK ? o - EK : o) + k] * inv) * Z[o + k];
+        }
     }
     return s;
 }
@@ -905,10 +950,13 @@ __device__ __forceinline__ real sx_tile_item(const SxVArgs<real> &a, int my0, in
 // The body of k_sx_vertex_sweep, shared with the one-workgroup
 // k_sx_tiny_iterate (four blocks side by side).
 // SPLIT (speculative sessions): the new P and (P, step) go to Po / PFo
+// lidx: the padded block list's LDS copy (SxVArgs::idxp); x0s: the raw
+// x[0] of each vertex (then the items divide by their metric in parallel and
+// the walk takes proj_simplex_column_div), null: the walk divides
 template <typename real, int NT, bool SPLIT = false>
 __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk, int t, real *xs,
                                                 real *ms, real *red, real *part_out,
-                                                unsigned *lidx = nullptr) {
+                                                unsigned *lidx = nullptr, real *x0s = nullptr) {
     const int K = a.c.K, vb = a.vb;
     const int vl = t / K;
     const int k = t - vl * K;
@@ -939,18 +987,32 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
         j1 -= b0;
         __syncthreads();
         if (live) {
-            xs[t] = sx_item_sum_from(a, v, k, lidx, j0, j1, inv);
+            const real x = a.zoff ? sx_item_sum_off(a, k, lidx, j0, j1, inv)
+                                  : sx_item_sum_from(a, v, k, lidx, j0, j1, inv);
+            if (x0s) {  // (ref src/proj_simplex_metric.cpp:44, :49)
+                xs[t] = x / ga;
+                if (k == 0) x0s[vl] = x;
+            } else {
+                xs[t] = x;
+            }
             ms[t] = ga;
         }
     } else if (live) {
-        xs[t] = sx_item_sum(a, v, k);
+        const real x = sx_item_sum(a, v, k);
+        if (x0s) {
+            xs[t] = x / ga;
+            if (k == 0) x0s[vl] = x;
+        } else {
+            xs[t] = x;
+        }
         ms[t] = ga;
     }
     __syncthreads();
     real dif = real(0);
     if (blk < a.nb && t < vb && v0 + t < a.V) {
         real *x = xs + t * K;
-        proj_simplex_column<real>(x, ms + t * K, K, real(1));
+        if (x0s) proj_simplex_column_div<real>(x, ms + t * K, K, x0s[t], real(1));
+        else proj_simplex_column<real>(x, ms + t * K, K, real(1));
         if (a.track == 2) {
             real mx = x[0];
             int l = 0;
@@ -995,9 +1057,10 @@ __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     __shared__ real xs[NT], ms[NT];
     __shared__ real red[NT / kWave];
     __shared__ unsigned lidx[kSxPadPer * NT];
+    __shared__ real x0s[NT];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
-    sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk, lidx);
+    sx_vertex_block<real, NT, SPLIT>(a, blk, threadIdx.x, xs, ms, red, a.part + blk, lidx, x0s);
 }
 
 // the padded lists (SxVArgs::idxp) and their width: the largest block's
@@ -1009,15 +1072,22 @@ __global__ void k_sx_block_max(int nb, int vb, int V, const int *__restrict__ pt
     const long v0 = (long)b * vb, v1 = min(v0 + vb, (long)V);
     atomicMax(capb, ptr[v1] - ptr[v0]);
 }
+// (K > 0: Z offsets, SxVArgs::zoff; else the addresses)
 __global__ void k_sx_pad_idx(long n, int capb, int vb, int V, const int *__restrict__ ptr,
-                             const unsigned *__restrict__ idx, unsigned *__restrict__ idxp) {
+                             const unsigned *__restrict__ idx, unsigned *__restrict__ idxp,
+                             long E, int K) {
     const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
     const long b = q / capb;
     const int j = (int)(q - b * capb);
     const long v0 = b * vb, v1 = min(v0 + vb, (long)V);
     const int j0 = ptr[v0];
-    idxp[q] = j < ptr[v1] - j0 ? idx[j0 + j] : 0u;
+    unsigned x = 0u;
+    if (j < ptr[v1] - j0) {
+        const unsigned ad = idx[j0 + j];
+        x = K ? (unsigned)(ad >= (unsigned long)E ? E * K + (ad - E) * (long)K : (long)ad * K) : ad;
+    }
+    idxp[q] = x;
 }
 
 // Tile-ordered sessions: one workgroup per tile block of M * vb vertices (M
@@ -2078,7 +2148,8 @@ class SimplexSession final : public SessionBase {
     // (P, explicit step) pairs per (v, k), ghosts included: written with P
     // by the vertex sweep, one access per edge end in the edge sweep
     DevBuf<SxR2<real>> PF_;
-    DevBuf<real> Zu_, Zv_, A1_, wz_, part_, opart_, Obj_, Dif_;
+    DevBuf<real> Zu_, A1_, wz_, part_, opart_, Obj_, Dif_;
+    real *zv_ = nullptr;  // the v ends' Z (inside Zu_'s allocation)
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
     // stored prox weights/thresholds of the non-linear losses for odd K (one
     // (e, k) per lane); even K takes two per lane and recomputes them from
@@ -2106,6 +2177,7 @@ class SimplexSession final : public SessionBase {
     // the one-GPU fused sweep's workgroups: snt_ lanes, svb_ vertices,
     // snb_ blocks (PFDR_SX_NT = 64, 128, 256; fused_sweep_setup)
     int snt_ = kBlock, svb_ = 0, snb_ = 0;
+    bool zoff_ = false;  // the padded lists hold Z offsets (SxVArgs::zoff)
     void fused_sweep_setup();
     void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
@@ -2335,8 +2407,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     const size_t EKn = EK_ ? EK_ : 1;
     // Zv carries the received contributions (the senders' W*Z) after its
     // E*K entries for the fused vertex sweep
-    Zu_.alloc(EKn);
-    Zv_.alloc(EKn + (size_t)R_ * K_);
+    // one allocation, u ends then v ends (zv_ = Zu_.p + EKn): the fused
+    // sweep's padded lists address both sides from one base (SxVArgs::zoff)
+    Zu_.alloc(2 * EKn + (size_t)R_ * K_);
+    zv_ = Zu_.p + EKn;
     GI_.alloc(VgK);
     sx_pw_ = K_ % 2 != 0;
     if (sx_pw_ && c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
@@ -2362,7 +2436,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     hctrl_->difRcd = difRcd_;
     PFDR_HIP(hipMemcpyAsync(ctrl_.p, hctrl_, sizeof(Ctrl<real>), hipMemcpyHostToDevice, s));
 
-    if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, Zv_.p);
+    if (EK_) k_sx_z_init<real><<<grid_for(EK_), kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, P_.p, Zu_.p, zv_);
     precondition(true);
     invV_.alloc(V_);
     k_sx_inv_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, K_, invAux_.p, invV_.p);
@@ -2449,7 +2523,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     graphs = graphs_ok_ ? 1 : 0;
     device_bytes = (int64_t)(Eu_.n + Ev_.n + inc_.ptr.n + inc_.idx.n) * 4;
     for (DevBuf<real> *b : {&La_d1_, &La_f_, &Q_, &P_, &Pavg_, &Ga_, &GaQ_, &invAux_, &lab_,
-                            &Zu_, &Zv_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
+                            &Zu_, &A1_, &Wd1u_, &Wd1v_, &Th_, &wz_, &part_, &opart_, &Obj_,
                             &Dif_, &terms_, &Px_[0], &Px_[1], &Px_[2], &route_.slice})
         device_bytes += (int64_t)(b->n * sizeof(real));
     device_bytes += (int64_t)((GI_.n + PF_.n + PFx_[0].n + PFx_[1].n + PFx_[2].n) *
@@ -2500,7 +2574,7 @@ void SimplexSession<real>::precondition(bool init) {
         pullK(Ga_);
         if (EK_) k_sx_subgrad<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, P_.p, Q_.p, Ga_.p,
                                                           GaQ_.p, first_recond ? nullptr : A1_.p,
-                                                          La_d1_.p, invAux_.p, Zu_.p, Zv_.p);
+                                                          La_d1_.p, invAux_.p, Zu_.p, zv_);
     }
     if (first_recond) A1_.alloc(EK_ ? EK_ : 1);  // a leaves La_d1 for good
     k_sx_hessian<real><<<gV, kBlock, 0, s>>>(VK_, c_, La_f_.p, P_.p, Q_.p, Ga_.p);
@@ -2514,7 +2588,7 @@ void SimplexSession<real>::precondition(bool init) {
     pullK(GaQ_);
     if (EK_ && !init)
         k_sx_recond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, A1_.p, invAux_.p, Ga_.p,
-                                                     GaQ_.p, P_.p, Q_.p, Zu_.p, Zv_.p);
+                                                     GaQ_.p, P_.p, Q_.p, Zu_.p, zv_);
     k_sx_gi_pack<real><<<grid_for((long)Vg_ * K_), kBlock, 0, s>>>((long)Vg_ * K_, Ga_.p,
                                                                   invAux_.p, GI_.p);
     if (EK_ && Th_.p)
@@ -2579,8 +2653,10 @@ void SimplexSession<real>::fused_sweep_setup() {
         if (h > 0 && h <= kSxPadPer * snt_ && n <= 3 * E_) {  // (2E list entries, at most 1.5 x)
             capb_ = h;
             idxp_.alloc((size_t)n);
+            // (one GPU: no received entries; one edge weight until A1 exists)
+            zoff_ = la_u_ && 2 * EK_ + K_ <= 0xffffffffL;
             k_sx_pad_idx<<<grid_for(n), kBlock, 0, s>>>(n, h, svb_, V_, inc_.ptr.p, inc_.idx.p,
-                                                        idxp_.p);
+                                                        idxp_.p, E_, zoff_ ? K_ : 0);
             PFDR_HIP(hipGetLastError());
         }
     }
@@ -2664,13 +2740,13 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
         const int xm = xcd_fit(nb, sx_xcd_e_);
         if (pair == 2)
             k_sx_edge_sweep<real, 2><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
-                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Zu_.p, zv_, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                nullptr,
                                                                rho_, c, nb, xm);
         else
             k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
-                                                               Zu_.p, Zv_.p, A1_.p, La_d1_.p, GI_.p,
+                                                               Zu_.p, zv_, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                nullptr,
                                                                rho_, c, nb, xm);
@@ -2685,12 +2761,14 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     a.Po = Po; a.PFo = PFo;
     a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = c;
     a.terms = seqdif_ ? terms_.p : nullptr;
-    a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
+    a.Zu = Zu_.p; a.Zv = zv_; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
     a.invV = A1_.p ? nullptr : invV_.p;
     a.la0 = la0_; a.la_u = la_u_ ? 1 : 0;
     a.nop = plazy_ ? 1 : 0;
     a.idxp = idxp_.p;
     a.capb = capb_;
+    a.zoff = zoff_ ? 1 : 0;
+    a.EK = (unsigned)EK_;
     if (vb_) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.vb = svb_;
@@ -2747,24 +2825,24 @@ void SimplexSession<real>::push_wz() {
     if (n) {
         k_sx_pack_wz<real><<<grid_for(n * K_), kBlock, 0, stream>>>(n, K_, E_, halo_->push_addr.p,
                                                                     Eu_.p, Ev_.p, A1_.p, La_d1_.p, GI_.p,
-                                                                    Zu_.p, Zv_.p, buf);
+                                                                    Zu_.p, zv_, buf);
         PFDR_HIP(hipGetLastError());
     }
-    halo_->push_packed(buf, Zv_.p + EK_, eb, stream);  // the tail of Zv (vertex sweep)
+    halo_->push_packed(buf, zv_ + EK_, eb, stream);  // the tail of Zv (vertex sweep)
 }
 
 template <typename real>
 void SimplexSession<real>::tiny_chunk(int n) {
     const bool gated = track_ || rec_obj_;
     SxTinyArgs<real> t{};
-    t.EK = EK_; t.c = c_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Zu = Zu_.p; t.Zv = Zv_.p;
+    t.EK = EK_; t.c = c_; t.Eu = Eu_.p; t.Ev = Ev_.p; t.Zu = Zu_.p; t.Zv = zv_;
     t.A1 = A1_.p; t.La_d1 = La_d1_.p; t.Wd1u = Wd1u_.p; t.Wd1v = Wd1v_.p; t.Th = Th_.p;
     t.GI = GI_.p; t.rho = rho_;
     SxVArgs<real> &a = t.va;
     a.V = V_; a.vb = vb_; a.E = E_; a.c = c_; a.ptr = inc_.ptr.p; a.idx = inc_.idx.p;
     a.wz = wz_.p; a.Ga = Ga_.p; a.GaQ = GaQ_.p; a.Q = Q_.p; a.P = P_.p; a.PF = PF_.p;
     a.lab = lab_.p; a.track = track_; a.part = part_.p; a.ctrl = nullptr;
-    a.Zu = Zu_.p; a.Zv = Zv_.p; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
+    a.Zu = Zu_.p; a.Zv = zv_; a.A1 = A1_.p; a.La_d1 = La_d1_.p; a.invAux = invAux_.p;
     a.nb = nbs_; a.xcd = 0;
     t.ctrl = gated ? ctrl_.p : nullptr;
     t.Dif = rec_dif_ ? Dif_.p : nullptr;
