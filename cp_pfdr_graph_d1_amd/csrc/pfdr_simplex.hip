@@ -1051,6 +1051,7 @@ __device__ __forceinline__ void sx_vertex_block(const SxVArgs<real> &a, int blk,
 
 constexpr int kSxPadPer = 8;  // entries of a padded block list per lane, at most
 constexpr int kSxNtDefault = 256;  // the fused sweep's workgroup width (fused_sweep_setup)
+constexpr int kSxMDefault = 2;     // its vertex blocks per workgroup (fused_sweep_setup)
 template <typename real, int NT, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void k_sx_vertex_sweep(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
@@ -1096,15 +1097,19 @@ __global__ void k_sx_pad_idx(long n, int capb, int vb, int V, const int *__restr
 // workgroup's load rounds and projection walk M times the work: the sweep
 // is bound by the latency of those serial phases, not by its bytes.
 
-template <typename real, bool SPLIT, bool WA, int M>
+// ST: staged tile sums (the block's record); else the CSR gather, from the
+// block's padded list in LDS (SxVArgs::idxp over M * vb vertices) when there
+// is one -- M items per lane, their gathers in flight together
+template <typename real, bool SPLIT, bool WA, int M, bool ST = true>
 __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     using L = SxTileLds<real, M>;
     __shared__ real xs[L::items], ms[L::items], x0s[L::items];
     __shared__ real red[M][kBlock / kWave];
-    __shared__ real zl[L::cap];
-    __shared__ real al[WA ? L::cap : 1];
+    __shared__ real zl[ST ? L::cap : 1];
+    __shared__ real al[ST && WA ? L::cap : 1];
     __shared__ int rt[2 * (kSxRuns + 1)];
+    __shared__ unsigned lidx[ST ? 1 : kSxPadPer * kBlock];
     const int blk = xcd_block(blockIdx.x, a.nb, a.xcd);
     if (blk >= a.nb) return;
     const int t = threadIdx.x;
@@ -1138,11 +1143,54 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
             j1[u] = a.ptr[vi[u] + 1];
         }
     }
-    if (a.trec[(long)blk * kSxRec] > 0) {  // block-uniform
+    if (ST && a.trec[(long)blk * kSxRec] > 0) {  // block-uniform
         sx_tile_stage<real, WA, M>(a, blk, t, zl, al, rt);
 #pragma unroll
         for (int u = 0; u < M; u++)
             if (live[u]) x[u] = sx_tile_item(a, j0[u] - b0, j1[u] - b0, kk[u], inv[u], zl, al, WA);
+    } else if (!ST && a.idxp) {  // the padded list (SxVArgs::idxp) into LDS
+        const long lb = (long)blk * a.capb;
+        for (int q = t; q < a.capb; q += kBlock) lidx[q] = a.idxp[lb + q];
+        __syncthreads();
+        if (a.zoff && !a.A1) {
+            // Z offsets, one splitting weight la0 * 1/Aux per item: the M
+            // items' 8 gathers each in flight together, added in order
+            const real *Z = a.Zu;
+            real w[M];
+            int j[M], e[M];
+#pragma unroll
+            for (int u = 0; u < M; u++) {
+                w[u] = a.la0 * inv[u];
+                j[u] = live[u] ? j0[u] - b0 : 0;
+                e[u] = live[u] ? j1[u] - b0 : 0;
+            }
+            for (;;) {
+                bool more = false;
+#pragma unroll
+                for (int u = 0; u < M; u++) more |= j[u] < e[u];
+                if (!more) break;
+                real z[M][8];
+#pragma unroll
+                for (int u = 0; u < M; u++)
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        z[u][q] = j[u] + q < e[u] ? Z[lidx[j[u] + q] + kk[u]] : real(0);
+#pragma unroll
+                for (int u = 0; u < M; u++) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (j[u] + q < e[u]) x[u] += w[u] * z[u][q];
+                    j[u] += 8;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < M; u++)
+                if (live[u])
+                    x[u] = a.zoff ? sx_item_sum_off(a, kk[u], lidx, j0[u] - b0, j1[u] - b0, inv[u])
+                                  : sx_item_sum_from(a, vi[u], kk[u], lidx, j0[u] - b0,
+                                                     j1[u] - b0, inv[u]);
+        }
     } else {
 #pragma unroll
         for (int u = 0; u < M; u++)
@@ -2178,6 +2226,9 @@ class SimplexSession final : public SessionBase {
     // snb_ blocks (PFDR_SX_NT = 64, 128, 256; fused_sweep_setup)
     int snt_ = kBlock, svb_ = 0, snb_ = 0;
     bool zoff_ = false;  // the padded lists hold Z offsets (SxVArgs::zoff)
+    // the one-GPU fused sweep on workgroups of M vertex blocks (M items per
+    // lane, k_sx_vertex_tile without staging; PFDR_SX_M = 1, 2, 4): sxm_ > 1
+    int sxm_ = 1;
     void fused_sweep_setup();
     void build_sx_tiles();
     // one La_d1 for every edge (k_sx_uniform_check at setup): a kernel argument
@@ -2232,6 +2283,15 @@ class SimplexSession final : public SessionBase {
         if (halo_) halo_->pull(PF_.p, K_ * (int)sizeof(SxR2<real>), stream);
     }
     void push_wz();
+    template <bool SPLIT>
+    void launch_m_s(const SxVArgs<real> &a) {
+        const int g = xcd_grid(a.nb, a.xcd);
+        if (sxm_ == 2) k_sx_vertex_tile<real, SPLIT, false, 2, false><<<g, kBlock, 0, stream>>>(a);
+        else k_sx_vertex_tile<real, SPLIT, false, 4, false><<<g, kBlock, 0, stream>>>(a);
+    }
+    void launch_m(const SxVArgs<real> &a, bool split) {
+        split ? launch_m_s<true>(a) : launch_m_s<false>(a);
+    }
     template <bool SPLIT>
     void launch_fused(const SxVArgs<real> &a, int g) {
         if (snt_ == 64) k_sx_vertex_sweep<real, 64, SPLIT><<<g, 64, 0, stream>>>(a);
@@ -2631,7 +2691,16 @@ void SimplexSession<real>::fused_sweep_setup() {
     const char *ntv = getenv("PFDR_SX_NT");
     const int nt = ntv ? atoi(ntv) : kSxNtDefault;
     if (nt != 64 && nt != 128 && nt != 256) throw std::runtime_error("PFDR_SX_NT: 64, 128 or 256");
-    if ((!track_ || seqdif_) && !trec_.p && K_ <= nt) {
+    const char *mv = getenv("PFDR_SX_M");
+    sxm_ = mv ? atoi(mv) : kSxMDefault;
+    if (sxm_ != 1 && sxm_ != 2 && sxm_ != 4) throw std::runtime_error("PFDR_SX_M: 1, 2 or 4");
+    if (trec_.p) sxm_ = 1;  // (the staged sweep has its own blocks)
+    if (sxm_ > 1) {  // workgroups of sxm_ vertex blocks (their partials: the 256-lane sweep's)
+        tbv_ = sxm_ * vb_;
+        nbt_ = (int)((V_ + tbv_ - 1) / tbv_);
+        svb_ = tbv_;  // (the padded lists below cover a workgroup's vertices)
+        snb_ = nbt_;
+    } else if ((!track_ || seqdif_) && !trec_.p && K_ <= nt) {
         snt_ = nt;
         svb_ = nt / K_;
         snb_ = (int)((V_ + svb_ - 1) / svb_);
@@ -2651,6 +2720,7 @@ void SimplexSession<real>::fused_sweep_setup() {
         PFDR_HIP(hipStreamSynchronize(s));
         const long n = (long)snb_ * h;
         if (h > 0 && h <= kSxPadPer * snt_ && n <= 3 * E_) {  // (2E list entries, at most 1.5 x)
+            // (sxm_ > 1: lists of kSxPadPer * 256 entries at most, as snt_ = 256)
             capb_ = h;
             idxp_.alloc((size_t)n);
             // (one GPU: no received entries; one edge weight until A1 exists)
@@ -2702,7 +2772,7 @@ void SimplexSession<real>::body() {
     const Ctrl<real> *c = gated ? ctrl_.p : nullptr;
     sweeps(c, 0);
     // (the staged tile sweep writes the 256-lane fused sweep's partials)
-    const int nparts = trec_.p ? nbs_ : vb_ ? snb_ : nbw_;
+    const int nparts = (trec_.p || sxm_ > 1) ? nbs_ : vb_ ? snb_ : nbw_;
     if (seqdif_) {
         // the reference's sequential sum (ref :655-689), then its decision
         ProfScope ps(prof, "seq_evolution", s);
@@ -2782,6 +2852,12 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
             a.nb = nbt_;
             a.xcd = xcd_fit(nbt_, sx_xcd_v_);
             launch_tile(a, Po != nullptr, A1_.p || !la_u_);  // (weights staged with the runs)
+        } else if (sxm_ > 1) {  // workgroups of sxm_ vertex blocks, the CSR gather
+            a.nparts = nbs_;
+            a.vb = vb_;
+            a.nb = nbt_;
+            a.xcd = xcd_fit(nbt_, sx_xcd_v_);
+            launch_m(a, Po != nullptr);
         } else if (Po) {
             launch_fused<true>(a, g);
         } else {

@@ -164,7 +164,8 @@ def test_sx_tile_order_identical(gpu_lib, dt, K, al, difRcd):
 @pytest.mark.parametrize("K,al", [(10, 0.1), (3, 0.0), (64, 1.0), (7, 0.1)])
 def test_sx_fused_widths_identical(gpu_lib, dt, K, al):
     """The one-GPU fused sweep on workgroups of 64, 128 or 256 lanes
-    (PFDR_SX_NT), with and without the padded block lists (PFDR_SX_PAD=0):
+    (PFDR_SX_NT) or of 2 / 4 vertex blocks (PFDR_SX_M), with and without the
+    padded block lists (PFDR_SX_PAD=0):
     identical iterates, counts and (sequential) Dif, tracked to a tolerance
     with reconditionings and at a fixed iteration count"""
     from cp_pfdr_graph_d1_amd import pfdr
@@ -179,8 +180,11 @@ def test_sx_fused_widths_identical(gpu_lib, dt, K, al):
     for kw in (dict(difTol=1e-6, difRcd=1e-2, evolution=pfdr.EVOLUTION_SEQUENTIAL),
                dict(difTol=0.0, difRcd=0.0)):
         res = []
-        for env in ({"PFDR_SX_NT": "256"}, {"PFDR_SX_NT": "128"}, {"PFDR_SX_NT": "64"},
-                    {"PFDR_SX_NT": "64", "PFDR_SX_PAD": "0"}, {"PFDR_SX_NT": "256", "PFDR_SX_PAD": "0"}):
+        for env in ({"PFDR_SX_M": "1"}, {"PFDR_SX_M": "2"}, {"PFDR_SX_M": "4"},
+                    {"PFDR_SX_M": "2", "PFDR_SX_PAD": "0"}, {"PFDR_SX_M": "1", "PFDR_SX_NT": "128"},
+                    {"PFDR_SX_M": "1", "PFDR_SX_NT": "64"},
+                    {"PFDR_SX_M": "1", "PFDR_SX_NT": "64", "PFDR_SX_PAD": "0"},
+                    {"PFDR_SX_M": "1", "PFDR_SX_PAD": "0"}):
             with _env(PFDR_SX_TINY="0", **env):
                 s = pfdr.Session(pfdr.PFDR_KIND_SIMPLEX, dt, V, Eu.size, Eu, Ev, La, Q.copy(), Q,
                                  K=K, al=al, rho=1.0, condMin=0.1, itMax=120, record_dif=True, **kw)
