@@ -266,7 +266,11 @@ class QuadSession final : public SessionBase {
     DevBuf<unsigned short> luv_;  // both ends mod 256 (k_edge_sweep_tl)
     DevBuf<int> erec_;            // per edge block: u blocks and v runs (k_edge_sweep_tl)
     DevBuf<int> ustart_, tptr_, tstart_, tlen_, tok_, trec_;
+    DevBuf<Slots12> ptab_;        // slot patterns of the record blocks' runs (k_run_hash)
+    DevBuf<int> prec_;            // per record block: its runs' offsets into ptab_
     void build_tiles();
+    void build_patterns(const unsigned short *d2, long n);
+    void build_tile_runs();
     Ctrl<real> *hctrl_ = nullptr;  // pinned mirror
     int nbv_, nbe_, nbn_, rows_nb_, rows_cpb_;
     int it_ = 0;
@@ -891,7 +895,6 @@ void QuadSession<real>::setup_graph(const pfdr_problem *p) {
 template <typename real>
 void QuadSession<real>::build_tiles() {
     hipStream_t s = stream;
-    const int nb = grid_for(V_);
     const long R = halo_ ? halo_->R : 0;
     {
         const long n = 2 * E_ + R, ng = n / kSlotGroup + 1;  // (+1: tile_sum's whole groups)
@@ -900,7 +903,17 @@ void QuadSession<real>::build_tiles() {
         slots_.alloc(ng);
         k_pack_slots<<<grid_for(ng), kBlock, 0, s>>>(ng, n, d2.p, slots_.p);
         PFDR_HIP(hipGetLastError());
+        build_tile_runs();
+        build_patterns(d2.p, n);
     }  // (d2's block is reused only once the stream is idle, dev_free)
+}
+
+// the record and run tables of the tiled blocks (see tile_sum)
+template <typename real>
+void QuadSession<real>::build_tile_runs() {
+    hipStream_t s = stream;
+    const int nb = grid_for(V_);
+    const long R = halo_ ? halo_->R : 0;
     luv_.alloc((size_t)E_);
     k_tile_luv<<<grid_for(E_), kBlock, 0, s>>>(E_, Eu_.p, Ev_.p, luv_.p);
     {
@@ -956,6 +969,107 @@ void QuadSession<real>::build_tiles() {
     }
     tiled_blocks = n;
     record_blocks = nr;
+}
+
+// Slot patterns (k_run_hash): when the record blocks' runs repeat a few
+// slot sequences (regular grids), the distinct ones go to a small table
+// (ptab_) and each block's runs point into it (prec_), so the vertex sweep
+// streams no per-entry slots; runs that hash alike are verified equal
+// entry by entry (k_run_verify) before the table is used.  Off when the
+// patterns do not repeat (the jittered headline) or PFDR_TILE_PATTERNS=0.
+template <typename real>
+void QuadSession<real>::build_patterns(const unsigned short *d2, long n) {
+    const char *e = getenv("PFDR_TILE_PATTERNS");
+    if ((e && e[0] == '0') || !record_blocks) return;
+    hipStream_t s = stream;
+    const int nb = grid_for(V_);
+    const long nr = (long)nb * kPrec;
+    std::vector<unsigned long long> hh(nr);
+    std::vector<int> rec((size_t)nb * kTileRec);
+    {
+        DevBuf<unsigned long long> h(nr);
+        k_run_hash<<<grid_for(nr), kBlock, 0, s>>>(nb, E_, tok_.p, trec_.p, d2, h.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipMemcpyAsync(hh.data(), h.p, sizeof(unsigned long long) * nr,
+                                hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipMemcpyAsync(rec.data(), trec_.p, sizeof(int) * rec.size(),
+                                hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+    }
+    constexpr size_t kMaxPatterns = 65536;
+    std::unordered_map<unsigned long long, int> pat;
+    std::vector<long long> pA;
+    std::vector<int> pLen, pOff, prec(nr, 0);
+    std::vector<long long> repA(nr, -1);
+    long groups = 0;
+    for (long id = 0; id < nr; id++) {
+        if (hh[id] == ~0ull) continue;
+        auto it = pat.find(hh[id]);
+        int pi;
+        if (it == pat.end()) {
+            const int b = (int)(id / kPrec), q = (int)(id % kPrec);
+            const int *r = &rec[(size_t)b * kTileRec];
+            const long long A = q == 0 ? r[0] : E_ + r[1 + 2 * q];
+            const int len = q == 0 ? r[1] : r[2 + 2 * q];
+            pi = (int)pA.size();
+            pat.emplace(hh[id], pi);
+            pA.push_back(A);
+            pLen.push_back(len);
+            pOff.push_back((int)groups);
+            groups += ((A & 7) + len + 7) / 8;
+            if (pat.size() > kMaxPatterns || groups * kSlotGroup > n / 4) return;  // no repeats
+        } else {
+            pi = it->second;
+        }
+        prec[id] = pOff[pi];
+        repA[id] = pA[pi];
+    }
+    if (!groups) return;
+    {   // same hash, same slots: checked entry by entry on the device
+        DevBuf<long long> dr(nr);
+        DevBuf<int> bad(1);
+        PFDR_HIP(hipMemcpyAsync(dr.p, repA.data(), sizeof(long long) * nr, hipMemcpyHostToDevice, s));
+        PFDR_HIP(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+        k_run_verify<<<grid_for(nr), kBlock, 0, s>>>(nb, E_, tok_.p, trec_.p, d2, dr.p, bad.p);
+        PFDR_HIP(hipGetLastError());
+        int hb = 1;
+        PFDR_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        if (hb) return;
+    }
+    // the table: each pattern's groups packed from its representative's
+    // slots (12 bits each, as k_pack_slots; entries outside the run are 0)
+    std::vector<Slots12> tab((size_t)groups);
+    std::vector<unsigned short> sl;
+    for (size_t pi = 0; pi < pA.size(); pi++) {
+        const long long A = pA[pi], g0 = A / kSlotGroup;
+        const int len = pLen[pi];
+        const long gn = ((A & 7) + len + 7) / 8;
+        if (!gn) continue;
+        sl.assign((size_t)gn * kSlotGroup, 0);
+        PFDR_HIP(hipMemcpy(sl.data() + (A - g0 * kSlotGroup), d2 + A, sizeof(unsigned short) * len,
+                           hipMemcpyDeviceToHost));
+        for (long g = 0; g < gn; g++) {
+            unsigned long long lo = 0, hi = 0;
+            for (int q = 0; q < kSlotGroup; q++) {
+                const unsigned long long x = sl[(size_t)g * kSlotGroup + q] & 0xfffu;
+                const int bit = 12 * q;
+                if (bit + 12 <= 64) lo |= x << bit;
+                else if (bit >= 64) hi |= x << (bit - 64);
+                else { lo |= x << bit; hi |= x >> (64 - bit); }
+            }
+            Slots12 &t = tab[(size_t)pOff[pi] + g];
+            t.w[0] = (unsigned)lo;
+            t.w[1] = (unsigned)(lo >> 32);
+            t.w[2] = (unsigned)hi;
+        }
+    }
+    ptab_.alloc((size_t)groups);
+    prec_.alloc((size_t)nr);
+    PFDR_HIP(hipMemcpyAsync(ptab_.p, tab.data(), sizeof(Slots12) * groups, hipMemcpyHostToDevice, s));
+    PFDR_HIP(hipMemcpyAsync(prec_.p, prec.data(), sizeof(int) * nr, hipMemcpyHostToDevice, s));
+    PFDR_HIP(hipStreamSynchronize(s));
+    slot_patterns = (int64_t)pA.size();
 }
 
 // Split incidence for the vertex sweep (split_sum): when the edges are
@@ -1357,7 +1471,7 @@ VArgs<real> QuadSession<real>::vargs(int bbeg, int bend, const Ctrl<real> *c) {
     a.late = fuse_ ? 1 : 0;
     a.E = E_;
     if (tiled_) {
-        a.slots = slots_.p; a.trec = trec_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
+        a.slots = slots_.p; a.trec = trec_.p; a.ptab = ptab_.p; a.prec = prec_.p; a.deg8 = deg8_.p; a.ustart = ustart_.p; a.tptr = tptr_.p; a.tstart = tstart_.p;
         a.tlen = tlen_.p; a.tok = tok_.p;
         a.zs = Z2_.p; a.invAux = invAux_.p; a.a0 = cw_ * la0_;
         a.gi = gi_.p;  // (Ga, 1/Aux) in one load

@@ -380,17 +380,23 @@ __device__ __forceinline__ real tile_sum(int V, long E, int blk, int v,
 // the runs in its lanes, and the u-end and v-end groups are loaded in the
 // same round -- two groups in flight per lane -- before one barrier.
 constexpr int kRecRuns = 14, kTileRec = 32;
+constexpr int kPrec = 16;  // runs per block in prec: the u run, then up to 15 v runs
+
 template <typename real, bool ZD = false>
 __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
                                              const unsigned char *__restrict__ deg8,
                                              const Slots12 *__restrict__ slots,
                                              const int *__restrict__ trec,
                                              const real *__restrict__ wz, real *lds, int *wt,
-                                             real wv = real(1)) {
+                                             real wv = real(1),
+                                             const Slots12 *__restrict__ ptab = nullptr,
+                                             const int *__restrict__ prec = nullptr) {
     constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const int dg = v < V ? deg8[v] : 0;
     const int rv = lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
+    // pattern offsets of the runs (prec, with the record; null: per-entry slots)
+    const int pr = prec && lane < kPrec ? prec[(long)blk * kPrec + lane] : 0;
     int dinc = dg;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -421,6 +427,7 @@ __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
         Slots12 d[2];
         Pk<real, VE> x[2][ZV];
         long gb[2], lo[2], hi[2];
+        int pg[2];  // the group's entry in the pattern table
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int k = min(b + u * kBlock + tid, tot - 1);
@@ -433,20 +440,24 @@ __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
             r = min(r, kWave - 1);
             const int sr = __shfl(st, r, kWave), lr = __shfl(ln, r, kWave);
             const int pb = __shfl(P, max(r - 1, 0), kWave);
+            const int pv = __shfl(pr, min(r + 1, kWave - 1), kWave);
             if (k < ngu) {
                 gb[u] = fu + k;
                 lo[u] = us;
                 hi[u] = (long)us + nu;
+                pg[u] = __builtin_amdgcn_readlane(pr, 0) + k;
             } else {
                 const long A = E + sr;
-                gb[u] = A / G + (kv - (r > 0 ? pb : 0));
+                const int gi = kv - (r > 0 ? pb : 0);
+                gb[u] = A / G + gi;
                 lo[u] = A;
                 hi[u] = A + lr;
+                pg[u] = pv + gi;
             }
         }
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            d[u] = slots[gb[u]];
+            d[u] = prec ? ptab[pg[u]] : slots[gb[u]];
 #pragma unroll
             for (int z = 0; z < ZV; z++) x[u][z] = ldv<real, VE>(wz + gb[u] * G + z * VE);
         }
@@ -627,6 +638,66 @@ static __global__ void k_tile_rec(int nb, const int *__restrict__ ustart,
         r[4 + 2 * q] = tlen[t0 + q];
     }
     tok[b] = 2;
+}
+
+// ------------------------------------------------ slot patterns -------
+// On regular graphs most record blocks' runs carry the same slot sequences
+// (on C2 every interior block is one x-row of the grid; on C5 the 640-vertex
+// rows give five phases).  A run's PATTERN = (its first address mod 8, its
+// length, its slots); the distinct patterns go to a small table of packed
+// groups (ptab, aligned as each run's groups are) and each record block gets
+// the table offset of every run (prec: 16 ints beside its record), so the
+// vertex sweep reads no per-entry slot stream (12 B per 8 contributions).
+__device__ __forceinline__ bool rec_run(const int *r, long E, int q, long &A, int &len) {
+    const int nt = r[2];
+    if (q == 0) {
+        A = r[0];
+        len = r[1];
+    } else if (q <= nt) {
+        A = E + r[1 + 2 * q];
+        len = r[2 + 2 * q];
+    } else {
+        return false;
+    }
+    return true;
+}
+
+// hash of run q of record block b (~0: no run / not a record block)
+static __global__ void k_run_hash(int nb, long E, const int *__restrict__ tok,
+                                  const int *__restrict__ trec, const unsigned short *__restrict__ d2,
+                                  unsigned long long *__restrict__ h) {
+    const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (long)nb * kPrec) return;
+    const int b = (int)(id / kPrec), q = (int)(id - (long)b * kPrec);
+    unsigned long long x = ~0ull;
+    long A;
+    int len;
+    if (tok[b] == 2 && rec_run(trec + (long)b * kTileRec, E, q, A, len)) {
+        x = 0x9e3779b97f4a7c15ull * (unsigned long long)((A & 7) + 1) ^ (unsigned long long)len << 20;
+        for (int i = 0; i < len; i++) {
+            x ^= d2[A + i] + 0x9e3779b97f4a7c15ull + (x << 6) + (x >> 2);
+            x *= 0xbf58476d1ce4e5b9ull;
+        }
+        if (x == ~0ull) x = 0;
+    }
+    h[id] = x;
+}
+
+// every run's slots equal those of its pattern's representative (else *bad)
+static __global__ void k_run_verify(int nb, long E, const int *__restrict__ tok,
+                                    const int *__restrict__ trec,
+                                    const unsigned short *__restrict__ d2,
+                                    const long long *__restrict__ repA, int *__restrict__ bad) {
+    const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (long)nb * kPrec) return;
+    const int b = (int)(id / kPrec), q = (int)(id - (long)b * kPrec);
+    long A;
+    int len;
+    if (tok[b] != 2 || !rec_run(trec + (long)b * kTileRec, E, q, A, len)) return;
+    const long R = repA[id];
+    bool ok = R >= 0 && (R & 7) == (A & 7);
+    for (int i = 0; ok && i < len; i++) ok = d2[A + i] == d2[R + i];
+    if (!ok) atomicAdd(bad, 1);
 }
 
 // deg8[v] = the vertex's CSR entries (clamped; blocks with a larger one are
@@ -2140,6 +2211,8 @@ struct VArgs {
     long E;
     const Slots12 *slots;
     const int *trec;        // per-block records (tile_sum_rec; tok == 2)
+    const Slots12 *ptab;    // slot patterns (null: per-entry slots; see k_run_hash)
+    const int *prec;        // per record block: its runs' pattern offsets
     const unsigned char *deg8;
     const int *ustart, *tptr, *tstart, *tlen, *tok;
     // Z-direct (tiled single-GPU sessions with one edge weight, no A1): the
@@ -2267,7 +2340,7 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     const int tk = a.slots ? a.tok[blk] : 0;  // block-uniform
     if (tk == 2)
         x = tile_sum_rec<real, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
-                                   lds, scan + 3 * kTileRuns, wv);
+                                   lds, scan + 3 * kTileRuns, wv, a.ptab, a.prec);
     else if (tk)
         x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);

@@ -1101,7 +1101,8 @@ __global__ void k_sx_pad_idx(long n, int capb, int vb, int V, const int *__restr
 // block's padded list in LDS (SxVArgs::idxp over M * vb vertices) when there
 // is one -- M items per lane, their gathers in flight together
 template <typename real, bool SPLIT, bool WA, int M, bool ST = true>
-__global__ __launch_bounds__(kBlock) void k_sx_vertex_tile(SxVArgs<real> a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ST || M > 2 || sizeof(real) > 4 ? 1 : 8)))
+void k_sx_vertex_tile(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     using L = SxTileLds<real, M>;
     __shared__ real xs[L::items], ms[L::items], x0s[L::items];

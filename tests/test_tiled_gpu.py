@@ -159,3 +159,39 @@ def test_tiled_sparse_rows(gpu_lib, oracle_port, dt):
     print(q)
     assert q["tiled_blocks"] > 0
     assert np.array_equal(X, Xo)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("shape,conn", [((72, 64, 64), 6), ((640, 40, 12), 6), ((300, 260), 8)])
+def test_slot_patterns_identical(gpu_lib, oracle_port, dt, shape, conn):
+    """Regular grids: the record blocks' runs repeat a few slot sequences, which
+    the vertex sweep reads from a small pattern table (k_run_hash) instead of
+    the per-entry slot stream -- the same sums bit for bit: equal to the
+    per-entry run (PFDR_TILE_PATTERNS=0) and to the oracle, fixed k and
+    converged with reconditionings"""
+    import os
+    V, Eu, Ev = _grid(shape, conn, 1)
+    Y = piecewise_observation(shape, 3, dt)
+    out = []
+    for pat in ("1", "0"):
+        os.environ["PFDR_TILE_PATTERNS"] = pat
+        try:
+            s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                             np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5,
+                             condMin=1e-3, difTol=1e-6, difRcd=1e-3, itMax=400, record_dif=True)
+            try:
+                q = s.query("slot_patterns")
+                s.run(400)
+                out.append((s.result(), q))
+            finally:
+                s.close()
+        finally:
+            del os.environ["PFDR_TILE_PATTERNS"]
+    ((X1, it1, _, D1), q1), ((X0, it0, _, D0), q0) = out
+    print(shape, "patterns", q1, "it", it1)
+    assert q1 > 0 and q0 == 0
+    assert it1 == it0 and np.array_equal(X1, X0) and np.array_equal(D1[:it1], D0[:it0])
+    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
+                                                 np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
+                                                 0, 0, None, 1.5, 1e-3, 1e-3, 1e-6, 400, dif=True)
+    assert ito == it1 and np.array_equal(X1, Xo)
