@@ -178,7 +178,8 @@ def test_slot_patterns_identical(gpu_lib, oracle_port, dt, shape, conn):
         try:
             s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
                              np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5,
-                             condMin=1e-3, difTol=1e-6, difRcd=1e-3, itMax=400, record_dif=True)
+                             condMin=1e-3, difTol=1e-6, difRcd=1e-3, itMax=400, record_dif=True,
+                             evolution=pfdr.EVOLUTION_SEQUENTIAL)
             try:
                 q = s.query("slot_patterns")
                 s.run(400)
