@@ -169,24 +169,17 @@ class RcclTransport final : public Transport {
     ncclComm_t comm_;
     bool owned_ = false;             // a split communicator: destroyed with the transport
     ncclComm_t parent_ = nullptr;    // the communicator it was split from (comm_add_child)
-    // PFDR_RCCL_SELF=1 (test flag): operations that move nothing still issue
-    // real RCCL calls -- a 1-rank all-reduce / broadcast, and a grouped
-    // send / receive of a 4-byte token to this rank itself where an exchange
-    // or a chain step has no peer -- so that a 1-rank communicator runs
-    // (and hipGraph-captures) the same RCCL operations as the ranks of a
-    // real partition, instead of returning early
+    // PFDR_RCCL_SELF=1 (test flag): the collectives of a 1-rank
+    // communicator (all-reduces, broadcasts) are issued as real RCCL calls
+    // instead of returning early, so that a one-GPU run executes -- and
+    // hipGraph-captures -- the RCCL operations a real partition's chain,
+    // decision and objective use.  (A grouped send / receive to the rank
+    // itself, which would cover the point-to-point exchanges, crashed inside
+    // RCCL on this image: gpurun_out/r6p)
     bool self_ = false;
-    DevBuf<int> tok_;
-    void self_token(hipStream_t s) {
-        ck(ncclGroupStart(), "group start");
-        ck(ncclSend(tok_.p, 4, ncclChar, rank, comm_, s), "self send");
-        ck(ncclRecv(tok_.p + 1, 4, ncclChar, rank, comm_, s), "self recv");
-        ck(ncclGroupEnd(), "group end");
-    }
     void init_self() {
         const char *e = getenv("PFDR_RCCL_SELF");
         self_ = e && e[0] == '1';
-        if (self_) tok_.alloc(2);
     }
     static void ck(ncclResult_t r, const char *what) {
         if (r != ncclSuccess) {
@@ -235,10 +228,7 @@ class RcclTransport final : public Transport {
                   peers_bytes(rbytes, rank);
         bool any = false;  // (an exchange with nothing to move issues no RCCL call)
         for (int q = 0; q < nranks; q++) any = any || (q != rank && (sbytes[q] || rbytes[q]));
-        if (!any) {
-            if (self_) self_token(s);
-            return;
-        }
+        if (!any) return;
         ck(ncclGroupStart(), "group start");
         for (int q = 0; q < nranks; q++) {
             if (q == rank) continue;
@@ -257,16 +247,12 @@ class RcclTransport final : public Transport {
         if (rank > 0) {
             last_op = "chain recv of " + std::to_string(bytes) + " B from " + std::to_string(rank - 1);
             ck(ncclRecv(dev, bytes, ncclChar, rank - 1, comm_, s), "chain recv");
-        } else if (self_) {
-            self_token(s);
         }
     }
     void chain_send(const void *dev, size_t bytes, hipStream_t s) override {
         if (rank + 1 < nranks) {
             last_op = "chain send of " + std::to_string(bytes) + " B to " + std::to_string(rank + 1);
             ck(ncclSend(dev, bytes, ncclChar, rank + 1, comm_, s), "chain send");
-        } else if (self_) {
-            self_token(s);
         }
     }
     void broadcast(void *dev, size_t bytes, int root, hipStream_t s) override {

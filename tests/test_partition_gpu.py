@@ -370,12 +370,12 @@ class _env:
 
 @pytest.mark.parametrize("kind", ["l1", "simplex"])
 def test_rccl_single_rank_real_calls_graph_replay(gpu_lib, kind):
-    """PFDR_RCCL_SELF=1: a 1-rank communicator issues every RCCL operation a
-    real partition would (the exchanges and chain steps as grouped
-    send / receive pairs to itself, the all-reduces and broadcasts as 1-rank
-    collectives) instead of returning early, and the chunks of iterations
+    """PFDR_RCCL_SELF=1: a 1-rank communicator issues its collectives (the
+    evolution chain's all-reduce and broadcast, the setup's all-reduces) as
+    real RCCL calls instead of returning early, and the chunks of iterations
     capture them in hipGraphs: the iterates, counts and Dif equal the
-    single-GPU session's bit for bit"""
+    single-GPU session's bit for bit.  (Point-to-point to the rank itself
+    crashed inside RCCL on this image: not exercised.)"""
     import ctypes as C
     from cp_pfdr_graph_d1_amd import partition as P
     from cp_pfdr_graph_d1_amd import pfdr
@@ -429,7 +429,8 @@ def test_rccl_single_rank_real_calls_graph_replay(gpu_lib, kind):
 @pytest.mark.parametrize("spec", ["auto", "serial", "off"])
 def test_rccl_single_rank_real_calls_headline_conv(gpu_lib, spec):
     """the converged full-size headline (10M vertices, 60M edges, difTol
-    1e-5) as a 1-rank RCCL partition with PFDR_RCCL_SELF=1, in every
+    1e-5) as a 1-rank RCCL partition with PFDR_RCCL_SELF=1 (real 1-rank
+    collectives), in every
     speculation mode: auto (the evolution chain on a split communicator and a
     second stream), serial (one stream, one communicator), off (the plain
     loop, its chunks captured in hipGraphs with the RCCL calls inside):
