@@ -162,7 +162,7 @@ def test_tiled_sparse_rows(gpu_lib, oracle_port, dt):
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
-@pytest.mark.parametrize("shape,conn", [((72, 64, 64), 6), ((640, 40, 12), 6), ((512, 150), 8)])
+@pytest.mark.parametrize("shape,conn", [((72, 64, 64), 6), ((640, 40, 12), 6), ((512, 600), 8)])
 def test_slot_patterns_identical(gpu_lib, oracle_port, dt, shape, conn):
     """Regular grids: the record blocks' runs repeat a few slot sequences, which
     the vertex sweep reads from a small pattern table (k_run_hash) instead of
