@@ -865,6 +865,14 @@ struct ColArgs {
     int gate;
 };
 
+// acc + x y in double: f32 operands multiply exactly in double, so one fma
+// rounds as the product and the sum would; f64 keeps the multiply and add
+template <typename real>
+__device__ __forceinline__ double dacc(double acc, double x, double y) {
+    if (sizeof(real) == 4) return fma(x, y, acc);
+    return acc + x * y;
+}
+
 template <typename real, int EPI>
 __device__ __forceinline__ void col_epilogue(const ColArgs<real> &a, long col, real acc) {
     if (EPI == EPI_STORE || EPI == EPI_SELF) {
@@ -893,10 +901,12 @@ __device__ __forceinline__ void col_epilogue(const ColArgs<real> &a, long col, r
 
 // One wave64 per column: 16-byte loads of the column (and of w, which
 // every wave re-reads from L2), wave-shuffle reduction, fused epilogue.
-// The products and sums run in double whatever `real` (HBM-bound: the f64
-// arithmetic is free), so a tree-reduced f32 dot product lies closer to the
-// exact one than the reference's sequential f32 sum, not just as close
-// (tests/test_fullsize_pin_gpu.py: the yardstick is the reference's f64 run).
+// The products and sums run in double whatever `real` (HBM-bound), so a
+// tree-reduced f32 dot product lies closer to the exact one than the
+// reference's sequential f32 sum, not just as close (tests/
+// test_fullsize_pin_gpu.py: the yardstick is the reference's f64 run).  The
+// product of two f32 values is exact in double, so one fma per term rounds
+// exactly as a multiply and an add would (f64 fma: one instruction, not two).
 // ref: diag of A^tA :102-110, pseudo-inverse :126-134, apply A^tA
 // :368-376, gradient -A^t R :432-440, forward :462-464.
 template <typename real, int EPI>
@@ -915,10 +925,10 @@ __global__ __launch_bounds__(256) void k_col_dot(ColArgs<real> a) {
             Pk<real, VW> x = ldv<real, VW>(c + (size_t)i * VW);
             Pk<real, VW> y = ldv<real, VW>(w + (size_t)i * VW);
 #pragma unroll
-            for (int j = 0; j < VW; j++) acc += (double)x.v[j] * (double)y.v[j];
+            for (int j = 0; j < VW; j++) acc = dacc<real>(acc, x.v[j], y.v[j]);
         }
     } else {
-        for (int i = lane; i < a.len; i += 64) acc += (double)c[i] * (double)w[i];
+        for (int i = lane; i < a.len; i += 64) acc = dacc<real>(acc, c[i], w[i]);
     }
     acc = wave_sum(acc);
     if (lane != 0) return;
@@ -1164,13 +1174,13 @@ __global__ __launch_bounds__(256) void k_rows_partial(
 #pragma unroll
                 for (int q = 0; q < 4; q++)
 #pragma unroll
-                    for (int j = 0; j < VW; j++) acc[j] += (double)c[q].v[j] * x[q];
+                    for (int j = 0; j < VW; j++) acc[j] = dacc<real>(acc[j], c[q].v[j], x[q]);
             }
             for (; v < v1; v++) {
                 Pk<real, VW> c = ldv<real, VW>(A + (size_t)N * v + n0);
                 const double x = (double)xp[v].x;
 #pragma unroll
-                for (int j = 0; j < VW; j++) acc[j] += (double)c.v[j] * x;
+                for (int j = 0; j < VW; j++) acc[j] = dacc<real>(acc[j], c.v[j], x);
             }
 #pragma unroll
             for (int j = 0; j < VW; j++) part[(size_t)b * N + n0 + j] = acc[j];
@@ -1178,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_rows_partial(
     } else {
         for (int n = threadIdx.x; n < N; n += kBlock) {
             double acc = 0.0;
-            for (int v = v0; v < v1; v++) acc += (double)A[(size_t)N * v + n] * (double)xp[v].x;
+            for (int v = v0; v < v1; v++) acc = dacc<real>(acc, A[(size_t)N * v + n], xp[v].x);
             part[(size_t)b * N + n] = acc;
         }
     }
