@@ -410,6 +410,7 @@ def main():
     split_blocks = sess.query("split_blocks") if quad else 0
     tiled_blocks = sess.query("tiled_blocks")  # (simplex: edges in tile order)
     record_blocks = sess.query("record_blocks")  # (simplex: tile blocks staged from their runs)
+    slot_patterns = sess.query("slot_patterns")  # (tiled quadratic: distinct run slot patterns)
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     seqdif = sess.query("seqdif")
     # which speculative mode ran (PFDR_SPEC / pfdr_problem.spec): the decision
@@ -504,6 +505,7 @@ def main():
             "split_incidence_blocks": split_blocks,
             "tiled_blocks": tiled_blocks,
             "record_blocks": record_blocks,
+            "slot_patterns": slot_patterns,
             "sequential_evolution": bool(seqdif),
             "speculation": spec_ran,
             **({"symv_upper_triangle": bool(symv)} if wl.dominant == "symv" else {}),
