@@ -410,7 +410,10 @@ def main():
     split_blocks = sess.query("split_blocks") if quad else 0
     tiled_blocks = sess.query("tiled_blocks")  # (simplex: edges in tile order)
     record_blocks = sess.query("record_blocks")  # (simplex: tile blocks staged from their runs)
-    slot_patterns = sess.query("slot_patterns")  # (tiled quadratic: distinct run slot patterns)
+    try:  # (tiled quadratic: distinct run slot patterns; a library before round 6 has no key)
+        slot_patterns = sess.query("slot_patterns")
+    except pfdr.PFDRError:
+        slot_patterns = None
     symv = sess.query("symv") if quad else 0  # A^tA from its block upper triangle
     seqdif = sess.query("seqdif")
     # which speculative mode ran (PFDR_SPEC / pfdr_problem.spec): the decision
