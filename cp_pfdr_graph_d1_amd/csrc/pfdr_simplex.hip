@@ -710,6 +710,7 @@ struct SxVArgs {
     // term, no side / received tests (one GPU, 2 EK + K < 2^32)
     int zoff;
     unsigned EK;
+    int zfast;  // the group sweep may address Z by 32-bit offsets (one GPU, one weight)
 };
 
 template <typename real>
@@ -1314,8 +1315,11 @@ constexpr long kZv = 1L << 62, kRecv = 1L << 61;  // staged Z offset: v-side / r
 // (1M vertices), group sweep ms: 1 item 2.0, 2 items 1.69, 4 items 2.2-3.1
 constexpr int SXU = 2;
 
-template <typename real, bool SPLIT>
-__global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
+// FAST: launched while SxVArgs::zfast holds and there is no A1 (the 32-bit
+// offset sums only: fewer registers, more workgroups in flight)
+template <typename real, bool SPLIT, bool FAST = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FAST && sizeof(real) == 4 ? 8 : 1)))
+void k_sx_vertex_group(SxVArgs<real> a) {
     if (a.ctrl && a.ctrl->halt) return;
     extern __shared__ double lds_group[];
     __shared__ real red[kBlock / kWave];
@@ -1337,7 +1341,18 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
     __syncthreads();
     const int jb = lptr[0], nj = lptr[nv] - jb;
     const bool staged = nj <= SxGroup<real>::kInc * NV;
-    if (staged) {
+    // one GPU, one edge weight, no A1 (SxVArgs::zfast): the incidences as
+    // 32-bit Z offsets (u end e: e K, v end: EK + e K), and every term's
+    // splitting weight the item's one product la0 * 1/Aux
+    const bool fast = FAST;
+    unsigned *zo32 = reinterpret_cast<unsigned *>(zo);
+    if (staged && fast) {
+        for (int q = t; q < nj; q += kBlock) {
+            const unsigned ad = a.idx[jb + q];
+            zo32[q] = ad >= (unsigned)a.E ? a.EK + (ad - (unsigned)a.E) * (unsigned)K : ad * (unsigned)K;
+        }
+        __syncthreads();
+    } else if (staged) {
         const bool lu = a.la_u != 0;
         const real la0 = a.la0;
         for (int q = t; q < nj; q += kBlock) {
@@ -1372,7 +1387,36 @@ __global__ __launch_bounds__(kBlock) void k_sx_vertex_group(SxVArgs<real> a) {
         real m[SXU];  // the metric, loaded with the first round of the sum's loads
 #pragma unroll
         for (int u = 0; u < SXU; u++) m[u] = ok[u] ? a.Ga[i[u]] : real(1);
-        if (staged) {
+        if (staged && fast) {
+            const real *Z = a.Zu;
+            real w[SXU];
+            int j[SXU], j1[SXU];
+#pragma unroll
+            for (int u = 0; u < SXU; u++) {
+                w[u] = ok[u] ? a.la0 * sx_inv(a, v0 + vl[u], i[u]) : real(0);
+                j[u] = ok[u] ? lptr[vl[u]] - jb : 0;
+                j1[u] = ok[u] ? lptr[vl[u] + 1] - jb : 0;
+            }
+            for (;;) {
+                bool more = false;
+#pragma unroll
+                for (int u = 0; u < SXU; u++) more |= j[u] < j1[u];
+                if (!more) break;  // 8 K-run loads per item, added in order
+                real zq[SXU][8];
+#pragma unroll
+                for (int u = 0; u < SXU; u++)
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        zq[u][q] = j[u] + q < j1[u] ? Z[zo32[j[u] + q] + k[u]] : real(0);
+#pragma unroll
+                for (int u = 0; u < SXU; u++) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (j[u] + q < j1[u]) x[u] += w[u] * zq[u][q];
+                    j[u] += 8;
+                }
+            }
+        } else if (!FAST && staged) {
             real inv[SXU];
             int j[SXU], j1[SXU];
 #pragma unroll
@@ -2314,7 +2358,11 @@ class SimplexSession final : public SessionBase {
     void launch_wide(SxVArgs<real> a) {
         if (gnv_) {  // groups of gnv_ vertices, columns in LDS
             a.vb = gnv_;
-            k_sx_vertex_group<real, SPLIT><<<nbw_, kBlock, SxGroup<real>::bytes(K_, gnv_), stream>>>(a);
+            const size_t lds = SxGroup<real>::bytes(K_, gnv_);
+            if (a.zfast && !a.A1)
+                k_sx_vertex_group<real, SPLIT, true><<<nbw_, kBlock, lds, stream>>>(a);
+            else
+                k_sx_vertex_group<real, SPLIT><<<nbw_, kBlock, lds, stream>>>(a);
         } else {
             k_sx_vertex_wide<real, SPLIT><<<nbw_, kBlock, 0, stream>>>(a);
         }
@@ -2840,6 +2888,7 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
     a.capb = capb_;
     a.zoff = zoff_ ? 1 : 0;
     a.EK = (unsigned)EK_;
+    a.zfast = (!halo_ && la_u_ && 2 * EK_ + K_ <= 0xffffffffL) ? 1 : 0;
     if (vb_) {
         ProfScope ps(prof, "sx_vertex_sweep", s);
         a.vb = svb_;
