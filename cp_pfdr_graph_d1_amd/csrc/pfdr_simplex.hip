@@ -1314,12 +1314,17 @@ constexpr long kZv = 1L << 62, kRecv = 1L << 61;  // staged Z offset: v-side / r
 // items per lane in flight in the group sweep's sums: C4's law at K = 100
 // (1M vertices), group sweep ms: 1 item 2.0, 2 items 1.69, 4 items 2.2-3.1
 constexpr int SXU = 2;
+#ifndef PFDR_SXU_FAST
+#define PFDR_SXU_FAST 4
+#endif
+constexpr int kSxuFast = PFDR_SXU_FAST;  // (the fast variant's, fewer registers per item)
 
 // FAST: launched while SxVArgs::zfast holds and there is no A1 (the 32-bit
 // offset sums only: fewer registers, more workgroups in flight)
 template <typename real, bool SPLIT, bool FAST = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FAST && sizeof(real) == 4 ? 8 : 1)))
 void k_sx_vertex_group(SxVArgs<real> a) {
+    constexpr int XU = FAST ? kSxuFast : SXU;  // items per lane in the sums
     if (a.ctrl && a.ctrl->halt) return;
     extern __shared__ double lds_group[];
     __shared__ real red[kBlock / kWave];
@@ -1368,15 +1373,15 @@ void k_sx_vertex_group(SxVArgs<real> a) {
         __syncthreads();
     }
     // (1) ordered sums (ref :636-648), divided by their metric (the first
-    // pass's x[d] / m[d], ref :44, :49), raw x[0] aside; SXU items per lane,
-    // their SXU x 8 K-run loads of Z in flight together
-    for (int it0 = t; it0 < nitems; it0 += SXU * kBlock) {
-        real x[SXU];
-        int vl[SXU], k[SXU];
-        long i[SXU];
-        bool ok[SXU];
+    // pass's x[d] / m[d], ref :44, :49), raw x[0] aside; XU items per lane,
+    // their XU x 8 K-run loads of Z in flight together
+    for (int it0 = t; it0 < nitems; it0 += XU * kBlock) {
+        real x[XU];
+        int vl[XU], k[XU];
+        long i[XU];
+        bool ok[XU];
 #pragma unroll
-        for (int u = 0; u < SXU; u++) {
+        for (int u = 0; u < XU; u++) {
             const int it = it0 + u * kBlock;
             ok[u] = it < nitems;
             vl[u] = ok[u] ? it / K : 0;
@@ -1384,15 +1389,15 @@ void k_sx_vertex_group(SxVArgs<real> a) {
             i[u] = v0 * K + (ok[u] ? it : 0);
             x[u] = real(0);
         }
-        real m[SXU];  // the metric, loaded with the first round of the sum's loads
+        real m[XU];  // the metric, loaded with the first round of the sum's loads
 #pragma unroll
-        for (int u = 0; u < SXU; u++) m[u] = ok[u] ? a.Ga[i[u]] : real(1);
+        for (int u = 0; u < XU; u++) m[u] = ok[u] ? a.Ga[i[u]] : real(1);
         if (staged && fast) {
             const real *Z = a.Zu;
-            real w[SXU];
-            int j[SXU], j1[SXU];
+            real w[XU];
+            int j[XU], j1[XU];
 #pragma unroll
-            for (int u = 0; u < SXU; u++) {
+            for (int u = 0; u < XU; u++) {
                 w[u] = ok[u] ? a.la0 * sx_inv(a, v0 + vl[u], i[u]) : real(0);
                 j[u] = ok[u] ? lptr[vl[u]] - jb : 0;
                 j1[u] = ok[u] ? lptr[vl[u] + 1] - jb : 0;
@@ -1400,16 +1405,16 @@ void k_sx_vertex_group(SxVArgs<real> a) {
             for (;;) {
                 bool more = false;
 #pragma unroll
-                for (int u = 0; u < SXU; u++) more |= j[u] < j1[u];
+                for (int u = 0; u < XU; u++) more |= j[u] < j1[u];
                 if (!more) break;  // 8 K-run loads per item, added in order
-                real zq[SXU][8];
+                real zq[XU][8];
 #pragma unroll
-                for (int u = 0; u < SXU; u++)
+                for (int u = 0; u < XU; u++)
 #pragma unroll
                     for (int q = 0; q < 8; q++)
                         zq[u][q] = j[u] + q < j1[u] ? Z[zo32[j[u] + q] + k[u]] : real(0);
 #pragma unroll
-                for (int u = 0; u < SXU; u++) {
+                for (int u = 0; u < XU; u++) {
 #pragma unroll
                     for (int q = 0; q < 8; q++)
                         if (j[u] + q < j1[u]) x[u] += w[u] * zq[u][q];
@@ -1417,10 +1422,10 @@ void k_sx_vertex_group(SxVArgs<real> a) {
                 }
             }
         } else if (!FAST && staged) {
-            real inv[SXU];
-            int j[SXU], j1[SXU];
+            real inv[XU];
+            int j[XU], j1[XU];
 #pragma unroll
-            for (int u = 0; u < SXU; u++) {
+            for (int u = 0; u < XU; u++) {
                 inv[u] = ok[u] ? sx_inv(a, v0 + vl[u], i[u]) : real(0);
                 j[u] = ok[u] ? lptr[vl[u]] - jb : 0;
                 j1[u] = ok[u] ? lptr[vl[u] + 1] - jb : 0;
@@ -1428,12 +1433,12 @@ void k_sx_vertex_group(SxVArgs<real> a) {
             for (;;) {
                 bool more = false;
 #pragma unroll
-                for (int u = 0; u < SXU; u++) more |= j[u] < j1[u];
+                for (int u = 0; u < XU; u++) more |= j[u] < j1[u];
                 if (!more) break;  // 8 K-run loads per item, added in order
-                real zq[SXU][8], aq[SXU][8];
-                bool rq[SXU][8];
+                real zq[XU][8], aq[XU][8];
+                bool rq[XU][8];
 #pragma unroll
-                for (int u = 0; u < SXU; u++)
+                for (int u = 0; u < XU; u++)
 #pragma unroll
                     for (int q = 0; q < 8; q++) {
                         rq[u][q] = true;
@@ -1447,7 +1452,7 @@ void k_sx_vertex_group(SxVArgs<real> a) {
                         }
                     }
 #pragma unroll
-                for (int u = 0; u < SXU; u++) {
+                for (int u = 0; u < XU; u++) {
 #pragma unroll
                     for (int q = 0; q < 8; q++)
                         if (j[u] + q < j1[u])
@@ -1457,11 +1462,11 @@ void k_sx_vertex_group(SxVArgs<real> a) {
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < SXU; u++)  // (a hub-sized group: the CSR from memory)
+            for (int u = 0; u < XU; u++)  // (a hub-sized group: the CSR from memory)
                 if (ok[u]) x[u] = sx_item_sum(a, v0 + vl[u], k[u]);
         }
 #pragma unroll
-        for (int u = 0; u < SXU; u++) {
+        for (int u = 0; u < XU; u++) {
             if (!ok[u]) continue;
             if (k[u] == 0) x0s[vl[u]] = x[u];
             xs[k[u] * st + vl[u]] = x[u] / m[u];
