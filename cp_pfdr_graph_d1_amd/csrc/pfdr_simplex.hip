@@ -1315,9 +1315,9 @@ constexpr long kZv = 1L << 62, kRecv = 1L << 61;  // staged Z offset: v-side / r
 // (1M vertices), group sweep ms: 1 item 2.0, 2 items 1.69, 4 items 2.2-3.1
 constexpr int SXU = 2;
 #ifndef PFDR_SXU_FAST
-#define PFDR_SXU_FAST 4
+#define PFDR_SXU_FAST 2
 #endif
-constexpr int kSxuFast = PFDR_SXU_FAST;  // (the fast variant's, fewer registers per item)
+constexpr int kSxuFast = PFDR_SXU_FAST;  // (fast variant: 3 or 4 spill at eight waves)
 
 // FAST: launched while SxVArgs::zfast holds and there is no A1 (the 32-bit
 // offset sums only: fewer registers, more workgroups in flight)
