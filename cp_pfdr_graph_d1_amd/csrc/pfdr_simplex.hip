@@ -447,13 +447,14 @@ __global__ void k_sx_prox_store(long EK, int K, const int *__restrict__ Eu,
 // is normalised
 template <typename real>
 __global__ void k_sx_gi_pack(long n, const real *__restrict__ Ga, const real *__restrict__ invAux,
-                             SxR2<real> *__restrict__ GI) {
+                             SxR2<real> *__restrict__ GI, real *__restrict__ GaU) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SxR2<real> q;
     q.x = Ga[i];
     q.y = invAux[i];
     GI[i] = q;
+    if (GaU) GaU[i] = q.x;
 }
 
 // normalise the metric of each vertex by its maximum (ref :360-369)
@@ -557,13 +558,25 @@ __device__ __forceinline__ void sx_st(T *p, const Pk<T, N> &x) { *reinterpret_ca
 // index division are paid once per pair)
 // one lane's L entries [i, i + L) of the (edge, label) sweep, i < EK: the
 // body of k_sx_edge_sweep, shared with the one-workgroup k_sx_tiny_iterate
+// one GPU before any reconditioning: 1/Aux is one value per vertex
+// (invV, SxVArgs::invV) and La_d1 may be one value (la0), so the lane reads
+// the metric alone per (v, k) (GaU: Ga before its normalisation, 4 B)
+// instead of the (Ga, 1/Aux) pair (8 B) at each end; GaU null: off
+template <typename real>
+struct SxEdgeFast {
+    const real *GaU, *invV;
+    real la0;
+    int la_u;
+};
+
 template <typename real, int L>
 __device__ __forceinline__ void sx_edge_lane(
     long i, long EK, const SxConst<real> &c, const int *__restrict__ Eu,
     const int *__restrict__ Ev, const SxR2<real> *PF, real *Zu, real *Zv,
     const real *__restrict__ A1, const real *__restrict__ La_d1,
     const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
-    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *wz, real rho) {
+    const real *__restrict__ Wd1v, const real *__restrict__ Th, real *wz, real rho,
+    SxEdgeFast<real> f = SxEdgeFast<real>{}) {
     const int K = c.K;
     long e;
     int k;
@@ -575,7 +588,8 @@ __device__ __forceinline__ void sx_edge_lane(
         e = i / K;
         k = (int)(i - e * K);
     }
-    const long u = (long)Eu[e] * K + k, v = (long)Ev[e] * K + k;
+    const int eu = Eu[e], ev = Ev[e];
+    const long u = (long)eu * K + k, v = (long)ev * K + k;
     Pk<real, L> zu = sx_ld<real, L>(Zu + i), zv = sx_ld<real, L>(Zv + i);
     // (P, explicit step) of both entries in one access per end: the sweep
     // is bound by its texture-address work (profiles/r2/r2zj_c4_counters)
@@ -592,20 +606,32 @@ __device__ __forceinline__ void sx_edge_lane(
 #pragma unroll
     for (int j = 0; j < L; j++) { wsu[j] = wsv[j] = real(0); gpu[j] = gpv[j] = real(1); }
     if ((c.loss != LOSS_LINEAR && !Th) || wz) {
-        la = La_d1[e];
-        // (Ga, 1/Aux) of both entries of a pair in one access at each end
-        // (u, v even: K is even when L = 2) -- the sweep is bound by its
-        // texture-address work, not by bytes (profiles/r2/r2zj_c4_counters)
-        const Pk<SxR2<real>, L> gpu_ = sx_ld<SxR2<real>, L>(GI + u);
-        const Pk<SxR2<real>, L> gpv_ = sx_ld<SxR2<real>, L>(GI + v);
+        la = f.la_u ? f.la0 : La_d1[e];
+        if (f.GaU && !A1) {  // (the metric per (v, k), 1/Aux per vertex)
+            const Pk<real, L> gu_ = sx_ld<real, L>(f.GaU + u), gv_ = sx_ld<real, L>(f.GaU + v);
+            const real iu = f.invV[eu], iv = f.invV[ev];
 #pragma unroll
-        for (int j = 0; j < L; j++) {
-            const real an = A1 ? A1[i + j] : la;
-            const SxR2<real> gu = gpu_.v[j], gv = gpv_.v[j];
-            wsu[j] = an * gu.y;
-            wsv[j] = an * gv.y;
-            gpu[j] = gu.x;
-            gpv[j] = gv.x;
+            for (int j = 0; j < L; j++) {
+                wsu[j] = la * iu;
+                wsv[j] = la * iv;
+                gpu[j] = gu_.v[j];
+                gpv[j] = gv_.v[j];
+            }
+        } else {
+            // (Ga, 1/Aux) of both entries of a pair in one access at each end
+            // (u, v even: K is even when L = 2) -- the sweep is bound by its
+            // texture-address work, not by bytes (profiles/r2/r2zj_c4_counters)
+            const Pk<SxR2<real>, L> gpu_ = sx_ld<SxR2<real>, L>(GI + u);
+            const Pk<SxR2<real>, L> gpv_ = sx_ld<SxR2<real>, L>(GI + v);
+#pragma unroll
+            for (int j = 0; j < L; j++) {
+                const real an = A1 ? A1[i + j] : la;
+                const SxR2<real> gu = gpu_.v[j], gv = gpv_.v[j];
+                wsu[j] = an * gu.y;
+                wsv[j] = an * gv.y;
+                gpu[j] = gu.x;
+                gpv[j] = gv.x;
+            }
         }
     }
     Pk<real, L> du{}, dv{}, th{};
@@ -643,13 +669,13 @@ __global__ __launch_bounds__(256) void k_sx_edge_sweep(
     const real *__restrict__ A1, const real *__restrict__ La_d1,
     const SxR2<real> *__restrict__ GI, const real *__restrict__ Wd1u,
     const real *__restrict__ Wd1v, const real *__restrict__ Th, real *__restrict__ wz, real rho,
-    const Ctrl<real> *ctrl, int nb, int xcd) {
+    const Ctrl<real> *ctrl, int nb, int xcd, SxEdgeFast<real> f) {
     if (ctrl && ctrl->halt) return;
     const int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;
     const long i = ((long)blk * blockDim.x + threadIdx.x) * L;
     if (i >= EK) return;
-    sx_edge_lane<real, L>(i, EK, c, Eu, Ev, PF, Zu, Zv, A1, La_d1, GI, Wd1u, Wd1v, Th, wz, rho);
+    sx_edge_lane<real, L>(i, EK, c, Eu, Ev, PF, Zu, Zv, A1, La_d1, GI, Wd1u, Wd1v, Th, wz, rho, f);
 }
 
 // Fused vertex sweep (K <= 64): ordered DR average, metric projection,
@@ -2249,6 +2275,7 @@ class SimplexSession final : public SessionBase {
     DevBuf<real> Zu_, A1_, wz_, part_, opart_, Obj_, Dif_;
     real *zv_ = nullptr;  // the v ends' Z (inside Zu_'s allocation)
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
+    DevBuf<real> GaU_;       // its Ga half alone (one GPU: the edge sweep's SxEdgeFast)
     // stored prox weights/thresholds of the non-linear losses for odd K (one
     // (e, k) per lane); even K takes two per lane and recomputes them from
     // the factors (C4: 1.076 -> 0.950 ms, r1zw; odd K stored: 1.24 vs 1.30 ms)
@@ -2290,6 +2317,17 @@ class SimplexSession final : public SessionBase {
     // readers of P (objective, reconditioning, result)
     bool plazy_ = false;
     void sync_p(int t);
+    // the edge sweep's metric-only gathers (SxEdgeFast): one GPU, before A1
+    SxEdgeFast<real> efast() const {
+        SxEdgeFast<real> f{};
+        f.la0 = la0_;
+        f.la_u = la_u_ ? 1 : 0;
+        if (GaU_.p && !A1_.p) {
+            f.GaU = GaU_.p;
+            f.invV = invV_.p;
+        }
+        return f;
+    }
     // the fused vertex sweep forms W*Z from the gathered Z and W (K contiguous
     // words per incidence), so the edge sweep neither reads W nor writes
     // contributions: 28 instead of 44 streamed bytes per (e, k) (C4: 2.42 ->
@@ -2526,6 +2564,7 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     Zu_.alloc(2 * EKn + (size_t)R_ * K_);
     zv_ = Zu_.p + EKn;
     GI_.alloc(VgK);
+    if (!halo_ && E_ > 0) GaU_.alloc(VgK);
     sx_pw_ = K_ % 2 != 0;
     if (sx_pw_ && c_.loss != LOSS_LINEAR) { Wd1u_.alloc(EKn); Wd1v_.alloc(EKn); Th_.alloc(EKn); }
     wz_.alloc(2 * EKn + (size_t)R_ * K_);  // [side][e][k], then the received tail
@@ -2704,7 +2743,7 @@ void SimplexSession<real>::precondition(bool init) {
         k_sx_recond_edge<real><<<gE, kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, A1_.p, invAux_.p, Ga_.p,
                                                      GaQ_.p, P_.p, Q_.p, Zu_.p, zv_);
     k_sx_gi_pack<real><<<grid_for((long)Vg_ * K_), kBlock, 0, s>>>((long)Vg_ * K_, Ga_.p,
-                                                                  invAux_.p, GI_.p);
+                                                                  invAux_.p, GI_.p, GaU_.p);
     if (EK_ && Th_.p)
         k_sx_prox_store<real><<<gE, kBlock, 0, s>>>(EK_, K_, Eu_.p, Ev_.p, A1_.p, La_d1_.p, GI_.p,
                                                     Wd1u_.p, Wd1v_.p, Th_.p);
@@ -2867,13 +2906,13 @@ void SimplexSession<real>::sweeps(const Ctrl<real> *c, int t) {
                                                                Zu_.p, zv_, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                nullptr,
-                                                               rho_, c, nb, xm);
+                                                               rho_, c, nb, xm, efast());
         else
             k_sx_edge_sweep<real, 1><<<xcd_grid(nb, xm), kBlock, 0, s>>>(EK_, c_, Eu_.p, Ev_.p, PFin,
                                                                Zu_.p, zv_, A1_.p, La_d1_.p, GI_.p,
                                                                Wd1u_.p, Wd1v_.p, Th_.p,
                                                                nullptr,
-                                                               rho_, c, nb, xm);
+                                                               rho_, c, nb, xm, efast());
     }
     if (halo_) {
         ProfScope ps(prof, "halo_push", s);
