@@ -318,8 +318,11 @@ __global__ __launch_bounds__(64 * WG) void k_gram_v(int P, long K, const real *_
 // significant bits, m = x - h rounded to 8, l = x - h - m: no bits lost), and
 // a product x y is formed from the six pieces whose weight reaches 2^-16 of
 // it (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16, accumulated in
-// f32; the pieces left out (ml, lm, ll) weigh <= 2^-23 of each product,
-// below the f32 rounding of the sum.  Six bf16 MFMAs of 16 k do the work of
+// f32; the pieces left out (ml, lm, ll) weigh about 2^-23 of each product
+// (up to ~2^-22 when the truncated leading piece leaves m near its bound;
+// tests/test_gram_split_cpu.py checks <= 2^-21), at the f32 rounding of the
+// sum.  A NaN in a tile (an overflow split into pieces of both signs, or an
+// infinite element) sends the whole Gram to the exact-f32 tile (gram()).  Six bf16 MFMAs of 16 k do the work of
 // eight f32 ones of 2 k at a sixteenth of the rate per flop: 2.7x the f32
 // matrix-core throughput.  Same blocks, tiles and chunks
 // as k_gram_v; the staging splits each element once, into three bf16

@@ -1,5 +1,6 @@
-"""GPU: the simplex beyond K = 64 labels (one wave per vertex, the metric
-projection on the whole wave, pfdr_proj.hpp) at sizes where the evolution
+"""GPU: the simplex beyond K = 64 labels (groups of vertices with their
+columns in LDS, or past the LDS one wave per vertex with the projection on
+the whole wave, pfdr_proj.hpp) at sizes where the evolution
 is summed in the reference's sequential rounding and the session decides
 speculatively (P and (P, step) ping-ponged): the stopping iteration, every
 Dif and P equal the restatement's (itself pinned to the reference on the
@@ -34,9 +35,9 @@ def _problem(n, K, dt, seed=4, weak=False):
                          ids=["K130", "K1100", "K2000-f64", "K3500"])
 @pytest.mark.parametrize("difTol", [1e-3, 1.0], ids=["l1", "labels"])
 def test_wide_speculative_matches_restatement(gpu_lib, K, n, dt, difTol):
-    """K = 130 and 1,100: groups of vertices with their columns in LDS (64
-    and 4 per group); K = 2,000 (f64) and 3,500 (f32): past the LDS, one wave
-    per vertex with the columns and active sets in memory"""
+    """K = 130 and 1,100: groups of vertices with their columns in LDS (16
+    and 4 per group, SxGroup::nv_for); K = 2,000 (f64) and 3,500 (f32): past
+    the LDS, one wave per vertex with the columns and active sets in memory"""
     import oracle
     from cp_pfdr_graph_d1_amd import pfdr
     labels = difTol >= 1
