@@ -390,12 +390,11 @@ __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
                                              const real *__restrict__ wz, real *lds, int *wt,
                                              real wv = real(1),
                                              const Slots12 *__restrict__ ptab = nullptr,
-                                             const int *__restrict__ prec = nullptr,
-                                             int rv_in = 0, bool have_rv = false) {
+                                             const int *__restrict__ prec = nullptr) {
     constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     const int dg = v < V ? deg8[v] : 0;
-    const int rv = have_rv ? rv_in : lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
+    const int rv = lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
     // pattern offsets of the runs (prec, with the record; null: per-entry slots)
     const int pr = prec && lane < kPrec ? prec[(long)blk * kPrec + lane] : 0;
     int dinc = dg;
@@ -638,7 +637,6 @@ static __global__ void k_tile_rec(int nb, const int *__restrict__ ustart,
         r[3 + 2 * q] = tstart[t0 + q];
         r[4 + 2 * q] = tlen[t0 + q];
     }
-    r[kTileRec - 1] = 1;  // (a record: the vertex sweep reads no tok for it)
     tok[b] = 2;
 }
 
@@ -2349,15 +2347,10 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
     const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
-    // the block's record first (its last word marks it valid): a record
-    // block reads no tok, one dependent load round fewer
-    const int lane = threadIdx.x & (kWave - 1);
-    const int rv = a.slots && lane < kTileRec ? a.trec[(long)blk * kTileRec + lane] : 0;
-    const bool rec = a.slots && __builtin_amdgcn_readlane(rv, kTileRec - 1) != 0;  // block-uniform
-    const int tk = rec ? 2 : a.slots ? a.tok[blk] : 0;
+    const int tk = a.slots ? a.tok[blk] : 0;  // block-uniform
     if (tk == 2)
         x = tile_sum_rec<real, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
-                                   lds, scan + 3 * kTileRuns, wv, a.ptab, a.prec, rv, true);
+                                   lds, scan + 3 * kTileRuns, wv, a.ptab, a.prec);
     else if (tk)
         x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
