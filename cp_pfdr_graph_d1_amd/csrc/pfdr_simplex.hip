@@ -62,12 +62,16 @@ __device__ __forceinline__ real sx_a(long i, long e, const real *__restrict__ A1
 
 // prox weights and threshold (ref :287-306), operation for operation
 template <typename real>
-__device__ __forceinline__ void sx_prox_weights(real wu, real wv, real gu, real gv, real la,
-                                                real &du, real &dv, real &th) {
-    const real a = wu / gu, b = wv / gv, s = a + b;
+__device__ __forceinline__ void sx_prox_ab(real a, real b, real la, real &du, real &dv, real &th) {
+    const real s = a + b;
     th = la * s / (a * b);
     du = a / s;
     dv = b / s;
+}
+template <typename real>
+__device__ __forceinline__ void sx_prox_weights(real wu, real wv, real gu, real gv, real la,
+                                                real &du, real &dv, real &th) {
+    sx_prox_ab(wu / gu, wv / gv, la, du, dv, th);
 }
 
 // ------------------------------------------------ metric projection ----
@@ -562,12 +566,23 @@ __device__ __forceinline__ void sx_st(T *p, const Pk<T, N> &x) { *reinterpret_ca
 // (invV, SxVArgs::invV) and La_d1 may be one value (la0), so the lane reads
 // the metric alone per (v, k) (GaU: Ga before its normalisation, 4 B)
 // instead of the (Ga, 1/Aux) pair (8 B) at each end; GaU null: off
+// AW (one La_d1 value as well): the ratio W / Ga = (la0 * 1/Aux[v]) /
+// Ga[v, k] of every (v, k), formed once with the reference's operations
+// (k_sx_aw) -- the same for every edge at v, so the lane divides only for
+// the threshold and the two weights (3 IEEE divisions per entry, not 5)
 template <typename real>
 struct SxEdgeFast {
-    const real *GaU, *invV;
+    const real *GaU, *invV, *AW;
     real la0;
     int la_u;
 };
+
+template <typename real>
+__global__ void k_sx_aw(long n, int K, real la0, const real *__restrict__ invV,
+                        const real *__restrict__ GaU, real *__restrict__ AW) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) AW[i] = (la0 * invV[i / K]) / GaU[i];
+}
 
 template <typename real, int L>
 __device__ __forceinline__ void sx_edge_lane(
@@ -607,7 +622,9 @@ __device__ __forceinline__ void sx_edge_lane(
     for (int j = 0; j < L; j++) { wsu[j] = wsv[j] = real(0); gpu[j] = gpv[j] = real(1); }
     if ((c.loss != LOSS_LINEAR && !Th) || wz) {
         la = f.la_u ? f.la0 : La_d1[e];
-        if (f.GaU && !A1) {  // (the metric per (v, k), 1/Aux per vertex)
+        if (f.AW && !A1 && !wz) {
+            // (the ratios AW below replace the weights and the metric)
+        } else if (f.GaU && !A1) {  // (the metric per (v, k), 1/Aux per vertex)
             const Pk<real, L> gu_ = sx_ld<real, L>(f.GaU + u), gv_ = sx_ld<real, L>(f.GaU + v);
             const real iu = f.invV[eu], iv = f.invV[ev];
 #pragma unroll
@@ -635,7 +652,11 @@ __device__ __forceinline__ void sx_edge_lane(
         }
     }
     Pk<real, L> du{}, dv{}, th{};
-    if (c.loss != LOSS_LINEAR) {
+    if (c.loss != LOSS_LINEAR && f.AW && !A1 && !Th) {  // (wsu / gpu never formed)
+        const Pk<real, L> au = sx_ld<real, L>(f.AW + u), av = sx_ld<real, L>(f.AW + v);
+#pragma unroll
+        for (int j = 0; j < L; j++) sx_prox_ab<real>(au.v[j], av.v[j], la, du.v[j], dv.v[j], th.v[j]);
+    } else if (c.loss != LOSS_LINEAR) {
         if (Th) {
             du = sx_ld<real, L>(Wd1u + i);
             dv = sx_ld<real, L>(Wd1v + i);
@@ -2276,6 +2297,7 @@ class SimplexSession final : public SessionBase {
     real *zv_ = nullptr;  // the v ends' Z (inside Zu_'s allocation)
     DevBuf<SxR2<real>> GI_;  // (Ga before normalisation, 1/Aux) per (v, k), ghosts included
     DevBuf<real> GaU_;       // its Ga half alone (one GPU: the edge sweep's SxEdgeFast)
+    DevBuf<real> AW_;        // W / Ga per (v, k) with one La_d1 value (SxEdgeFast::AW)
     // stored prox weights/thresholds of the non-linear losses for odd K (one
     // (e, k) per lane); even K takes two per lane and recomputes them from
     // the factors (C4: 1.076 -> 0.950 ms, r1zw; odd K stored: 1.24 vs 1.30 ms)
@@ -2325,6 +2347,7 @@ class SimplexSession final : public SessionBase {
         if (GaU_.p && !A1_.p) {
             f.GaU = GaU_.p;
             f.invV = invV_.p;
+            f.AW = AW_.p;
         }
         return f;
     }
@@ -2593,6 +2616,10 @@ SimplexSession<real>::SimplexSession(const pfdr_problem *p) {
     precondition(true);
     invV_.alloc(V_);
     k_sx_inv_vertex<real><<<nbv_, kBlock, 0, s>>>(V_, K_, invAux_.p, invV_.p);
+    if (GaU_.p && la_u_ && c_.loss != LOSS_LINEAR) {  // (the edge sweep's ratios, before A1)
+        AW_.alloc(VK_);
+        k_sx_aw<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, K_, la0_, invV_.p, GaU_.p, AW_.p);
+    }
     k_sx_explicit<real><<<grid_for(VK_), kBlock, 0, s>>>(VK_, c_, P_.p, GaQ_.p, Q_.p, PF_.p);
     PFDR_HIP(hipGetLastError());
     pullPF();
