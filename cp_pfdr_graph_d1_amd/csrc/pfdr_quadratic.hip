@@ -235,6 +235,8 @@ class QuadSession final : public SessionBase {
     // first reconditioning, then A1_[e]; (Ga, invAux) pairs of every vertex
     DevBuf<real> A1_;
     DevBuf<R2<real>> gi_;
+    DevBuf<real> rr_;  // per-vertex (cw la0 / Aux) / Ga of the ratio edge sweep (rat())
+    bool rat_env_ = true;  // PFDR_EDGE_RATIO=0: the (Ga, invAux) pair sweep throughout
     real cw_ = real(0);
     DevBuf<real> R_, vpart_, opart_, Obj_, Dif_, red_, csum_;
     DevBuf<double> Rpart_;  // k_rows_partial's double partials
@@ -325,6 +327,10 @@ class QuadSession final : public SessionBase {
     // received terms with its own weight like the local ones)
     bool zd_ranks_ = false;
     bool zdirect() const { return tiled_ && !A1_.p && (halo_ ? zd_ranks_ : !la_it()); }
+    // one edge weight and no W * Z stream (until the first reconditioning):
+    // the tiled edge sweep reads the ends' formed ratios (k_ratio_vertex)
+    // instead of their (Ga, invAux) pairs
+    bool rat() const { return rat_env_ && zdirect() && !la_it(); }
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
@@ -628,6 +634,17 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         tr.wait(s);
         zd_ranks_ = all == 0;
     }
+    {
+        const char *e = getenv("PFDR_EDGE_RATIO");
+        rat_env_ = !(e && e[0] == '0');
+    }
+    if (rat()) {  // cw_ and la0_ are known from here (owned and ghost ends)
+        rr_.alloc(Vg_ + 2);  // (+2: the tiled edge sweep stages vertex pairs)
+        PFDR_HIP(hipMemsetAsync(rr_.p, 0, (Vg_ + 2) * sizeof(real), s));
+        k_ratio_vertex<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, cw_, la0_, Ga_.p, invAux_.p,
+                                                              rr_.p);
+        PFDR_HIP(hipGetLastError());
+    }
     pins_.release();
     stopped_ = (itMax_ <= 0);
     interior_edges = E_;
@@ -636,7 +653,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
-                            &pre_, &Z2_, &A1_, &wz_, &R_,
+                            &pre_, &Z2_, &A1_, &wz_, &R_, &rr_,
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_, &spart_})
         acc(b->n * sizeof(real));
     acc(Rpart_.n * sizeof(double));
@@ -1366,6 +1383,7 @@ void QuadSession<real>::precondition(bool init) {
     }
     k_gi_pack<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, Ga_.p, invAux_.p, gi_.p);
     PFDR_HIP(hipGetLastError());
+    if (!init && !rat()) rr_.release();  // (A1 from the first reconditioning on)
     if (!init) {
         // forward step with the new metric from the gradient taken before
         // reconditioning (ref :448-464)
@@ -1426,10 +1444,12 @@ void QuadSession<real>::edge_sweep(long ebeg, long eend, const Ctrl<real> *c, co
     if (tiled_ && !fuse_ && rg.nb0 == nb && ebeg % EB == 0 && (eend % EB == 0 || eend == E_)) {
         // edge blocks [ebeg / EB, ...) of the tile order (a partitioned rank
         // sweeps its interior blocks and the rest in two launches)
-        auto k = (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true> : k_edge_sweep_tl<real, false>;
+        auto k = rr_.p ? k_edge_sweep_tl<real, true, true>
+                 : (!la_it() && !A1_.p) ? k_edge_sweep_tl<real, true>
+                                        : k_edge_sweep_tl<real, false>;
         k<<<g, kBlock, 0, s>>>(E_, V_, Eu_.p, luv_.p, erec_.p, Ev_.p, xr_, Z2_.p, A1_.p, cw_,
                                gi_.p, la_it(), la0_, zdirect() ? nullptr : wz_.p, rho_, c,
-                               (int)(ebeg / EB), nb, xm);
+                               (int)(ebeg / EB), nb, xm, rr_.p);
         return;
     }
     if (tiled_) throw std::logic_error("tiled edge sweep: range not on edge blocks");

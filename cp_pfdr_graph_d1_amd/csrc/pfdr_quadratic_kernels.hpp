@@ -1431,6 +1431,18 @@ __global__ void k_gi_pack(int n, const real *__restrict__ Ga, const real *__rest
     gi[v] = q;
 }
 
+// per-vertex ratio of the RAT edge sweeps: the splitting weight of every
+// edge at v over v's metric, (cw * la0 * invAux) / Ga -- bit for bit the
+// quotient prox_weights forms from edge_full's wu when a_e = cw * la0
+template <typename real>
+__global__ void k_ratio_vertex(int n, real cw, real la0, const real *__restrict__ Ga,
+                               const real *__restrict__ invAux, real *__restrict__ rr) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const real a0 = cw * la0;
+    rr[v] = (a0 * invAux[v]) / Ga[v];
+}
+
 // the prox weights and threshold of an edge from its splitting weights,
 // the metric of its ends and its TV weight — the operations of the
 // reference's precomputation (ref :252-259), recomputed in every edge sweep
@@ -1757,14 +1769,27 @@ constexpr int kErecS = 8;    // rec[kErecS + 2r]: start of run r (INT_MAX if r >
 // the staged u range is [ub0 * 256 + uoff, + span), span = largest - smallest + 1
 constexpr int kErec = kErecS + 2 * kEbRuns;
 // UNI: one weight La_d1 for every edge (la0) and no A1 (before any
-// reconditioning): a_e = cw * la0 is one value, computed once per lane
-template <typename real, bool UNI>
+// reconditioning): a_e = cw * la0 is one value, computed once per lane.
+// RAT (UNI, Z-direct): each end's ratio (cw * la0 / Aux) / Ga comes formed
+// (k_ratio_vertex) -- one 4/8-byte gather per end instead of the (Ga,
+// invAux) pair, and three divisions per edge instead of five
+template <typename real>
+__device__ __forceinline__ void edge_ratio(const R2<real> &pu, const R2<real> &pv, real a, real b,
+                                           real la, real &zu, real &zv, real rho) {
+    const real s = a + b, th = la * s / (a * b);
+    edge_update<real>(pu, pv, zu, zv, a / s, b / s, th, rho);
+}
+
+template <typename real, bool UNI, bool RAT = false>
 __device__ __forceinline__ void tl_gather(
     long E, int V, const int *__restrict__ Eu, const unsigned short *__restrict__ luv,
     const int *__restrict__ rec, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
-    real *__restrict__ wz, real rho, int blk, R2<real> *s_xp, R2<real> *s_gi) {
+    real *__restrict__ wz, real rho, int blk, R2<real> *s_xp, R2<real> *s_gi,
+    const real *__restrict__ rr = nullptr) {
+    static_assert(!RAT || UNI, "ratios need one edge weight");
+    real *s_r = reinterpret_cast<real *>(s_gi);  // RAT: the staged ratios
     constexpr int EPT = Vec<real>::kPer16B;
     constexpr int NUB = TlBlocks<real>::v, SPAN = NUB * kBlock;
     const int tid = threadIdx.x;
@@ -1783,6 +1808,7 @@ __device__ __forceinline__ void tl_gather(
     Pk<real, 2 * EPT> z{};
     Pk<real, EPT> la{}, a{};
     R2<real> pu[EPT], pv[EPT], gu[EPT], gv[EPT];
+    real ru[EPT], rv[EPT];
     if (full) {  // Z side-major (tiled sessions): zu at e, zv at E + e
         ib = ldv<unsigned short, EPT>(luv + e0);
         const Pk<real, EPT> zu = ldv<real, EPT>(Z2 + e0), zv = ldv<real, EPT>(Z2 + E + e0);
@@ -1805,18 +1831,22 @@ __device__ __forceinline__ void tl_gather(
     constexpr bool PAIRS = sizeof(real) == 4;
     const int sb = su & ~1, so = su - sb;  // PAIRS: entries counted from sb
     R2<real> sx[NS0], sg[NS0];
+    real sr[NS0];
     Pk<real, 4> px{}, pg{};
+    Pk<real, 2> pr{};
     if (staged) {
         if (PAIRS) {
             const int j = min(tid, (span + so - 1) >> 1);  // (the arrays carry 2 spare vertices)
             px = ldv<real, 4>(reinterpret_cast<const real *>(xp + sb) + 4 * j);
-            pg = ldv<real, 4>(reinterpret_cast<const real *>(gi + sb) + 4 * j);
+            if (RAT) pr = ldv<real, 2>(rr + sb + 2 * j);
+            else pg = ldv<real, 4>(reinterpret_cast<const real *>(gi + sb) + 4 * j);
         } else {
 #pragma unroll
             for (int q = 0; q < NS0; q++) {
                 const int i = su + min(q * kBlock + tid, span - 1);
                 sx[q] = xp[i];
-                sg[q] = gi[i];
+                if (RAT) sr[q] = rr[i];
+                else sg[q] = gi[i];
             }
         }
     }
@@ -1849,7 +1879,8 @@ __device__ __forceinline__ void tl_gather(
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
             pv[j] = xp[iv[j]];
-            gv[j] = gi[iv[j]];
+            if (RAT) rv[j] = rr[iv[j]];
+            else gv[j] = gi[iv[j]];
         }
     }
     if (staged) {
@@ -1858,16 +1889,19 @@ __device__ __forceinline__ void tl_gather(
             if (2 * tid < span + so) {       // the pair starts inside the staged range
                 if (i0 >= 0) {
                     s_xp[i0].x = px.v[0]; s_xp[i0].y = px.v[1];
-                    s_gi[i0].x = pg.v[0]; s_gi[i0].y = pg.v[1];
+                    if (RAT) s_r[i0] = pr.v[0];
+                    else { s_gi[i0].x = pg.v[0]; s_gi[i0].y = pg.v[1]; }
                 }
                 if (i0 + 1 < span) {
                     s_xp[i0 + 1].x = px.v[2]; s_xp[i0 + 1].y = px.v[3];
-                    s_gi[i0 + 1].x = pg.v[2]; s_gi[i0 + 1].y = pg.v[3];
+                    if (RAT) s_r[i0 + 1] = pr.v[1];
+                    else { s_gi[i0 + 1].x = pg.v[2]; s_gi[i0 + 1].y = pg.v[3]; }
                 }
             }
             for (int i = 2 * kBlock - so + tid; i < span; i += kBlock) {  // wide ranges
                 s_xp[i] = xp[su + i];
-                s_gi[i] = gi[su + i];
+                if (RAT) s_r[i] = rr[su + i];
+                else s_gi[i] = gi[su + i];
             }
         } else {
 #pragma unroll
@@ -1875,12 +1909,14 @@ __device__ __forceinline__ void tl_gather(
                 const int i = q * kBlock + tid;
                 if (i < span) {
                     s_xp[i] = sx[q];
-                    s_gi[i] = sg[q];
+                    if (RAT) s_r[i] = sr[q];
+                    else s_gi[i] = sg[q];
                 }
             }
             for (int i = NS0 * kBlock + tid; i < span; i += kBlock) {  // wide ranges
                 s_xp[i] = xp[su + i];
-                s_gi[i] = gi[su + i];
+                if (RAT) s_r[i] = rr[su + i];
+                else s_gi[i] = gi[su + i];
             }
         }
     }
@@ -1902,14 +1938,16 @@ __device__ __forceinline__ void tl_gather(
 #pragma unroll
             for (int j = 0; j < EPT; j++) {
                 pu[j] = s_xp[ku[j]];
-                gu[j] = s_gi[ku[j]];
+                if (RAT) ru[j] = s_r[ku[j]];
+                else gu[j] = s_gi[ku[j]];
             }
         } else {
             const Pk<int, EPT> iu = ldv<int, EPT>(Eu + e0);
 #pragma unroll
             for (int j = 0; j < EPT; j++) {
                 pu[j] = xp[iu.v[j]];
-                gu[j] = gi[iu.v[j]];
+                if (RAT) ru[j] = rr[iu.v[j]];
+                else gu[j] = gi[iu.v[j]];
             }
         }
         if (UNI) {
@@ -1925,9 +1963,13 @@ __device__ __forceinline__ void tl_gather(
         }
         Pk<real, EPT> ou, ov;
 #pragma unroll
-        for (int j = 0; j < EPT; j++)
-            edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
-                            z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        for (int j = 0; j < EPT; j++) {
+            if (RAT)
+                edge_ratio<real>(pu[j], pv[j], ru[j], rv[j], la0, z.v[2 * j], z.v[2 * j + 1], rho);
+            else
+                edge_full<real>(pu[j], pv[j], gu[j], gv[j], a.v[j], la.v[j], z.v[2 * j],
+                                z.v[2 * j + 1], ou.v[j], ov.v[j], rho);
+        }
         Pk<real, EPT> zu, zv;
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
@@ -1936,7 +1978,7 @@ __device__ __forceinline__ void tl_gather(
         }
         stv<real, EPT>(Z2 + e0, zu);
         stv<real, EPT>(Z2 + E + e0, zv);
-        if (wz) {  // block-uniform; null: the vertex sweep forms W * Z itself
+        if (!RAT && wz) {  // block-uniform; null: the vertex sweep forms W * Z itself
             stv<real, EPT>(wz + e0, ou);
             stv<real, EPT>(wz + E + e0, ov);
         }
@@ -1945,11 +1987,14 @@ __device__ __forceinline__ void tl_gather(
             const int u = Eu[e], v = Ev[e];
             real zu = Z2[e], zv = Z2[E + e], ou, ov;
             const real l = la_at(e, La_d1, la0);
-            edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou, ov,
-                            rho);
+            if (RAT)
+                edge_ratio<real>(xp[u], xp[v], rr[u], rr[v], la0, zu, zv, rho);
+            else
+                edge_full<real>(xp[u], xp[v], gi[u], gi[v], A1 ? A1[e] : cw * l, l, zu, zv, ou,
+                                ov, rho);
             Z2[e] = zu;
             Z2[E + e] = zv;
-            if (wz) {
+            if (!RAT && wz) {
                 wz[e] = ou;
                 wz[E + e] = ov;
             }
@@ -1958,13 +2003,14 @@ __device__ __forceinline__ void tl_gather(
 }
 
 
-template <typename real, bool UNI>
+template <typename real, bool UNI, bool RAT = false>
 __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     long E, int V, const int *__restrict__ Eu, const unsigned short *__restrict__ luv,
     const int *__restrict__ erec, const int *__restrict__ Ev,
     const R2<real> *__restrict__ xp, real *__restrict__ Z2, const real *__restrict__ A1, real cw,
     const R2<real> *__restrict__ gi, const real *__restrict__ La_d1, real la0,
-    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int b0, int nb, int xcd) {
+    real *__restrict__ wz, real rho, const Ctrl<real> *ctrl, int b0, int nb, int xcd,
+    const real *__restrict__ rr = nullptr) {
     if (ctrl && ctrl->halt) return;
     constexpr int SPAN = TlBlocks<real>::v * kBlock;
     __shared__ R2<real> s_xp[SPAN];
@@ -1972,8 +2018,8 @@ __global__ __launch_bounds__(256) void k_edge_sweep_tl(
     int blk = xcd_block(blockIdx.x, nb, xcd);
     if (blk >= nb) return;  // whole block
     blk += b0;  // edge blocks [b0, b0 + nb) of this launch
-    tl_gather<real, UNI>(E, V, Eu, luv, erec + (long)blk * kErec, Ev, xp, Z2, A1, cw, gi, La_d1,
-                         la0, wz, rho, blk, s_xp, s_gi);
+    tl_gather<real, UNI, RAT>(E, V, Eu, luv, erec + (long)blk * kErec, Ev, xp, Z2, A1, cw, gi,
+                              La_d1, la0, wz, rho, blk, s_xp, s_gi, rr);
 }
 
 // luv[p] = (Eu[p] mod 256) | (Ev[p] mod 256) << 8: both ends within their blocks
