@@ -430,6 +430,9 @@ def main():
         knames["edge_sweep"] = ["k_edge_sweep_tl"]
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
+    if not quad and 0 < getattr(wl, "K", 0) <= 64:  # workgroups of M vertex blocks (default),
+        # or the one-block sweep (PFDR_SX_M=1)
+        knames["sx_vertex_sweep"] = ["k_sx_vertex_tile", "k_sx_vertex_sweep"]
     if not quad and getattr(wl, "K", 0) > 64:  # group sweep (LDS columns), or a wave per vertex
         knames["sx_vertex_sweep"] = ["k_sx_vertex_group", "k_sx_vertex_wide"]
         knames["sx_vertex_wide"] = ["k_sx_vertex_group", "k_sx_vertex_wide"]
