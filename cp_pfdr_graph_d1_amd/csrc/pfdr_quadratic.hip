@@ -236,7 +236,7 @@ class QuadSession final : public SessionBase {
     DevBuf<real> A1_;
     DevBuf<R2<real>> gi_;
     DevBuf<real> rr_;  // per-vertex (cw la0 / Aux) / Ga of the ratio edge sweep (rat())
-    bool rat_env_ = true;  // PFDR_EDGE_RATIO=0: the (Ga, invAux) pair sweep throughout
+    bool rat_on_ = false;  // rr_ formed at setup (see rat())
     real cw_ = real(0);
     DevBuf<real> R_, vpart_, opart_, Obj_, Dif_, red_, csum_;
     DevBuf<double> Rpart_;  // k_rows_partial's double partials
@@ -330,7 +330,7 @@ class QuadSession final : public SessionBase {
     // one edge weight and no W * Z stream (until the first reconditioning):
     // the tiled edge sweep reads the ends' formed ratios (k_ratio_vertex)
     // instead of their (Ga, invAux) pairs
-    bool rat() const { return rat_env_ && zdirect() && !la_it(); }
+    bool rat() const { return rat_on_ && zdirect() && !la_it(); }
     int blo_ = 0, bhi_ = 0;
     bool overlap_ = false;
     void plan_overlap();
@@ -634,17 +634,6 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
         tr.wait(s);
         zd_ranks_ = all == 0;
     }
-    {
-        const char *e = getenv("PFDR_EDGE_RATIO");
-        rat_env_ = !(e && e[0] == '0');
-    }
-    if (rat()) {  // cw_ and la0_ are known from here (owned and ghost ends)
-        rr_.alloc(Vg_ + 2);  // (+2: the tiled edge sweep stages vertex pairs)
-        PFDR_HIP(hipMemsetAsync(rr_.p, 0, (Vg_ + 2) * sizeof(real), s));
-        k_ratio_vertex<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, cw_, la0_, Ga_.p, invAux_.p,
-                                                              rr_.p);
-        PFDR_HIP(hipGetLastError());
-    }
     pins_.release();
     stopped_ = (itMax_ <= 0);
     interior_edges = E_;
@@ -653,7 +642,7 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
     auto acc = [&](size_t b) { device_bytes += (int64_t)b; };
     acc(Eu_.n * 4 + Ev_.n * 4);
     for (DevBuf<real> *b : {&La_d1_, &La_l1_, &Y_, &A_, &L_, &diag_, &Ga_, &invAux_, &Th_l1_, &absval_,
-                            &pre_, &Z2_, &A1_, &wz_, &R_, &rr_,
+                            &pre_, &Z2_, &A1_, &wz_, &R_,
                             &vpart_, &opart_, &Obj_, &Dif_, &xout_, &Rsum_, &xfull_, &spart_})
         acc(b->n * sizeof(real));
     acc(Rpart_.n * sizeof(double));
@@ -729,6 +718,24 @@ QuadSession<real>::QuadSession(const pfdr_problem *p) {
             }
             speculative = serial ? 2 : 1;
         }
+    }
+    {
+        // the ratio edge sweep where it pays: not beside an overlapped
+        // evolution chain, whose kernels the faster sweep (eight waves per
+        // SIMD against the pair sweep's seven) leaves no room to run in --
+        // converged headline 0.570 ms/iter against 0.524 (f6d).
+        // PFDR_EDGE_RATIO=0 / 1: never / wherever it applies.
+        const char *e = getenv("PFDR_EDGE_RATIO");
+        rat_on_ = e && *e ? e[0] != '0' : speculative != 1;
+    }
+    if (rat()) {  // cw_ and la0_ are known from here (owned and ghost ends)
+        rr_.alloc(Vg_ + 2);  // (+2: the tiled edge sweep stages vertex pairs)
+        PFDR_HIP(hipMemsetAsync(rr_.p, 0, (Vg_ + 2) * sizeof(real), s));
+        k_ratio_vertex<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, cw_, la0_, Ga_.p, invAux_.p,
+                                                              rr_.p);
+        PFDR_HIP(hipGetLastError());
+        device_bytes += (int64_t)(rr_.n * sizeof(real));
+        edge_ratio = 1;
     }
     xr_ = xw_ = xp_.p;
     // a speculative session launches directly on its two streams: the
@@ -1383,7 +1390,10 @@ void QuadSession<real>::precondition(bool init) {
     }
     k_gi_pack<real><<<grid_for(Vg_), kBlock, 0, s>>>(Vg_, Ga_.p, invAux_.p, gi_.p);
     PFDR_HIP(hipGetLastError());
-    if (!init && !rat()) rr_.release();  // (A1 from the first reconditioning on)
+    if (!init && !rat() && rr_.p) {  // (A1 from the first reconditioning on)
+        rr_.release();
+        edge_ratio = 0;
+    }
     if (!init) {
         // forward step with the new metric from the gradient taken before
         // reconditioning (ref :448-464)

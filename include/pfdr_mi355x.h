@@ -263,8 +263,12 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
  * "dense_exact" (1: the dense products run in the reference's sequential
  * order, bit-exact; small single-GPU problems), "tiled_blocks" (vertex
  * blocks staging tile-ordered contributions) and "record_blocks" (of those,
- * the blocks whose runs fit one per-block record), "speculative" (1: the
- * evolution sums run beside the next iteration's sweeps). */
+ * the blocks whose runs fit one per-block record), "slot_patterns" (distinct
+ * slot sequences of those records' runs, 0: per-entry slots), "speculative"
+ * (1: the evolution sums run beside the next iteration's sweeps on a second
+ * stream, 2: after them on the session stream), "edge_ratio" (1: the tiled
+ * edge sweep reads each end's (c La_d1 / Aux) / Ga formed once per vertex;
+ * until the first reconditioning). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 

@@ -196,3 +196,40 @@ def test_slot_patterns_identical(gpu_lib, oracle_port, dt, shape, conn):
                                                  np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
                                                  0, 0, None, 1.5, 1e-3, 1e-3, 1e-6, 400, dif=True)
     assert ito == it1 and np.array_equal(X1, Xo)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("rcd", [0.0, 1e-3])
+def test_edge_ratio_identical(gpu_lib, oracle_port, dt, rcd):
+    """One edge weight, Z-direct: the tiled edge sweep reads each end's
+    (c La_d1 / Aux) / Ga formed once per vertex (k_ratio_vertex) instead of
+    the (Ga, 1/Aux) pair -- the quotients prox_weights forms, bit for bit:
+    equal to the pair sweep (PFDR_EDGE_RATIO=0) and to the oracle; with
+    reconditioning the session returns to the pair sweep at the first one"""
+    import os
+    shape = (72, 64, 64)
+    V, Eu, Ev = _grid(shape, 6, 1)
+    Y = piecewise_observation(shape, 3, dt)
+    out = []
+    for rat in ("1", "0"):
+        os.environ["PFDR_EDGE_RATIO"] = rat
+        try:
+            s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                             np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5,
+                             condMin=1e-3, difTol=1e-6, difRcd=rcd, itMax=300, record_dif=True,
+                             evolution=pfdr.EVOLUTION_SEQUENTIAL)
+            try:
+                q = s.query("edge_ratio")
+                s.run(300)
+                out.append((s.result(), q))
+            finally:
+                s.close()
+        finally:
+            del os.environ["PFDR_EDGE_RATIO"]
+    ((X1, it1, _, D1), q1), ((X0, it0, _, D0), q0) = out
+    assert q1 == 1 and q0 == 0
+    assert it1 == it0 and np.array_equal(X1, X0) and np.array_equal(D1[:it1], D0[:it0])
+    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
+                                                 np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
+                                                 0, 0, None, 1.5, 1e-3, rcd, 1e-6, 300, dif=True)
+    assert ito == it1 and np.array_equal(X1, Xo)
