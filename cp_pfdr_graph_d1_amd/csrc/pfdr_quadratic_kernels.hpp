@@ -390,13 +390,17 @@ __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
                                              const real *__restrict__ wz, real *lds, int *wt,
                                              real wv = real(1),
                                              const Slots12 *__restrict__ ptab = nullptr,
-                                             const int *__restrict__ prec = nullptr) {
+                                             const int *__restrict__ prec = nullptr,
+                                             bool pre = false, int pre_rv = 0, int pre_pr = 0,
+                                             int pre_dg = 0) {
     constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    const int dg = v < V ? deg8[v] : 0;
-    const int rv = lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
+    // (pre: the record, pattern offsets and degree came with the caller's
+    // first load round, see vertex_block)
+    const int dg = pre ? pre_dg : v < V ? deg8[v] : 0;
+    const int rv = pre ? pre_rv : lane < kTileRec ? trec[(long)blk * kTileRec + lane] : 0;
     // pattern offsets of the runs (prec, with the record; null: per-entry slots)
-    const int pr = prec && lane < kPrec ? prec[(long)blk * kPrec + lane] : 0;
+    const int pr = pre ? pre_pr : prec && lane < kPrec ? prec[(long)blk * kPrec + lane] : 0;
     int dinc = dg;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -2393,10 +2397,23 @@ __device__ __forceinline__ void vertex_block(const VArgs<real> &a, int blk, real
     // ZD: the vertex's splitting weight, as the edge sweep forms it (a * invAux)
     const real wv = ZD && v < a.V ? a.a0 * (a.gi ? o.ia : a.invAux[v]) : real(1);
     real x;
+    // the block's record, pattern offsets and degree in the same load round
+    // as its tok and the vertex operands (every block has a record slot; only
+    // tok == 2 blocks read it): two dependent rounds to the contributions
+    // instead of three
+    const bool pre = a.slots && a.trec;  // launch-uniform
+    int pre_rv = 0, pre_pr = 0, pre_dg = 0;
+    if (pre) {
+        const int lane = threadIdx.x & (kWave - 1);
+        pre_rv = lane < kTileRec ? a.trec[(long)blk * kTileRec + lane] : 0;
+        pre_pr = a.prec && lane < kPrec ? a.prec[(long)blk * kPrec + lane] : 0;
+        pre_dg = v < a.V ? a.deg8[v] : 0;
+    }
     const int tk = a.slots ? a.tok[blk] : 0;  // block-uniform
     if (tk == 2)
         x = tile_sum_rec<real, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
-                                   lds, scan + 3 * kTileRuns, wv, a.ptab, a.prec);
+                                   lds, scan + 3 * kTileRuns, wv, a.ptab, a.prec, pre, pre_rv,
+                                   pre_pr, pre_dg);
     else if (tk)
         x = tile_sum<real, GB, ZD>(a.V, a.E, blk, v, a.deg8, a.slots, a.ustart, a.tptr, a.tstart,
                                    a.tlen, ZD ? a.zs : a.wz, lds, scan, wv);
