@@ -57,6 +57,59 @@ bool comm_aborted(void *comm) {
     return g_aborted.count(comm) != 0;
 }
 
+// The split communicator of a parent (Transport::split), kept while the
+// parent lives: the sessions a partition runs on one communicator reuse it
+// instead of paying a collective ncclCommSplit (own streams and buffers)
+// and its teardown per session.  One user at a time: a second live session
+// on the same parent gets a split of its own (`busy`).  Released with the
+// parent (comm_release_split), or dropped once the watchdog aborted it.
+struct SplitEntry {
+    void *child;
+    bool busy;
+};
+static std::map<void *, SplitEntry> g_split;
+
+void *comm_split_take(void *parent) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    auto it = g_split.find(parent);
+    if (it == g_split.end() || it->second.busy) return nullptr;
+    if (g_aborted.count(it->second.child) || g_aborted.count(parent)) return nullptr;
+    it->second.busy = true;
+    return it->second.child;
+}
+
+bool comm_split_keep(void *parent, void *child) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    if (g_split.count(parent)) return false;  // (one kept per parent; this one is the caller's)
+    g_split[parent] = SplitEntry{child, true};
+    g_children[parent].insert(child);
+    return true;
+}
+
+void comm_split_return(void *parent, void *child) {
+    std::lock_guard<std::mutex> l(g_aborted_m);
+    auto it = g_split.find(parent);
+    if (it != g_split.end() && it->second.child == child) it->second.busy = false;
+}
+
+void comm_release_split(void *parent) {
+    void *child = nullptr;
+    {
+        std::lock_guard<std::mutex> l(g_aborted_m);
+        auto it = g_split.find(parent);
+        if (it == g_split.end()) return;
+        child = it->second.child;
+        g_split.erase(it);
+        auto k = g_children.find(parent);
+        if (k != g_children.end()) {
+            k->second.erase(child);
+            if (k->second.empty()) g_children.erase(k);
+        }
+        if (g_aborted.erase(child)) return;  // released by the abort
+    }
+    (void)ncclCommDestroy((ncclComm_t)child);
+}
+
 // a communicator just created at the address of one the watchdog aborted
 // (released by ncclCommAbort, its handle never destroyed): the entry is stale
 void comm_created(void *comm) {
@@ -98,6 +151,7 @@ extern "C" int pfdr_comm_init(void **comm_out, int nranks, int rank, const void 
 
 extern "C" int pfdr_comm_destroy(void *comm) {
     if (!comm) return PFDR_OK;
+    pfdr::comm_release_split(comm);  // (its kept split communicator first)
     {   // aborted by the watchdog: already released, forget the handle
         std::lock_guard<std::mutex> l(pfdr::g_aborted_m);
         if (pfdr::g_aborted.erase(comm)) return PFDR_OK;

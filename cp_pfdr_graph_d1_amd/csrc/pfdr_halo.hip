@@ -168,6 +168,7 @@ void Transport::alltoallv_host(const std::vector<std::vector<int64_t>> &send,
 class RcclTransport final : public Transport {
     ncclComm_t comm_;
     bool owned_ = false;             // a split communicator: destroyed with the transport
+    bool kept_ = false;              // the parent's kept split communicator: given back
     ncclComm_t parent_ = nullptr;    // the communicator it was split from (comm_add_child)
     // PFDR_RCCL_SELF=1 (test flag): the collectives of a 1-rank
     // communicator (all-reduces, broadcasts) are issued as real RCCL calls
@@ -196,6 +197,7 @@ class RcclTransport final : public Transport {
         init_self();
     }
     ~RcclTransport() override {
+        if (kept_) comm_split_return(parent_, comm_);
         if (!owned_) return;
         comm_forget_child(parent_, comm_);  // (no abort through the parent after this)
         if (comm_aborted(comm_)) comm_created(comm_);  // released by the abort
@@ -207,16 +209,26 @@ class RcclTransport final : public Transport {
     void on_timeout() override { comm_abort(comm_); }  // (its split ones first)
     std::unique_ptr<Transport> split(hipStream_t) override {
         last_op = "communicator split";
-        ncclComm_t nc = nullptr;
-        // its own resources (streams, buffers): operations on the two
-        // communicators must not be ordered behind each other
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.splitShare = 0;
-        ck(ncclCommSplit(comm_, 0, rank, &nc, &cfg), "comm split");
-        comm_created(nc);
-        comm_add_child(comm_, nc);
+        // the parent's kept split communicator when free (every rank runs
+        // the same sessions on its communicator, so all take it or all
+        // split, collectively); PFDR_SPLIT_CACHE=0: a new one per session
+        const char *e = getenv("PFDR_SPLIT_CACHE");
+        const bool cache = !(e && e[0] == '0');
+        ncclComm_t nc = cache ? (ncclComm_t)comm_split_take(comm_) : nullptr;
+        bool kept = nc != nullptr;
+        if (!nc) {
+            // its own resources (streams, buffers): operations on the two
+            // communicators must not be ordered behind each other
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.splitShare = 0;
+            ck(ncclCommSplit(comm_, 0, rank, &nc, &cfg), "comm split");
+            comm_created(nc);
+            kept = cache && comm_split_keep(comm_, nc);
+            if (!kept) comm_add_child(comm_, nc);
+        }
         std::unique_ptr<RcclTransport> t(new RcclTransport(nc, nranks, rank));
-        t->owned_ = true;
+        t->owned_ = !kept;
+        t->kept_ = kept;
         t->parent_ = comm_;
         return std::unique_ptr<Transport>(t.release());
     }

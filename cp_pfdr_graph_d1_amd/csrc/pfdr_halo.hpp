@@ -88,6 +88,13 @@ void comm_created(void *comm);  // forget a stale aborted entry at this address
 // forget it before destroying it
 void comm_add_child(void *parent, void *child);
 void comm_forget_child(void *parent, void *child);
+// the split communicator kept with `parent` (pfdr_comm.hip): take it if kept
+// and free (null otherwise), keep a new one (false: one is kept already, the
+// caller owns this one), give it back, release it with the parent
+void *comm_split_take(void *parent);
+bool comm_split_keep(void *parent, void *child);
+void comm_split_return(void *parent, void *child);
+void comm_release_split(void *parent);
 std::unique_ptr<Transport> make_loopback_transport(void *hub, int nranks, int rank);
 // wake every rank waiting on the hub with an error (a rank failed)
 void loopback_abort(void *hub, const char *reason);

@@ -150,6 +150,7 @@ std::vector<ncclComm_t> group_comms(DeviceConfig &c, const std::vector<int> &dev
     for (ncclComm_t cm : c.comms) ok = ok && !comm_aborted(cm);
     if (!ok) {
         for (ncclComm_t cm : c.comms) {  // aborted ones were released by ncclCommAbort
+            comm_release_split(cm);  // (its kept split communicator first)
             if (comm_aborted(cm)) comm_created(cm);  // forget the released handle
             else (void)ncclCommDestroy(cm);
         }

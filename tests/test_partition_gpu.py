@@ -425,6 +425,68 @@ def test_rccl_single_rank_real_calls_graph_replay(gpu_lib, kind):
     assert np.array_equal(D1[:it1], D0[:it0])
 
 
+def test_rccl_split_communicator_kept(gpu_lib):
+    """Speculative sessions on one RCCL communicator reuse the split
+    communicator kept with it (one collective ncclCommSplit per parent, not
+    per session); a second session alive at the same time splits its own;
+    PFDR_SPLIT_CACHE=0 splits per session.  Every session's iterates, count
+    and Dif equal the single-GPU session's."""
+    import ctypes as C
+    import time
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation
+    lib = pfdr.load()
+    dt = np.float32
+    shape = (128, 96)
+    V = int(np.prod(shape))
+    Eu, Ev = grid_graph(shape, 4)
+    args = (pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+            np.zeros(V, dt), piecewise_observation(shape, 3, dt))
+    kw = dict(La_l1=np.full(V, 0.01, dt), rho=1.5, condMin=1e-3, difTol=1e-5, difRcd=0.0,
+              itMax=1000, record_dif=True, evolution=pfdr.EVOLUTION_SEQUENTIAL)
+    s = pfdr.Session(*args, **kw)
+    s.run(1000)
+    X0, it0, _, D0 = s.result()
+    s.close()
+
+    def check(sess):
+        sess.run(1000)
+        X, it, _, D = sess.result()
+        assert it == it0 and np.array_equal(X, X0) and np.array_equal(D[:it], D0[:it0])
+
+    idb = (C.c_char * 128)()
+    assert lib.pfdr_comm_unique_id(idb) == 0
+    comm = C.c_void_p()
+    assert lib.pfdr_comm_init(C.byref(comm), 1, 0, idb) == 0, lib.pfdr_last_error()
+    extra = dict(nranks=1, rank=0, comm=comm.value, comm_kind=P.COMM_RCCL, vtx_begin=0,
+                 V_global=V)
+    setup = {}
+    try:
+        for cache in ("1", "0"):
+            with _env(PFDR_SPLIT_CACHE=cache):
+                ts = []
+                for _ in range(3):
+                    t = time.perf_counter()
+                    a1 = pfdr.Session(*args, **kw, **extra)
+                    ts.append(time.perf_counter() - t)
+                    try:
+                        assert a1.query("speculative") == 1
+                        a2 = pfdr.Session(*args, **kw, **extra)  # alive beside it: its own split
+                        try:
+                            check(a2)
+                        finally:
+                            a2.close()
+                        check(a1)
+                    finally:
+                        a1.close()
+                setup[cache] = ts
+    finally:
+        lib.pfdr_comm_destroy(comm)
+    print("session setup (s), split kept:", ["%.4f" % t for t in setup["1"]],
+          "split per session:", ["%.4f" % t for t in setup["0"]])
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("spec", ["auto", "serial", "off"])
 def test_rccl_single_rank_real_calls_headline_conv(gpu_lib, spec):

@@ -6,7 +6,8 @@ speculatively (P and (P, step) ping-ponged): the stopping iteration, every
 Dif and P equal the restatement's (itself pinned to the reference on the
 golden cases simplex_k65 .. simplex_k1500), for the l1 evolution and the
 label-change count, with K in registers (K = 130) and in memory (K = 1100).
-Also the partitioned wide-K session (K-wide halos) against one GPU."""
+Also the partitioned wide-K session (K-wide halos) against one GPU, and
+speculating over 3 ranks (both concurrency modes) against the restatement."""
 import numpy as np
 import pytest
 
@@ -82,6 +83,34 @@ def test_wide_partitioned_matches_single(gpu_lib, K, n, dt):
                                       K=K, al=0.1, **kw)
     assert it == it1 == 30
     assert np.array_equal(X, X1)
+
+
+@pytest.mark.parametrize("K,n", [(130, 40), (1100, 12)], ids=["K130", "K1100"])
+@pytest.mark.parametrize("spec", [0, 1], ids=["overlapped", "serial"])
+def test_wide_partitioned_speculative_matches_restatement(gpu_lib, K, n, spec):
+    """3 loopback ranks, difRcd = 0 and the sequential evolution: the
+    partition decides four iterations deep (depth 4 from 3 ranks), the chain
+    on a second stream over the split transport (overlapped) or on the session
+    stream (serial, PFDR_SPEC_SERIAL) -- the group sweep's K-wide halos and the
+    speculative pipeline together: stopping iteration, every Dif and P equal
+    the restatement's"""
+    import oracle
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    dt = np.float32
+    V, Eu, Ev, Q = _problem(n, K, dt)
+    La = np.full(Eu.size, 0.05, dt)
+    X, it, _, D, info = P.solve_loopback(3, pfdr.PFDR_KIND_SIMPLEX, dt, Eu, Ev, La, Q.copy(), Q,
+                                         K=K, al=0.1, rho=1.0, condMin=0.1, difRcd=0.0,
+                                         difTol=1e-3, itMax=300, record_dif=True,
+                                         evolution=pfdr.EVOLUTION_SEQUENTIAL, spec=spec)
+    assert all(q["speculative"] == spec + 1 for q in info["queries"])
+    Po, ito, _, Difo = oracle.Oracle("port").loss_d1_simplex(
+        Q.copy(), Q, K, Eu, Ev, La, 0.1, None, 1.0, 0.1, 0.0, 1e-3, 300, dif=True)
+    print("K %d spec %d: it %d / %d" % (K, spec, it, ito))
+    assert 20 < it == ito < 300
+    assert np.array_equal(D[:it], Difo[:ito])
+    assert np.array_equal(X, Po)
 
 
 @pytest.mark.parametrize("D", [3, 7, 31, 64, 100, 1024, 1025, 4000])
