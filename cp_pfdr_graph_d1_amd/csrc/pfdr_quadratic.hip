@@ -236,6 +236,7 @@ class QuadSession final : public SessionBase {
     DevBuf<real> A1_;
     DevBuf<R2<real>> gi_;
     DevBuf<real> rr_;  // per-vertex (cw la0 / Aux) / Ga of the ratio edge sweep (rat())
+    int vpair_cap_ = 0;  // pair vertex sweep: entries of the largest record block (0: off)
     bool rat_on_ = false;  // rr_ formed at setup (see rat())
     real cw_ = real(0);
     DevBuf<real> R_, vpart_, opart_, Obj_, Dif_, red_, csum_;
@@ -993,6 +994,25 @@ void QuadSession<real>::build_tile_runs() {
     }
     tiled_blocks = n;
     record_blocks = nr;
+    // the pair vertex sweep (k_vertex_sweep_pair): f32 sessions whose every
+    // block is a record block, when two blocks' lists still leave LDS for
+    // seven workgroups per CU (the kernel's seven waves per SIMD): C5 (6
+    // entries per vertex) vertex sweep 3.15-3.22 -> 2.83-2.85 ms, C2 -2 %;
+    // the headline's 12 per vertex would halve the resident workgroups
+    // (0.174 -> 0.226 ms, f6j), so it keeps the one-block sweep.
+    // PFDR_VPAIR=0: the one-block sweep throughout
+    const char *e = getenv("PFDR_VPAIR");
+    if (sizeof(real) == 4 && nr == nb && !(e && e[0] == '0')) {
+        DevBuf<int> ent(nb);
+        k_rec_entries<<<grid_for(nb), kBlock, 0, s>>>(V_, nb, inc_.ptr.p, tok_.p, ent.p);
+        PFDR_HIP(hipGetLastError());
+        PFDR_HIP(hipMemcpyAsync(h.data(), ent.p, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+        PFDR_HIP(hipStreamSynchronize(s));
+        const int cap = std::max(1, *std::max_element(h.begin(), h.end()));
+        const size_t per_wg = 2 * (size_t)cap * sizeof(real) + 2048;  // (+ the static arrays)
+        if (per_wg * 7 <= 160 * 1024) vpair_cap_ = cap;
+        vertex_pair = vpair_cap_;
+    }
 }
 
 // Slot patterns (k_run_hash): when the record blocks' runs repeat a few
@@ -1533,6 +1553,16 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
     if (pad_ && bend2 <= bbeg2) {
         k_vertex_sweep_pad<real><<<xcd_grid(a.nb, a.xcd), kBlock, 0, s>>>(
             a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
+        return;
+    }
+    if (vpair_cap_ && bend2 <= bbeg2) {  // pairs of record blocks, one range
+        const int np = (a.nb + 1) / 2;
+        a.xcd = xcd_fit(np, xcd_v_);
+        const size_t lb = 2 * (size_t)vpair_cap_ * sizeof(real);
+        if (zdirect())
+            k_vertex_sweep_pair<real, true><<<xcd_grid(np, a.xcd), kBlock, lb, s>>>(a, vpair_cap_);
+        else
+            k_vertex_sweep_pair<real><<<xcd_grid(np, a.xcd), kBlock, lb, s>>>(a, vpair_cap_);
         return;
     }
     if (zdirect())

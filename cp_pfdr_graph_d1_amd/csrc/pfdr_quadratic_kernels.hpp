@@ -492,6 +492,134 @@ __device__ __forceinline__ real tile_sum_rec(int V, long E, int blk, int v,
     return s;
 }
 
+// tile_sum_rec for two consecutive record blocks b0, b0 + 1 in one
+// workgroup (the pair vertex sweep): both records in one register (lanes
+// 0..31 block b0's, 32..63 block b0 + 1's; kTileRec = 32 ints each, so one
+// load), both blocks' runs in one register (lane 32 h + r: block b0 + h's run
+// r), both blocks' groups in one list (b0's first), each scattered into its
+// block's LDS list (lds + h cap) -- every lane keeps two vertices' gathers
+// in flight where the one-block sweep keeps one, at the same eight waves per
+// SIMD.  Each vertex's sum runs over its block's list in CSR order, as in
+// tile_sum_rec: the same sums bit for bit.
+template <typename real, bool ZD = false>
+__device__ __forceinline__ void tile_sum_rec2(int V, long E, int b0, int v0, int v1,
+                                              const unsigned char *__restrict__ deg8,
+                                              const Slots12 *__restrict__ slots,
+                                              const int *__restrict__ trec,
+                                              const real *__restrict__ wz, real *lds, int cap,
+                                              int *wt, real wv0, real wv1,
+                                              const Slots12 *__restrict__ ptab,
+                                              const int *__restrict__ prec, real &x0, real &x1) {
+    static_assert(kTileRec == 32 && kWave == 64 && kPrec == 16, "two records per wave register");
+    constexpr int VE = Vec<real>::kPer16B, G = kSlotGroup, ZV = G / VE, NW = kBlock / kWave;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int dg0 = v0 < V ? deg8[v0] : 0, dg1 = v1 < V ? deg8[v1] : 0;
+    const int rv = trec[(long)b0 * kTileRec + lane];
+    // pattern offsets: lane 16 h + q holds block b0 + h's entry q
+    const int pr = prec ? prec[(long)b0 * kPrec + (lane & 31)] : 0;
+    int i0 = dg0, i1 = dg1;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y0 = __shfl_up(i0, o, kWave), y1 = __shfl_up(i1, o, kWave);
+        if (lane >= o) {
+            i0 += y0;
+            i1 += y1;
+        }
+    }
+    if (lane == kWave - 1) {
+        wt[w] = i0;
+        wt[NW + w] = i1;
+    }
+    const int us0 = __builtin_amdgcn_readlane(rv, 0), nu0 = __builtin_amdgcn_readlane(rv, 1);
+    const int nt0 = __builtin_amdgcn_readlane(rv, 2);
+    const int us1 = __builtin_amdgcn_readlane(rv, 32), nu1 = __builtin_amdgcn_readlane(rv, 33);
+    const int nt1 = __builtin_amdgcn_readlane(rv, 34);
+    const int hf = lane >> 5, rl = lane & 31;
+    const int st = __shfl(rv, 32 * hf + min(3 + 2 * rl, 31), kWave);
+    const int ln = __shfl(rv, 32 * hf + min(4 + 2 * rl, 31), kWave);
+    int P = 0;
+    if (rl < (hf ? nt1 : nt0) && ln > 0) {
+        const long A = E + st;
+        P = (int)((A + ln - 1) / G - A / G + 1);
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {  // inclusive prefix within each half
+        const int y = __shfl_up(P, o, kWave);
+        if (rl >= o) P += y;
+    }
+    const int ngv0 = __builtin_amdgcn_readlane(P, 31), ngv1 = __builtin_amdgcn_readlane(P, 63);
+    const long fu0 = us0 / G, fu1 = us1 / G;
+    const int ngu0 = nu0 > 0 ? (int)((us0 + nu0 - 1) / G - fu0 + 1) : 0;
+    const int ngu1 = nu1 > 0 ? (int)((us1 + nu1 - 1) / G - fu1 + 1) : 0;
+    const int tot0 = ngu0 + ngv0, tot = tot0 + ngu1 + ngv1;
+    const int pu0 = __builtin_amdgcn_readlane(pr, 0), pu1 = __builtin_amdgcn_readlane(pr, 16);
+    for (int b = 0; b < tot; b += 2 * kBlock) {
+        Slots12 d[2];
+        Pk<real, VE> x[2][ZV];
+        long gb[2];
+        int lo[2], hi[2], pg[2], hb[2];  // lo, hi: the run's bounds relative to the group, clamped
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int k = min(b + u * kBlock + tid, tot - 1);
+            const int h = k >= tot0;
+            const int kk = k - (h ? tot0 : 0);
+            const int ngu = h ? ngu1 : ngu0;
+            const int kv = kk - ngu;
+            // the group's run in its block (both halves' tables walked by
+            // every lane: the loop bounds stay uniform)
+            int ra = 0, rb = 0;
+            for (int q = 0; q < nt0; q++) ra += __builtin_amdgcn_readlane(P, q) <= kv;
+            for (int q = 0; q < nt1; q++) rb += __builtin_amdgcn_readlane(P, 32 + q) <= kv;
+            const int r = min(h ? rb : ra, 31), base = 32 * h;
+            const int sr = __shfl(st, base + r, kWave), lr = __shfl(ln, base + r, kWave);
+            const int pb = __shfl(P, base + max(r - 1, 0), kWave);
+            const int pv = __shfl(pr, 16 * h + min(r + 1, 15), kWave);
+            hb[u] = h;
+            long L, H;
+            if (kk < ngu) {
+                gb[u] = (h ? fu1 : fu0) + kk;
+                L = h ? us1 : us0;
+                H = L + (h ? nu1 : nu0);
+                pg[u] = (h ? pu1 : pu0) + kk;
+            } else {
+                const long A = E + sr;
+                const int gi = kv - (r > 0 ? pb : 0);
+                gb[u] = A / G + gi;
+                L = A;
+                H = A + lr;
+                pg[u] = pv + gi;
+            }
+            lo[u] = (int)max(L - gb[u] * G, -1L);
+            hi[u] = (int)min(H - gb[u] * G, (long)G + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            d[u] = prec ? ptab[pg[u]] : slots[gb[u]];
+#pragma unroll
+            for (int z = 0; z < ZV; z++) x[u][z] = ldv<real, VE>(wz + gb[u] * G + z * VE);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (b + u * kBlock + tid < tot) {
+                real *l = lds + (hb[u] ? cap : 0);
+#pragma unroll
+                for (int q = 0; q < G; q++)
+                    if (q >= lo[u] && q < hi[u]) l[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
+            }
+    }
+    __syncthreads();
+    int my0 = i0 - dg0, my1 = i1 - dg1;
+    for (int q = 0; q < w; q++) {
+        my0 += wt[q];
+        my1 += wt[NW + q];
+    }
+    real s0 = real(0), s1 = real(0);
+    for (int j = 0; j < dg0; j++) s0 += ZD ? wv0 * lds[my0 + j] : lds[my0 + j];
+    for (int j = 0; j < dg1; j++) s1 += ZD ? wv1 * lds[cap + my1 + j] : lds[cap + my1 + j];
+    x0 = s0;
+    x1 = s1;
+}
+
 // tile-order keys: (u block, v block) in the high bits, edge position the
 // value; a partitioned rank (split) puts the edges with a ghost end after
 // all the others (bit 2 vbits)
@@ -2460,6 +2588,85 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
     lb = a.nb - 1 - lb;
     if (lb >= a.bsplit) lb += a.bjump;
     vertex_block<real, GB, ZD>(a, a.bbeg + lb, lds, red, scan, halt);
+}
+
+// The pair vertex sweep (single-GPU or one range of record blocks only,
+// every block a record block, f32): a workgroup takes the consecutive
+// blocks 2p, 2p + 1 of the launch (pairs walked last to first, as
+// k_vertex_sweep walks blocks), both blocks' contributions staged together
+// (tile_sum_rec2) into a dynamic LDS list of 2 cap entries, cap = the
+// largest record block's entry count; an odd last block runs alone.  Block
+// partials stay per vertex block.
+template <typename real, bool ZD = false>
+__global__ __launch_bounds__(256, VSweep<real>::waves - 1) void k_vertex_sweep_pair(VArgs<real> a,
+                                                                               int cap) {
+    int halt = 0;
+    if (a.ctrl) {
+        if (!a.late) {
+            if (a.ctrl->halt) return;
+        } else {
+            halt = a.ctrl->halt;
+        }
+    }
+    extern __shared__ __attribute__((aligned(16))) unsigned char vpair_lds[];
+    real *lds = reinterpret_cast<real *>(vpair_lds);
+    __shared__ real red[2][kBlock / kWave];
+    __shared__ int scan[3 * kTileRuns + 2 * (kBlock / kWave)];  // (the degree totals)
+    const int np = (a.nb + 1) / 2;
+    int lp = xcd_block(blockIdx.x, np, a.xcd);
+    if (lp >= np) return;
+    lp = np - 1 - lp;
+    const int b0 = a.bbeg + 2 * lp;
+    const bool odd = 2 * lp + 1 >= a.nb;  // the odd last block runs alone (block-uniform)
+    const int v0 = b0 * kBlock + threadIdx.x, v1 = v0 + kBlock;
+    const VOps<real> o0 = vertex_ops(a, v0);
+    const real wv0 = ZD && v0 < a.V ? a.a0 * (a.gi ? o0.ia : a.invAux[v0]) : real(1);
+    real x0, x1 = real(0);
+    if (odd) {
+        x0 = tile_sum_rec<real, ZD>(a.V, a.E, b0, v0, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
+                                    lds, scan + 3 * kTileRuns, wv0, a.ptab, a.prec);
+        if (halt) return;
+        real n0, d0;
+        vertex_finish(a, v0, x0, o0, n0, d0);
+        if (a.track) {
+            n0 = block_sum(n0, red[0]);
+            d0 = block_sum(d0, red[1]);
+            if (threadIdx.x == 0) {
+                a.part[2 * b0] = n0;
+                a.part[2 * b0 + 1] = d0;
+            }
+        }
+        return;
+    }
+    const VOps<real> o1 = vertex_ops(a, v1);
+    const real wv1 = ZD && v1 < a.V ? a.a0 * (a.gi ? o1.ia : a.invAux[v1]) : real(1);
+    tile_sum_rec2<real, ZD>(a.V, a.E, b0, v0, v1, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz, lds,
+                            cap, scan + 3 * kTileRuns, wv0, wv1, a.ptab, a.prec, x0, x1);
+    if (halt) return;  // block-uniform (a.late)
+    real n0, d0, n1, d1;
+    vertex_finish(a, v0, x0, o0, n0, d0);
+    vertex_finish(a, v1, x1, o1, n1, d1);
+    if (a.track) {
+        n0 = block_sum(n0, red[0]);
+        d0 = block_sum(d0, red[1]);
+        n1 = block_sum(n1, red[0]);
+        d1 = block_sum(d1, red[1]);
+        if (threadIdx.x == 0) {
+            a.part[2 * b0] = n0;
+            a.part[2 * b0 + 1] = d0;
+            a.part[2 * b0 + 2] = n1;
+            a.part[2 * b0 + 3] = d1;
+        }
+    }
+}
+
+// entries of each record block's list (0 for the others): the pair sweep's
+// LDS list per block is the largest
+static __global__ void k_rec_entries(int V, int nb, const int *__restrict__ ptr,
+                                     const int *__restrict__ tok, int *__restrict__ out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    out[b] = tok[b] == 2 ? ptr[min((b + 1) * kBlock, V)] - ptr[b * kBlock] : 0;
 }
 
 // Vertex sweep of a small graph (the fused-decision range) whose edge sweep

@@ -502,6 +502,7 @@ extern "C" int pfdr_session_query(pfdr_session *s, const char *what, int64_t *va
     else if (!strcmp(what, "record_blocks")) *value = s->impl->record_blocks;
     else if (!strcmp(what, "slot_patterns")) *value = s->impl->slot_patterns;
     else if (!strcmp(what, "edge_ratio")) *value = s->impl->edge_ratio;
+    else if (!strcmp(what, "vertex_pair")) *value = s->impl->vertex_pair;
     else if (!strcmp(what, "ustaged")) *value = s->impl->ustaged;
     else if (!strcmp(what, "symv")) *value = s->impl->symv;
     else if (!strcmp(what, "tiny")) *value = s->impl->tiny;

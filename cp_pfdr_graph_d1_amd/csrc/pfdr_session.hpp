@@ -67,6 +67,7 @@ class SessionBase {
     int64_t record_blocks = 0;  // of those, blocks read through a one-load record (tile_sum_rec)
     int64_t slot_patterns = 0;  // distinct slot patterns of their runs (0: per-entry slots)
     int64_t edge_ratio = 0;     // 1: the tiled edge sweep reads formed per-vertex ratios
+    int64_t vertex_pair = 0;    // >0: pair vertex sweep, entries of the largest record block
     int64_t ustaged = 0;       // edge sweep stages the u ends (k_edge_sweep_us)
     int64_t symv = 0;          // A^tA products from the block upper triangle
     int64_t tiny = 0;          // small graph: iterations in one workgroup launch

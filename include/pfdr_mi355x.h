@@ -268,7 +268,8 @@ int64_t pfdr_session_device_bytes(pfdr_session *s);
  * (1: the evolution sums run beside the next iteration's sweeps on a second
  * stream, 2: after them on the session stream), "edge_ratio" (1: the tiled
  * edge sweep reads each end's (c La_d1 / Aux) / Ga formed once per vertex;
- * until the first reconditioning). */
+ * until the first reconditioning), "vertex_pair" (> 0: the vertex sweep takes
+ * two record blocks per workgroup, the value the largest block's entries). */
 int pfdr_session_query(pfdr_session *s, const char *what, int64_t *value);
 void pfdr_session_destroy(pfdr_session *s);
 

@@ -233,3 +233,45 @@ def test_edge_ratio_identical(gpu_lib, oracle_port, dt, rcd):
                                                  np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
                                                  0, 0, None, 1.5, 1e-3, rcd, 1e-6, 300, dif=True)
     assert ito == it1 and np.array_equal(X1, Xo)
+
+
+@pytest.mark.parametrize("track", [False, True])
+def test_vertex_pair_identical(gpu_lib, oracle_port, track):
+    """Regular f32 grids with at most ~10 entries per vertex: the vertex
+    sweep takes two record blocks per workgroup (k_vertex_sweep_pair; an odd
+    block count leaves the last one alone) -- the same sums, iterates and
+    evolution partials as the one-block sweep (PFDR_VPAIR=0) and the oracle"""
+    import os
+    dt = np.float32
+    shape = (72, 63, 63)  # 1,117 vertex blocks, the last one partial
+    V, Eu, Ev = _grid(shape, 6, 1)
+    Y = piecewise_observation(shape, 3, dt)
+    it_max = 300 if track else 20
+    kw = dict(difTol=1e-6, difRcd=1e-3, record_dif=True,
+              evolution=pfdr.EVOLUTION_SEQUENTIAL) if track else dict(difTol=0.0, difRcd=0.0)
+    out = []
+    for pair in ("1", "0"):
+        os.environ["PFDR_VPAIR"] = pair
+        try:
+            s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, np.full(Eu.size, 0.1, dt),
+                             np.zeros(V, dt), Y, La_l1=np.full(V, 0.01, dt), rho=1.5,
+                             condMin=1e-3, itMax=it_max, **kw)
+            try:
+                q = s.query("vertex_pair")
+                s.run(it_max)
+                out.append((s.result(), q))
+            finally:
+                s.close()
+        finally:
+            del os.environ["PFDR_VPAIR"]
+    ((X1, it1, _, D1), q1), ((X0, it0, _, D0), q0) = out
+    print("pair cap", q1, "it", it1)
+    assert q1 > 0 and q0 == 0
+    assert it1 == it0 and np.array_equal(X1, X0)
+    if track:
+        assert np.array_equal(D1[:it1], D0[:it0])
+    Xo, ito, _, _ = oracle_port.quadratic_d1_l1(np.zeros(V, dt), Y, None, 0, Eu, Ev,
+                                                 np.full(Eu.size, 0.1, dt), np.full(V, 0.01, dt),
+                                                 0, 0, None, 1.5, 1e-3, kw["difRcd"],
+                                                 kw["difTol"], it_max, dif=True)
+    assert ito == it1 and np.array_equal(X1, Xo)
