@@ -1555,14 +1555,22 @@ void QuadSession<real>::vertex_sweep(int bbeg, int bend, const Ctrl<real> *c, co
             a, wzp_.p, pad_nmax_, ends_ ? pidx_.p : nullptr, ends_ ? xpe_.p : nullptr);
         return;
     }
-    if (vpair_cap_ && bend2 <= bbeg2) {  // pairs of record blocks, one range
-        const int np = (a.nb + 1) / 2;
-        a.xcd = xcd_fit(np, xcd_v_);
+    if (vpair_cap_ && bend2 <= bbeg2 && a.nb >= 2) {  // pairs of record blocks, one range
+        const int np = a.nb / 2;
         const size_t lb = 2 * (size_t)vpair_cap_ * sizeof(real);
-        if (zdirect())
-            k_vertex_sweep_pair<real, true><<<xcd_grid(np, a.xcd), kBlock, lb, s>>>(a, vpair_cap_);
-        else
-            k_vertex_sweep_pair<real><<<xcd_grid(np, a.xcd), kBlock, lb, s>>>(a, vpair_cap_);
+        if (a.nb & 1) {  // the odd last block first, on its own
+            VArgs<real> a1 = a;
+            a1.bbeg = a.bbeg + a.nb - 1;
+            a1.nb = 1;
+            a1.bsplit = 1;
+            a1.xcd = 0;
+            if (zdirect()) k_vertex_sweep<real, 8, true><<<1, kBlock, 0, s>>>(a1);
+            else k_vertex_sweep<real, 8><<<1, kBlock, 0, s>>>(a1);
+        }
+        a.xcd = xcd_fit(np, xcd_v_);
+        const int g = xcd_grid(np, a.xcd);
+        if (zdirect()) k_vertex_sweep_pair<real, true><<<g, kBlock, lb, s>>>(a, vpair_cap_);
+        else k_vertex_sweep_pair<real><<<g, kBlock, lb, s>>>(a, vpair_cap_);
         return;
     }
     if (zdirect())

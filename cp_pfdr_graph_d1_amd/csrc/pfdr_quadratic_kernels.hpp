@@ -557,7 +557,9 @@ __device__ __forceinline__ void tile_sum_rec2(int V, long E, int b0, int v0, int
         Slots12 d[2];
         Pk<real, VE> x[2][ZV];
         long gb[2];
-        int lo[2], hi[2], pg[2], hb[2];  // lo, hi: the run's bounds relative to the group, clamped
+        // the run's bounds relative to the group (clamped to [-1, G + 1]) and
+        // the block, packed: (lo + 1) | (hi + 1) << 4 | h << 8
+        int pg[2], mt[2];
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int k = min(b + u * kBlock + tid, tot - 1);
@@ -574,7 +576,6 @@ __device__ __forceinline__ void tile_sum_rec2(int V, long E, int b0, int v0, int
             const int sr = __shfl(st, base + r, kWave), lr = __shfl(ln, base + r, kWave);
             const int pb = __shfl(P, base + max(r - 1, 0), kWave);
             const int pv = __shfl(pr, 16 * h + min(r + 1, 15), kWave);
-            hb[u] = h;
             long L, H;
             if (kk < ngu) {
                 gb[u] = (h ? fu1 : fu0) + kk;
@@ -589,8 +590,8 @@ __device__ __forceinline__ void tile_sum_rec2(int V, long E, int b0, int v0, int
                 H = A + lr;
                 pg[u] = pv + gi;
             }
-            lo[u] = (int)max(L - gb[u] * G, -1L);
-            hi[u] = (int)min(H - gb[u] * G, (long)G + 1);
+            const int lo = (int)max(L - gb[u] * G, -1L), hi = (int)min(H - gb[u] * G, (long)G + 1);
+            mt[u] = (lo + 1) | (hi + 1) << 4 | h << 8;
         }
 #pragma unroll
         for (int u = 0; u < 2; u++) {
@@ -601,10 +602,11 @@ __device__ __forceinline__ void tile_sum_rec2(int V, long E, int b0, int v0, int
 #pragma unroll
         for (int u = 0; u < 2; u++)
             if (b + u * kBlock + tid < tot) {
-                real *l = lds + (hb[u] ? cap : 0);
+                real *l = lds + ((mt[u] >> 8) ? cap : 0);
+                const int lo = (mt[u] & 15) - 1, hi = ((mt[u] >> 4) & 15) - 1;
 #pragma unroll
                 for (int q = 0; q < G; q++)
-                    if (q >= lo[u] && q < hi[u]) l[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
+                    if (q >= lo && q < hi) l[slot12(d[u], q)] = x[u][q / VE].v[q % VE];
             }
     }
     __syncthreads();
@@ -2595,11 +2597,10 @@ __global__ __launch_bounds__(256, VSweep<real>::waves) void k_vertex_sweep(VArgs
 // blocks 2p, 2p + 1 of the launch (pairs walked last to first, as
 // k_vertex_sweep walks blocks), both blocks' contributions staged together
 // (tile_sum_rec2) into a dynamic LDS list of 2 cap entries, cap = the
-// largest record block's entry count; an odd last block runs alone.  Block
-// partials stay per vertex block.
+// largest record block's entry count; an odd last block is launched on its
+// own (k_vertex_sweep).  Block partials stay per vertex block.
 template <typename real, bool ZD = false>
-__global__ __launch_bounds__(256, VSweep<real>::waves - 1) void k_vertex_sweep_pair(VArgs<real> a,
-                                                                               int cap) {
+__global__ __launch_bounds__(256, 7) void k_vertex_sweep_pair(VArgs<real> a, int cap) {
     int halt = 0;
     if (a.ctrl) {
         if (!a.late) {
@@ -2612,37 +2613,21 @@ __global__ __launch_bounds__(256, VSweep<real>::waves - 1) void k_vertex_sweep_p
     real *lds = reinterpret_cast<real *>(vpair_lds);
     __shared__ real red[2][kBlock / kWave];
     __shared__ int scan[3 * kTileRuns + 2 * (kBlock / kWave)];  // (the degree totals)
-    const int np = (a.nb + 1) / 2;
+    const int np = a.nb / 2;  // (an odd last block: a k_vertex_sweep launch of its own)
     int lp = xcd_block(blockIdx.x, np, a.xcd);
     if (lp >= np) return;
     lp = np - 1 - lp;
     const int b0 = a.bbeg + 2 * lp;
-    const bool odd = 2 * lp + 1 >= a.nb;  // the odd last block runs alone (block-uniform)
     const int v0 = b0 * kBlock + threadIdx.x, v1 = v0 + kBlock;
     const VOps<real> o0 = vertex_ops(a, v0);
     const real wv0 = ZD && v0 < a.V ? a.a0 * (a.gi ? o0.ia : a.invAux[v0]) : real(1);
-    real x0, x1 = real(0);
-    if (odd) {
-        x0 = tile_sum_rec<real, ZD>(a.V, a.E, b0, v0, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz,
-                                    lds, scan + 3 * kTileRuns, wv0, a.ptab, a.prec);
-        if (halt) return;
-        real n0, d0;
-        vertex_finish(a, v0, x0, o0, n0, d0);
-        if (a.track) {
-            n0 = block_sum(n0, red[0]);
-            d0 = block_sum(d0, red[1]);
-            if (threadIdx.x == 0) {
-                a.part[2 * b0] = n0;
-                a.part[2 * b0 + 1] = d0;
-            }
-        }
-        return;
-    }
-    const VOps<real> o1 = vertex_ops(a, v1);
-    const real wv1 = ZD && v1 < a.V ? a.a0 * (a.gi ? o1.ia : a.invAux[v1]) : real(1);
+    real x0, x1;
+    // block b0 + 1's operands after the sum (registers), its weight now
+    const real wv1 = ZD && v1 < a.V ? a.a0 * (a.gi ? a.gi[v1].y : a.invAux[v1]) : real(1);
     tile_sum_rec2<real, ZD>(a.V, a.E, b0, v0, v1, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz, lds,
                             cap, scan + 3 * kTileRuns, wv0, wv1, a.ptab, a.prec, x0, x1);
     if (halt) return;  // block-uniform (a.late)
+    const VOps<real> o1 = vertex_ops(a, v1);
     real n0, d0, n1, d1;
     vertex_finish(a, v0, x0, o0, n0, d0);
     vertex_finish(a, v1, x1, o1, n1, d1);
