@@ -428,6 +428,12 @@ def main():
         knames["edge_sweep"] = ["k_edge_sweep_us"]
     if quad and sess.query("tiled_blocks"):  # tile-ordered edges (large single-GPU graphs)
         knames["edge_sweep"] = ["k_edge_sweep_tl"]
+    try:  # two record blocks per workgroup (regular f32 grids; a library before round 6 has no key)
+        vpair = quad and sess.query("vertex_pair") > 0
+    except pfdr.PFDRError:
+        vpair = False
+    if vpair:  # (an odd last block runs in a k_vertex_sweep launch of its own)
+        knames["vertex_sweep"] = ["k_vertex_sweep_pair", "k_vertex_sweep"]
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
     if not quad and 0 < getattr(wl, "K", 0) <= 64:  # workgroups of M vertex blocks (default),
