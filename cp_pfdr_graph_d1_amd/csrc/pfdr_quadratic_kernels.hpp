@@ -2444,13 +2444,14 @@ struct VOps {
 // terms (tracked) or the dense modes (P kept until their forward step); an
 // untracked identity / diagonal-A sweep overwrites both (8 B per vertex).
 template <typename real>
-__device__ __forceinline__ VOps<real> vertex_ops(const VArgs<real> &a, int v) {
+__device__ __forceinline__ VOps<real> vertex_ops(const VArgs<real> &a, int v,
+                                                 const R2<real> *gpre = nullptr) {
     VOps<real> o;
     if (v < a.V) {
         if (a.track || !a.fwd) o.q = a.xp[v];
         real g = real(0);
         if (a.gi) {
-            const R2<real> p = a.gi[v];
+            const R2<real> p = gpre ? *gpre : a.gi[v];  // (gpre: loaded by the caller)
             g = p.x;
             o.ia = p.y;
         } else if (a.fwd || a.l1uni) {
@@ -2622,12 +2623,15 @@ __global__ __launch_bounds__(256, 7) void k_vertex_sweep_pair(VArgs<real> a, int
     const VOps<real> o0 = vertex_ops(a, v0);
     const real wv0 = ZD && v0 < a.V ? a.a0 * (a.gi ? o0.ia : a.invAux[v0]) : real(1);
     real x0, x1;
-    // block b0 + 1's operands after the sum (registers), its weight now
-    const real wv1 = ZD && v1 < a.V ? a.a0 * (a.gi ? a.gi[v1].y : a.invAux[v1]) : real(1);
+    // block b0 + 1's metric pair now (its weight), its other operands after
+    // the sum (registers)
+    R2<real> g1{};
+    if (a.gi && v1 < a.V) g1 = a.gi[v1];
+    const real wv1 = ZD && v1 < a.V ? a.a0 * (a.gi ? g1.y : a.invAux[v1]) : real(1);
     tile_sum_rec2<real, ZD>(a.V, a.E, b0, v0, v1, a.deg8, a.slots, a.trec, ZD ? a.zs : a.wz, lds,
                             cap, scan + 3 * kTileRuns, wv0, wv1, a.ptab, a.prec, x0, x1);
     if (halt) return;  // block-uniform (a.late)
-    const VOps<real> o1 = vertex_ops(a, v1);
+    const VOps<real> o1 = vertex_ops(a, v1, a.gi ? &g1 : nullptr);
     real n0, d0, n1, d1;
     vertex_finish(a, v0, x0, o0, n0, d0);
     vertex_finish(a, v1, x1, o1, n1, d1);
