@@ -207,7 +207,8 @@ def solve_loopback(k, kind, dtype, Eu, Ev, La_d1, X0, Y, A=None, La_l1=None,
             queries[r] = {q: s.query(q) for q in ("ghosts", "speculative", "seqdif")}
             if kind != pfdr.PFDR_KIND_SIMPLEX:
                 queries[r].update({q: s.query(q) for q in ("split_blocks", "ustaged", "tiled_blocks",
-                                                            "record_blocks")})
+                                                            "record_blocks", "edge_ratio",
+                                                            "vertex_pair")})
             s.run(itMax)
             results[r] = s.result()
             s.close()

@@ -143,6 +143,38 @@ def test_partitioned_headline_slab_matches_single(gpu_lib):
     assert np.array_equal(X, Xs)
 
 
+@pytest.mark.parametrize("k", [2, 3])
+def test_partitioned_tiled_ratio_matches_single(gpu_lib, k):
+    """tiled ranks (590K / 393K vertices each) with one edge weight, untracked:
+    every rank's edge sweep reads the formed per-vertex ratios of its owned
+    and ghost ends (k_ratio_vertex over the pulled metric) -- the iterate
+    equals the single-GPU session's (itself on the ratio edge sweep and the
+    pair vertex sweep) bit for bit"""
+    from cp_pfdr_graph_d1_amd import partition as P
+    from cp_pfdr_graph_d1_amd import pfdr
+    from cp_pfdr_graph_d1_amd.graphs import grid_graph, piecewise_observation
+    dt = np.float32
+    shape = (128, 96, 96)
+    V = int(np.prod(shape))
+    Eu, Ev = grid_graph(shape, 6)
+    Eu, Ev = Eu.astype(np.int32), Ev.astype(np.int32)
+    Y = piecewise_observation(shape, 5, dt)
+    La = np.full(Eu.size, 0.1, dt)
+    L1 = np.full(V, 0.01, dt)
+    X0 = np.zeros(V, dt)
+    s = pfdr.Session(pfdr.PFDR_KIND_L1, dt, V, Eu.size, Eu, Ev, La, X0, Y, La_l1=L1, itMax=20)
+    assert s.query("edge_ratio") == 1 and s.query("vertex_pair") > 0
+    s.run(20)
+    Xs, its, _, _ = s.result()
+    s.close()
+    X, it, _, _, info = P.solve_loopback(k, pfdr.PFDR_KIND_L1, dt, Eu, Ev, La, X0, Y, La_l1=L1,
+                                         itMax=20)
+    print([(q["tiled_blocks"], q["edge_ratio"], q["vertex_pair"]) for q in info["queries"]])
+    assert all(q["tiled_blocks"] > 0 and q["edge_ratio"] == 1 for q in info["queries"])
+    assert it == its == 20
+    assert np.array_equal(X, Xs)
+
+
 def test_rccl_transport_single_rank(gpu_lib):
     """the RCCL transport code path (comm init, grouped send/recv, all-reduce,
     broadcast, chain) on a 1-rank communicator: equals the plain session"""
