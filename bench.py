@@ -436,6 +436,10 @@ def main():
         knames["vertex_sweep"] = ["k_vertex_sweep_pair", "k_vertex_sweep"]
     if symv:
         knames["symv"] = ["k_symv_tiles", "k_symv_finish"]
+    # the dense direct products (N > 0): the column dots and the row partials
+    # with their fixed-order finish
+    knames["gemv_cols"] = ["k_col_dot"]
+    knames["gemv_rows"] = ["k_rows_partial", "k_rows_finish"]
     if not quad and 0 < getattr(wl, "K", 0) <= 64:  # workgroups of M vertex blocks (default),
         # or the one-block sweep (PFDR_SX_M=1)
         knames["sx_vertex_sweep"] = ["k_sx_vertex_tile", "k_sx_vertex_sweep"]
